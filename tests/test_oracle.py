@@ -1,0 +1,172 @@
+"""Pin the CPU oracle against the reference's own outputs (tests/golden/).
+
+Every vector here was produced by importing the reference
+(tests/golden/make_golden.py); the oracle must reproduce each one exactly.
+"""
+import ctypes as C
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, load_golden
+from oracle import oracle as orc
+from oracle import synth
+
+REF_REGISTERED = (1, 2, 3, 4, 5, 6, 7, 255)   # methods registered in the reference here
+
+
+@pytest.fixture(scope="module")
+def codecs():
+    return load_golden("codecs.json")
+
+
+def test_rle_vectors(codecs):
+    for rec in codecs:
+        d = bytes.fromhex(rec["data"])
+        assert orc.rle_encode(d).hex() == rec["rle"]["out"], rec["name"]
+
+
+def test_huffman_vectors(codecs):
+    for rec in codecs:
+        d = bytes.fromhex(rec["data"])
+        got = orc.huff_encode(d)
+        if rec["huffman"]["ok"]:
+            assert got is not None and got.hex() == rec["huffman"]["out"], rec["name"]
+        else:
+            assert got is None, rec["name"]
+
+
+def test_dictionary_vectors(codecs):
+    n = 0
+    for rec in codecs:
+        if "dictionary" in rec:
+            d = bytes.fromhex(rec["data"])
+            assert orc.dict_encode(d).hex() == rec["dictionary"]["out"], rec["name"]
+            n += 1
+    assert n > 20
+
+
+def test_should_use_vectors(codecs):
+    for rec in codecs:
+        d = bytes.fromhex(rec["data"])
+        for mid in (1, 2, 3, 4):
+            assert orc.should_use(mid, d) == rec["should_use"][str(mid)], (rec["name"], mid)
+
+
+def test_entropy_table_matches_scalar_numpy():
+    # the vectorised table must equal the reference's scalar p*np.log2(p) terms
+    for n in (100, 1024, 4096):
+        t = orc.entropy_table(n)
+        for c in (1, 2, 3, 7, 31, 32, 100, n // 3, n - 1, n):
+            p = c / n
+            assert t[c] == p * np.log2(p)
+
+
+def test_huffman_code_tables():
+    for rec in load_golden("huffman_codes.json"):
+        hist = [tuple(x) for x in rec["hist"]]
+        got = orc.huff_code_table(hist)
+        assert {str(k): v for k, v in got.items()} == rec["codes"], hist[:4]
+
+
+def test_decode_kats():
+    for rec in load_golden("decode_kat.json"):
+        body = bytes.fromhex(rec["body"])
+        if rec["ok"]:
+            out = orc.decompress_body(body, rec["orig_size"], REF_REGISTERED)
+            assert out.hex() == rec["out"], rec["name"]
+        else:
+            with pytest.raises(ValueError, match="Marker mismatch"):
+                orc.decompress_body(body, rec["orig_size"], REF_REGISTERED)
+
+
+def _input_for(rec):
+    data = synth.generate(rec["size"], rec["seed"])
+    assert hashlib.sha256(data).hexdigest() == rec["input_sha256"]
+    return data
+
+
+def test_whole_files_native_and_reference():
+    checked = 0
+    for rec in load_golden("files.json"):
+        if rec["mode"] not in ("native", "reference"):
+            continue
+        if set(rec["methods"]) - {1, 2, 3, 4, 9, 255}:
+            continue        # id 5 (zlib DEFLATE) encode is SURVEY §8(f) "next"; decode is tested
+        data = _input_for(rec)
+        blob, stats = orc.compress_file_bytes(data, rec["chunk"], rec["mode"], rec["methods"])
+        with open(os.path.join(GOLDEN, rec["file"]), "rb") as f:
+            ref = f.read()
+        assert hashlib.sha256(blob).hexdigest() == rec["output_sha256"], rec["name"]
+        assert blob == ref
+        assert stats == rec["stats"], rec["name"]
+        checked += 1
+    assert checked >= 20
+
+
+def test_whole_files_decode():
+    for rec in load_golden("files.json"):
+        data = _input_for(rec)
+        with open(os.path.join(GOLDEN, rec["file"]), "rb") as f:
+            blob = f.read()
+        if blob[:4] != b"AMBC":
+            assert blob == data       # stored raw (adaptive_compressor.py:241-247)
+            with pytest.raises(ValueError, match="Magic mismatch"):
+                orc.decompress_file_bytes(blob)
+            continue
+        assert orc.decompress_file_bytes(blob, REF_REGISTERED) == data, rec["name"]
+
+
+def test_config1_behaviour():
+    rec = load_golden("config1.json")
+    data = synth.random_bytes(rec["size"], rec["seed"])
+    assert hashlib.sha256(data).hexdigest() == rec["input_sha256"]
+    blob, stats = orc.compress_file_bytes(data, rec["chunk"], "reference", REF_REGISTERED)
+    assert rec["output_equals_input"] and blob == data
+    assert stats == rec["stats"]
+    with pytest.raises(ValueError, match=rec["decompress_exception"]["msg"]):
+        orc.decompress_file_bytes(blob)
+
+
+def test_synth_c_matches_numpy():
+    for n, seed in ((1, 1), (1000, 2), (300000, 20250418), (1 << 20, 7)):
+        assert orc.synth(n, seed) == synth.generate(n, seed)
+    assert orc.random_bytes(12345, 9) == synth.random_bytes(12345, 9)
+
+
+def test_synth_pinned_sha():
+    # pins the "ambc-mixed v1" stream definition
+    d = synth.generate(1 << 20, 20250418)
+    assert hashlib.sha256(d).hexdigest() == \
+        "925fb804a49288d2eacf9f5036f89fbc31fa0b35e91e834e5b3d0479ea8969fd"
+
+
+def _liblz4():
+    try:
+        return C.CDLL("liblz4.so.1")
+    except OSError:
+        pytest.skip("system liblz4 not present")
+
+
+def test_lz4_frames_decode_with_system_liblz4():
+    lz = _liblz4()
+    lz.LZ4_decompress_safe.argtypes = [C.c_char_p, C.c_void_p, C.c_int, C.c_int]
+    lz.LZ4_decompress_safe.restype = C.c_int
+    mixed = synth.generate(1 << 20, 3)
+    cases = [bytes(4096), b"a" * 13, b"abcdefghijkl" * 300, os.urandom(4096)]
+    cases += [mixed[o:o + n] for o, n in ((0, 4096), (70000, 4096), (140000, 8192),
+                                           (400000, 65536), (5, 1024), (9, 17))]
+    for d in cases:
+        fr = orc.lz4_frame_encode(d)
+        assert fr[:6] == b"\x04\x22\x4d\x18\x68\x40"
+        assert fr[14] == (orc.xxh32(fr[4:14]) >> 8) & 0xFF
+        bs = int.from_bytes(fr[15:19], "little")
+        if bs & 0x80000000:
+            assert fr[19:19 + (bs & 0x7FFFFFFF)] == d
+            continue
+        out = C.create_string_buffer(len(d) + 16)
+        r = lz.LZ4_decompress_safe(fr[19:19 + bs], out, bs, len(d) + 16)
+        assert r == len(d) and out.raw[:r] == d
+        assert orc.decode_chunk(9, fr, len(d)) == d
