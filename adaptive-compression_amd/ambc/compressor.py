@@ -1,0 +1,317 @@
+"""Drop-in AdaptiveCompressor for the MI355X path.
+
+Same constructor, attributes, ``compress(input_file, output_file)`` /
+``decompress(input_file, output_file)`` file API and stats dicts as the
+reference (adaptive_compressor.py:49-700).  The two chunk loops
+(``_adaptive_compress`` :363-394 with its selector :537-590, and
+``_adaptive_decompress`` :396-454) are ONE C-ABI call each into
+libambc_hip.so; the container header, MD5 and the whole-file raw fallback stay
+here exactly as the reference writes them.
+
+Chunking: the reference tries 8 candidate sizes at every position.  This
+engine runs a single chunk size C (``chunk_size=``, default 4096), i.e.
+``CHUNK_SIZE_CANDIDATES = [C]``, in one of two modes:
+
+* ``mode='native'``    every C-byte chunk is decided independently (the
+  reference's ``_pick_best_chunk_and_method(chunk, 0)`` + ``_process_chunk``
+  per chunk);
+* ``mode='reference'`` byte-identical to the reference loop with
+  ``CHUNK_SIZE_CANDIDATES=[C]``, including its remainder-raw rule (the first
+  chunk nothing compresses swallows the rest of the file as one raw chunk).
+
+The multi-size adaptive search is SURVEY §8(f) "next".
+"""
+import ctypes as C
+import hashlib
+import os
+import threading
+import time
+
+import numpy as np
+
+from . import _lib
+from .container import (FORMAT_VERSION, MAGIC_NUMBER, MARKER_BYTES, MARKER_LENGTH,
+                        build_header, marker_bytes_aligned, parse_header,
+                        update_compressed_size)
+from .methods import DECODE_METHODS, GPU_METHODS, NoCompression
+from .registry import (DEFAULT_CHUNK_SIZE, DEFAULT_METHODS, HOST_LIBRARY_IDS, METHOD_CHUNK_PREFS,
+                       METHOD_NAMES, method_mask)
+
+_TERMS = {}
+
+
+def entropy_terms(n):
+    """numpy's ``p * np.log2(p)`` for p = c/n, c = 0..n -- the exact terms
+    HuffmanCompression.should_use sums (compression_methods.py:566-571).  The
+    kernel only consults them when its fp64 entropy is within 1e-9 of 7.0."""
+    t = _TERMS.get(n)
+    if t is None:
+        c = np.arange(n + 1, dtype=np.float64)
+        p = c / float(n)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            t = p * np.log2(p)
+        t[0] = 0.0
+        t = np.ascontiguousarray(t)
+        if len(_TERMS) < 16:
+            _TERMS[n] = t
+    return t
+
+
+class AdaptiveCompressor:
+    MAGIC_NUMBER = MAGIC_NUMBER
+    FORMAT_VERSION = FORMAT_VERSION
+    CHUNK_SIZE_CANDIDATES = [DEFAULT_CHUNK_SIZE]
+
+    def __init__(self, marker_max_length=32, sample_size=10000, *, chunk_size=None,
+                 mode="native", methods=None, devices=None):
+        self.marker_max_length = marker_max_length
+        self.sample_size = sample_size
+        self.marker_finder = None          # the reference's finder is never called (:303-310)
+        self.marker_bytes = None
+        self.marker_length = 0
+        self.marker_pattern = ""
+        self.marker_bytes_aligned = b""
+        self.marker_byte_length = 0
+        self.use_multithreading = False
+        self.max_workers = max(1, (os.cpu_count() or 2) - 1)
+        self.progress_callback = None
+        if mode not in ("native", "reference"):
+            raise ValueError("mode must be 'native' or 'reference'")
+        self.mode = mode
+        if chunk_size is not None:
+            self.CHUNK_SIZE_CANDIDATES = [int(chunk_size)]
+        ids = tuple(DEFAULT_METHODS if methods is None else [m for m in methods if m != 255])
+        method_mask(ids)                    # validates: GPU encoders only
+        self.compression_methods = [GPU_METHODS[i]() for i in sorted(set(ids))] + [NoCompression()]
+        # decode side: every id the reference registers here (+ LZ4, which it
+        # registers when python-lz4 is installed)
+        self.method_lookup = {i: cls() for i, cls in DECODE_METHODS.items()}
+        for m in self.compression_methods:
+            self.method_lookup[m.type_id] = m
+        self.method_names = dict(METHOD_NAMES)
+        self.method_chunk_prefs = dict(METHOD_CHUNK_PREFS)
+        self.devices = list(devices) if devices else None
+        self.chunk_stats = None
+
+    # -- API parity helpers (adaptive_compressor.py:179-194) --------------------
+    def set_progress_callback(self, callback):
+        self.progress_callback = callback
+
+    def _update_progress(self, stage, current, total, current_chunk=None, total_chunks=None):
+        if self.progress_callback:
+            self.progress_callback(stage, current, total, current_chunk, total_chunks)
+
+    def enable_multithreading(self, max_workers=None):
+        self.use_multithreading = True
+        if max_workers:
+            self.max_workers = max_workers
+        print(f"Multithreading enabled with {self.max_workers} workers")
+
+    def disable_multithreading(self):
+        self.use_multithreading = False
+        print("Multithreading disabled")
+
+    def _init_marker(self, marker_bytes, marker_length):
+        self.marker_bytes = marker_bytes
+        self.marker_length = marker_length
+        self.marker_pattern = "".join(format(b, "08b") for b in marker_bytes)[:marker_length]
+        self.marker_bytes_aligned = marker_bytes_aligned(marker_bytes, marker_length)
+        self.marker_byte_length = (marker_length + 7) // 8
+
+    def _find_marker(self, file_data, sample_size):
+        return MARKER_BYTES, MARKER_LENGTH
+
+    # -- engine ------------------------------------------------------------------
+    @property
+    def chunk_size(self):
+        cands = list(self.CHUNK_SIZE_CANDIDATES)
+        if len(cands) != 1:
+            raise NotImplementedError(
+                "multi-size CHUNK_SIZE_CANDIDATES search is SURVEY §8(f) 'next'; "
+                "set chunk_size=C (CHUNK_SIZE_CANDIDATES=[C])")
+        return int(cands[0])
+
+    def _params(self, n):
+        C_ = self.chunk_size
+        p = _lib.Params()
+        p.chunk_size = C_
+        p.mode = _lib.MODE_REFERENCE if self.mode == "reference" else _lib.MODE_NATIVE
+        p.method_mask = method_mask([m.type_id for m in self.compression_methods])
+        for i in range(16):
+            lo, hi = self.method_chunk_prefs.get(i, (1, 0))
+            p.pref_min[i], p.pref_max[i] = max(0, lo), min(hi, 0xFFFFFFFF)
+        keep = [entropy_terms(C_)]
+        p.ent_full = keep[0].ctypes.data
+        if n % C_:
+            keep.append(entropy_terms(n % C_))
+            p.ent_tail = keep[1].ctypes.data
+        return p, keep
+
+    def _ctx(self):
+        return _lib.default_context(self.devices)
+
+    def _adaptive_compress(self, file_data):
+        """One C-ABI call: input bytes -> .ambc body (packages + end chunk)."""
+        n = len(file_data)
+        p, keep = self._params(n)
+        ctx = self._ctx()
+        cap = ctx.lib.ambc_compress_bound(n, p.chunk_size)
+        out = bytearray(cap)
+        olen = C.c_uint64()
+        st = _lib.Stats()
+        rc = ctx.lib.ambc_compress_batch(ctx.h, _lib.addr(file_data), n, C.byref(p),
+                                         _lib.addr(out), cap, C.byref(olen), C.byref(st))
+        if rc == _lib.AMBC_E_RANGE:
+            import struct
+            raise struct.error("argument out of range")
+        _lib.check(rc, ctx.lib)
+        del keep
+        self._last_device_stats = st
+        self.chunk_stats = {
+            "total_chunks": int(st.total_chunks),
+            "compressed_chunks": int(st.compressed_chunks),
+            "raw_chunks": int(st.raw_chunks),
+            "method_usage": {m.type_id: int(st.method_usage[m.type_id])
+                             for m in self.compression_methods},
+            "bytes_saved": int(st.bytes_saved),
+            "original_size": n,
+            "compressed_size_without_overhead": int(st.payload_bytes),
+            "overhead_bytes": int(st.overhead_bytes),
+        }
+        self.method_usage_ids = [m.type_id for m in self.compression_methods]
+        return bytes(memoryview(out)[:olen.value])
+
+    def _adaptive_decompress(self, data, orig_size):
+        """One C-ABI call for every GPU-routable chunk; ids 5/6/7 through the
+        reference's library wrappers."""
+        if self.marker_bytes_aligned not in (b"", MARKER_BYTES):
+            raise NotImplementedError("only the reference's constant 32-bit marker is supported")
+        ctx = self._ctx()
+        data = bytes(data)
+        out = bytearray(max(orig_size, 1))
+        reg = (C.c_uint64 * 4)()
+        for t in self.method_lookup:
+            reg[t >> 6] |= 1 << (t & 63)
+        cap = 1 << 12
+        while True:
+            hc = (_lib.HostChunk * cap)()
+            nh = C.c_uint32()
+            st = _lib.Stats()
+            rc = ctx.lib.ambc_decompress_ex(ctx.h, _lib.addr(data), len(data), orig_size, reg,
+                                            _lib.addr(out), hc, cap, C.byref(nh), C.byref(st))
+            if rc == _lib.AMBC_E_CAPACITY and nh.value > cap:
+                cap = nh.value
+                continue
+            if rc == _lib.AMBC_E_MARKER:
+                raise ValueError("Marker mismatch in chunk header.")
+            _lib.check(rc, ctx.lib)
+            break
+        for i in range(nh.value):
+            h = hc[i]
+            payload = data[h.body_off:h.body_off + h.clen]
+            dec = self.method_lookup[h.type].decompress(payload, h.orig)
+            end = min(h.out_off + len(dec), orig_size)
+            if end > h.out_off:
+                out[h.out_off:end] = dec[:end - h.out_off]
+        self._last_device_stats = st
+        return bytes(memoryview(out)[:orig_size])
+
+    # -- stats (adaptive_compressor.py:257-284,482-532) ---------------------------
+    def _build_stats_raw(self, original_size, elapsed):
+        tput = original_size / (1024 * 1024 * elapsed) if elapsed > 0 else 0.0
+        chunk_stats = {"total_chunks": 1, "compressed_chunks": 0, "raw_chunks": 1,
+                       "method_usage": {}, "bytes_saved": 0, "original_size": original_size,
+                       "compressed_size_without_overhead": original_size, "overhead_bytes": 0}
+        return {"original_size": original_size, "compressed_size": original_size, "ratio": 1.0,
+                "percent_reduction": 0.0, "elapsed_time": elapsed,
+                "throughput_mb_per_sec": tput, "chunk_stats": chunk_stats, "overhead_bytes": 0,
+                "compression_efficiency": 1.0}
+
+    def _calculate_compression_stats(self, orig_size, comp_size, elapsed):
+        if orig_size == 0:
+            ratio, pr = 1.0, 0.0
+        else:
+            ratio = comp_size / orig_size
+            pr = (1.0 - ratio) * 100.0
+        throughput = orig_size / (1024 * 1024 * elapsed) if elapsed > 0 else 0.0
+        cs = self.chunk_stats
+        if cs["compressed_chunks"] > 0:
+            cdata = cs["compressed_size_without_overhead"]
+            ocs = 0
+            for mid, cnt in cs["method_usage"].items():
+                if mid != 255 and cnt > 0:
+                    ocs += cnt / cs["total_chunks"] * orig_size
+            eff = cdata / ocs if ocs > 0 else 1.0
+        else:
+            eff = 1.0
+        return {"original_size": orig_size, "compressed_size": comp_size, "ratio": ratio,
+                "percent_reduction": pr, "elapsed_time": elapsed,
+                "throughput_mb_per_sec": throughput, "chunk_stats": cs,
+                "overhead_bytes": cs.get("overhead_bytes", 0),
+                "compression_efficiency": eff}
+
+    def _calculate_decompression_stats(self, csize, dsize, elapsed):
+        tput = dsize / (1024 * 1024 * elapsed) if elapsed > 0 else 0.0
+        return {"compressed_size": csize, "decompressed_size": dsize, "elapsed_time": elapsed,
+                "throughput_mb_per_sec": tput}
+
+    # -- file API (adaptive_compressor.py:221-301) ----------------------------------
+    def compress_bytes(self, file_data):
+        """compress() without the files: returns (container bytes, stats)."""
+        start = time.time()
+        marker_bytes, marker_len = self._find_marker(file_data, self.sample_size)
+        self._init_marker(marker_bytes, marker_len)
+        digest = {}
+        th = threading.Thread(target=lambda: digest.setdefault("md5", hashlib.md5(file_data).digest()))
+        th.start()                               # MD5 overlaps the device work
+        try:
+            body = self._adaptive_compress(file_data)
+        finally:
+            th.join()
+        header = build_header(marker_bytes, marker_len, digest["md5"], len(file_data))
+        final_size = len(header) + len(body)
+        if final_size > len(file_data):
+            print("Compression bigger than original => store raw.")
+            return bytes(file_data), self._build_stats_raw(len(file_data), time.time() - start)
+        header = update_compressed_size(header, len(body))
+        return header + body, self._calculate_compression_stats(len(file_data), final_size,
+                                                                 time.time() - start)
+
+    def compress(self, input_file, output_file):
+        start = time.time()
+        with open(input_file, "rb") as f:
+            file_data = f.read()
+        blob, stats = self.compress_bytes(file_data)
+        with open(output_file, "wb") as f:
+            f.write(blob)
+        stats["elapsed_time"] = time.time() - start
+        if stats["elapsed_time"] > 0:
+            stats["throughput_mb_per_sec"] = len(file_data) / (1024 * 1024 * stats["elapsed_time"])
+        return stats
+
+    def decompress_bytes(self, cdata):
+        hdr = parse_header(cdata)
+        self._init_marker(hdr["marker_bytes"], hdr["marker_length"])
+        body = cdata[hdr["header_size"]:]
+        out = self._adaptive_decompress(body, hdr["original_size"])
+        if hashlib.md5(out).digest() != hdr["checksum"]:
+            raise ValueError("Checksum mismatch => possibly corrupted file.")
+        return out
+
+    def decompress(self, input_file, output_file):
+        start = time.time()
+        with open(input_file, "rb") as f:
+            cdata = f.read()
+        hdr = parse_header(cdata)
+        self._init_marker(hdr["marker_bytes"], hdr["marker_length"])
+        body = cdata[hdr["header_size"]:]
+        decompressed = self._adaptive_decompress(body, hdr["original_size"])
+        with open(output_file, "wb") as f:
+            f.write(decompressed)
+        if hashlib.md5(decompressed).digest() != hdr["checksum"]:
+            raise ValueError("Checksum mismatch => possibly corrupted file.")
+        return self._calculate_decompression_stats(len(cdata), len(decompressed),
+                                                   time.time() - start)
+
+
+HOST_LIBRARY_IDS = HOST_LIBRARY_IDS

@@ -1,0 +1,282 @@
+"""CompressionMethod plugins (the reference's operator interface).
+
+Same contract as compression_methods.py:7-67: ``type_id``,
+``compress(data) -> bytes``, ``decompress(data, original_length) -> bytes``,
+``should_use(data, threshold=0.9) -> bool``, ``calculate_overhead() -> int``,
+exceptions raised like the reference's.
+
+* ids 1, 3, 4, 9 (RLE, Huffman, Delta, LZ4) and 255 run on the GPU through
+  libambc_hip (single-chunk calls of the same kernels the batched path uses);
+* id 2 (Dictionary) decodes on the GPU; its encoder is SURVEY §8(f) "next";
+* ids 5, 6, 7 are the reference's own stdlib library wrappers
+  (advanced_compression.py:71-213) -- the selector never routes to them, they
+  are registered so that reference-produced files holding such chunks decode.
+
+The batched engine (compressor.py) does not call these per chunk: it makes one
+C-ABI call for the whole body.
+"""
+import bz2
+import ctypes as C
+import lzma
+import struct
+import zlib
+from abc import ABC, abstractmethod
+
+from . import _lib
+from .container import MARKER_BYTES
+
+_HDR = struct.Struct("<BBIII")
+_END = MARKER_BYTES + b"\x00\x00" + b"\x00\x00" + b"\x00" * 8
+
+
+class CompressionMethod(ABC):
+    """compression_methods.py:7-67"""
+
+    @property
+    @abstractmethod
+    def type_id(self):
+        ...
+
+    @abstractmethod
+    def compress(self, data):
+        ...
+
+    @abstractmethod
+    def decompress(self, data, original_length):
+        ...
+
+    def should_use(self, data, threshold=0.9):
+        return True
+
+    def calculate_overhead(self):
+        return 0
+
+
+def _ctx():
+    return _lib.default_context()
+
+
+def _gpu_encode(mid, data):
+    data = bytes(data)
+    n = len(data)
+    if n == 0:
+        return b""
+    if n > _lib.MAX_CHUNK:
+        raise ValueError(f"single-chunk GPU encode is limited to {_lib.MAX_CHUNK} bytes")
+    ctx = _ctx()
+    cap = 2 * n + 1344                    # RLE worst case 2n; Huffman table + ~1.13n bits
+    out = (C.c_uint8 * cap)()
+    olen = C.c_uint32()
+    rc = ctx.lib.ambc_encode_method(ctx.h, mid, _lib.addr(data), n, C.addressof(out), cap,
+                                    C.byref(olen))
+    if rc == _lib.AMBC_E_CODEC:
+        # the reference raises here (Huffman on 1 or 256 distinct symbols)
+        raise ValueError(f"method {mid} cannot encode this input")
+    _lib.check(rc, ctx.lib)
+    return bytes(out[:olen.value])
+
+
+def _gpu_should_use(data):
+    """should_use bits from the selector kernel: {1: RLE, 3: Huffman, 4: Delta}."""
+    data = bytes(data)
+    n = len(data)
+    if n == 0:
+        return {1: False, 3: False, 4: False}
+    if n > _lib.MAX_CHUNK:
+        raise ValueError(f"single-chunk analysis is limited to {_lib.MAX_CHUNK} bytes")
+    from .compressor import entropy_terms
+    ctx = _ctx()
+    p = _lib.Params()
+    p.chunk_size = (n + 15) & ~15
+    p.method_mask = (1 << 1) | (1 << 3)
+    for i in range(16):
+        p.pref_min[i], p.pref_max[i] = 0, 0xFFFFFFFF
+    tail = entropy_terms(n)
+    p.ent_full = tail.ctypes.data if n == p.chunk_size else None
+    p.ent_tail = tail.ctypes.data if n != p.chunk_size else None
+    ids = (C.c_uint8 * 1)()
+    pl = (C.c_uint32 * 1)()
+    su = (C.c_uint8 * 1)()
+    _lib.check(ctx.lib.ambc_analyze(ctx.h, _lib.addr(data), n, C.byref(p), C.addressof(ids),
+                                    C.addressof(pl), C.addressof(su)), ctx.lib)
+    return {1: bool(su[0] & 2), 3: bool(su[0] & 8), 4: bool(su[0] & 16)}
+
+
+def _gpu_decode(mid, data, original_length):
+    """method.decompress through the batched GPU decoder (one package)."""
+    data = bytes(data)
+    body = MARKER_BYTES + _HDR.pack(mid, 0, original_length, original_length, len(data)) + data + _END
+    ctx = _ctx()
+    out = (C.c_uint8 * max(1, original_length))()
+    st = _lib.Stats()
+    reg = (C.c_uint64 * 4)()
+    for t in (1, 2, 3, 4, 9, 255):
+        reg[t >> 6] |= 1 << (t & 63)
+    nh = C.c_uint32()
+    _lib.check(ctx.lib.ambc_decompress_ex(ctx.h, _lib.addr(body), len(body), original_length, reg,
+                                          C.addressof(out), None, 0, C.byref(nh), C.byref(st)),
+               ctx.lib)
+    produced = min(int(st.payload_bytes), original_length)
+    return bytes(out[:produced])
+
+
+class RLECompression(CompressionMethod):
+    """compression_methods.py:70-180 on the GPU."""
+    type_id = 1
+
+    def compress(self, data):
+        return _gpu_encode(1, data)
+
+    def decompress(self, data, original_length):
+        if not data:
+            return b""
+        return _gpu_decode(1, data, original_length)
+
+    def should_use(self, data, threshold=0.9):
+        return _gpu_should_use(data)[1]
+
+
+class DictionaryCompression(CompressionMethod):
+    """compression_methods.py:183-343 -- GPU decoder; encoder is SURVEY §8(f) next."""
+    type_id = 2
+
+    def __init__(self, window_size=4096, lookahead_size=32):
+        self.window_size = window_size
+        self.lookahead_size = lookahead_size
+
+    def compress(self, data):
+        raise NotImplementedError("Dictionary (id 2) GPU encoder is not built yet (SURVEY §8(f))")
+
+    def decompress(self, data, original_length):
+        if not data:
+            return b""
+        return _gpu_decode(2, data, original_length)
+
+    def should_use(self, data, threshold=0.9):
+        return False
+
+
+class HuffmanCompression(CompressionMethod):
+    """compression_methods.py:346-574 on the GPU."""
+    type_id = 3
+
+    def compress(self, data):
+        return _gpu_encode(3, data)
+
+    def decompress(self, data, original_length):
+        if not data:
+            return b""
+        return _gpu_decode(3, data, original_length)
+
+    def should_use(self, data, threshold=0.9):
+        return _gpu_should_use(data)[3]
+
+
+class DeltaCompression(CompressionMethod):
+    """compression_methods.py:577-667 on the GPU (never selected: len == n)."""
+    type_id = 4
+
+    def compress(self, data):
+        return _gpu_encode(4, data)
+
+    def decompress(self, data, original_length):
+        if not data:
+            return b""
+        return _gpu_decode(4, data, original_length)
+
+    def should_use(self, data, threshold=0.9):
+        return _gpu_should_use(data)[4]
+
+
+class LZ4Compression(CompressionMethod):
+    """advanced_compression.py:266-307 -- LZ4 frame from the gfx950 encoder
+    ("ambc-lz4 greedy v1" block parse, LZ4F one-block frame layout)."""
+    type_id = 9
+
+    def compress(self, data):
+        return _gpu_encode(9, data)
+
+    def decompress(self, data, original_length):
+        if not data:
+            return b""
+        return _gpu_decode(9, data, original_length)
+
+    def should_use(self, data, threshold=0.9):
+        # advanced_compression.py:298-307: entropy > 8.1 is impossible for bytes
+        return len(data) >= 1024
+
+
+class NoCompression(CompressionMethod):
+    """compression_methods.py:670-713"""
+    type_id = 255
+
+    def compress(self, data):
+        return bytes(data)
+
+    def decompress(self, data, original_length):
+        if len(data) < original_length:
+            return bytes(data) + b"\x00" * (original_length - len(data))
+        return bytes(data[:original_length])
+
+
+# ---- the reference's stdlib library wrappers (decode of ids 5/6/7) -----------
+def _fit(b, n):
+    return b[:n] if len(b) > n else b + bytes(n - len(b))
+
+
+class DeflateCompression(CompressionMethod):
+    """advanced_compression.py:71-107"""
+    type_id = 5
+
+    def compress(self, data, level=9):
+        return zlib.compress(data, level=level) if data else b""
+
+    def decompress(self, data, original_length):
+        if not data:
+            return b""
+        try:
+            return _fit(zlib.decompress(data), original_length)
+        except Exception:  # noqa: BLE001 -- reference returns zeros on error
+            return bytes(original_length)
+
+
+class Bzip2Compression(CompressionMethod):
+    """advanced_compression.py:112-150"""
+    type_id = 6
+
+    def compress(self, data, level=9):
+        return bz2.compress(data, compresslevel=level) if data else b""
+
+    def decompress(self, data, original_length):
+        if not data:
+            return b""
+        try:
+            return _fit(bz2.decompress(data), original_length)
+        except Exception:  # noqa: BLE001
+            return bytes(original_length)
+
+
+class LZMACompression(CompressionMethod):
+    """advanced_compression.py:155-213"""
+    type_id = 7
+
+    def compress(self, data):
+        if not data:
+            return b""
+        c = lzma.LZMACompressor(format=lzma.FORMAT_XZ, check=lzma.CHECK_CRC64,
+                                filters=[{"id": lzma.FILTER_LZMA2, "dict_size": 1 << 24}])
+        return c.compress(data) + c.flush()
+
+    def decompress(self, data, original_length):
+        if not data:
+            return b""
+        try:
+            return _fit(lzma.decompress(data), original_length)
+        except Exception:  # noqa: BLE001
+            return bytes(original_length)
+
+
+GPU_METHODS = {1: RLECompression, 3: HuffmanCompression, 4: DeltaCompression, 9: LZ4Compression}
+DECODE_METHODS = {1: RLECompression, 2: DictionaryCompression, 3: HuffmanCompression,
+                  4: DeltaCompression, 5: DeflateCompression, 6: Bzip2Compression,
+                  7: LZMACompression, 9: LZ4Compression, 255: NoCompression}

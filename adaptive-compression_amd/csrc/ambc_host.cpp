@@ -1,0 +1,839 @@
+// ambc_host.cpp -- the C-ABI of libambc_hip.so (include/ambc.h).
+//
+// Host orchestration only: device workspaces, streams, H2D/D2H, the serial
+// chunk-header walk of _adaptive_decompress (adaptive_compressor.py:399-445,
+// which cannot be parallelised without the lengths it reads) and the launch
+// sequences.  Every byte of codec work runs in the HIP kernels; there is no
+// CPU codec path here.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/ambc.h"
+#include "ambc_internal.h"
+
+using namespace ambc;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                   \
+    do {                                                                               \
+        hipError_t _e = (expr);                                                        \
+        if (_e != hipSuccess)                                                          \
+            return fail(AMBC_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+bool trace_on() {
+    static int on = -1;
+    if (on < 0) on = getenv("AMBC_TRACE") ? 1 : 0;
+    return on == 1;
+}
+#define TRACE(...)                                                   \
+    do {                                                             \
+        if (trace_on()) { fprintf(stderr, "[ambc] " __VA_ARGS__); fputc('\n', stderr); fflush(stderr); } \
+    } while (0)
+
+uint64_t now_ns() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+struct Buf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap && p) return hipSuccess;
+        if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
+        size_t want = std::max<size_t>(bytes, 256);
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    template <typename T> T* as() const { return reinterpret_cast<T*>(p); }
+    void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
+};
+
+struct Dev {
+    int id = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[6] = {};
+    Buf in, out, slots, plen, ids, sizes, off, scan_tmp, acc, ent_full, ent_tail;
+    Buf body, jobs, produced, dout, scratch, seg;
+    uint64_t t_encode = 0, t_scan = 0, t_compact = 0;
+};
+
+}  // namespace
+
+struct ambc_ctx {
+    std::vector<Dev> devs;
+};
+
+// a chunk's scratch slot: winners are < n bytes; forced single-method encodes
+// (ambc_encode_method) can reach 2n (RLE) or ~1.13n + 1284 (Huffman), plus the
+// Huffman bit staging area behind the payload
+static uint32_t slot_stride_for(uint32_t C, bool forced = false) {
+    const uint32_t need = forced ? 3 * C + 1344 : C + 64;
+    return (need + 15) & ~15u;
+}
+
+extern "C" {
+
+int ambc_abi_version(void) { return AMBC_ABI_VERSION; }
+const char* ambc_last_error(void) { return g_err.c_str(); }
+
+int ambc_device_count(int* count) {
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess) { *count = 0; return fail(AMBC_E_DEVICE, hipGetErrorString(e)); }
+    *count = c;
+    return AMBC_OK;
+}
+
+int ambc_init(const int* device_ids, int n_devices, ambc_ctx** out) {
+    if (!out) return fail(AMBC_E_INVAL, "out is NULL");
+    *out = nullptr;
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || count == 0)
+        return fail(AMBC_E_DEVICE, "no HIP device available (libambc_hip has no CPU fallback)");
+    std::unique_ptr<ambc_ctx> ctx(new ambc_ctx());
+    int nd = n_devices > 0 ? n_devices : 1;
+    for (int i = 0; i < nd; i++) {
+        Dev d;
+        d.id = device_ids ? device_ids[i] : i;
+        if (d.id < 0 || d.id >= count) return fail(AMBC_E_INVAL, "device id out of range");
+        HIPCHK(hipSetDevice(d.id));
+        hipDeviceProp_t prop;
+        HIPCHK(hipGetDeviceProperties(&prop, d.id));
+        if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+            return fail(AMBC_E_DEVICE, std::string("libambc_hip is built for gfx950, device is ") +
+                                           prop.gcnArchName);
+        HIPCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+        for (auto& ev : d.ev) HIPCHK(hipEventCreate(&ev));
+        ctx->devs.push_back(d);
+    }
+    *out = ctx.release();
+    return AMBC_OK;
+}
+
+void ambc_destroy(ambc_ctx* ctx) {
+    if (!ctx) return;
+    for (auto& d : ctx->devs) {
+        (void)hipSetDevice(d.id);
+        (void)hipStreamSynchronize(d.stream);
+        for (Buf* b : {&d.in, &d.out, &d.slots, &d.plen, &d.ids, &d.sizes, &d.off, &d.scan_tmp,
+                       &d.acc, &d.ent_full, &d.ent_tail, &d.body, &d.jobs, &d.produced, &d.dout,
+                       &d.scratch, &d.seg})
+            b->release();
+        for (auto& ev : d.ev) (void)hipEventDestroy(ev);
+        (void)hipStreamDestroy(d.stream);
+    }
+    delete ctx;
+}
+
+uint64_t ambc_compress_bound(uint64_t n, uint32_t chunk) {
+    if (chunk == 0) return 0;
+    return n + (uint64_t)HDR * ((n + chunk - 1) / chunk) + END_CHUNK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// compress (device resident)
+// ---------------------------------------------------------------------------
+static int check_params(const ambc_params* p) {
+    if (!p) return fail(AMBC_E_INVAL, "params is NULL");
+    const uint32_t C = p->chunk_size;
+    if (C < 16 || C > AMBC_MAX_CHUNK || (C & 15))
+        return fail(AMBC_E_INVAL, "chunk_size must be a multiple of 16 in [16, 65536]");
+    if (p->mode > 1) return fail(AMBC_E_INVAL, "mode must be AMBC_MODE_NATIVE or AMBC_MODE_REFERENCE");
+    const uint32_t allowed = (1u << AMBC_M_RLE) | (1u << AMBC_M_HUFFMAN) | (1u << AMBC_M_DELTA) |
+                             (1u << AMBC_M_LZ4);
+    if (p->method_mask & ~allowed)
+        return fail(AMBC_E_INVAL, "method_mask holds ids without a GPU encoder (allowed: 1, 3, 4, 9)");
+    return AMBC_OK;
+}
+
+static int compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params* p, uint8_t* d_out,
+                       uint64_t out_cap, uint64_t* out_len, ambc_stats* st) {
+    int rc = check_params(p);
+    if (rc) return rc;
+    const uint32_t C = p->chunk_size;
+    const uint64_t M64 = (n + C - 1) / C;
+    if (M64 > 0x7FFFFFFFull) return fail(AMBC_E_INVAL, "too many chunks for one device call");
+    const uint32_t M = (uint32_t)M64;
+    const bool end = !(p->flags & AMBC_FLAG_NO_END_CHUNK);
+    const uint64_t bound = ambc_compress_bound(n, C) - (end ? 0 : END_CHUNK);
+    if (out_cap < bound) return fail(AMBC_E_CAPACITY, "device output capacity < ambc_compress_bound");
+    HIPCHK(hipSetDevice(d.id));
+    hipStream_t s = d.stream;
+    const uint64_t t0 = now_ns();
+    const uint32_t stride = slot_stride_for(C);
+    HIPCHK(d.slots.ensure((size_t)std::max<uint32_t>(M, 1) * stride));
+    HIPCHK(d.plen.ensure((size_t)(M + 1) * 4));
+    HIPCHK(d.ids.ensure((size_t)M + 16));
+    HIPCHK(d.sizes.ensure((size_t)(M + 1) * 8));
+    HIPCHK(d.off.ensure((size_t)(M + 1) * 8));
+    HIPCHK(d.acc.ensure(260 * 8));
+    // exact entropy tables (optional)
+    const double* ef = nullptr;
+    const double* et = nullptr;
+    if (p->ent_full) {
+        HIPCHK(d.ent_full.ensure((size_t)(C + 1) * 8));
+        HIPCHK(hipMemcpyAsync(d.ent_full.p, p->ent_full, (size_t)(C + 1) * 8, hipMemcpyHostToDevice, s));
+        ef = d.ent_full.as<double>();
+    }
+    const uint32_t tail = (uint32_t)(n % C);
+    if (p->ent_tail && tail) {
+        HIPCHK(d.ent_tail.ensure((size_t)(tail + 1) * 8));
+        HIPCHK(hipMemcpyAsync(d.ent_tail.p, p->ent_tail, (size_t)(tail + 1) * 8, hipMemcpyHostToDevice, s));
+        et = d.ent_tail.as<double>();
+    }
+    EncArgs ea{};
+    ea.in = d_in;
+    ea.n_total = n;
+    ea.chunk_size = C;
+    ea.n_chunks = M;
+    ea.slots = d.slots.as<uint8_t>();
+    ea.slot_stride = stride;
+    ea.method_mask = p->method_mask;
+    ea.plen = d.plen.as<uint32_t>();
+    ea.ids = d.ids.as<uint8_t>();
+    ea.sizes = d.sizes.as<uint64_t>();
+    ea.ent_full = ef;
+    ea.ent_tail = et;
+    for (int i = 0; i < 16; i++) { ea.pref_min[i] = p->pref_min[i]; ea.pref_max[i] = p->pref_max[i]; }
+
+    TRACE("compress_on n=%llu M=%u C=%u", (unsigned long long)n, M, C);
+    HIPCHK(hipEventRecord(d.ev[0], s));
+    HIPCHK(launch_encode(ea, s));
+    HIPCHK(hipEventRecord(d.ev[1], s));
+    if (trace_on()) { HIPCHK(hipStreamSynchronize(s)); TRACE("encode done"); }
+
+    // reference mode: the first chunk with no winner swallows the remainder
+    uint32_t R = M;
+    if (p->mode == AMBC_MODE_REFERENCE && M) {
+        std::vector<uint8_t> ids(M);
+        HIPCHK(hipMemcpyAsync(ids.data(), d.ids.p, M, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        for (uint32_t k = 0; k < M; k++) if (ids[k] == 255) { R = k; break; }
+        if (R < M && n - (uint64_t)R * C > 0xFFFFFFFFull)
+            return fail(AMBC_E_RANGE, "raw remainder does not fit the u32 chunk fields (struct.error)");
+    }
+    HIPCHK(hipMemsetAsync(d.sizes.as<uint64_t>() + R, 0, 8, s));
+    size_t tmpb = 0;
+    HIPCHK(scan_sizes(nullptr, nullptr, R + 1, nullptr, &tmpb, s));
+    HIPCHK(d.scan_tmp.ensure(tmpb));
+    TRACE("scan tmp=%zu", tmpb);
+    HIPCHK(scan_sizes(d.sizes.as<uint64_t>(), d.off.as<uint64_t>(), R + 1, d.scan_tmp.p, &tmpb, s));
+    HIPCHK(hipEventRecord(d.ev[2], s));
+    if (trace_on()) { HIPCHK(hipStreamSynchronize(s)); TRACE("scan done"); }
+    CompactArgs ca{};
+    ca.slots = d.slots.as<uint8_t>();
+    ca.slot_stride = stride;
+    ca.plen = d.plen.as<uint32_t>();
+    ca.ids = d.ids.as<uint8_t>();
+    ca.off = d.off.as<uint64_t>();
+    ca.n_chunks = R;
+    ca.n_total = n;
+    ca.chunk_size = C;
+    ca.out = d_out;
+    HIPCHK(launch_compact(ca, s));
+    HIPCHK(hipEventRecord(d.ev[3], s));
+    if (trace_on()) { HIPCHK(hipStreamSynchronize(s)); TRACE("compact done"); }
+    HIPCHK(hipMemsetAsync(d.acc.p, 0, 260 * 8, s));
+    HIPCHK(launch_stats(d.ids.as<uint8_t>(), d.plen.as<uint32_t>(), R, n, C, d.acc.as<uint64_t>(), s));
+    uint64_t body_len = 0;
+    HIPCHK(hipMemcpyAsync(&body_len, d.off.as<uint64_t>() + R, 8, hipMemcpyDeviceToHost, s));
+    std::vector<uint64_t> acc(260);
+    HIPCHK(hipMemcpyAsync(acc.data(), d.acc.p, 260 * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    TRACE("stats done body_len=%llu", (unsigned long long)body_len);
+    uint64_t rem = 0;
+    if (R < M) {
+        rem = n - (uint64_t)R * C;
+        uint8_t h[HDR] = {0xFF, 0xFF, 0, 0, 255, 0};
+        for (int b = 0; b < 4; b++) {
+            h[6 + b] = (uint8_t)(rem >> (8 * b));
+            h[10 + b] = (uint8_t)(rem >> (8 * b));
+            h[14 + b] = (uint8_t)(rem >> (8 * b));
+        }
+        HIPCHK(hipMemcpy(d_out + body_len, h, HDR, hipMemcpyHostToDevice));
+        HIPCHK(launch_copy(d_out + body_len + HDR, d_in + (uint64_t)R * C, rem, s));
+        body_len += HDR + rem;
+    }
+    if (end) {
+        HIPCHK(launch_end_chunk(d_out + body_len, s));
+        body_len += END_CHUNK;
+    }
+    HIPCHK(hipEventRecord(d.ev[4], s));
+    HIPCHK(hipStreamSynchronize(s));
+    TRACE("tail done");
+    float ms_enc = 0, ms_scan = 0, ms_cmp = 0, ms_all = 0;
+    HIPCHK(hipEventElapsedTime(&ms_enc, d.ev[0], d.ev[1]));
+    HIPCHK(hipEventElapsedTime(&ms_scan, d.ev[1], d.ev[2]));
+    HIPCHK(hipEventElapsedTime(&ms_cmp, d.ev[2], d.ev[3]));
+    HIPCHK(hipEventElapsedTime(&ms_all, d.ev[0], d.ev[4]));
+    d.t_encode = (uint64_t)(ms_enc * 1e6);
+    d.t_scan = (uint64_t)(ms_scan * 1e6);
+    d.t_compact = (uint64_t)(ms_cmp * 1e6);
+    *out_len = body_len;
+    if (st) {
+        std::memset(st, 0, sizeof *st);
+        for (int i = 0; i < 256; i++) st->method_usage[i] = acc[i];
+        st->method_usage[255] = 0;   // the reference counts compressed chunks only
+        st->compressed_chunks = acc[256];
+        st->total_chunks = R + (R < M ? 1 : 0);
+        st->raw_chunks = st->total_chunks - st->compressed_chunks;
+        st->payload_bytes = acc[258];
+        st->bytes_saved = acc[259];
+        st->overhead_bytes = (uint64_t)HDR * st->compressed_chunks + (end ? END_CHUNK : 0);
+        st->kernel_ns = (uint64_t)(ms_all * 1e6);
+        st->total_ns = now_ns() - t0;
+    }
+    return AMBC_OK;
+}
+
+extern "C" int ambc_compress_device(ambc_ctx* ctx, int dev, const void* d_in, uint64_t n,
+                                    const ambc_params* p, void* d_out, uint64_t out_cap,
+                                    uint64_t* out_len, ambc_stats* st, void* stream) {
+    (void)stream;
+    if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) return fail(AMBC_E_INVAL, "bad ctx/dev");
+    if (!out_len) return fail(AMBC_E_INVAL, "out_len is NULL");
+    return compress_on(ctx->devs[dev], (const uint8_t*)d_in, n, p, (uint8_t*)d_out, out_cap, out_len, st);
+}
+
+static void add_stats(ambc_stats* a, const ambc_stats& b) {
+    for (int i = 0; i < 256; i++) a->method_usage[i] += b.method_usage[i];
+    a->total_chunks += b.total_chunks;
+    a->compressed_chunks += b.compressed_chunks;
+    a->raw_chunks += b.raw_chunks;
+    a->bytes_saved += b.bytes_saved;
+    a->payload_bytes += b.payload_bytes;
+    a->overhead_bytes += b.overhead_bytes;
+    a->kernel_ns = std::max(a->kernel_ns, b.kernel_ns);
+}
+
+extern "C" int ambc_compress_batch(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const ambc_params* p,
+                                   uint8_t* out, uint64_t out_cap, uint64_t* out_len, ambc_stats* st) {
+    if (!ctx || (!in && n) || !out || !out_len) return fail(AMBC_E_INVAL, "NULL argument");
+    int rc = check_params(p);
+    if (rc) return rc;
+    const uint64_t t0 = now_ns();
+    const uint32_t C = p->chunk_size;
+    const uint64_t M = (n + C - 1) / C;
+    int G = (int)ctx->devs.size();
+    if (p->mode == AMBC_MODE_REFERENCE || M < (uint64_t)G * 4) G = 1;  // remainder rule is global
+    ambc_stats total{};
+    std::vector<uint64_t> lens(G, 0);
+    std::vector<int> rcs(G, 0);
+    std::vector<std::string> errs(G);
+    std::vector<uint64_t> h2d(G, 0), d2h(G, 0);
+    // (multi-device: run the shards concurrently, then gather in file order)
+    std::vector<ambc_stats> sst(G);
+    std::vector<std::thread> th;
+    for (int g = 0; g < G; g++) {
+        auto fn = [&, g]() {
+            Dev& d = ctx->devs[g];
+            const uint64_t k0 = M * g / G, k1 = M * (g + 1) / G;
+            const uint64_t b0 = k0 * C, b1 = std::min<uint64_t>(k1 * C, n);
+            const uint64_t sn = b1 - b0;
+            ambc_params q = *p;
+            if (g != G - 1) { q.flags |= AMBC_FLAG_NO_END_CHUNK; q.ent_tail = nullptr; }
+            const uint64_t bound = ambc_compress_bound(sn, C);
+            auto body = [&]() -> int {
+                TRACE("shard %d sn=%llu", g, (unsigned long long)sn);
+                HIPCHK(hipSetDevice(d.id));
+                HIPCHK(d.in.ensure(sn + 64));
+                HIPCHK(d.out.ensure(bound + 64));
+                uint64_t t = now_ns();
+                if (sn) HIPCHK(hipMemcpyAsync(d.in.p, in + b0, sn, hipMemcpyHostToDevice, d.stream));
+                HIPCHK(hipStreamSynchronize(d.stream));
+                h2d[g] = now_ns() - t;
+                TRACE("h2d done");
+                return compress_on(d, d.in.as<uint8_t>(), sn, &q, d.out.as<uint8_t>(), d.out.cap,
+                                   &lens[g], &sst[g]);
+            };
+            rcs[g] = body();
+            if (rcs[g]) errs[g] = g_err;
+        };
+        if (G == 1) fn();
+        else th.emplace_back(fn);
+    }
+    for (auto& t : th) t.join();
+    for (int g = 0; g < G; g++)
+        if (rcs[g]) return fail(rcs[g], errs[g]);
+    uint64_t tot = 0;
+    for (int g = 0; g < G; g++) tot += lens[g];
+    if (tot > out_cap) return fail(AMBC_E_CAPACITY, "output buffer too small for the body");
+    uint64_t o = 0;
+    for (int g = 0; g < G; g++) {
+        Dev& d = ctx->devs[g];
+        HIPCHK(hipSetDevice(d.id));
+        uint64_t t = now_ns();
+        HIPCHK(hipMemcpyAsync(out + o, d.out.p, lens[g], hipMemcpyDeviceToHost, d.stream));
+        HIPCHK(hipStreamSynchronize(d.stream));
+        d2h[g] = now_ns() - t;
+        o += lens[g];
+        add_stats(&total, sst[g]);
+    }
+    *out_len = tot;
+    if (st) {
+        *st = total;
+        for (int g = 0; g < G; g++) { st->h2d_ns += h2d[g]; st->d2h_ns += d2h[g]; }
+        st->total_ns = now_ns() - t0;
+    }
+    return AMBC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// per-chunk plugin entry points
+// ---------------------------------------------------------------------------
+static int run_encode_only(Dev& d, const uint8_t* h_in, uint64_t n, const ambc_params* p,
+                           uint32_t flags, std::vector<uint8_t>& ids, std::vector<uint32_t>& plen,
+                           std::vector<uint8_t>* su, std::vector<uint8_t>* slot0) {
+    const uint32_t C = p->chunk_size;
+    const uint32_t M = (uint32_t)((n + C - 1) / C);
+    HIPCHK(hipSetDevice(d.id));
+    hipStream_t s = d.stream;
+    const uint32_t stride = slot_stride_for(C, (flags & ENC_FORCE) != 0);
+    HIPCHK(d.in.ensure(n + 64));
+    HIPCHK(d.slots.ensure((size_t)std::max<uint32_t>(M, 1) * stride));
+    HIPCHK(d.plen.ensure((size_t)(M + 1) * 4));
+    HIPCHK(d.ids.ensure((size_t)M + 16));
+    HIPCHK(d.sizes.ensure((size_t)(M + 1) * 8));
+    HIPCHK(d.seg.ensure((size_t)M + 16));
+    if (n) HIPCHK(hipMemcpyAsync(d.in.p, h_in, n, hipMemcpyHostToDevice, s));
+    const double* ef = nullptr;
+    const double* et = nullptr;
+    if (p->ent_full) {
+        HIPCHK(d.ent_full.ensure((size_t)(C + 1) * 8));
+        HIPCHK(hipMemcpyAsync(d.ent_full.p, p->ent_full, (size_t)(C + 1) * 8, hipMemcpyHostToDevice, s));
+        ef = d.ent_full.as<double>();
+    }
+    const uint32_t tail = (uint32_t)(n % C);
+    if (p->ent_tail && tail) {
+        HIPCHK(d.ent_tail.ensure((size_t)(tail + 1) * 8));
+        HIPCHK(hipMemcpyAsync(d.ent_tail.p, p->ent_tail, (size_t)(tail + 1) * 8, hipMemcpyHostToDevice, s));
+        et = d.ent_tail.as<double>();
+    }
+    EncArgs ea{};
+    ea.in = d.in.as<uint8_t>();
+    ea.n_total = n;
+    ea.chunk_size = C;
+    ea.n_chunks = M;
+    ea.slots = d.slots.as<uint8_t>();
+    ea.slot_stride = stride;
+    ea.method_mask = p->method_mask;
+    ea.plen = d.plen.as<uint32_t>();
+    ea.ids = d.ids.as<uint8_t>();
+    ea.sizes = d.sizes.as<uint64_t>();
+    ea.ent_full = ef;
+    ea.ent_tail = et;
+    ea.su = su ? d.seg.as<uint8_t>() : nullptr;
+    ea.flags = flags;
+    for (int i = 0; i < 16; i++) { ea.pref_min[i] = p->pref_min[i]; ea.pref_max[i] = p->pref_max[i]; }
+    HIPCHK(launch_encode(ea, s));
+    ids.resize(M);
+    plen.resize(M);
+    if (M) {
+        HIPCHK(hipMemcpyAsync(ids.data(), d.ids.p, M, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(plen.data(), d.plen.p, (size_t)M * 4, hipMemcpyDeviceToHost, s));
+    }
+    if (su) {
+        su->resize(M);
+        if (M) HIPCHK(hipMemcpyAsync(su->data(), d.seg.p, M, hipMemcpyDeviceToHost, s));
+    }
+    if (slot0) {
+        slot0->resize(stride);
+        HIPCHK(hipMemcpyAsync(slot0->data(), d.slots.p, stride, hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    return AMBC_OK;
+}
+
+extern "C" int ambc_encode_method(ambc_ctx* ctx, int method_id, const uint8_t* in, uint32_t n,
+                                  uint8_t* out, uint32_t out_cap, uint32_t* out_len) {
+    if (!ctx || ctx->devs.empty() || !out_len || (!in && n)) return fail(AMBC_E_INVAL, "NULL argument");
+    if (method_id != AMBC_M_RLE && method_id != AMBC_M_HUFFMAN && method_id != AMBC_M_LZ4 &&
+        method_id != AMBC_M_DELTA)
+        return fail(AMBC_E_INVAL, "ambc_encode_method supports ids 1, 3, 4 and 9");
+    if (n == 0) { *out_len = 0; return AMBC_OK; }          // every codec: empty -> b''
+    if (n > AMBC_MAX_CHUNK) return fail(AMBC_E_INVAL, "single-chunk encode is limited to 65536 bytes");
+    ambc_params p{};
+    p.chunk_size = (n + 15) & ~15u;
+    p.method_mask = 1u << method_id;
+    for (int i = 0; i < 16; i++) { p.pref_min[i] = 0; p.pref_max[i] = 0xFFFFFFFFu; }
+    std::vector<uint8_t> ids, slot;
+    std::vector<uint32_t> plen;
+    int rc = run_encode_only(ctx->devs[0], in, n, &p, ENC_FORCE, ids, plen, nullptr, &slot);
+    if (rc) return rc;
+    if (ids[0] != method_id) return fail(AMBC_E_CODEC, "codec raises on this input");
+    if (plen[0] > out_cap) return fail(AMBC_E_CAPACITY, "output buffer too small");
+    std::memcpy(out, slot.data(), plen[0]);
+    *out_len = plen[0];
+    return AMBC_OK;
+}
+
+extern "C" int ambc_analyze(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const ambc_params* p,
+                            uint8_t* ids_out, uint32_t* plen_out, uint8_t* su_out) {
+    if (!ctx || ctx->devs.empty() || (!in && n)) return fail(AMBC_E_INVAL, "NULL argument");
+    int rc = check_params(p);
+    if (rc) return rc;
+    std::vector<uint8_t> ids, su;
+    std::vector<uint32_t> plen;
+    rc = run_encode_only(ctx->devs[0], in, n, p, ENC_ANALYZE, ids, plen, &su, nullptr);
+    if (rc) return rc;
+    if (ids_out) std::memcpy(ids_out, ids.data(), ids.size());
+    if (plen_out) std::memcpy(plen_out, plen.data(), plen.size() * 4);
+    if (su_out) std::memcpy(su_out, su.data(), su.size());
+    return AMBC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// decompress
+// ---------------------------------------------------------------------------
+namespace {
+
+constexpr uint32_t STAGE_DEC = 16384;   // must match ambc_decode.hip
+
+bool registered_id(const uint64_t reg[4], uint32_t t) { return (reg[t >> 6] >> (t & 63)) & 1; }
+
+uint32_t rd32le(const uint8_t* p) { return p[0] | p[1] << 8 | p[2] << 16 | (uint32_t)p[3] << 24; }
+
+// upper bound of an LZ4 frame's decoded content (for scratch sizing); 0 if unknown/small
+uint64_t lz4_content_bound(const uint8_t* p, uint32_t plen) {
+    if (plen < 7 || rd32le(p) != 0x184D2204u) return 0;
+    const uint32_t flg = p[4], bd = p[5];
+    const uint32_t bsid = (bd >> 4) & 7;
+    if (bsid < 4) return 0;
+    const uint64_t bmax = 1ull << (8 + 2 * bsid);
+    uint64_t hp = 6;
+    if ((flg >> 3) & 1) {
+        if (hp + 8 > plen) return 0;
+        uint64_t cs = 0;
+        for (int b = 0; b < 8; b++) cs |= (uint64_t)p[hp + b] << (8 * b);
+        return cs;
+    }
+    if (flg & 1) hp += 4;
+    hp += 1;
+    uint64_t bound = 0;
+    while (hp + 4 <= plen) {
+        const uint32_t bs = rd32le(p + hp);
+        hp += 4;
+        if (bs == 0) break;
+        const uint32_t sz = bs & 0x7FFFFFFFu;
+        bound += (bs & 0x80000000u) ? sz : bmax;
+        hp += sz + (((flg >> 4) & 1) ? 4 : 0);
+    }
+    return bound;
+}
+
+struct Walk {
+    std::vector<DecJob> jobs;
+    std::vector<uint32_t> src_index;   // job -> package ordinal
+    std::vector<ambc_host_chunk> host;
+    uint64_t total = 0;
+    uint64_t scratch = 0;
+    bool marker_error = false;
+};
+
+// _adaptive_decompress header walk (adaptive_compressor.py:399-445)
+void walk_body(const uint8_t* body, uint64_t blen, uint64_t orig_size, const uint64_t reg[4],
+               const std::map<uint32_t, uint64_t>& known, Walk& w) {
+    uint64_t pos = 0, out = 0;
+    uint32_t ord = 0;
+    while (pos < blen) {
+        if (pos + HDR > blen) break;
+        if (!(body[pos] == 0xFF && body[pos + 1] == 0xFF && body[pos + 2] == 0 && body[pos + 3] == 0)) {
+            w.marker_error = true;
+            return;
+        }
+        const uint32_t t = body[pos + 4];
+        const uint32_t orig = rd32le(body + pos + 10);
+        const uint32_t clen = rd32le(body + pos + 14);
+        pos += HDR;
+        if (t == 0) break;
+        if (pos + clen > blen) break;
+        DecJob j{};
+        j.body_off = pos;
+        j.clen = clen;
+        j.orig = orig;
+        j.scratch_off = ~0ull;
+        j.scratch_cap = 0;
+        uint64_t expect;
+        if (!registered_id(reg, t)) {
+            j.type = DEC_VERBATIM;
+            expect = clen;
+        } else if (t == 5 || t == 6 || t == 7) {
+            j.type = DEC_SKIP;
+            expect = clen ? orig : 0;
+        } else {
+            j.type = t;
+            switch (t) {
+            case 255: expect = orig; break;
+            case 4: expect = clen ? std::min(clen, orig) : 0; break;
+            default: expect = clen ? orig : 0; break;
+            }
+            if (t == 9 && clen) {
+                const uint64_t cb = lz4_content_bound(body + pos, clen);
+                if (cb > STAGE_DEC) { j.scratch_off = w.scratch; j.scratch_cap = cb; w.scratch += (cb + 15) & ~15ull; }
+            }
+            if (t == 2 && clen && (uint64_t)orig + 256 > STAGE_DEC) {
+                j.scratch_off = w.scratch; j.scratch_cap = (uint64_t)orig + 256;
+                w.scratch += (j.scratch_cap + 15) & ~15ull;
+            }
+        }
+        auto it = known.find(ord);
+        if (it != known.end()) expect = it->second;
+        j.expect = (uint32_t)std::min<uint64_t>(expect, 0xFFFFFFFFull);
+        j.out_off = out;
+        if (j.type == DEC_SKIP) {
+            ambc_host_chunk h{pos, out, clen, orig, t, 0};
+            w.host.push_back(h);
+        }
+        w.jobs.push_back(j);
+        w.src_index.push_back(ord);
+        out += expect;
+        pos += clen;
+        ord++;
+        if (out >= orig_size) break;
+    }
+    w.total = out;
+}
+
+}  // namespace
+
+static int decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t orig_size,
+                         const uint64_t reg[4], uint8_t* out, std::vector<ambc_host_chunk>& host,
+                         ambc_stats* st) {
+    const uint64_t t0 = now_ns();
+    HIPCHK(hipSetDevice(d.id));
+    hipStream_t s = d.stream;
+    HIPCHK(d.body.ensure(blen + 64));
+    uint64_t t = now_ns();
+    if (blen) HIPCHK(hipMemcpyAsync(d.body.p, body, blen, hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const uint64_t h2d = now_ns() - t;
+    std::map<uint32_t, uint64_t> known;
+    Walk w;
+    uint64_t walk_ns = 0, kern_ns = 0;
+    for (int iter = 0; iter < 64; iter++) {
+        w = Walk();
+        t = now_ns();
+        walk_body(body, blen, orig_size, reg, known, w);
+        walk_ns += now_ns() - t;
+        if (w.marker_error) return fail(AMBC_E_MARKER, "Marker mismatch in chunk header.");
+        const uint32_t nj = (uint32_t)w.jobs.size();
+        const uint64_t cap = std::max(w.total, orig_size) + 64;
+        HIPCHK(d.dout.ensure(cap));
+        HIPCHK(d.jobs.ensure((size_t)std::max<uint32_t>(nj, 1) * sizeof(DecJob)));
+        HIPCHK(d.produced.ensure((size_t)std::max<uint32_t>(nj, 1) * 4));
+        HIPCHK(d.scratch.ensure(w.scratch + 64));
+        if (nj) HIPCHK(hipMemcpyAsync(d.jobs.p, w.jobs.data(), nj * sizeof(DecJob), hipMemcpyHostToDevice, s));
+        if (w.total < orig_size) HIPCHK(hipMemsetAsync(d.dout.as<uint8_t>() + w.total, 0, orig_size - w.total, s));
+        DecArgs a{};
+        a.body = d.body.as<uint8_t>();
+        a.out = d.dout.as<uint8_t>();
+        a.out_cap = cap;
+        a.jobs = d.jobs.as<DecJob>();
+        a.n_jobs = nj;
+        a.scratch = d.scratch.as<uint8_t>();
+        a.produced = d.produced.as<uint32_t>();
+        HIPCHK(hipEventRecord(d.ev[0], s));
+        HIPCHK(launch_decode(a, s));
+        HIPCHK(hipEventRecord(d.ev[1], s));
+        std::vector<uint32_t> prod(nj);
+        if (nj) HIPCHK(hipMemcpyAsync(prod.data(), d.produced.p, nj * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, d.ev[0], d.ev[1]));
+        kern_ns += (uint64_t)(ms * 1e6);
+        bool redo = false;
+        for (uint32_t i = 0; i < nj; i++) {
+            if (prod[i] == 0xFFFFFFFFu) return fail(AMBC_E_DEVICE, "decode job failed");
+            if (prod[i] != w.jobs[i].expect) { known[w.src_index[i]] = prod[i]; redo = true; }
+        }
+        if (!redo) break;
+    }
+    t = now_ns();
+    HIPCHK(hipMemcpyAsync(out, d.dout.p, orig_size, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    host = w.host;
+    if (st) {
+        std::memset(st, 0, sizeof *st);
+        st->total_chunks = w.jobs.size();
+        st->payload_bytes = w.total;   // bytes the chunks produced before the final pad/truncate
+        st->h2d_ns = h2d;
+        st->d2h_ns = now_ns() - t;
+        st->walk_ns = walk_ns;
+        st->kernel_ns = kern_ns;
+        st->total_ns = now_ns() - t0;
+    }
+    return AMBC_OK;
+}
+
+extern "C" int ambc_decompress_ex(ambc_ctx* ctx, const uint8_t* body, uint64_t body_len,
+                                  uint64_t orig_size, const uint64_t registered[4], uint8_t* out,
+                                  ambc_host_chunk* host_chunks, uint32_t host_cap, uint32_t* n_host,
+                                  ambc_stats* st) {
+    if (!ctx || ctx->devs.empty() || (!body && body_len) || (!out && orig_size))
+        return fail(AMBC_E_INVAL, "NULL argument");
+    uint64_t reg[4] = {0, 0, 0, 0};
+    if (registered) std::memcpy(reg, registered, sizeof reg);
+    else for (uint32_t t : {1u, 2u, 3u, 4u, 5u, 6u, 7u, 9u, 255u}) reg[t >> 6] |= 1ull << (t & 63);
+    std::vector<ambc_host_chunk> host;
+    int rc = decompress_on(ctx->devs[0], body, body_len, orig_size, reg, out, host, st);
+    if (rc) return rc;
+    if (n_host) *n_host = (uint32_t)host.size();
+    if (host.size() > host_cap) {
+        if (!host_chunks && !n_host) return fail(AMBC_E_HOSTCODEC, "body has zlib/bz2/lzma chunks");
+        if (host.size() > host_cap) return fail(AMBC_E_CAPACITY, "host_chunks capacity too small");
+    }
+    for (size_t i = 0; i < host.size(); i++) host_chunks[i] = host[i];
+    return AMBC_OK;
+}
+
+extern "C" int ambc_decompress_batch(ambc_ctx* ctx, const uint8_t* body, uint64_t body_len,
+                                     uint64_t orig_size, uint8_t* out, ambc_stats* st) {
+    uint32_t nh = 0;
+    int rc = ambc_decompress_ex(ctx, body, body_len, orig_size, nullptr, out, nullptr, 0, &nh, st);
+    if (rc == AMBC_E_CAPACITY && nh) return fail(AMBC_E_HOSTCODEC, "body has zlib/bz2/lzma chunks: use ambc_decompress_ex");
+    return rc;
+}
+
+// ---------------------------------------------------------------------------
+// memory helpers, synth, timings
+// ---------------------------------------------------------------------------
+extern "C" void* ambc_host_alloc(uint64_t bytes) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, std::max<uint64_t>(bytes, 1), hipHostMallocDefault) != hipSuccess) {
+        g_err = "hipHostMalloc failed";
+        return nullptr;
+    }
+    return p;
+}
+extern "C" void ambc_host_free(void* p) { if (p) (void)hipHostFree(p); }
+
+extern "C" void* ambc_device_alloc(ambc_ctx* ctx, int dev, uint64_t bytes) {
+    if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) { g_err = "bad ctx/dev"; return nullptr; }
+    if (hipSetDevice(ctx->devs[dev].id) != hipSuccess) return nullptr;
+    void* p = nullptr;
+    if (hipMalloc(&p, std::max<uint64_t>(bytes, 1)) != hipSuccess) { g_err = "hipMalloc failed"; return nullptr; }
+    return p;
+}
+extern "C" void ambc_device_free(ambc_ctx* ctx, int dev, void* p) {
+    if (!ctx || !p || dev < 0 || dev >= (int)ctx->devs.size()) return;
+    (void)hipSetDevice(ctx->devs[dev].id);
+    (void)hipFree(p);
+}
+extern "C" int ambc_memcpy_h2d(ambc_ctx* ctx, int dev, void* dst, const void* src, uint64_t bytes) {
+    if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) return fail(AMBC_E_INVAL, "bad ctx/dev");
+    HIPCHK(hipSetDevice(ctx->devs[dev].id));
+    HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    return AMBC_OK;
+}
+extern "C" int ambc_memcpy_d2h(ambc_ctx* ctx, int dev, void* dst, const void* src, uint64_t bytes) {
+    if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) return fail(AMBC_E_INVAL, "bad ctx/dev");
+    HIPCHK(hipSetDevice(ctx->devs[dev].id));
+    HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return AMBC_OK;
+}
+extern "C" int ambc_synchronize(ambc_ctx* ctx, int dev) {
+    if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) return fail(AMBC_E_INVAL, "bad ctx/dev");
+    HIPCHK(hipSetDevice(ctx->devs[dev].id));
+    HIPCHK(hipDeviceSynchronize());
+    return AMBC_OK;
+}
+
+static uint64_t mix64h(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+static void synth_segments(uint64_t n, uint64_t seed, std::vector<uint64_t>& seg) {
+    uint64_t s = seed, pos = 0, idx = 0;
+    while (pos < n) {
+        s += 0x9E3779B97F4A7C15ULL;
+        uint64_t L = 1024 + mix64h(s) % 130049ULL;
+        if (L > n - pos) L = n - pos;
+        seg.push_back(pos); seg.push_back(L); seg.push_back(idx);
+        pos += L; idx++;
+    }
+}
+
+extern "C" void ambc_synth_fill(uint8_t* out, uint64_t n, uint64_t seed) {
+    static const char* V[16] = {"alpha", "beta", "gamma", "delta", "the",  "quick", "brown", "fox",
+                                "jumps", "over", "lazy",  "dog",   "data", "chunk", "marker", "stream"};
+    std::vector<uint64_t> seg;
+    synth_segments(n, seed, seg);
+    const size_t ns = seg.size() / 3;
+    unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> th;
+    for (unsigned w = 0; w < nt; w++) {
+        th.emplace_back([&, w]() {
+            for (size_t g = w; g < ns; g += nt) {
+                const uint64_t p = seg[3 * g], L = seg[3 * g + 1], id = seg[3 * g + 2];
+                uint8_t* o = out + p;
+                const uint64_t base = mix64h(seed ^ (id * 0xD1B54A32D192ED03ULL));
+                if (id % 3 == 0) std::memset(o, 0, L);
+                else if (id % 3 == 1) {
+                    for (uint64_t j = 0; j * 8 < L; j++) {
+                        const uint64_t v = mix64h(base + (j + 1) * 0x9E3779B97F4A7C15ULL);
+                        for (int b = 0; b < 8 && j * 8 + b < L; b++) o[j * 8 + b] = (uint8_t)(v >> (8 * b));
+                    }
+                } else {
+                    uint64_t q = 0;
+                    for (uint64_t j = 0; q < L; j++) {
+                        const char* wd = V[mix64h(base + (j + 1) * 0x9E3779B97F4A7C15ULL) >> 60];
+                        for (; *wd && q < L; wd++) o[q++] = (uint8_t)*wd;
+                        if (q < L) o[q++] = ' ';
+                    }
+                }
+            }
+        });
+    }
+    for (auto& t : th) t.join();
+}
+
+extern "C" int ambc_synth_device(ambc_ctx* ctx, int dev, void* d_out, uint64_t n, uint64_t seed) {
+    if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) return fail(AMBC_E_INVAL, "bad ctx/dev");
+    Dev& d = ctx->devs[dev];
+    HIPCHK(hipSetDevice(d.id));
+    std::vector<uint64_t> seg;
+    synth_segments(n, seed, seg);
+    const uint32_t ns = (uint32_t)(seg.size() / 3);
+    HIPCHK(d.seg.ensure(seg.size() * 8 + 8));
+    HIPCHK(hipMemcpyAsync(d.seg.p, seg.data(), seg.size() * 8, hipMemcpyHostToDevice, d.stream));
+    HIPCHK(launch_synth((uint8_t*)d_out, n, d.seg.as<uint64_t>(), ns, seed, d.stream));
+    HIPCHK(hipStreamSynchronize(d.stream));
+    return AMBC_OK;
+}
+
+extern "C" int ambc_last_kernel_times(ambc_ctx* ctx, int dev, uint64_t* encode_ns, uint64_t* scan_ns,
+                                      uint64_t* compact_ns) {
+    if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) return fail(AMBC_E_INVAL, "bad ctx/dev");
+    Dev& d = ctx->devs[dev];
+    if (encode_ns) *encode_ns = d.t_encode;
+    if (scan_ns) *scan_ns = d.t_scan;
+    if (compact_ns) *compact_ns = d.t_compact;
+    return AMBC_OK;
+}

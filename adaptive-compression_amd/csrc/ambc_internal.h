@@ -1,0 +1,85 @@
+// Internal launch structures shared by ambc_kernels.hip and ambc_host.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ambc {
+
+constexpr uint32_t HDR = 18;       // chunk header: marker4 type k used4 orig4 clen4
+constexpr uint32_t END_CHUNK = 16; // _create_end_chunk (u16 used field)
+constexpr uint32_t LZ4_HASH_BITS = 12;
+constexpr uint32_t ENC_FORCE = 1;    // CompressionMethod.compress(chunk) semantics
+constexpr uint32_t ENC_ANALYZE = 2;  // also evaluate every should_use
+
+// per-chunk encode: one 64-lane workgroup per chunk
+struct EncArgs {
+    const uint8_t* in;       // device input
+    uint64_t n_total;        // bytes in this shard/job
+    uint32_t chunk_size;
+    uint32_t n_chunks;
+    uint8_t* slots;          // n_chunks * slot_stride scratch payloads
+    uint32_t slot_stride;
+    uint32_t method_mask;
+    uint32_t* plen;          // payload length per chunk
+    uint8_t* ids;            // method id per chunk (255 raw)
+    uint64_t* sizes;         // 18 + plen per chunk (scan input)
+    const double* ent_full;  // optional exact entropy terms (device)
+    const double* ent_tail;
+    uint8_t* su;             // optional: per-chunk should_use bits (1<<1 RLE, 1<<3 Huffman, 1<<4 Delta)
+    uint32_t flags;          // ENC_FORCE: encode with the single enabled method, no gates
+    uint32_t pref_min[16];
+    uint32_t pref_max[16];
+};
+
+// gather the packages into the body at their scanned offsets
+struct CompactArgs {
+    const uint8_t* slots;
+    uint32_t slot_stride;
+    const uint32_t* plen;
+    const uint8_t* ids;
+    const uint64_t* off;     // exclusive scan of sizes (n_chunks+1)
+    uint32_t n_chunks;       // packages to write
+    uint64_t n_total;
+    uint32_t chunk_size;
+    uint8_t* out;
+};
+
+// one decode job per chunk package (built by the host header walk)
+struct DecJob {
+    uint64_t body_off;  // payload offset in body
+    uint64_t out_off;   // output offset
+    uint64_t scratch_off;  // device scratch for outputs that overshoot orig (~0 = none)
+    uint64_t scratch_cap;
+    uint32_t clen;
+    uint32_t orig;
+    uint32_t type;      // method id, or 256 = copy verbatim, 257 = skip (host codec)
+    uint32_t expect;    // bytes the host walk assumed this chunk produces
+};
+
+struct DecArgs {
+    const uint8_t* body;
+    uint8_t* out;
+    uint64_t out_cap;       // bytes writable in out
+    const DecJob* jobs;
+    uint32_t n_jobs;
+    uint8_t* scratch;
+    uint32_t* produced;     // actual produced bytes per job
+};
+
+constexpr uint32_t DEC_VERBATIM = 256;
+constexpr uint32_t DEC_SKIP = 257;
+
+// launchers (ambc_kernels.hip)
+hipError_t launch_encode(const EncArgs& a, hipStream_t s);
+hipError_t launch_compact(const CompactArgs& a, hipStream_t s);
+hipError_t launch_end_chunk(uint8_t* dst, hipStream_t s);
+hipError_t launch_stats(const uint8_t* ids, const uint32_t* plen, uint32_t n_chunks,
+                        uint64_t n_total, uint32_t chunk_size, uint64_t* acc, hipStream_t s);
+hipError_t scan_sizes(const uint64_t* sizes, uint64_t* off, uint32_t count, void* tmp,
+                      size_t* tmp_bytes, hipStream_t s);
+hipError_t launch_copy(uint8_t* dst, const uint8_t* src, uint64_t len, hipStream_t s);
+hipError_t launch_decode(const DecArgs& a, hipStream_t s);
+hipError_t launch_synth(uint8_t* out, uint64_t n, const uint64_t* seg, uint32_t nseg,
+                        uint64_t seed, hipStream_t s);
+
+}  // namespace ambc

@@ -1,0 +1,166 @@
+/*
+ * ambc.h -- C-ABI of libambc_hip.so, the MI355X (gfx950) implementation of the
+ * per-chunk method-selection + encode/decode loop of
+ * KalharPandya/adaptive-compression's AdaptiveCompressor.
+ *
+ * The reference has no FFI of its own (it is pure Python).  These entry points
+ * replace its two hot loops, exactly where SURVEY.md §8(b) places the boundary:
+ *
+ *   ambc_compress_batch    replaces AdaptiveCompressor._adaptive_compress
+ *                          (adaptive_compressor.py:363-394) together with
+ *                          _pick_best_chunk_and_method (:537-590),
+ *                          _process_chunk (:631-700), _create_chunk (:609-621)
+ *                          and _create_end_chunk (:595-607): input bytes in,
+ *                          .ambc body (chunk packages + 16-B end chunk) out.
+ *   ambc_decompress_batch  replaces AdaptiveCompressor._adaptive_decompress
+ *   ambc_decompress_ex     (adaptive_compressor.py:396-454): body in, original
+ *                          bytes out, with the reference's lenient rules.
+ *   ambc_compress_bound    worst-case body size (n + 18*ceil(n/C) + 16).
+ *
+ * The 47-byte header, MD5 and the whole-file raw fallback
+ * (adaptive_compressor.py:221-255,312-358) stay in the Python host layer
+ * (adaptive-compression_amd/ambc/compressor.py); see INTEGRATION.md for the
+ * ctypes binding a maintainer adds to the reference.
+ *
+ * Conventions: every buffer is caller-allocated; the library never keeps a
+ * pointer after a call returns.  Calls block; ctypes releases the GIL around
+ * them.  One ambc_ctx per host thread.  Return 0 on success, a negative
+ * AMBC_E* code otherwise; ambc_last_error() gives a thread-local message.
+ * There is no CPU fallback: without a usable gfx950 device ambc_init fails.
+ */
+#ifndef AMBC_H
+#define AMBC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AMBC_ABI_VERSION 1
+
+#define AMBC_OK 0
+#define AMBC_E_INVAL (-1)     /* bad argument */
+#define AMBC_E_DEVICE (-2)    /* HIP runtime error / no gfx950 device */
+#define AMBC_E_NOMEM (-3)     /* device or pinned allocation failed */
+#define AMBC_E_RANGE (-4)     /* a u32 chunk field would overflow (reference: struct.error) */
+#define AMBC_E_MARKER (-5)    /* "Marker mismatch in chunk header." (reference ValueError) */
+#define AMBC_E_CAPACITY (-6)  /* output buffer too small */
+#define AMBC_E_HOSTCODEC (-7) /* body holds ids 5/6/7 chunks: use ambc_decompress_ex */
+#define AMBC_E_CODEC (-8)     /* the codec raises in the reference (e.g. Huffman on 1 or 256 symbols) */
+
+#define AMBC_MODE_NATIVE 0    /* every C-byte chunk decided independently */
+#define AMBC_MODE_REFERENCE 1 /* CHUNK_SIZE_CANDIDATES=[C] loop incl. the remainder-raw rule */
+
+#define AMBC_FLAG_NO_END_CHUNK 1u /* shard bodies for multi-GPU reassembly */
+
+/* GPU-routable method ids (bit i of method_mask = method id i) */
+#define AMBC_M_RLE 1
+#define AMBC_M_DICT 2  /* decode only (encoder: SURVEY §8(f) next) */
+#define AMBC_M_HUFFMAN 3
+#define AMBC_M_DELTA 4 /* never selected: payload length == n (compression_methods.py:598-608) */
+#define AMBC_M_LZ4 9
+#define AMBC_M_RAW 255
+
+#define AMBC_MAX_CHUNK 65536u
+
+typedef struct ambc_ctx ambc_ctx;
+
+typedef struct {
+    uint32_t chunk_size;    /* C: 16 <= C <= 65536, multiple of 16 */
+    uint32_t mode;          /* AMBC_MODE_* */
+    uint32_t method_mask;   /* enabled method ids (bits 1..15) */
+    uint32_t flags;         /* AMBC_FLAG_* */
+    uint32_t pref_min[16];  /* method_chunk_prefs (adaptive_compressor.py:114-127) */
+    uint32_t pref_max[16];
+    /* Optional numpy-exact entropy terms p*np.log2(p) indexed by count
+     * (HuffmanCompression.should_use, compression_methods.py:566-574); used only
+     * when the fp64 entropy lies within 1e-9 of the 7.0 threshold.  NULL: the
+     * device log2 is used for those near-ties too. */
+    const double* ent_full; /* n == chunk_size, length chunk_size+1 */
+    const double* ent_tail; /* n == total % chunk_size, length (total % chunk_size)+1 */
+} ambc_params;
+
+typedef struct {
+    uint64_t method_usage[256]; /* compressed chunks per method id (stats dict) */
+    uint64_t total_chunks, compressed_chunks, raw_chunks;
+    uint64_t bytes_saved, payload_bytes, overhead_bytes;
+    uint64_t kernel_ns;  /* device time of the kernels (hipEvents) */
+    uint64_t h2d_ns, d2h_ns, walk_ns, total_ns;
+} ambc_stats;
+
+/* A chunk the GPU leaves to the host (ids 5/6/7: zlib/bz2/lzma). */
+typedef struct {
+    uint64_t body_off; /* payload offset in the body */
+    uint64_t out_off;  /* where its decoded bytes go in the output */
+    uint32_t clen;     /* payload length */
+    uint32_t orig;     /* original_length field */
+    uint32_t type;
+    uint32_t reserved;
+} ambc_host_chunk;
+
+int ambc_abi_version(void);
+const char* ambc_last_error(void);
+
+int ambc_device_count(int* count);
+int ambc_init(const int* device_ids, int n_devices, ambc_ctx** out);
+void ambc_destroy(ambc_ctx* ctx);
+
+uint64_t ambc_compress_bound(uint64_t n, uint32_t chunk);
+
+/* Host buffers in, host buffers out (H2D -> kernels -> D2H). */
+int ambc_compress_batch(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const ambc_params* p,
+                        uint8_t* out, uint64_t out_cap, uint64_t* out_len, ambc_stats* st);
+
+int ambc_decompress_batch(ambc_ctx* ctx, const uint8_t* body, uint64_t body_len,
+                          uint64_t orig_size, uint8_t* out, ambc_stats* st);
+
+/* As ambc_decompress_batch; ids 5/6/7 chunks are not decoded but listed in
+ * host_chunks (capacity host_cap, count in *n_host) for the caller to fill.
+ * registered[id>>6] bit (id&63) marks ids with a registered method
+ * (method_lookup); an unregistered id's payload is copied verbatim
+ * (adaptive_compressor.py:432-435).  NULL registered = {1,2,3,4,5,6,7,9,255}. */
+int ambc_decompress_ex(ambc_ctx* ctx, const uint8_t* body, uint64_t body_len, uint64_t orig_size,
+                       const uint64_t registered[4], uint8_t* out, ambc_host_chunk* host_chunks,
+                       uint32_t host_cap, uint32_t* n_host, ambc_stats* st);
+
+/* Device-resident variants (inputs already in HBM; used by bench.py and the
+ * multi-GPU path).  dev = index into the ctx's device list; stream may be NULL. */
+int ambc_compress_device(ambc_ctx* ctx, int dev, const void* d_in, uint64_t n,
+                         const ambc_params* p, void* d_out, uint64_t out_cap, uint64_t* out_len,
+                         ambc_stats* st, void* stream);
+
+/* Single-chunk plugin calls (CompressionMethod API, compression_methods.py:7-67).
+ * ambc_encode_method = method.compress(chunk) for id 1, 3, 4 or 9 (n <= 65536),
+ * no gates; AMBC_E_CODEC where the reference raises.  ambc_analyze returns, per
+ * C-byte chunk, the winning id, its payload length and the should_use bits
+ * (1<<1 RLE, 1<<3 Huffman, 1<<4 Delta) the selector evaluated. */
+int ambc_encode_method(ambc_ctx* ctx, int method_id, const uint8_t* in, uint32_t n, uint8_t* out,
+                       uint32_t out_cap, uint32_t* out_len);
+int ambc_analyze(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const ambc_params* p, uint8_t* ids,
+                 uint32_t* payload_len, uint8_t* should_use);
+
+/* memory / device helpers (so the Python layer needs no PyTorch) */
+void* ambc_host_alloc(uint64_t bytes);        /* pinned */
+void ambc_host_free(void* p);
+void* ambc_device_alloc(ambc_ctx* ctx, int dev, uint64_t bytes);
+void ambc_device_free(ambc_ctx* ctx, int dev, void* p);
+int ambc_memcpy_h2d(ambc_ctx* ctx, int dev, void* d_dst, const void* h_src, uint64_t bytes);
+int ambc_memcpy_d2h(ambc_ctx* ctx, int dev, void* h_dst, const void* d_src, uint64_t bytes);
+int ambc_synchronize(ambc_ctx* ctx, int dev);
+
+/* "ambc-mixed v1" synthetic input: host fill and device fill */
+void ambc_synth_fill(uint8_t* out, uint64_t n, uint64_t seed);
+int ambc_synth_device(ambc_ctx* ctx, int dev, void* d_out, uint64_t n, uint64_t seed);
+
+/* bench instrumentation: average device time (ns) of the dominant kernel
+ * (k_encode) over the last compress call, measured with HIP events on the
+ * stream it was launched on. */
+int ambc_last_kernel_times(ambc_ctx* ctx, int dev, uint64_t* encode_ns, uint64_t* scan_ns,
+                           uint64_t* compact_ns);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,59 @@
+"""CPU-side checks of the C-ABI library (no compute calls without a GPU)."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from conftest import REPO, gpu_present
+
+
+def header_functions():
+    with open(os.path.join(REPO, "include", "ambc.h")) as f:
+        src = f.read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(ambc_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    from ambc import _lib
+    lib = _lib.load()
+    decl = header_functions()
+    assert len(decl) >= 20
+    for name in decl:
+        assert hasattr(lib, name), name
+    assert set(decl) == set(_lib.EXPORTS)
+
+
+def test_abi_version_and_bound():
+    from ambc import _lib
+    lib = _lib.load()
+    assert lib.ambc_abi_version() == 1
+    assert lib.ambc_compress_bound(0, 4096) == 16
+    assert lib.ambc_compress_bound(4096, 4096) == 4096 + 18 + 16
+    assert lib.ambc_compress_bound(4097, 4096) == 4097 + 36 + 16
+    assert lib.ambc_compress_bound(1 << 32, 4096) == (1 << 32) + 18 * (1 << 20) + 16
+
+
+def test_library_is_gfx950_code_object():
+    path = os.path.join(REPO, "adaptive-compression_amd", "ambc", "libambc_hip.so")
+    with open(path, "rb") as f:
+        blob = f.read()
+    assert b"gfx950" in blob
+
+
+@pytest.mark.skipif(gpu_present(), reason="checks the no-device failure path")
+def test_no_device_fails_loudly():
+    from ambc import _lib
+    with pytest.raises(_lib.AmbcUnavailable):
+        _lib.Context()
+    lib = _lib.load()
+    h = C.c_void_p()
+    assert lib.ambc_init(None, 1, C.byref(h)) != 0
+    assert "no" in _lib.last_error(lib).lower() or _lib.last_error(lib)
+
+
+def test_missing_library_raises(tmp_path):
+    from ambc import _lib
+    with pytest.raises(_lib.AmbcUnavailable):
+        _lib.load(str(tmp_path / "nope.so"))

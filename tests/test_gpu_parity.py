@@ -1,0 +1,253 @@
+"""GPU parity: the HIP path (through the C-ABI) against the reference's golden
+vectors and the CPU oracle, bit-exact (integer/byte work, no tolerance)."""
+import ctypes as C
+import hashlib
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, load_golden
+from oracle import oracle as orc
+from oracle import synth
+
+pytestmark = pytest.mark.gpu
+
+REF_REGISTERED = (1, 2, 3, 4, 5, 6, 7, 255)
+
+
+@pytest.fixture(scope="module")
+def ctx(hip_lib):
+    from ambc import _lib
+    return _lib.default_context()
+
+
+def _compressor(**kw):
+    from ambc import AdaptiveCompressor
+    return AdaptiveCompressor(**kw)
+
+
+def _norm(stats):
+    st = json.loads(json.dumps(stats))
+    st.pop("elapsed_time", None)
+    st.pop("throughput_mb_per_sec", None)
+    return st
+
+
+def analyze(ctx, data, chunk, methods=(1, 3, 4, 9), prefs=None):
+    from ambc import _lib
+    from ambc.compressor import entropy_terms
+    from ambc.registry import METHOD_CHUNK_PREFS, method_mask
+    prefs = METHOD_CHUNK_PREFS if prefs is None else prefs
+    n = len(data)
+    M = (n + chunk - 1) // chunk
+    p = _lib.Params()
+    p.chunk_size = chunk
+    p.method_mask = method_mask(methods)
+    for i in range(16):
+        lo, hi = prefs.get(i, (1, 0))
+        p.pref_min[i], p.pref_max[i] = lo, min(hi, 0xFFFFFFFF)
+    tf = entropy_terms(chunk)
+    p.ent_full = tf.ctypes.data
+    tt = entropy_terms(n % chunk) if n % chunk else None
+    p.ent_tail = tt.ctypes.data if tt is not None else None
+    ids = (C.c_uint8 * M)()
+    pl = (C.c_uint32 * M)()
+    su = (C.c_uint8 * M)()
+    _lib.check(ctx.lib.ambc_analyze(ctx.h, _lib.addr(data), n, C.byref(p), C.addressof(ids),
+                                    C.addressof(pl), C.addressof(su)), ctx.lib)
+    return list(ids), list(pl), list(su)
+
+
+# ---------------------------------------------------------------------------
+# whole files vs the reference's own .ambc outputs
+# ---------------------------------------------------------------------------
+def test_golden_files_bit_exact(ctx):
+    n = 0
+    for rec in load_golden("files.json"):
+        if rec["mode"] not in ("native", "reference"):
+            continue
+        if set(rec["methods"]) - {1, 3, 4, 9, 255}:
+            continue
+        data = synth.generate(rec["size"], rec["seed"])
+        comp = _compressor(chunk_size=rec["chunk"], mode=rec["mode"], methods=rec["methods"])
+        blob, stats = comp.compress_bytes(data)
+        with open(os.path.join(GOLDEN, rec["file"]), "rb") as f:
+            ref = f.read()
+        assert hashlib.sha256(blob).hexdigest() == rec["output_sha256"], rec["name"]
+        assert blob == ref
+        assert _norm(stats) == rec["stats"], rec["name"]
+        n += 1
+    assert n >= 20
+
+
+def test_golden_files_decode(ctx):
+    for rec in load_golden("files.json"):
+        data = synth.generate(rec["size"], rec["seed"])
+        with open(os.path.join(GOLDEN, rec["file"]), "rb") as f:
+            blob = f.read()
+        comp = _compressor()
+        if blob[:4] != b"AMBC":
+            with pytest.raises(ValueError, match="Magic mismatch"):
+                comp.decompress_bytes(blob)
+            continue
+        assert comp.decompress_bytes(blob) == data, rec["name"]
+
+
+def test_decode_kats_match_reference(ctx):
+    from ambc.methods import DECODE_METHODS
+    comp = _compressor()
+    comp.method_lookup = {i: DECODE_METHODS[i]() for i in REF_REGISTERED}
+    comp._init_marker(b"\xff\xff\x00\x00", 32)
+    for rec in load_golden("decode_kat.json"):
+        body = bytes.fromhex(rec["body"])
+        if rec["ok"]:
+            out = comp._adaptive_decompress(body, rec["orig_size"])
+            assert out.hex() == rec["out"], rec["name"]
+        else:
+            with pytest.raises(ValueError, match="Marker mismatch"):
+                comp._adaptive_decompress(body, rec["orig_size"])
+
+
+def test_config1_behaviour(ctx):
+    rec = load_golden("config1.json")
+    data = synth.random_bytes(rec["size"], rec["seed"])
+    comp = _compressor(chunk_size=4096, mode="reference", methods=(1, 3, 4))
+    blob, stats = comp.compress_bytes(data)
+    assert blob == data
+    assert _norm(stats) == rec["stats"]
+    with pytest.raises(ValueError, match="Magic mismatch"):
+        comp.decompress_bytes(blob)
+
+
+# ---------------------------------------------------------------------------
+# per-codec vectors through the plugin API
+# ---------------------------------------------------------------------------
+def test_codec_vectors_plugins(ctx):
+    from ambc.methods import DeltaCompression, HuffmanCompression, RLECompression
+    rle, huf, dlt = RLECompression(), HuffmanCompression(), DeltaCompression()
+    for rec in load_golden("codecs.json"):
+        d = bytes.fromhex(rec["data"])
+        if len(d) > 65536:
+            continue
+        assert rle.compress(d).hex() == rec["rle"]["out"], rec["name"]
+        assert dlt.compress(d).hex() == rec["delta"]["out"], rec["name"]
+        if rec["huffman"]["ok"]:
+            assert huf.compress(d).hex() == rec["huffman"]["out"], rec["name"]
+        else:
+            with pytest.raises(ValueError):
+                huf.compress(d)
+        assert rle.should_use(d) == rec["should_use"]["1"], rec["name"]
+        assert huf.should_use(d) == rec["should_use"]["3"], rec["name"]
+        assert dlt.should_use(d) == rec["should_use"]["4"], rec["name"]
+
+
+def test_codec_plugin_roundtrips(ctx):
+    from ambc.methods import (DeltaCompression, HuffmanCompression, LZ4Compression,
+                              RLECompression)
+    mixed = synth.generate(1 << 20, 9)
+    cases = [bytes(4096), b"x" * 70, mixed[:4096], mixed[70000:74096], mixed[140000:148192],
+             os.urandom(3000), b"ab" * 2000, mixed[5:1029]]
+    for d in cases:
+        for m in (RLECompression(), HuffmanCompression(), DeltaCompression(), LZ4Compression()):
+            try:
+                enc = m.compress(d)
+            except ValueError:
+                assert isinstance(m, HuffmanCompression)
+                continue
+            assert m.decompress(enc, len(d)) == d, (type(m).__name__, len(d))
+        # LZ4 bytes are this project's parse: pinned to the oracle
+        assert LZ4Compression().compress(d) == orc.lz4_frame_encode(d)
+
+
+# ---------------------------------------------------------------------------
+# per-chunk decisions and whole bodies vs the oracle (incl. LZ4)
+# ---------------------------------------------------------------------------
+CASES = [(1 << 20, 20250418, 4096), (1 << 20, 7, 1024), (300000, 3, 2048), (1 << 20, 11, 8192),
+         (777777, 5, 16384), (400000, 13, 65536), (123457, 17, 4096), (50000, 19, 32768)]
+
+
+@pytest.mark.parametrize("n,seed,chunk", CASES)
+def test_decisions_match_oracle(ctx, n, seed, chunk):
+    data = synth.generate(n, seed)
+    ids, pl, su = analyze(ctx, data, chunk)
+    p = orc.make_params(chunk, "native", (1, 3, 4, 9), n_total=n)
+    oids, opl = orc.decide_all(data, p)
+    bad = [k for k in range(len(ids)) if (ids[k], pl[k]) != (oids[k], opl[k])]
+    assert not bad, [(k, ids[k], pl[k], oids[k], opl[k]) for k in bad[:8]]
+    # should_use bits vs the oracle restatement for every chunk
+    for k in range(0, len(ids), max(1, len(ids) // 64)):
+        ch = data[k * chunk:(k + 1) * chunk]
+        assert bool(su[k] & 2) == orc.should_use(1, ch), k
+        assert bool(su[k] & 16) == orc.should_use(4, ch), k
+        assert bool(su[k] & 8) == orc.should_use(3, ch), k
+
+
+@pytest.mark.parametrize("n,seed,chunk", CASES)
+@pytest.mark.parametrize("mode", ["native", "reference"])
+def test_bodies_match_oracle(ctx, n, seed, chunk, mode):
+    data = synth.generate(n, seed)
+    comp = _compressor(chunk_size=chunk, mode=mode, methods=(1, 3, 4, 9))
+    body = comp._adaptive_compress(data)
+    ref, st = orc.compress_body(data, orc.make_params(chunk, mode, (1, 3, 4, 9), n_total=n))
+    assert len(body) == len(ref)
+    assert body == ref
+    assert comp.chunk_stats["compressed_chunks"] == st.compressed_chunks
+    assert comp.chunk_stats["bytes_saved"] == st.bytes_saved
+    assert comp._adaptive_decompress(body, n) == data
+
+
+def test_random_edge_inputs(ctx):
+    rnd = random.Random(5)
+    pieces = [bytes(4096), bytes([7]) * 5000, os.urandom(9000), b"abc" * 3000,
+              bytes(range(256)) * 20, synth.generate(20000, 23)]
+    for trial in range(12):
+        data = b"".join(rnd.choice(pieces)[:rnd.randrange(1, 9000)] for _ in range(rnd.randrange(1, 9)))
+        chunk = rnd.choice([16, 32, 48, 256, 1024, 1040, 4096, 8192])
+        comp = _compressor(chunk_size=chunk, methods=(1, 3, 4, 9))
+        body = comp._adaptive_compress(data)
+        ref, _ = orc.compress_body(data, orc.make_params(chunk, "native", (1, 3, 4, 9),
+                                                         n_total=len(data)))
+        assert body == ref, (trial, chunk, len(data))
+        assert comp._adaptive_decompress(body, len(data)) == data
+
+
+def test_empty_and_tiny_files(ctx):
+    for data in (b"", b"a", b"ab" * 8, bytes(47)):
+        comp = _compressor(chunk_size=4096)
+        blob, stats = comp.compress_bytes(data)
+        ref, rstats = orc.compress_file_bytes(data, 4096, "native", (1, 3, 4, 9))
+        assert blob == ref
+
+
+def test_large_roundtrip_and_checksums(ctx):
+    """Size-independent properties at 256 MiB: round trip + per-chunk decision
+    checksum against the (multi-threaded) oracle."""
+    from ambc import _lib
+    n = 256 << 20
+    data = np.empty(n, dtype=np.uint8)
+    ctx.lib.ambc_synth_fill(data.ctypes.data, n, 20250418)
+    ref = orc.synth(1 << 20, 20250418)
+    assert data[:1 << 20].tobytes() == ref
+    comp = _compressor(chunk_size=4096)
+    body = comp._adaptive_compress(data.tobytes())
+    oref, st = orc.compress_body(data.tobytes(), orc.make_params(4096, "native", (1, 3, 4, 9),
+                                                                 n_total=n), nthreads=0)
+    assert hashlib.sha256(body).digest() == hashlib.sha256(oref).digest()
+    assert comp._adaptive_decompress(body, n) == data.tobytes()
+    del _lib
+
+
+def test_device_synth_matches_host(ctx):
+    from ambc import _lib
+    n = (32 << 20) + 12345
+    d = ctx.lib.ambc_device_alloc(ctx.h, 0, n)
+    try:
+        _lib.check(ctx.lib.ambc_synth_device(ctx.h, 0, d, n, 99), ctx.lib)
+        got = (C.c_uint8 * n)()
+        _lib.check(ctx.lib.ambc_memcpy_d2h(ctx.h, 0, C.addressof(got), d, n), ctx.lib)
+    finally:
+        ctx.lib.ambc_device_free(ctx.h, 0, d)
+    assert bytes(got) == orc.synth(n, 99)
