@@ -1,0 +1,224 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X compress path (BASELINE.json metric).
+
+A step = one device-resident compress of the whole per-GPU input (configs[1]:
+4 GiB "ambc-mixed v1" synthetic mixed-entropy bytes, chunk 4096, native mode,
+GPU methods {RLE, Huffman, Delta, LZ4}) into a device-resident .ambc body;
+with N > 1 ranks every rank compresses its own 4 GiB (weak scaling) and the
+step also reassembles the body in file order on rank 0 over RCCL
+(ambc.distributed).  value = input bytes of all ranks / time (GB/s, 1e9).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \\
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
+"""
+import argparse
+import ctypes as C
+import glob
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [REPO, os.path.join(REPO, "adaptive-compression_amd")]
+
+METRIC = ("compress GB/s + ratio, 4 GiB synthetic mixed-entropy @ chunk=4096; "
+          "decompress round-trip bit-exact")
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--size", type=int, default=4 << 30, help="input bytes per GPU")
+    ap.add_argument("--chunk", type=int, default=4096)
+    ap.add_argument("--mode", default="native", choices=["native", "reference"])
+    ap.add_argument("--methods", default="1,3,4,9")
+    ap.add_argument("--seed", type=int, default=20250418)
+    ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    return ap.parse_args()
+
+
+def cpu_baseline(args, threads):
+    """The CPU restatement (oracle, "port") on a bounded prefix of the same
+    workload, on the host cores; the reference itself is pure Python and is
+    not present on the GPU box (BASELINE.md §2-3 has its numbers)."""
+    os.environ.setdefault("OMP_NUM_THREADS", str(threads))
+    from oracle import oracle as orc
+    probe = 16 << 20
+    data = orc.synth(probe, args.seed)
+    p = orc.make_params(args.chunk, "native", [int(x) for x in args.methods.split(",")],
+                        n_total=probe)
+    t = time.time()
+    orc.compress_body(data, p, nthreads=threads)
+    rate = probe / max(time.time() - t, 1e-6)
+    n = int(min(args.size, max(probe, rate * args.cpu_seconds)))
+    n -= n % args.chunk
+    data = orc.synth(n, args.seed)
+    p = orc.make_params(args.chunk, "native", [int(x) for x in args.methods.split(",")],
+                        n_total=n)
+    t = time.time()
+    body, _ = orc.compress_body(data, p, nthreads=threads)
+    dt = time.time() - t
+    return {"value": round(n / dt / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": f"first {n} bytes (seed {args.seed}) of the same stream, chunk "
+                      f"{args.chunk}, oracle/ambc_oracle.c OpenMP restatement, "
+                      f"{dt:.1f} s wall, ratio {len(body) / n:.4f}"}
+
+
+def pmc_traffic(workload):
+    """HBM bytes per k_encode launch from a committed rocprofv3 --pmc summary
+    (scripts/pmc_summary.py), if one exists for this workload."""
+    best = None
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*.json"))):
+        try:
+            with open(f) as fh:
+                d = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        if d.get("workload") == workload and d.get("hbm_bytes_per_launch"):
+            best = d
+    return best
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    from ambc import _lib
+    from ambc.compressor import entropy_terms
+    from ambc.registry import METHOD_CHUNK_PREFS, method_mask
+
+    ctx = _lib.Context([local])
+    lib = ctx.lib
+    n = args.size
+    methods = [int(x) for x in args.methods.split(",")]
+    p = _lib.Params()
+    p.chunk_size = args.chunk
+    p.mode = _lib.MODE_REFERENCE if args.mode == "reference" else _lib.MODE_NATIVE
+    p.method_mask = method_mask(methods)
+    for i in range(16):
+        lo, hi = METHOD_CHUNK_PREFS.get(i, (1, 0))
+        p.pref_min[i], p.pref_max[i] = lo, min(hi, 0xFFFFFFFF)
+    tabs = [entropy_terms(args.chunk)]
+    p.ent_full = tabs[0].ctypes.data
+    if n % args.chunk:
+        tabs.append(entropy_terms(n % args.chunk))
+        p.ent_tail = tabs[1].ctypes.data
+    if world > 1:
+        p.flags |= _lib.FLAG_NO_END_CHUNK
+
+    d_in = torch.empty(n, dtype=torch.uint8, device=dev)
+    _lib.check(lib.ambc_synth_device(ctx.h, 0, d_in.data_ptr(), n, args.seed + rank), lib)
+    cap = lib.ambc_compress_bound(n, args.chunk)
+    # rank 0 compresses straight into the front of the reassembly buffer
+    out_cap = cap * (world if rank == 0 and world > 1 else 1) + 64
+    d_out = torch.empty(out_cap, dtype=torch.uint8, device=dev)
+    olen = C.c_uint64()
+    st = _lib.Stats()
+    enc_ns = []
+
+    def step():
+        _lib.check(lib.ambc_compress_device(ctx.h, 0, d_in.data_ptr(), n, C.byref(p),
+                                            d_out.data_ptr(), cap, C.byref(olen), C.byref(st),
+                                            None), lib)
+        e = C.c_uint64()
+        lib.ambc_last_kernel_times(ctx.h, 0, C.byref(e), None, None)
+        enc_ns.append(e.value)
+        if world > 1:
+            from ambc.distributed import reassemble
+            reassemble(d_out[:olen.value], dst=0, out=d_out if rank == 0 else None)
+
+    for _ in range(args.warmup):
+        step()
+    enc_ns.clear()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    dt = time.perf_counter() - t0
+    body_len = olen.value
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([dt, float(body_len)], dtype=torch.float64, device=dev)
+        tmax = t.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tsum = t.clone()
+        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        dt = float(tmax[0].item())
+        body_total = float(tsum[1].item()) + 16
+    else:
+        body_total = float(body_len)
+
+    verified = None
+    if not args.no_verify and rank == 0:
+        # bit-exact round trip of the last step's body (outside the timed region)
+        body_host = d_out[:body_len if world == 1 else body_len].cpu().numpy().tobytes()
+        if world > 1:
+            body_host += b"\xff\xff" + b"\x00" * 14
+        from ambc import AdaptiveCompressor
+        comp = AdaptiveCompressor(chunk_size=args.chunk, mode=args.mode, methods=methods)
+        back = comp._adaptive_decompress(body_host, n)
+        verified = back == d_in.cpu().numpy().tobytes()
+        log(f"round trip bit-exact: {verified}")
+
+    result = None
+    if rank == 0:
+        total_in = n * world * args.steps
+        value = total_in / dt / 1e9
+        enc_avg = sum(enc_ns) / max(1, len(enc_ns))
+        algo_bytes = n + body_len                       # read input once + write body once
+        achieved = algo_bytes / (enc_avg * 1e-9) / 1e9 if enc_avg else 0.0
+        workload = f"ambc-mixed-v1 {n >> 30} GiB/GPU chunk={args.chunk} {args.mode}"
+        pmc = pmc_traffic(workload)
+        result = {
+            "metric": METRIC, "value": round(value, 3), "unit": "GB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": workload, "input_bytes_per_gpu": n, "chunk_size": args.chunk,
+                       "mode": args.mode, "methods": methods, "seed": args.seed,
+                       "ratio": round(body_total / (n * world), 5),
+                       "parallelism": f"chunk-shard dp{world}" if world > 1 else "single GPU",
+                       "round_trip_bit_exact": verified},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
+                         "kernel": "k_encode", "kernel_ms": round(enc_avg * 1e-6, 3),
+                         "algorithmic_bytes_per_launch": algo_bytes},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+            result["cpu_baseline"] = cpu_baseline(args, threads)
+        else:
+            result["cpu_baseline"] = None
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
