@@ -43,22 +43,32 @@ struct EncSmem {
     uint8_t order[256];
 };
 
-template <int BS>
-struct Blk {
-    uint32_t w[BS / 4];
-    __device__ __forceinline__ uint32_t byte(int t) const { return (w[t >> 2] >> (8 * (t & 3))) & 0xFFu; }
-    __device__ __forceinline__ void load(const uint8_t* p) {
+// Visit the bytes of a lane's block [b0, b0+BS) 16 at a time (one ds_read_b128
+// per step; the 16-byte body is unrolled, the sub-block loop is not, which
+// keeps the kernel small enough for the instruction cache).
+// f(p, c, nx): position, byte, following byte (zero padding past the data).
+template <int BS, typename F>
+__device__ __forceinline__ void for_block_bytes(const uint8_t* chunk, uint32_t b0, F&& f) {
+#pragma unroll 1
+    for (int q = 0; q < BS / 16; q++) {
+        const uint32_t base = b0 + 16 * q;
+        const uint4 v = *reinterpret_cast<const uint4*>(chunk + base);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        const uint32_t nxt = chunk[base + 16];
 #pragma unroll
-        for (int j = 0; j < BS / 16; j++) {
-            uint4 v = reinterpret_cast<const uint4*>(p)[j];
-            w[4 * j] = v.x; w[4 * j + 1] = v.y; w[4 * j + 2] = v.z; w[4 * j + 3] = v.w;
+        for (int t = 0; t < 16; t++) {
+            const uint32_t c = (w[t >> 2] >> (8 * (t & 3))) & 0xFFu;
+            const uint32_t nx = t < 15 ? ((w[(t + 1) >> 2] >> (8 * ((t + 1) & 3))) & 0xFFu) : nxt;
+            f(base + t, c, nx);
         }
     }
-};
+}
 
+// unaligned 4-byte little-endian read from LDS via two aligned dword reads
 __device__ __forceinline__ uint32_t lds_rd32(const uint8_t* base, uint32_t i) {
-    return (uint32_t)base[i] | (uint32_t)base[i + 1] << 8 | (uint32_t)base[i + 2] << 16 |
-           (uint32_t)base[i + 3] << 24;
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(base);
+    const uint32_t a = i >> 2;
+    return __builtin_amdgcn_alignbyte(w[a + 1], w[a], i & 3);
 }
 
 __device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
@@ -67,25 +77,46 @@ __device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) 
 __device__ uint32_t xxh32_desc(uint32_t n) {
     const uint32_t P1 = 2654435761U, P2 = 2246822519U, P3 = 3266489917U, P4 = 668265263U,
                    P5 = 374761393U;
-    uint8_t b[10] = {0x68, 0x40, (uint8_t)n, (uint8_t)(n >> 8), (uint8_t)(n >> 16),
-                     (uint8_t)(n >> 24), 0, 0, 0, 0};
     uint32_t h = P5 + 10u;
-    for (int i = 0; i < 8; i += 4) {
-        uint32_t v = b[i] | b[i + 1] << 8 | b[i + 2] << 16 | (uint32_t)b[i + 3] << 24;
-        h = rotl32(h + v * P3, 17) * P4;
-    }
-    for (int i = 8; i < 10; i++) h = rotl32(h + b[i] * P5, 11) * P1;
+    h = rotl32(h + (0x68u | 0x40u << 8 | (n & 0xFFFFu) << 16) * P3, 17) * P4;
+    h = rotl32(h + (n >> 16) * P3, 17) * P4;
+    h = rotl32(h + 0u * P5, 11) * P1;
+    h = rotl32(h + 0u * P5, 11) * P1;
     h ^= h >> 15; h *= P2; h ^= h >> 13; h *= P3; h ^= h >> 16;
     return h;
 }
 
 __device__ __forceinline__ uint32_t ext_len(uint32_t v) { return v >= 15 ? (v - 15) / 255 + 1 : 0; }
 
-// lane-parallel write of an LZ4 length extension (v >= 15) at dst
-__device__ __forceinline__ void put_ext(uint8_t* dst, uint32_t v, uint32_t lane) {
-    uint32_t x = v - 15, nb = x / 255 + 1;
-    for (uint32_t t = lane; t < nb; t += 64) dst[t] = t + 1 < nb ? 255 : (uint8_t)(x % 255);
+// byte t of an LZ4 length extension for value v (>= 15) of xl bytes
+__device__ __forceinline__ uint32_t ext_byte(uint32_t v, uint32_t xl, uint32_t t) {
+    return t + 1 < xl ? 255u : (v - 15) % 255u;
 }
+
+// frame header byte q (0..18) of a one-block LZ4F frame; bs = block size field
+__device__ __forceinline__ uint8_t lz4_hdr_byte(uint32_t q, uint32_t n, uint32_t bs) {
+    if (q < 4) return (uint8_t)(0x184D2204u >> (8 * q));
+    if (q == 4) return 0x68;   // FLG: v01, block independence, content size
+    if (q == 5) return 0x40;   // BD: 64 KiB max block
+    if (q < 14) return q < 10 ? (uint8_t)(n >> (8 * (q - 6))) : 0;
+    if (q == 14) return (uint8_t)((xxh32_desc(n) >> 8) & 0xFF);
+    return (uint8_t)(bs >> (8 * (q - 15)));
+}
+
+#ifdef AMBC_STAMPS
+// diagnostic build only: phase cycle sums via s_memtime, lane 0 adds to A.stamps[phase]
+#define STAMP_DECL uint64_t _st_t = __builtin_amdgcn_s_memtime();
+#define STAMP(ph)                                                                      \
+    do {                                                                               \
+        __builtin_amdgcn_s_waitcnt(0xC07F);                                            \
+        const uint64_t _t = __builtin_amdgcn_s_memtime();                              \
+        if (lane == 0 && A.stamps) atomicAdd(&A.stamps[ph], (unsigned long long)(_t - _st_t)); \
+        _st_t = _t;                                                                    \
+    } while (0)
+#else
+#define STAMP_DECL
+#define STAMP(ph) do {} while (0)
+#endif
 
 template <int CMAX>
 __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
@@ -99,6 +130,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
     const uint32_t n = (uint32_t)min((uint64_t)A.chunk_size, A.n_total - pos0);
     const uint8_t* src = A.in + pos0;
     uint8_t* slot = A.slots + (uint64_t)k * A.slot_stride;
+    STAMP_DECL
 
     // ---- stage the chunk in LDS (16 B per lane per load, coalesced) ----
     {
@@ -113,9 +145,9 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         for (uint32_t i = n + lane; i < (uint32_t)CMAX + 64; i += 64) S.chunk[i] = 0;
         for (uint32_t i = lane; i < 256; i += 64) { S.hist[i] = 0; S.first[i] = 0xFFFFFFFFu; }
     }
-    __syncthreads();
+    wave_sync();
 
-    // ---- pass A: histogram, RLE pairs, RLE sample count ----
+    // ---- pass A: histogram, RLE pairs, RLE / Delta should_use samples ----
     const uint32_t ss = n < 1000 ? n : 1000;
     const uint32_t step = max(1u, n / ss);
     uint32_t pairs = 0, samp = 0, dsamp = 0;
@@ -123,33 +155,24 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
 #pragma unroll 1
     for (int r = 0; r < ROUNDS; r++) {
         const uint32_t b0 = (uint32_t)(r * 64 + lane) * BS;
-        Blk<BS> B;
-        B.load(S.chunk + b0);
         const uint32_t prevb = b0 ? S.chunk[b0 - 1] : 0x100u;
-        const uint32_t nextb = S.chunk[b0 + BS];
         int lb = -1;
         {
             uint32_t prev = prevb;
-#pragma unroll
-            for (int t = 0; t < BS; t++) {
-                uint32_t c = B.byte(t);
-                if (b0 + t < n && c != prev) lb = (int)(b0 + t);
+            for_block_bytes<BS>(S.chunk, b0, [&](uint32_t p, uint32_t c, uint32_t) {
+                if (p < n && c != prev) lb = (int)p;
                 prev = c;
-            }
+            });
         }
         const int rs = wave_excl_max(lb, rs_carry);  // run start of position b0-1
         rs_carry = max(rs_carry, wave_max_i32(lb));
         uint32_t off = b0 == 0 ? 254u : (uint32_t)((int)(b0 - 1) - rs) % 255u;
         uint32_t ph = b0 % step;
-        uint32_t prev = prevb, cur = B.byte(0), rc = 0;
-#pragma unroll
-        for (int t = 0; t < BS; t++) {
-            const uint32_t p = b0 + t;
-            const uint32_t c = B.byte(t);
+        uint32_t prev = prevb, cur = S.chunk[b0], rc = 0;
+        for_block_bytes<BS>(S.chunk, b0, [&](uint32_t p, uint32_t c, uint32_t nx) {
             const bool valid = p < n;
             off = c != prev ? 0u : (off == 254u ? 0u : off + 1u);
             if (valid && off == 0) pairs++;
-            const uint32_t nx = t + 1 < BS ? B.byte(t + 1) : nextb;
             if (valid && ph == 0 && p + 1 < n) {
                 samp += c == nx;
                 dsamp += (c > nx ? c - nx : nx - c) < 32u;
@@ -160,13 +183,14 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                 else { atomicAdd(&S.hist[cur], rc); cur = c; rc = 1; }
             }
             prev = c;
-        }
+        });
         if (rc) atomicAdd(&S.hist[cur], rc);
     }
-    pairs = wave_sum(pairs);
-    samp = wave_sum(samp);
-    dsamp = wave_sum(dsamp);
-    __syncthreads();
+    pairs = wave_sum_u32(pairs);
+    samp = wave_sum_u32(samp);
+    dsamp = wave_sum_u32(dsamp);
+    wave_sync();
+    STAMP(0);
 
     const uint32_t mm = A.method_mask;
     const bool force = A.flags & ENC_FORCE;
@@ -194,17 +218,13 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
 #pragma unroll 1
         for (int r = 0; r < ROUNDS; r++) {
             const uint32_t b0 = (uint32_t)(r * 64 + lane) * BS;
-            Blk<BS> B;
-            B.load(S.chunk + b0);
             uint32_t prev = b0 ? S.chunk[b0 - 1] : 0x100u;
-#pragma unroll
-            for (int t = 0; t < BS; t++) {
-                const uint32_t c = B.byte(t);
-                if (b0 + t < n && c != prev) atomicMin(&S.first[c], b0 + t);
+            for_block_bytes<BS>(S.chunk, b0, [&](uint32_t p, uint32_t c, uint32_t) {
+                if (p < n && c != prev) atomicMin(&S.first[c], p);
                 prev = c;
-            }
+            });
         }
-        __syncthreads();
+        wave_sync();
         uint32_t f[4], rk[4] = {0, 0, 0, 0};
 #pragma unroll
         for (int j = 0; j < 4; j++) f[j] = S.first[lane + 64 * j];
@@ -217,7 +237,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
 #pragma unroll
         for (int j = 0; j < 4; j++)
             if (f[j] != 0xFFFFFFFFu) S.order[rk[j]] = (uint8_t)(lane + 64 * j);
-        __syncthreads();
+        wave_sync();
     };
 
     uint32_t kdist = 0;
@@ -234,7 +254,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                 part += p * log2(p);
             }
         }
-        kdist = wave_sum(kc);
+        kdist = wave_sum_u32(kc);
         double tot = wave_sum(part);
         double H = -__shfl(tot, 0);
         if (fabs(H - 7.0) <= 1e-9) {
@@ -256,7 +276,8 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         }
         huff_su = n >= 100 && H < 7.0;
         if (eligible(3) && (force || huff_su) && kdist >= 2 && kdist <= 255) {
-            // tree: slot s holds the active node whose first symbol is s
+            // tree: slot s holds the active node whose first symbol is s; merge the two
+            // smallest (weight, first symbol) keys (heapq order, :482-494)
             uint32_t key[4];
             uint32_t nid[4];
 #pragma unroll
@@ -286,7 +307,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                     }
                 }
             }
-            __syncthreads();
+            wave_sync();
             const uint32_t root = 256 + kdist - 2;
             uint32_t nb = 0, maxlen = 0;
 #pragma unroll
@@ -305,9 +326,9 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                     maxlen = max(maxlen, len);
                 }
             }
-            nb = wave_sum(nb);
+            nb = wave_sum_u32(nb);
             maxlen = (uint32_t)wave_max_i32((int)maxlen);
-            __syncthreads();
+            wave_sync();
             if (maxlen <= 32) {
                 const uint32_t l = 1 + 5 * kdist + 4 + (nb + 7) / 8;
                 if (l + HDR < best) { best = l + HDR; win = 3; wlen = l; }
@@ -315,18 +336,23 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         }
     }
 
+    STAMP(1);
     // ---- LZ4 (id 9): frame = 15 B header + 4 B block size + block + 4 B end mark ----
+    // "ambc-lz4 greedy v1": cand(i) = last j < i with the same 12-bit hash, valid
+    // iff the 4 bytes match; greedy from the first valid position; matches start
+    // at i <= n-12 and end by n-5 (LZ4 block end rules).
     if (eligible(9) && (force || n >= 1024) && best > 42) {
         uint16_t* last = reinterpret_cast<uint16_t*>(S.region);
         for (uint32_t i = lane; i < (1u << LZ4_HASH_BITS); i += 64) last[i] = 0xFFFF;
-        __syncthreads();
+        wave_sync();
         // LZ4 wins iff block < budget; forced (single-method) encodes fall back to a
         // stored block once the compressed block would reach n (LZ4F rule)
         const uint32_t budget = force ? n : best - 41;
-        const int mlim = (int)n - 12;       // last position a match may start (LZ4 end rule); <0: none
+        const int mlim = (int)n - 12;       // last position a match may start; <0: none
         uint8_t* blk = slot + 19;
         uint32_t emitted = 0, anchor = 0, nextp = 0;
         bool alive = true;
+        constexpr uint32_t LCAP = 64;       // per-lane precomputed match length cap
 #pragma unroll 1
         for (int base = 0; base <= mlim && alive; base += 64) {
             const int i = base + (int)lane;
@@ -348,97 +374,130 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
             }
             const bool valid = act && cand >= 0 && lds_rd32(S.chunk, (uint32_t)cand) == v;
             const uint64_t vm = __ballot(valid);
-            __syncthreads();
+            wave_sync();
             if (act && (peers >> lane) == 1ull) last[h] = (uint16_t)i;
-            // greedy walk over this round's positions
+            STAMP(2);
+            if (base + 63 < (int)nextp) continue;   // round lies inside the previous match
+            // per-lane match length, dword compares, capped at LCAP
+            uint32_t L = 0;
+            if (valid && (uint32_t)i >= nextp) {
+                const uint32_t lim = n - 5 - (uint32_t)i;
+                const uint32_t cap = min(lim, LCAP);
+                L = 4;
+                while (L < cap) {
+                    const uint32_t x = lds_rd32(S.chunk, (uint32_t)i + L) ^ lds_rd32(S.chunk, (uint32_t)cand + L);
+                    if (x) { L += (uint32_t)__builtin_ctz(x) >> 3; break; }
+                    L += 4;
+                }
+                L = min(L, lim);
+            }
+            STAMP(3);
+            // (1) scalar greedy walk: select this round's match starts (one bit per lane)
+            uint64_t sel = 0;
+            uint32_t np = nextp;
             while (true) {
-                const int rel = (int)nextp - base;
+                const int rel = (int)np - base;
                 if (rel > 63) break;
                 const uint64_t m = rel > 0 ? (vm & (~0ull << rel)) : vm;
                 if (!m) break;
-                const int L0 = __ffsll((long long)m) - 1;
-                const uint32_t j = (uint32_t)(base + L0);
-                const uint32_t c = (uint32_t)__shfl(cand, L0);
-                const uint32_t limit = n - 5 - j;
-                uint32_t L = 4;
-                while (L < limit) {
-                    const uint32_t idx = L + lane;
-                    const bool eq = idx < limit && S.chunk[c + idx] == S.chunk[j + idx];
-                    const uint64_t ne = __ballot(!eq);
-                    if (ne) { L += (uint32_t)(__ffsll((long long)ne) - 1); break; }
-                    L += 64;
+                const uint32_t L0 = (uint32_t)__builtin_ctzll(m);
+                const uint32_t j = (uint32_t)base + L0;
+                const uint32_t lim = n - 5 - j;
+                uint32_t Lj = readlane(L, L0);
+                if (Lj >= LCAP && Lj < lim) {
+                    // long match: extend cooperatively, 256 bytes per step
+                    const uint32_t c = readlane((uint32_t)cand, L0);
+                    while (Lj < lim) {
+                        const uint32_t p = Lj + 4 * lane;
+                        uint32_t fd = 0;
+                        bool eq = false;
+                        if (p < lim) {
+                            const uint32_t x = lds_rd32(S.chunk, j + p) ^ lds_rd32(S.chunk, c + p);
+                            eq = x == 0;
+                            fd = x ? (uint32_t)__builtin_ctz(x) >> 3 : 4;
+                        }
+                        const uint64_t ne = __ballot(!eq);
+                        if (ne) {
+                            const uint32_t lk = (uint32_t)__builtin_ctzll(ne);
+                            Lj += 4 * lk + readlane(fd, lk);
+                            break;
+                        }
+                        Lj += 256;
+                    }
+                    Lj = min(Lj, lim);
+                    if (lane == L0) L = Lj;
                 }
-                if (L > limit) L = limit;
-                const uint32_t lit = j - anchor, ml = L - 4;
-                const uint32_t seq = 1 + lit + ext_len(lit) + 2 + ext_len(ml);
-                if (emitted + seq + 1 >= budget) { alive = false; break; }
-                uint8_t* o = blk + emitted;
-                if (lane == 0) o[0] = (uint8_t)((lit >= 15 ? 15 : lit) << 4 | (ml >= 15 ? 15 : ml));
-                uint32_t q = 1;
-                if (lit >= 15) { put_ext(o + q, lit, lane); q += ext_len(lit); }
-                for (uint32_t t = lane; t < lit; t += 64) o[q + t] = S.chunk[anchor + t];
-                q += lit;
-                const uint32_t offv = j - c;
-                if (lane == 0) { o[q] = (uint8_t)offv; o[q + 1] = (uint8_t)(offv >> 8); }
-                q += 2;
-                if (ml >= 15) put_ext(o + q, ml, lane);
-                emitted += seq;
-                nextp = j + L;
-                anchor = nextp;
+                sel |= 1ull << L0;
+                np = __builtin_amdgcn_readfirstlane(j + Lj);
             }
-            __syncthreads();
+            if (sel) {
+                // (2) every selected lane emits its own sequence; literal start = the
+                // previous selected match's end (exclusive max-scan), output offset =
+                // exclusive prefix sum of the sequence sizes
+                const bool me = (sel >> lane) & 1ull;
+                const int pe = wave_excl_max(me ? i + (int)L : -1, (int)anchor);
+                const uint32_t lit = me ? (uint32_t)(i - pe) : 0u;
+                const uint32_t ml = me ? L - 4 : 0u;
+                const uint32_t xl = ext_len(lit), xm = ext_len(ml);
+                const uint32_t sz = me ? 1 + xl + lit + 2 + xm : 0u;
+                const uint32_t incl = wave_incl_sum(sz);
+                const uint32_t tot = readlane(incl, 63);
+                // the sequential walk gives up at the first sequence that makes
+                // block + 1 >= budget; the round total decides the same way
+                if (emitted + tot + 1 >= budget) { alive = false; break; }
+                if (me) {
+                    uint8_t* o = blk + emitted + incl - sz;
+                    o[0] = (uint8_t)((lit >= 15 ? 15 : lit) << 4 | (ml >= 15 ? 15 : ml));
+                    uint32_t q = 1;
+                    for (uint32_t t = 0; t < xl; t++) o[q + t] = (uint8_t)ext_byte(lit, xl, t);
+                    q += xl;
+                    for (uint32_t t = 0; t < lit; t++) o[q + t] = S.chunk[(uint32_t)pe + t];
+                    q += lit;
+                    const uint32_t offv = (uint32_t)(i - cand);
+                    o[q] = (uint8_t)offv;
+                    o[q + 1] = (uint8_t)(offv >> 8);
+                    q += 2;
+                    for (uint32_t t = 0; t < xm; t++) o[q + t] = (uint8_t)ext_byte(ml, xm, t);
+                }
+                emitted = __builtin_amdgcn_readfirstlane(emitted + tot);
+                anchor = np;
+            }
+            nextp = np;
+        }
+        uint32_t fin = 0, flit = 0, fxl = 0;
+        if (alive) {
+            flit = n - anchor;
+            fxl = ext_len(flit);
+            fin = 1 + fxl + flit;
+            if (emitted + fin >= budget) alive = false;
         }
         if (alive) {
-            const uint32_t lit = n - anchor;
-            const uint32_t fin = 1 + lit + ext_len(lit);
-            if (emitted + fin >= budget) alive = false;
-            else {
-                uint8_t* o = blk + emitted;
-                if (lane == 0) o[0] = (uint8_t)((lit >= 15 ? 15 : lit) << 4);
-                uint32_t q = 1;
-                if (lit >= 15) { put_ext(o + q, lit, lane); q += ext_len(lit); }
-                for (uint32_t t = lane; t < lit; t += 64) o[q + t] = S.chunk[anchor + t];
-                emitted += fin;
+            // final literals, frame header, block size, end mark
+            const uint32_t blen = emitted + fin;
+            uint8_t* o = blk + emitted;
+            for (uint32_t t = lane; t < fin + 4; t += 64) {
+                uint32_t b;
+                if (t == 0) b = (flit >= 15 ? 15 : flit) << 4;
+                else if (t < 1 + fxl) b = ext_byte(flit, fxl, t - 1);
+                else if (t < fin) b = S.chunk[anchor + t - 1 - fxl];
+                else b = 0;   // end mark
+                o[t] = (uint8_t)b;
             }
-        }
-        if (!alive && force) {
+            if (lane < 19) slot[lane] = lz4_hdr_byte(lane, n, blen);
+            win = 9;
+            wlen = blen + 23;
+            best = blen + 41;
+        } else if (force) {
             // stored block: 15 B header, size | 0x80000000, raw bytes, end mark
-            for (uint32_t t = lane; t < n; t += 64) blk[t] = S.chunk[t];
-            if (lane < 19) {
-                uint8_t b;
-                if (lane < 4) b = (uint8_t)(0x184D2204u >> (8 * lane));
-                else if (lane == 4) b = 0x68;
-                else if (lane == 5) b = 0x40;
-                else if (lane < 14) b = lane < 10 ? (uint8_t)(n >> (8 * (lane - 6))) : 0;
-                else if (lane == 14) b = (uint8_t)((xxh32_desc(n) >> 8) & 0xFF);
-                else b = (uint8_t)((n | 0x80000000u) >> (8 * (lane - 15)));
-                slot[lane] = b;
-            } else if (lane < 23) {
-                blk[n + lane - 19] = 0;
-            }
+            for (uint32_t t = lane; t < n + 4; t += 64) blk[t] = t < n ? S.chunk[t] : 0;
+            if (lane < 19) slot[lane] = lz4_hdr_byte(lane, n, n | 0x80000000u);
             win = 9;
             wlen = n + 23;
         }
-        if (alive) {
-            if (lane < 19) {
-                uint8_t b;
-                if (lane < 4) b = (uint8_t)(0x184D2204u >> (8 * lane));
-                else if (lane == 4) b = 0x68;
-                else if (lane == 5) b = 0x40;
-                else if (lane < 14) b = lane < 10 ? (uint8_t)(n >> (8 * (lane - 6))) : 0;
-                else if (lane == 14) b = (uint8_t)((xxh32_desc(n) >> 8) & 0xFF);
-                else b = (uint8_t)(emitted >> (8 * (lane - 15)));
-                slot[lane] = b;
-            } else if (lane < 23) {
-                blk[emitted + lane - 19] = 0;  // end mark
-            }
-            win = 9;
-            wlen = emitted + 23;
-            best = emitted + 41;
-        }
-        __syncthreads();
+        wave_sync();
     }
 
+    STAMP(5);
     // forced Delta (DeltaCompression.compress, compression_methods.py:585-608)
     if (force && ((mm >> 4) & 1u)) { win = 4; wlen = n; }
 
@@ -462,47 +521,39 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
 #pragma unroll 1
             for (int r = 0; r < ROUNDS; r++) {
                 const uint32_t b0 = (uint32_t)(r * 64 + lane) * BS;
-                Blk<BS> B;
-                B.load(S.chunk + b0);
                 const uint32_t prevb = b0 ? S.chunk[b0 - 1] : 0x100u;
                 int lb = -1;
                 uint32_t cnt = 0;
                 {
                     uint32_t prev = prevb;
-#pragma unroll
-                    for (int t = 0; t < BS; t++) {
-                        uint32_t c = B.byte(t);
-                        if (b0 + t < n && c != prev) lb = (int)(b0 + t);
+                    for_block_bytes<BS>(S.chunk, b0, [&](uint32_t p, uint32_t c, uint32_t) {
+                        if (p < n && c != prev) lb = (int)p;
                         prev = c;
-                    }
+                    });
                 }
                 const int rs = wave_excl_max(lb, rs_c);
                 rs_c = max(rs_c, wave_max_i32(lb));
                 const uint32_t off0 = b0 == 0 ? 254u : (uint32_t)((int)(b0 - 1) - rs) % 255u;
                 uint32_t off = off0, prev = prevb;
-#pragma unroll
-                for (int t = 0; t < BS; t++) {
-                    const uint32_t c = B.byte(t);
+                for_block_bytes<BS>(S.chunk, b0, [&](uint32_t p, uint32_t c, uint32_t) {
                     off = c != prev ? 0u : (off == 254u ? 0u : off + 1u);
-                    if (b0 + t < n && off == 0) cnt++;
+                    if (p < n && off == 0) cnt++;
                     prev = c;
-                }
+                });
                 const uint32_t incl = wave_incl_sum(cnt);
                 uint32_t idx = base_idx + incl - cnt;
                 off = off0; prev = prevb;
-#pragma unroll
-                for (int t = 0; t < BS; t++) {
-                    const uint32_t c = B.byte(t);
+                for_block_bytes<BS>(S.chunk, b0, [&](uint32_t p, uint32_t c, uint32_t) {
                     off = c != prev ? 0u : (off == 254u ? 0u : off + 1u);
-                    if (b0 + t < n && off == 0) {
-                        if (idx >= wb && idx < wb + CAPP) ps[idx - wb] = (uint16_t)(b0 + t);
+                    if (p < n && off == 0) {
+                        if (idx >= wb && idx < wb + CAPP) ps[idx - wb] = (uint16_t)p;
                         idx++;
                     }
                     prev = c;
-                }
-                base_idx += __shfl(incl, 63);
+                });
+                base_idx += readlane(incl, 63);
             }
-            __syncthreads();
+            wave_sync();
             const uint32_t we = min(pairs, wb + CAPP - 1);
             for (uint32_t j = wb + lane; j < we; j += 64) {
                 const uint32_t st = ps[j - wb];
@@ -510,7 +561,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                 slot[2 * j] = S.chunk[st];
                 slot[2 * j + 1] = (uint8_t)(en - st);
             }
-            __syncthreads();
+            wave_sync();
         }
     } else if (win == 3) {
         if (!first_done) compute_first();
@@ -533,24 +584,20 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         if (gstage) bits = reinterpret_cast<uint32_t*>(slot + ((wlen + 15) & ~15u));
         for (uint32_t w = lane; w < nwords + 1; w += 64) bits[w] = 0;
         if (gstage) __threadfence();
-        __syncthreads();
+        wave_sync();
         uint32_t bitbase = 0;
 #pragma unroll 1
         for (int r = 0; r < ROUNDS; r++) {
             const uint32_t b0 = (uint32_t)(r * 64 + lane) * BS;
-            Blk<BS> B;
-            B.load(S.chunk + b0);
             uint32_t my = 0;
-#pragma unroll
-            for (int t = 0; t < BS; t++)
-                if (b0 + t < n) my += S.clen[B.byte(t)];
+            for_block_bytes<BS>(S.chunk, b0, [&](uint32_t p, uint32_t c, uint32_t) {
+                if (p < n) my += S.clen[c];
+            });
             const uint32_t incl = wave_incl_sum(my);
             uint32_t bp = bitbase + incl - my;
             uint32_t cw = bp >> 5, acc = 0;
-#pragma unroll
-            for (int t = 0; t < BS; t++) {
-                if (b0 + t < n) {
-                    const uint32_t s = B.byte(t);
+            for_block_bytes<BS>(S.chunk, b0, [&](uint32_t p, uint32_t s, uint32_t) {
+                if (p < n) {
                     const uint32_t L = S.clen[s], cd = S.code[s];
                     const uint32_t o = bp & 31, w = bp >> 5;
                     if (w != cw) { if (acc) atomicOr(&bits[cw], acc); cw = w; acc = 0; }
@@ -564,13 +611,12 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                     }
                     bp += L;
                 }
-            }
+            });
             if (acc) atomicOr(&bits[cw], acc);
-            bitbase += __shfl(incl, 63);
+            bitbase += readlane(incl, 63);
         }
-        __syncthreads();
         if (gstage) __threadfence();
-        __syncthreads();
+        wave_sync();
         if (lane < 4) slot[hb + lane] = (uint8_t)(bitbase >> (8 * lane));
         for (uint32_t q = lane; q < nbytes; q += 64) {
             const uint32_t w = gstage ? __hip_atomic_load(&bits[q >> 2], __ATOMIC_RELAXED,
@@ -580,6 +626,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         }
     }
 
+    STAMP(6);
     if (lane == 0) {
         A.plen[k] = wlen;
         A.ids[k] = (uint8_t)win;

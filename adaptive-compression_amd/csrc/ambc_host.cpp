@@ -222,9 +222,23 @@ static int compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_param
     for (int i = 0; i < 16; i++) { ea.pref_min[i] = p->pref_min[i]; ea.pref_max[i] = p->pref_max[i]; }
 
     TRACE("compress_on n=%llu M=%u C=%u", (unsigned long long)n, M, C);
+    std::vector<unsigned long long> stamps;
+    if (getenv("AMBC_STAMPS")) {
+        HIPCHK(d.seg.ensure(64 * 8));
+        HIPCHK(hipMemsetAsync(d.seg.p, 0, 64 * 8, s));
+        ea.stamps = d.seg.as<unsigned long long>();
+    }
     HIPCHK(hipEventRecord(d.ev[0], s));
     HIPCHK(launch_encode(ea, s));
     HIPCHK(hipEventRecord(d.ev[1], s));
+    if (ea.stamps) {
+        stamps.resize(8);
+        HIPCHK(hipMemcpyAsync(stamps.data(), d.seg.p, 64, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        fprintf(stderr, "[ambc stamps] M=%u load+passA %.0f huff %.0f lz4hash %.0f lz4len %.0f lz4walk %.0f lz4tail %.0f emit %.0f seqs %.1f (cycles/chunk)\n",
+                M, stamps[0] / (double)M, stamps[1] / (double)M, stamps[2] / (double)M, stamps[3] / (double)M,
+                stamps[4] / (double)M, stamps[5] / (double)M, stamps[6] / (double)M, stamps[7] / (double)M);
+    }
     if (trace_on()) { HIPCHK(hipStreamSynchronize(s)); TRACE("encode done"); }
 
     // reference mode: the first chunk with no winner swallows the remainder

@@ -27,6 +27,7 @@ struct EncArgs {
     const double* ent_tail;
     uint8_t* su;             // optional: per-chunk should_use bits (1<<1 RLE, 1<<3 Huffman, 1<<4 Delta)
     uint32_t flags;          // ENC_FORCE: encode with the single enabled method, no gates
+    unsigned long long* stamps;  // diagnostic build (-DAMBC_STAMPS): per-phase cycle sums
     uint32_t pref_min[16];
     uint32_t pref_max[16];
 };

@@ -1,6 +1,11 @@
 // Wavefront (64-lane) primitives for gfx950.  Everything here assumes the
 // whole wave is active (EXEC all ones) -- callers keep control flow
 // wave-uniform around these helpers.
+//
+// Scans and reductions use DPP row shifts + row_bcast15/31 (VALU, a few cycles
+// each) instead of ds_bpermute shuffles (an LDS round trip each), and read the
+// result back with v_readlane.  Define AMBC_SHFL_PRIMITIVES to fall back to
+// the __shfl versions (debugging aid).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -9,35 +14,71 @@ namespace ambc {
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
-template <typename T>
-__device__ __forceinline__ T wave_sum(T v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-    return v;
+// only wavefront-scope ordering is needed inside a one-wave workgroup: LDS
+// instructions of a wave execute in order, so this is a compiler barrier and
+// never waits on outstanding global stores (unlike __syncthreads()).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = min(v, (uint32_t)__shfl_xor(v, o));
-    return v;
+__device__ __forceinline__ uint32_t readlane(uint32_t v, uint32_t l) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l);
 }
 
-__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        uint64_t t = __shfl_xor(v, o);
-        v = t < v ? t : v;
-    }
-    return v;
-}
+#define AMBC_DPP(old, v, ctrl, rm, bm, bc) \
+    ((uint32_t)__builtin_amdgcn_update_dpp((int)(old), (int)(v), ctrl, rm, bm, bc))
 
-__device__ __forceinline__ int wave_max_i32(int v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o));
-    return v;
-}
+#ifndef AMBC_SHFL_PRIMITIVES
 
 // inclusive prefix sum over lanes
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
+    v += AMBC_DPP(0, v, 0x111, 0xF, 0xF, true);   // row_shr:1
+    v += AMBC_DPP(0, v, 0x112, 0xF, 0xF, true);   // row_shr:2
+    v += AMBC_DPP(0, v, 0x114, 0xF, 0xF, true);   // row_shr:4
+    v += AMBC_DPP(0, v, 0x118, 0xF, 0xF, true);   // row_shr:8
+    v += AMBC_DPP(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1,3
+    v += AMBC_DPP(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2,3
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) { return readlane(wave_incl_sum(v), 63); }
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+    const uint32_t M = 0xFFFFFFFFu;
+    v = min(v, AMBC_DPP(M, v, 0x111, 0xF, 0xF, false));
+    v = min(v, AMBC_DPP(M, v, 0x112, 0xF, 0xF, false));
+    v = min(v, AMBC_DPP(M, v, 0x114, 0xF, 0xF, false));
+    v = min(v, AMBC_DPP(M, v, 0x118, 0xF, 0xF, false));
+    v = min(v, AMBC_DPP(M, v, 0x142, 0xA, 0xF, false));
+    v = min(v, AMBC_DPP(M, v, 0x143, 0xC, 0xF, false));
+    return readlane(v, 63);
+}
+
+// inclusive prefix max of signed values (identity INT_MIN)
+__device__ __forceinline__ int wave_incl_max_i32(int v) {
+    const int M = (int)0x80000000;
+    v = max(v, (int)AMBC_DPP(M, v, 0x111, 0xF, 0xF, false));
+    v = max(v, (int)AMBC_DPP(M, v, 0x112, 0xF, 0xF, false));
+    v = max(v, (int)AMBC_DPP(M, v, 0x114, 0xF, 0xF, false));
+    v = max(v, (int)AMBC_DPP(M, v, 0x118, 0xF, 0xF, false));
+    v = max(v, (int)AMBC_DPP(M, v, 0x142, 0xA, 0xF, false));
+    v = max(v, (int)AMBC_DPP(M, v, 0x143, 0xC, 0xF, false));
+    return v;
+}
+
+__device__ __forceinline__ int wave_max_i32(int v) { return (int)readlane((uint32_t)wave_incl_max_i32(v), 63); }
+
+// exclusive prefix max over lanes (lane 0 gets `init`)
+__device__ __forceinline__ int wave_excl_max(int v, int init) {
+    const int incl = wave_incl_max_i32(v);
+    const int ex = (int)AMBC_DPP(0x80000000u, incl, 0x138, 0xF, 0xF, false);  // wave_shr:1
+    return lane_id() == 0 ? init : max(ex, init);
+}
+
+#else  // __shfl fallbacks
+
 __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
     const uint32_t l = lane_id();
 #pragma unroll
@@ -47,8 +88,21 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
     }
     return v;
 }
-
-// exclusive prefix max over lanes (lane 0 gets `init`)
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = min(v, (uint32_t)__shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ int wave_max_i32(int v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o));
+    return v;
+}
 __device__ __forceinline__ int wave_excl_max(int v, int init) {
     const uint32_t l = lane_id();
     int x = v;
@@ -59,6 +113,25 @@ __device__ __forceinline__ int wave_excl_max(int v, int init) {
     }
     int ex = __shfl_up(x, 1);
     return l == 0 ? init : max(ex, init);
+}
+
+#endif
+
+// generic (64-bit / fp64) reductions stay on shuffles: off the hot loops
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        uint64_t t = __shfl_xor(v, o);
+        v = t < v ? t : v;
+    }
+    return v;
 }
 
 __device__ __forceinline__ uint32_t bcast0(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
