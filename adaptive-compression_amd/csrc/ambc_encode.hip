@@ -31,17 +31,21 @@ namespace ambc {
 
 template <int CMAX>
 struct EncSmem {
-    static constexpr int REGION = CMAX > 8192 ? CMAX : 8192;
+    // region = union, by lifetime: Huffman tree build (parent/pbit) + first
+    // occurrences (first/order) | LZ4 last[] hash table | RLE pair starts |
+    // Huffman bit staging.  Keeping it small keeps ~15 workgroups per CU.
+    static constexpr int REGION = (CMAX > 4096 ? CMAX : 4096) + 64;
     alignas(16) uint8_t chunk[CMAX + 64];      // zero padded
-    alignas(16) uint32_t region[REGION / 4];   // LZ4 last[] (u16) | RLE pair starts (u16) | Huffman bits
+    alignas(16) uint32_t region[REGION / 4];
     uint32_t hist[256];
-    uint32_t first[256];
     uint32_t code[256];
-    uint16_t parent[512];
-    uint8_t pbit[512];
     uint8_t clen[256];
-    uint8_t order[256];
+    __device__ __forceinline__ uint16_t* parent() { return reinterpret_cast<uint16_t*>(region); }
+    __device__ __forceinline__ uint8_t* pbit() { return reinterpret_cast<uint8_t*>(region) + 1024; }
+    __device__ __forceinline__ uint32_t* first() { return region + 384; }              // +1536 B
+    __device__ __forceinline__ uint8_t* order() { return reinterpret_cast<uint8_t*>(region) + 2560; }
 };
+static_assert((1u << LZ4_HASH_BITS) * 2 <= 4096, "LZ4 table must fit the region");
 
 // Visit the bytes of a lane's block [b0, b0+BS) 16 at a time (one ds_read_b128
 // per step; the 16-byte body is unrolled, the sub-block loop is not, which
@@ -143,7 +147,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
             for (uint32_t i = lane; i < n; i += 64) S.chunk[i] = src[i];
         }
         for (uint32_t i = n + lane; i < (uint32_t)CMAX + 64; i += 64) S.chunk[i] = 0;
-        for (uint32_t i = lane; i < 256; i += 64) { S.hist[i] = 0; S.first[i] = 0xFFFFFFFFu; }
+        for (uint32_t i = lane; i < 256; i += 64) S.hist[i] = 0;
     }
     wave_sync();
 
@@ -212,31 +216,33 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
     }
 
     // ---- Huffman (id 3) ----
-    bool first_done = false;
     auto compute_first = [&]() {
         // first occurrence per symbol (Counter insertion order) and the ranked order
+        uint32_t* first = S.first();
+        for (uint32_t i = lane; i < 256; i += 64) first[i] = 0xFFFFFFFFu;
+        wave_sync();
 #pragma unroll 1
         for (int r = 0; r < ROUNDS; r++) {
             const uint32_t b0 = (uint32_t)(r * 64 + lane) * BS;
             uint32_t prev = b0 ? S.chunk[b0 - 1] : 0x100u;
             for_block_bytes<BS>(S.chunk, b0, [&](uint32_t p, uint32_t c, uint32_t) {
-                if (p < n && c != prev) atomicMin(&S.first[c], p);
+                if (p < n && c != prev) atomicMin(&first[c], p);
                 prev = c;
             });
         }
         wave_sync();
         uint32_t f[4], rk[4] = {0, 0, 0, 0};
 #pragma unroll
-        for (int j = 0; j < 4; j++) f[j] = S.first[lane + 64 * j];
+        for (int j = 0; j < 4; j++) f[j] = first[lane + 64 * j];
 #pragma unroll 4
         for (int t = 0; t < 256; t++) {
-            const uint32_t ft = S.first[t];
+            const uint32_t ft = first[t];
 #pragma unroll
             for (int j = 0; j < 4; j++) rk[j] += ft < f[j];
         }
 #pragma unroll
         for (int j = 0; j < 4; j++)
-            if (f[j] != 0xFFFFFFFFu) S.order[rk[j]] = (uint8_t)(lane + 64 * j);
+            if (f[j] != 0xFFFFFFFFu) S.order()[rk[j]] = (uint8_t)(lane + 64 * j);
         wave_sync();
     };
 
@@ -260,12 +266,11 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         if (fabs(H - 7.0) <= 1e-9) {
             // near the threshold: reproduce numpy's sequential sum in first-occurrence order
             compute_first();
-            first_done = true;
             const double* tab = n == A.chunk_size ? A.ent_full : A.ent_tail;
             double e = 0.0;
             if (lane == 0) {
                 for (uint32_t q = 0; q < kdist; q++) {
-                    const uint32_t c = S.hist[S.order[q]];
+                    const uint32_t c = S.hist[S.order()[q]];
                     double t;
                     if (tab) t = tab[c];
                     else { const double p = (double)c / (double)n; t = p * log2(p); }
@@ -299,10 +304,10 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     if (lane + 64 * j == s1) {
-                        S.parent[nid[j]] = (uint16_t)(256 + m); S.pbit[nid[j]] = 0;
+                        S.parent()[nid[j]] = (uint16_t)(256 + m); S.pbit()[nid[j]] = 0;
                         key[j] = merged; nid[j] = 256 + m;
                     } else if (lane + 64 * j == s2) {
-                        S.parent[nid[j]] = (uint16_t)(256 + m); S.pbit[nid[j]] = 1;
+                        S.parent()[nid[j]] = (uint16_t)(256 + m); S.pbit()[nid[j]] = 1;
                         key[j] = 0xFFFFFFFFu;
                     }
                 }
@@ -316,9 +321,9 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                 if (c) {
                     uint32_t nd = s, len = 0, code = 0;
                     while (nd != root) {
-                        if (len < 32) code |= (uint32_t)S.pbit[nd] << len;
+                        if (len < 32) code |= (uint32_t)S.pbit()[nd] << len;
                         len++;
-                        nd = S.parent[nd];
+                        nd = S.parent()[nd];
                     }
                     S.clen[s] = (uint8_t)min(len, 255u);
                     S.code[s] = code;
@@ -564,13 +569,13 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
             wave_sync();
         }
     } else if (win == 3) {
-        if (!first_done) compute_first();
+        compute_first();   // (the LZ4 table may have overwritten an earlier order[])
         uint32_t* bits = S.region;
         const uint32_t kk = kdist;
         // table: [k][sym, count u32le] x k (first-occurrence order) [nbits u32le]
         if (lane == 0) slot[0] = (uint8_t)kk;
         for (uint32_t q = lane; q < kk; q += 64) {
-            const uint32_t s = S.order[q], c = S.hist[s];
+            const uint32_t s = S.order()[q], c = S.hist[s];
             uint8_t* e = slot + 1 + 5 * q;
             e[0] = (uint8_t)s; e[1] = (uint8_t)c; e[2] = (uint8_t)(c >> 8);
             e[3] = (uint8_t)(c >> 16); e[4] = (uint8_t)(c >> 24);

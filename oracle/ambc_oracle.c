@@ -416,12 +416,12 @@ EXPORT uint32_t orc_xxh32(const uint8_t* p, uint64_t len, uint32_t seed) {
 /* LZ4 ("ambc-lz4 greedy v1", this project's parse; frame = what            */
 /* LZ4F_compressFrame emits for one <=64 KiB block, advanced_compression.py */
 /* :272-281 calls lz4.frame.compress)                                        */
-/*   hash h(i) = (u32le(d+i) * 2654435761) >> (32-12)                        */
+/*   hash h(i) = (u32le(d+i) * 2654435761) >> (32-11)                        */
 /*   cand(i)   = max{ j < i : h(j) == h(i) };  valid iff the 4 bytes match   */
 /*   matchable i <= n-12; match end <= n-5 (LZ4 end-of-block rules)          */
 /*   greedy: take the match at the first valid position, jump past it       */
 /* ------------------------------------------------------------------------ */
-#define LZ4_HB 12
+#define LZ4_HB 11
 static inline uint32_t lz4_hash(uint32_t v) { return (v * 2654435761U) >> (32 - LZ4_HB); }
 
 static int64_t put_len(uint8_t* out, int64_t o, uint32_t v) {   /* ext bytes for v >= 15 */
