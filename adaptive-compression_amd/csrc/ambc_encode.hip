@@ -108,18 +108,23 @@ __device__ __forceinline__ uint8_t lz4_hdr_byte(uint32_t q, uint32_t n, uint32_t
 }
 
 #ifdef AMBC_STAMPS
-// diagnostic build only: phase cycle sums via s_memtime, lane 0 adds to A.stamps[phase]
-#define STAMP_DECL uint64_t _st_t = __builtin_amdgcn_s_memtime();
-#define STAMP(ph)                                                                      \
-    do {                                                                               \
-        __builtin_amdgcn_s_waitcnt(0xC07F);                                            \
-        const uint64_t _t = __builtin_amdgcn_s_memtime();                              \
-        if (lane == 0 && A.stamps) atomicAdd(&A.stamps[ph], (unsigned long long)(_t - _st_t)); \
-        _st_t = _t;                                                                    \
+// diagnostic build only: per-chunk phase cycle sums via s_memtime, written once
+// per chunk to A.stamps[k*8 + phase] (no atomics, so phases are not perturbed)
+#define STAMP_DECL uint64_t _st_t = __builtin_amdgcn_s_memtime(); uint64_t _acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define STAMP(ph)                                                  \
+    do {                                                           \
+        __builtin_amdgcn_s_waitcnt(0xC07F);                        \
+        const uint64_t _t = __builtin_amdgcn_s_memtime();          \
+        _acc[ph] += _t - _st_t;                                    \
+        _st_t = _t;                                                \
     } while (0)
+#define STAMP_FLUSH                                                \
+    if (lane == 0 && A.stamps)                                     \
+        for (int _p = 0; _p < 8; _p++) A.stamps[(uint64_t)k * 8 + _p] = _acc[_p];
 #else
 #define STAMP_DECL
 #define STAMP(ph) do {} while (0)
+#define STAMP_FLUSH
 #endif
 
 template <int CMAX>
@@ -397,44 +402,49 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                 L = min(L, lim);
             }
             STAMP(3);
-            // (1) scalar greedy walk: select this round's match starts (one bit per lane)
+            // (1) scalar greedy walk: select this round's match starts (one bit per
+            // lane).  p = next undecided position relative to base; everything here
+            // is wave-uniform (SALU + v_readlane).
             uint64_t sel = 0;
-            uint32_t np = nextp;
-            while (true) {
-                const int rel = (int)np - base;
-                if (rel > 63) break;
-                const uint64_t m = rel > 0 ? (vm & (~0ull << rel)) : vm;
+            uint32_t p = (int)nextp > base ? nextp - (uint32_t)base : 0u;
+            while (p < 64) {
+                p = __builtin_amdgcn_readfirstlane(p);
+                const uint64_t m = vm & (~0ull << p);
                 if (!m) break;
                 const uint32_t L0 = (uint32_t)__builtin_ctzll(m);
-                const uint32_t j = (uint32_t)base + L0;
-                const uint32_t lim = n - 5 - j;
                 uint32_t Lj = readlane(L, L0);
-                if (Lj >= LCAP && Lj < lim) {
-                    // long match: extend cooperatively, 256 bytes per step
-                    const uint32_t c = readlane((uint32_t)cand, L0);
-                    while (Lj < lim) {
-                        const uint32_t p = Lj + 4 * lane;
-                        uint32_t fd = 0;
-                        bool eq = false;
-                        if (p < lim) {
-                            const uint32_t x = lds_rd32(S.chunk, j + p) ^ lds_rd32(S.chunk, c + p);
-                            eq = x == 0;
-                            fd = x ? (uint32_t)__builtin_ctz(x) >> 3 : 4;
+                if (Lj >= LCAP) {
+                    const uint32_t j = (uint32_t)base + L0;
+                    const uint32_t lim = n - 5 - j;
+                    if (Lj < lim) {
+                        // long match: extend cooperatively, 256 bytes per step
+                        const uint32_t c = readlane((uint32_t)cand, L0);
+                        while (Lj < lim) {
+                            const uint32_t q = Lj + 4 * lane;
+                            uint32_t fd = 0;
+                            bool eq = false;
+                            if (q < lim) {
+                                const uint32_t x = lds_rd32(S.chunk, j + q) ^ lds_rd32(S.chunk, c + q);
+                                eq = x == 0;
+                                fd = x ? (uint32_t)__builtin_ctz(x) >> 3 : 4;
+                            }
+                            const uint64_t ne = __ballot(!eq);
+                            if (ne) {
+                                const uint32_t lk = (uint32_t)__builtin_ctzll(ne);
+                                Lj += 4 * lk + readlane(fd, lk);
+                                break;
+                            }
+                            Lj += 256;
                         }
-                        const uint64_t ne = __ballot(!eq);
-                        if (ne) {
-                            const uint32_t lk = (uint32_t)__builtin_ctzll(ne);
-                            Lj += 4 * lk + readlane(fd, lk);
-                            break;
-                        }
-                        Lj += 256;
+                        Lj = __builtin_amdgcn_readfirstlane(min(Lj, lim));
+                        if (lane == L0) L = Lj;
                     }
-                    Lj = min(Lj, lim);
-                    if (lane == L0) L = Lj;
                 }
                 sel |= 1ull << L0;
-                np = __builtin_amdgcn_readfirstlane(j + Lj);
+                p = L0 + Lj;
             }
+            const uint32_t np = (uint32_t)base + p;
+            STAMP(4);
             if (sel) {
                 // (2) every selected lane emits its own sequence; literal start = the
                 // previous selected match's end (exclusive max-scan), output offset =
@@ -468,6 +478,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                 anchor = np;
             }
             nextp = np;
+            STAMP(7);
         }
         uint32_t fin = 0, flit = 0, fxl = 0;
         if (alive) {
@@ -632,6 +643,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
     }
 
     STAMP(6);
+    STAMP_FLUSH
     if (lane == 0) {
         A.plen[k] = wlen;
         A.ids[k] = (uint8_t)win;

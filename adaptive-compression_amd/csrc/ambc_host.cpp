@@ -224,22 +224,23 @@ static int compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_param
     TRACE("compress_on n=%llu M=%u C=%u", (unsigned long long)n, M, C);
     std::vector<unsigned long long> stamps;
     if (getenv("AMBC_STAMPS")) {
-        HIPCHK(d.seg.ensure(64 * 8));
-        HIPCHK(hipMemsetAsync(d.seg.p, 0, 64 * 8, s));
+        HIPCHK(d.seg.ensure((size_t)std::max<uint32_t>(M, 1) * 64));
+        HIPCHK(hipMemsetAsync(d.seg.p, 0, (size_t)M * 64, s));
         ea.stamps = d.seg.as<unsigned long long>();
     }
     HIPCHK(hipEventRecord(d.ev[0], s));
     HIPCHK(launch_encode(ea, s));
     HIPCHK(hipEventRecord(d.ev[1], s));
     if (ea.stamps) {
-        stamps.resize(8);
-        HIPCHK(hipMemcpyAsync(stamps.data(), d.seg.p, 64, hipMemcpyDeviceToHost, s));
+        stamps.resize((size_t)M * 8);
+        HIPCHK(hipMemcpyAsync(stamps.data(), d.seg.p, (size_t)M * 64, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
-        fprintf(stderr, "[ambc stamps] M=%u load+passA %.0f huff %.0f lz4hash %.0f lz4len %.0f lz4walk %.0f lz4tail %.0f emit %.0f seqs %.1f (cycles/chunk)\n",
-                M, stamps[0] / (double)M, stamps[1] / (double)M, stamps[2] / (double)M, stamps[3] / (double)M,
-                stamps[4] / (double)M, stamps[5] / (double)M, stamps[6] / (double)M, stamps[7] / (double)M);
+        double sum[8] = {0};
+        for (size_t q = 0; q < stamps.size(); q++) sum[q & 7] += (double)stamps[q];
+        fprintf(stderr, "[ambc stamps] M=%u cycles/chunk: passA %.0f huff %.0f lz4hash %.0f lz4len %.0f "
+                "lz4walk %.0f lz4tail+emit %.0f final %.0f lz4emit %.0f\n", M, sum[0] / M, sum[1] / M,
+                sum[2] / M, sum[3] / M, sum[4] / M, sum[5] / M, sum[6] / M, sum[7] / M);
     }
-    if (trace_on()) { HIPCHK(hipStreamSynchronize(s)); TRACE("encode done"); }
 
     // reference mode: the first chunk with no winner swallows the remainder
     uint32_t R = M;
