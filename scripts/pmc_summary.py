@@ -1,0 +1,68 @@
+"""Summarise rocprofv3 runs of bench.py into profiles/ (per round).
+
+    python scripts/pmc_summary.py --round r1 --stats DIR --fetch DIR --write DIR --bench JSON
+
+* kernel stats: copies <stats>/run_kernel_stats.csv to profiles/<round>_kernel_stats.csv
+* HBM traffic of k_encode per launch from the two PMC passes (FETCH_SIZE and
+  WRITE_SIZE cannot share a pass on gfx950), with the MI355X_MICROARCH.md
+  correction: FETCH_SIZE counts half the bytes of 16-B-per-lane streaming
+  reads (k_encode's loads are global_load_dwordx4), so it is doubled;
+  WRITE_SIZE is taken as is.  Both counters are in KiB.
+  -> profiles/pmc_<round>.json (read by bench.py for roofline.traffic)
+"""
+import argparse
+import csv
+import json
+import os
+import shutil
+import statistics
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def counter(d, name, kernel="k_encode"):
+    vals = []
+    for f in os.listdir(d):
+        if f.endswith("counter_collection.csv"):
+            with open(os.path.join(d, f)) as fh:
+                for r in csv.DictReader(fh):
+                    if r["Counter_Name"] == name and r["Kernel_Name"].startswith(kernel):
+                        vals.append(float(r["Counter_Value"]))
+    return vals
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--round", required=True)
+    ap.add_argument("--stats")
+    ap.add_argument("--fetch")
+    ap.add_argument("--write")
+    ap.add_argument("--bench")
+    args = ap.parse_args()
+    out = os.path.join(REPO, "profiles")
+    os.makedirs(out, exist_ok=True)
+    if args.stats:
+        src = os.path.join(args.stats, "run_kernel_stats.csv")
+        shutil.copy(src, os.path.join(out, f"{args.round}_kernel_stats.csv"))
+    if args.fetch and args.write:
+        fetch = counter(args.fetch, "FETCH_SIZE")
+        write = counter(args.write, "WRITE_SIZE")
+        f_kib, w_kib = statistics.median(fetch), statistics.median(write)
+        rec = {"round": args.round, "kernel": "k_encode",
+               "fetch_size_kib_raw": f_kib, "write_size_kib": w_kib,
+               "fetch_bytes_corrected": f_kib * 1024 * 2, "write_bytes": w_kib * 1024,
+               "hbm_bytes_per_launch": int(f_kib * 1024 * 2 + w_kib * 1024),
+               "note": "FETCH_SIZE x2 (gfx950: 16-B-per-lane streaming reads count half), "
+                       "separate --pmc passes, median over launches"}
+        if args.bench:
+            with open(args.bench) as fh:
+                b = json.loads(fh.read().strip().splitlines()[-1])
+            rec["workload"] = b["config"]["workload"]
+            rec["algorithmic_bytes_per_launch"] = b["roofline"]["algorithmic_bytes_per_launch"]
+        with open(os.path.join(out, f"pmc_{args.round}.json"), "w") as fh:
+            json.dump(rec, fh, indent=1)
+        print(json.dumps(rec, indent=1))
+
+
+if __name__ == "__main__":
+    main()
