@@ -22,16 +22,46 @@
 
 namespace ambc {
 
-constexpr uint32_t STAGE = 16384;  // LDS output staging per package
+constexpr uint32_t STAGE = 8192;   // LDS output staging per package
+constexpr uint32_t PIN = 8192;     // LDS copy of the compressed payload
 constexpr uint32_t LUT_BITS = 10;
 
+#ifdef AMBC_STAMPS
+// diagnostic build only: per-job phase cycles in A.stamps[job*8 + phase]
+#define DSTAMP(ph)                                              \
+    do {                                                        \
+        __builtin_amdgcn_s_waitcnt(0xC07F);                     \
+        const uint64_t _t = __builtin_amdgcn_s_memtime();       \
+        if (lane == 0 && _stp) _stp[ph] = _t - _st_t;           \
+        _st_t = _t;                                             \
+    } while (0)
+#define DSTAMP_DECL                                             \
+    uint64_t _st_t = __builtin_amdgcn_s_memtime();              \
+    unsigned long long* _stp = A.stamps ? A.stamps + (uint64_t)blockIdx.x * 8 : nullptr;
+#define DSTAMP_PARAMS , unsigned long long* _stp, uint64_t& _st_t
+#define DSTAMP_ARGS , _stp, _st_t
+#else
+#define DSTAMP(ph) do {} while (0)
+#define DSTAMP_DECL
+#define DSTAMP_PARAMS
+#define DSTAMP_ARGS
+#endif
+
+constexpr uint32_t SRC_LIT = 0x8000;  // LZ4 source map: payload byte (else earlier output byte)
+
 struct DecSmem {
-    alignas(16) uint8_t stage[STAGE + 64];
-    uint32_t lut[1u << LUT_BITS];   // Huffman: leaf (sym | len<<8 | 1<<31) or node | 10<<16
-    uint16_t child[512][2];
-    unsigned long long w[256];
-    uint8_t syms[256];
-    int16_t idx[256];
+    alignas(16) uint8_t pin[PIN + 64];
+    union {
+        uint16_t src[STAGE];  // LZ4 block decode: source of every output byte
+        struct {
+            alignas(16) uint8_t stage[STAGE + 64];
+            uint32_t lut[1u << LUT_BITS];  // Huffman: leaf (sym | len<<8 | 1<<31) or node | 10<<16
+            uint16_t child[512][2];
+            unsigned long long w[256];
+            uint8_t syms[256];
+            int16_t idx[256];
+        };
+    };
     uint32_t misc[8];
 };
 
@@ -114,7 +144,7 @@ __device__ void dec_rle(const uint8_t* p, uint32_t plen, uint32_t orig, uint8_t*
         const uint32_t incl = wave_incl_sum(c);
         scan_lds[lane] = incl;
         const uint32_t tot = __shfl(incl, 63);
-        __syncthreads();
+        wave_sync();
         const uint32_t lim = min(tot, orig - o);
         for (uint32_t q = lane; q < lim; q += 64) {
             uint32_t lo = 0, hi = 63;  // first lane with incl > q
@@ -125,7 +155,7 @@ __device__ void dec_rle(const uint8_t* p, uint32_t plen, uint32_t orig, uint8_t*
             dst[o + q] = p[2 * (g + lo)];
         }
         o += lim;
-        __syncthreads();
+        wave_sync();
     }
     if (o < orig) wave_zero(dst + o, orig - o, lane);
 }
@@ -176,7 +206,7 @@ __device__ int64_t dec_huffman(const uint8_t* p, uint32_t plen, uint32_t orig, u
         S.misc[1] = (uint32_t)nf;
         S.misc[2] = (uint32_t)min(pos, (uint64_t)0xFFFFFFFFu);
     }
-    __syncthreads();
+    wave_sync();
     if (S.misc[0] || S.misc[1] < 2) return -1;   // IndexError paths
     const uint32_t nf = S.misc[1];
     uint64_t pos = S.misc[2];
@@ -212,7 +242,7 @@ __device__ int64_t dec_huffman(const uint8_t* p, uint32_t plen, uint32_t orig, u
             }
         }
     }
-    __syncthreads();
+    wave_sync();
     const uint32_t root = 256 + nf - 2;
     // LUT over LUT_BITS-bit prefixes
     for (uint32_t v = lane; v < (1u << LUT_BITS); v += 64) {
@@ -223,7 +253,7 @@ __device__ int64_t dec_huffman(const uint8_t* p, uint32_t plen, uint32_t orig, u
         }
         S.lut[v] = nd < 256 ? (0x80000000u | d << 8 | nd) : (LUT_BITS << 16 | nd);
     }
-    __syncthreads();
+    wave_sync();
     int64_t produced = 0;
     if (lane == 0) {
         uint64_t nbits = le_partial(p, pos, plen, 4);
@@ -357,9 +387,14 @@ __device__ int64_t dec_lz4(const uint8_t* p, uint32_t plen, uint8_t* dst, uint64
                 ml += 4;
                 if (op + ml > lim) return -1;
                 if (wave_ok) {
-                    __syncthreads();
-                    for (uint32_t t = lane; t < (uint32_t)ml; t += 64) dst[op + t] = dst[op - off + (t % (uint32_t)off)];
-                    __syncthreads();
+                    wave_sync();
+                    if (off >= ml) {
+                        for (uint32_t t = lane; t < (uint32_t)ml; t += 64) dst[op + t] = dst[op - off + t];
+                    } else {
+                        for (uint32_t t = lane; t < (uint32_t)ml; t += 64)
+                            dst[op + t] = dst[op - off + (t % (uint32_t)off)];
+                    }
+                    wave_sync();
                 } else if (lane == 0) {
                     for (uint64_t t = 0; t < ml; t++) dst[op + t] = dst[op - off + t];
                 }
@@ -372,11 +407,11 @@ __device__ int64_t dec_lz4(const uint8_t* p, uint32_t plen, uint8_t* dst, uint64
             if (xxh32(p + hp - sz, sz, 0) != rd32(hp)) return -1;
             hp += 4;
         }
-        __syncthreads();
+        wave_sync();
     }
     if (has_cck) {
         if (hp + 4 > plen) return -1;
-        __syncthreads();
+        wave_sync();
         uint32_t hsh = 0;
         if (lane == 0) hsh = xxh32(dst, op, 0);
         hsh = __shfl(hsh, 0);
@@ -384,6 +419,308 @@ __device__ int64_t dec_lz4(const uint8_t* p, uint32_t plen, uint8_t* dst, uint64
     }
     if (has_cs && op != csize) return -1;
     return (int64_t)op;
+}
+
+// ---------------------------------------------------------------------------
+// LZ4 frame, parallel form (output <= STAGE, payload < 32 KiB, no content
+// checksum).  Three phases instead of a byte-serial copy loop:
+//   1. the token stream is parsed by the whole wave in lock step from a
+//      256-byte register window (4 bytes per lane, bytes fetched with
+//      v_readlane, so the parse runs on the scalar unit); each sequence only
+//      records, per output byte, where the byte comes from: SRC_LIT|payload
+//      index for literals and stored blocks, the earlier output index for
+//      match bytes;
+//   2. pointer jumping over the source map until every entry names a payload
+//      byte (log2 of the longest match chain passes, usually 1-2);
+//   3. gather: out[q] = payload[src[q]], dword stores.
+// Validity checks are exactly dec_lz4's, in the same order.
+// Returns decoded length, -1 for an invalid frame, -2 for "use dec_lz4".
+// ---------------------------------------------------------------------------
+struct ByteWin {
+    uint32_t v;   // 4 payload bytes per lane
+    int32_t lo;   // payload index of lane 0's first byte (wave-uniform)
+};
+
+// g must point into device global memory with >= 3 readable bytes past g+plen
+// (the body buffer has 64 bytes of slack); the window is dword aligned.
+__device__ __forceinline__ void win_load(ByteWin& W, const uint8_t* g, uint32_t i, uint32_t plen,
+                                         uint32_t lane) {
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(g + i) & 3);
+    W.lo = (int32_t)__builtin_amdgcn_readfirstlane(i - mis);
+    const uint32_t* a = reinterpret_cast<const uint32_t*>(g + i - mis);
+    W.v = (W.lo + 4 * (int32_t)lane < (int32_t)plen) ? a[lane] : 0u;
+}
+
+__device__ __forceinline__ uint32_t win_byte(ByteWin& W, const uint8_t* g, uint32_t i, uint32_t plen,
+                                             uint32_t lane) {
+    uint32_t r = __builtin_amdgcn_readfirstlane((uint32_t)((int32_t)i - W.lo));
+    if (r >= 256) {  // uniform branch
+        win_load(W, g, i, plen, lane);
+        r = __builtin_amdgcn_readfirstlane((uint32_t)((int32_t)i - W.lo));
+    }
+    return __builtin_amdgcn_readfirstlane((readlane(W.v, r >> 2) >> ((r & 3) * 8)) & 0xFF);
+}
+
+// One sequence of an LZ4 block read speculatively from payload index x (token
+// byte tok), with dec_lz4's bounds checks: literal start y, literal length L,
+// offset position z, match length ml; returns the next token's index, TOK_END
+// (the literals reach the block end: last sequence) or TOK_ERR.
+constexpr uint32_t TOK_END = 0xFFFF, TOK_ERR = 0xFFFE;
+
+__device__ __forceinline__ uint32_t seq_parse(const uint8_t* g, uint32_t x, uint32_t tok, uint32_t end,
+                                              uint32_t& y, uint32_t& L, uint32_t& z, uint32_t& ml) {
+    y = x + 1;
+    L = tok >> 4;
+    if (L == 15) {
+        uint32_t b;
+        do { if (y >= end) return TOK_ERR; b = g[y++]; L += b; } while (b == 255);
+    }
+    if (y + L > end) return TOK_ERR;
+    z = y + L;
+    if (z == end) return TOK_END;
+    if (z + 2 > end) return TOK_ERR;
+    uint32_t w = z + 2;
+    ml = tok & 15;
+    if (ml == 15) {
+        uint32_t b;
+        do { if (w >= end) return TOK_ERR; b = g[w++]; ml += b; } while (b == 255);
+    }
+    ml += 4;
+    return w;
+}
+
+// source-map entries of one sequence (o = output index of its first literal).
+// Overlapping matches (off < ml) point into the period before the match, so no
+// entry's source chain grows with the match length.
+__device__ __forceinline__ void seq_write_lane(uint16_t* src, uint32_t o, uint32_t y, uint32_t L,
+                                               uint32_t off, uint32_t ml) {
+    for (uint32_t t = 0; t < L; t++) src[o + t] = (uint16_t)(SRC_LIT | (y + t));
+    const uint32_t m0 = o + L - off;
+    uint32_t c = 0;
+    for (uint32_t t = 0; t < ml; t++) {
+        src[o + L + t] = (uint16_t)(m0 + c);
+        if (++c == off) c = 0;
+    }
+}
+
+__device__ __forceinline__ void seq_write_wave(uint16_t* src, uint32_t o, uint32_t y, uint32_t L,
+                                               uint32_t off, uint32_t ml, uint32_t lane) {
+    for (uint32_t b = 0; b < L; b += 64)
+        if (b + lane < L) src[o + b + lane] = (uint16_t)(SRC_LIT | (y + b + lane));
+    if (ml == 0) return;
+    const uint32_t m0 = o + L - off;
+    const uint32_t lmod = lane % off;   // (b + lane) % off = (b % off + lane % off) mod off
+    uint32_t bmod = 0;
+    for (uint32_t b = 0; b < ml; b += 64) {
+        uint32_t c = bmod + lmod;
+        if (c >= off) c -= off;
+        if (b + lane < ml) src[o + L + b + lane] = (uint16_t)(m0 + c);
+        bmod = (bmod + 64) % off;
+    }
+}
+
+// One compressed block [hp, end) of a frame: the wave reads 256 payload bytes
+// at a time; every lane parses the 4 positions it holds as if a sequence began
+// there, the scalar unit then follows the real token chain through the window
+// (one v_readlane per sequence), and the marked sequences are laid out in
+// parallel (wave prefix sum of their output lengths).  Returns the output
+// index after the block or -1.
+constexpr uint32_t SEQ_LONG = 32;
+
+__device__ __forceinline__ int64_t lz4_block_par(const uint8_t* g, uint32_t hp, uint32_t end, uint32_t op, uint32_t lim,
+                                 uint32_t plen, uint16_t* src, uint32_t lane) {
+    uint32_t x0 = hp;
+    for (;;) {
+        if (x0 >= end) return -1;  // a token must start inside the block
+        const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(g + x0) & 3);
+        const uint32_t wlo = __builtin_amdgcn_readfirstlane(x0 - mis);
+        const uint32_t* a = reinterpret_cast<const uint32_t*>(g + x0 - mis);
+        const uint32_t wv = (wlo + 4 * lane < plen) ? a[lane] : 0u;
+        uint32_t nx[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t pos = wlo + 4 * lane + k;
+            uint32_t y, L, z, ml;
+            nx[k] = (pos >= x0 && pos < end) ? seq_parse(g, pos, (wv >> (8 * k)) & 0xFF, end, y, L, z, ml)
+                                             : TOK_ERR;
+        }
+        const uint32_t nA = nx[0] | nx[1] << 16, nB = nx[2] | nx[3] << 16;
+        // the token chain through this window (scalar)
+        uint64_t mk0 = 0, mk1 = 0, mk2 = 0, mk3 = 0;
+        uint32_t s = x0;
+        bool last = false;
+        for (;;) {
+            const uint32_t r = __builtin_amdgcn_readfirstlane(s - wlo);
+            if (r >= 256) break;
+            const uint64_t bit = 1ull << (r & 63);
+            const uint32_t q = r >> 6;
+            mk0 |= q == 0 ? bit : 0;
+            mk1 |= q == 1 ? bit : 0;
+            mk2 |= q == 2 ? bit : 0;
+            mk3 |= q == 3 ? bit : 0;
+            const uint32_t v = readlane((r & 2) ? nB : nA, r >> 2);
+            const uint32_t t = (r & 1) ? v >> 16 : v & 0xFFFF;
+            if (t == TOK_ERR) return -1;
+            if (t == TOK_END) { last = true; break; }
+            s = t;
+            if (s >= end) return -1;  // the block cannot end right after a match
+        }
+        // the marked sequences this lane holds
+        const uint64_t mw = lane < 16 ? mk0 : lane < 32 ? mk1 : lane < 48 ? mk2 : mk3;
+        const uint32_t bits = (uint32_t)(mw >> ((lane & 15) * 4)) & 15;
+        uint32_t ky[4], kL[4], koff[4], kml[4], ko[4];
+        uint32_t tot = 0;
+        bool lng = false;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            ky[k] = kL[k] = koff[k] = kml[k] = 0;
+            if ((bits >> k) & 1) {
+                const uint32_t pos = wlo + 4 * lane + k;
+                uint32_t y, L, z, ml = 0;
+                const uint32_t nt = seq_parse(g, pos, (wv >> (8 * k)) & 0xFF, end, y, L, z, ml);
+                ky[k] = y;
+                kL[k] = L;
+                if (nt != TOK_END) { koff[k] = (uint32_t)g[z] | (uint32_t)g[z + 1] << 8; kml[k] = ml; }
+                tot += L + kml[k];
+                lng |= L > SEQ_LONG || kml[k] > SEQ_LONG;
+            }
+        }
+        const uint32_t incl = wave_incl_sum(tot);
+        const uint32_t wtot = readlane(incl, 63);
+        uint32_t o = op + incl - tot;
+        bool bad = false;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            ko[k] = o;
+            if ((bits >> k) & 1) {
+                if (o + kL[k] > lim) bad = true;
+                o += kL[k];
+                if (kml[k]) {
+                    if (koff[k] == 0 || koff[k] > o || o + kml[k] > lim) bad = true;
+                    o += kml[k];
+                }
+            }
+        }
+        if (__any(bad)) return -1;
+        if (!lng) {
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if ((bits >> k) & 1) seq_write_lane(src, ko[k], ky[k], kL[k], koff[k], kml[k]);
+        }
+        // lanes holding a long sequence: written by the whole wave, one lane at a time
+        uint64_t lm = __ballot(lng);
+        while (lm) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(lm);
+            lm &= lm - 1;
+            const uint32_t lb = readlane(bits, l);
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if ((lb >> k) & 1)
+                    seq_write_wave(src, readlane(ko[k], l), readlane(ky[k], l), readlane(kL[k], l),
+                                   readlane(koff[k], l), readlane(kml[k], l), lane);
+        }
+        op += wtot;
+        if (last) return (int64_t)op;
+        x0 = s;
+    }
+}
+
+__device__ __forceinline__ int64_t dec_lz4_par(const uint8_t* p, uint32_t plen, uint16_t* src, uint32_t cap,
+                               uint32_t lane DSTAMP_PARAMS) {
+    if (plen > 0x7FFF || plen < 7) return -2;
+    ByteWin W;
+    win_load(W, p, 0, plen, lane);
+    auto B = [&](uint32_t i) { return win_byte(W, p, i, plen, lane); };
+    auto rd32 = [&](uint32_t q) { return B(q) | B(q + 1) << 8 | B(q + 2) << 16 | B(q + 3) << 24; };
+    if (rd32(0) != 0x184D2204u) return -1;
+    const uint32_t flg = B(4), bd = B(5);
+    if ((flg >> 6) != 1 || (flg & 0x02) || (bd & 0x8F)) return -1;
+    const uint32_t bsid = (bd >> 4) & 7;
+    if (bsid < 4) return -1;
+    if ((flg >> 2) & 1) return -2;  // content checksum: the byte-serial decoder hashes its output
+    const uint64_t bmax = 1ull << (8 + 2 * bsid);
+    uint32_t hp = 6;
+    uint64_t csize = 0;
+    const bool has_cs = (flg >> 3) & 1, has_bck = (flg >> 4) & 1, has_dict = flg & 1;
+    if (has_cs) {
+        if (hp + 8 > plen) return -1;
+        for (int b = 0; b < 8; b++) csize |= (uint64_t)B(hp + b) << (8 * b);
+        hp += 8;
+    }
+    if (has_dict) { if (hp + 4 > plen) return -1; hp += 4; }
+    if (hp >= plen) return -1;
+    if (((xxh32(p + 4, hp - 4, 0) >> 8) & 0xFF) != B(hp)) return -1;
+    hp++;
+    if (has_cs && csize > cap) return -1;
+    uint32_t op = 0;
+    for (;;) {
+        if (hp + 4 > plen) return -1;
+        const uint32_t bs = rd32(hp);
+        hp += 4;
+        if (bs == 0) break;
+        const uint32_t sz = bs & 0x7FFFFFFFu;
+        if (sz > bmax || (uint64_t)hp + sz > plen) return -1;
+        if (bs & 0x80000000u) {
+            if ((uint64_t)op + sz > cap) return -1;
+            for (uint32_t t = lane; t < sz; t += 64) src[op + t] = (uint16_t)(SRC_LIT | (hp + t));
+            op += sz;
+        } else {
+            const uint64_t lim = min((uint64_t)op + bmax, (uint64_t)cap);
+            const int64_t r = lz4_block_par(p, hp, hp + sz, op, (uint32_t)lim, plen, src, lane);
+            if (r < 0) return -1;
+            op = (uint32_t)r;
+        }
+        hp += sz;
+        if (has_bck) {
+            if (hp + 4 > plen) return -1;
+            if (xxh32(p + hp - sz, sz, 0) != rd32(hp)) return -1;
+            hp += 4;
+        }
+    }
+    if (has_cs && op != csize) return -1;
+    wave_sync();
+    DSTAMP(1);
+    uint32_t passes = 0;
+    (void)passes;
+    // pointer jumping: every pass at least doubles the distance each entry skips
+    for (;;) {
+        bool more = false;
+        for (uint32_t q0 = lane * 4; q0 < op; q0 += 256) {
+            uint32_t v[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) v[k] = q0 + k < op ? src[q0 + k] : SRC_LIT;
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (!(v[k] & SRC_LIT)) {
+                    v[k] = src[v[k]];
+                    src[q0 + k] = (uint16_t)v[k];
+                    more |= !(v[k] & SRC_LIT);
+                }
+        }
+        wave_sync();
+        passes++;
+        if (!__any(more)) break;
+    }
+    DSTAMP(2);
+#ifdef AMBC_STAMPS
+    if (lane == 0 && _stp) _stp[6] = passes;
+#endif
+    return (int64_t)op;
+}
+
+// out[0, m) = payload bytes named by the resolved source map
+__device__ void lz4_gather(uint8_t* out, const uint8_t* p, const uint16_t* src, uint32_t m,
+                           uint32_t lane) {
+    const uint32_t head = min((uint32_t)((4 - (reinterpret_cast<uintptr_t>(out) & 3)) & 3), m);
+    if (lane < head) out[lane] = p[src[lane] & 0x7FFF];
+    const uint32_t nw = (m - head) >> 2;
+    uint32_t* o32 = reinterpret_cast<uint32_t*>(out + head);
+    for (uint32_t w = lane; w < nw; w += 64) {
+        const uint32_t q = head + 4 * w;
+        o32[w] = (uint32_t)p[src[q] & 0x7FFF] | (uint32_t)p[src[q + 1] & 0x7FFF] << 8 |
+                 (uint32_t)p[src[q + 2] & 0x7FFF] << 16 | (uint32_t)p[src[q + 3] & 0x7FFF] << 24;
+    }
+    for (uint32_t i = head + (nw << 2) + lane; i < m; i += 64) out[i] = p[src[i] & 0x7FFF];
 }
 
 // Dictionary (id 2): serial by lane 0 (back-references into its own output)
@@ -422,44 +759,112 @@ __device__ int64_t dec_dict(const uint8_t* p, uint32_t plen, uint32_t orig, uint
     return __shfl(ret, 0);
 }
 
-__global__ __launch_bounds__(64) void k_decode(DecArgs A) {
-    __shared__ DecSmem S;
-    const uint32_t lane = threadIdx.x;
-    const DecJob J = A.jobs[blockIdx.x];
-    const uint8_t* p = A.body + J.body_off;
-    uint8_t* out = A.out + J.out_off;
+// raw / verbatim / skip / RLE / Delta: no LDS beyond a 64-entry scan
+__device__ __forceinline__ bool decode_light(const DecJob& J, const uint8_t* p, uint8_t* out,
+                                             uint32_t lane, uint32_t* scan, int64_t& produced) {
     const uint32_t orig = J.orig, clen = J.clen;
-    int64_t produced = 0;
     switch (J.type) {
     case DEC_SKIP:
         produced = J.expect;
-        break;
+        return true;
     case DEC_VERBATIM:
         wave_copy(out, p, clen, lane);
         produced = clen;
-        break;
+        return true;
     case 255: {
         const uint32_t m = min(clen, orig);
         wave_copy(out, p, m, lane);
         wave_zero(out + m, orig - m, lane);
         produced = orig;
-        break;
+        return true;
     }
     case 1:
-        if (clen == 0) break;
-        dec_rle(p, clen, orig, out, lane, reinterpret_cast<uint32_t*>(S.stage));
-        produced = orig;
-        break;
+        if (clen) { dec_rle(p, clen, orig, out, lane, scan); produced = orig; }
+        return true;
     case 4:
-        if (clen == 0) break;
-        produced = min(clen, orig);
-        dec_delta(p, (uint32_t)produced, out, lane);
-        break;
+        if (clen) { produced = min(clen, orig); dec_delta(p, (uint32_t)produced, out, lane); }
+        return true;
+    default:
+        return false;
+    }
+}
+
+__device__ __forceinline__ uint32_t job_index(const DecArgs& A) {
+    return A.list ? A.list[blockIdx.x] : blockIdx.x;
+}
+
+__device__ __forceinline__ void put_produced(const DecArgs& A, uint32_t j, int64_t produced,
+                                             uint32_t lane) {
+    if (lane == 0) A.produced[j] = (uint32_t)(produced < 0 ? 0xFFFFFFFFu : (uint32_t)produced);
+}
+
+__global__ __launch_bounds__(64) void k_decode_light(DecArgs A) {
+    __shared__ uint32_t scan[64];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t j = job_index(A);
+    const DecJob J = A.jobs[j];
+    int64_t produced = 0;
+    if (!decode_light(J, A.body + J.body_off, A.out + J.out_off, lane, scan, produced)) produced = -1;
+    put_produced(A, j, produced, lane);
+}
+
+// LZ4 frames the host routed here: content bound <= OUTMAX, payload < 32 KiB,
+// no content checksum -- so dec_lz4_par never asks for the serial decoder
+template <uint32_t OUTMAX>
+__global__ __launch_bounds__(64) void k_decode_lz4(DecArgs A) {
+    __shared__ uint16_t src[OUTMAX];
+    const uint32_t lane = threadIdx.x;
+    DSTAMP_DECL
+    const uint32_t j = job_index(A);
+    const DecJob J = A.jobs[j];
+    const uint8_t* g = A.body + J.body_off;
+    uint8_t* out = A.out + J.out_off;
+    const uint32_t orig = J.orig;
+    DSTAMP(0);
+    const int64_t r = dec_lz4_par(g, J.clen, src, OUTMAX, lane DSTAMP_ARGS);
+    wave_sync();
+    if (r < 0) {
+        wave_zero(out, orig, lane);
+    } else {
+        const uint32_t m = min((uint32_t)r, orig);
+        lz4_gather(out, g, src, m, lane);
+        wave_zero(out + m, orig - m, lane);
+    }
+    DSTAMP(3);
+#ifdef AMBC_STAMPS
+    if (lane == 0 && _stp) _stp[7] = 9;
+#endif
+    put_produced(A, j, r == -2 ? -1 : (int64_t)orig, lane);
+}
+
+// everything else: Huffman, Dictionary, LZ4 frames that need the serial decoder
+__global__ __launch_bounds__(64) void k_decode(DecArgs A) {
+    __shared__ DecSmem S;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t j = job_index(A);
+    const DecJob J = A.jobs[j];
+    const uint8_t* p = A.body + J.body_off;
+    const uint8_t* g = p;  // the payload in global memory
+    uint8_t* out = A.out + J.out_off;
+    const uint32_t orig = J.orig, clen = J.clen;
+    int64_t produced = 0;
+    if (decode_light(J, p, out, lane, reinterpret_cast<uint32_t*>(S.stage), produced)) {
+        put_produced(A, j, produced, lane);
+        return;
+    }
+    if ((J.type == 2 || J.type == 3 || J.type == 9) && clen && clen <= PIN) {
+        // serial parsers read the payload byte by byte: keep it in LDS
+        wave_copy(S.pin, p, clen, lane);
+        if (lane < 8) S.pin[clen + lane] = 0;
+        wave_sync();
+        p = S.pin;
+    }
+    switch (J.type) {
     case 3: {
         if (clen == 0) break;
         const bool staged = orig <= STAGE;
         int64_t r = dec_huffman(p, clen, orig, staged ? S.stage : out, S, lane);
-        __syncthreads();
+        wave_sync();
         if (r < 0) { wave_zero(out, orig, lane); produced = orig; }
         else {
             if (staged) wave_copy(out, S.stage, (uint64_t)r, lane);
@@ -473,8 +878,9 @@ __global__ __launch_bounds__(64) void k_decode(DecArgs A) {
         // the job's device scratch window sized by the host walk
         const bool staged = J.scratch_off == ~0ull;
         uint8_t* dst = staged ? S.stage : A.scratch + J.scratch_off;
+        (void)g;
         const int64_t r = dec_lz4(p, clen, dst, staged ? STAGE : J.scratch_cap, staged, S, lane);
-        __syncthreads();
+        wave_sync();
         if (r < 0) { wave_zero(out, orig, lane); }
         else {
             const uint64_t m = min((uint64_t)r, (uint64_t)orig);
@@ -490,7 +896,7 @@ __global__ __launch_bounds__(64) void k_decode(DecArgs A) {
         const bool staged = J.scratch_off == ~0ull;
         uint8_t* dst = staged ? S.stage : A.scratch + J.scratch_off;
         const int64_t r = dec_dict(p, clen, orig, dst, staged ? STAGE : J.scratch_cap, lane);
-        __syncthreads();
+        wave_sync();
         if (r < 0) { wave_zero(out, orig, lane); produced = orig; }
         else {
             if (staged) wave_copy(out, dst, (uint64_t)r, lane);
@@ -503,12 +909,17 @@ __global__ __launch_bounds__(64) void k_decode(DecArgs A) {
         produced = -1;
         break;
     }
-    if (lane == 0) A.produced[blockIdx.x] = (uint32_t)(produced < 0 ? 0xFFFFFFFFu : (uint32_t)produced);
+    put_produced(A, j, produced, lane);
 }
 
-hipError_t launch_decode(const DecArgs& a, hipStream_t s) {
-    if (a.n_jobs == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_decode, dim3(a.n_jobs), dim3(64), 0, s, a);
+hipError_t launch_decode(int kind, const DecArgs& a, hipStream_t s) {
+    if (a.n_list == 0) return hipSuccess;
+    switch (kind) {
+    case DEC_KIND_LIGHT: hipLaunchKernelGGL(k_decode_light, dim3(a.n_list), dim3(64), 0, s, a); break;
+    case DEC_KIND_LZ4_4K: hipLaunchKernelGGL(k_decode_lz4<4096>, dim3(a.n_list), dim3(64), 0, s, a); break;
+    case DEC_KIND_LZ4_8K: hipLaunchKernelGGL(k_decode_lz4<8192>, dim3(a.n_list), dim3(64), 0, s, a); break;
+    default: hipLaunchKernelGGL(k_decode, dim3(a.n_list), dim3(64), 0, s, a); break;
+    }
     return hipGetLastError();
 }
 

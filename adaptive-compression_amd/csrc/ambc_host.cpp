@@ -75,7 +75,7 @@ struct Dev {
     hipStream_t stream = nullptr;
     hipEvent_t ev[6] = {};
     Buf in, out, slots, plen, ids, sizes, off, scan_tmp, acc, ent_full, ent_tail;
-    Buf body, jobs, produced, dout, scratch, seg;
+    Buf body, jobs, produced, dout, scratch, seg, list;
     uint64_t t_encode = 0, t_scan = 0, t_compact = 0;
 };
 
@@ -527,7 +527,7 @@ extern "C" int ambc_analyze(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const 
 // ---------------------------------------------------------------------------
 namespace {
 
-constexpr uint32_t STAGE_DEC = 16384;   // must match ambc_decode.hip
+constexpr uint32_t STAGE_DEC = 8192;    // must match ambc_decode.hip STAGE
 
 bool registered_id(const uint64_t reg[4], uint32_t t) { return (reg[t >> 6] >> (t & 63)) & 1; }
 
@@ -535,17 +535,21 @@ uint32_t rd32le(const uint8_t* p) { return p[0] | p[1] << 8 | p[2] << 16 | (uint
 
 // upper bound of an LZ4 frame's decoded content (for scratch sizing); 0 if unknown/small
 uint64_t lz4_content_bound(const uint8_t* p, uint32_t plen) {
+    // Upper bound on what the frame can decode to: the block walk (a compressed
+    // block of sz bytes yields at most min(block max, 255*sz) bytes).  A declared
+    // content size above it can never match the decoded length, so the frame is
+    // invalid and needs no more room than the walk bound.
     if (plen < 7 || rd32le(p) != 0x184D2204u) return 0;
     const uint32_t flg = p[4], bd = p[5];
     const uint32_t bsid = (bd >> 4) & 7;
     if (bsid < 4) return 0;
     const uint64_t bmax = 1ull << (8 + 2 * bsid);
-    uint64_t hp = 6;
-    if ((flg >> 3) & 1) {
+    uint64_t hp = 6, cs = 0;
+    const bool has_cs = (flg >> 3) & 1;
+    if (has_cs) {
         if (hp + 8 > plen) return 0;
-        uint64_t cs = 0;
         for (int b = 0; b < 8; b++) cs |= (uint64_t)p[hp + b] << (8 * b);
-        return cs;
+        hp += 8;
     }
     if (flg & 1) hp += 4;
     hp += 1;
@@ -555,15 +559,16 @@ uint64_t lz4_content_bound(const uint8_t* p, uint32_t plen) {
         hp += 4;
         if (bs == 0) break;
         const uint32_t sz = bs & 0x7FFFFFFFu;
-        bound += (bs & 0x80000000u) ? sz : bmax;
-        hp += sz + (((flg >> 4) & 1) ? 4 : 0);
+        bound += (bs & 0x80000000u) ? sz : std::min<uint64_t>(bmax, 255ull * sz + 16);
+        hp += (uint64_t)sz + (((flg >> 4) & 1) ? 4 : 0);
     }
-    return bound;
+    return has_cs ? std::min(cs, bound) : bound;
 }
 
 struct Walk {
     std::vector<DecJob> jobs;
     std::vector<uint32_t> src_index;   // job -> package ordinal
+    std::vector<uint8_t> kind;         // job -> DEC_KIND_* kernel
     std::vector<ambc_host_chunk> host;
     uint64_t total = 0;
     uint64_t scratch = 0;
@@ -588,6 +593,7 @@ void walk_body(const uint8_t* body, uint64_t blen, uint64_t orig_size, const uin
         if (t == 0) break;
         if (pos + clen > blen) break;
         DecJob j{};
+        int kind = DEC_KIND_HEAVY;
         j.body_off = pos;
         j.clen = clen;
         j.orig = orig;
@@ -596,11 +602,14 @@ void walk_body(const uint8_t* body, uint64_t blen, uint64_t orig_size, const uin
         uint64_t expect;
         if (!registered_id(reg, t)) {
             j.type = DEC_VERBATIM;
+            kind = DEC_KIND_LIGHT;
             expect = clen;
         } else if (t == 5 || t == 6 || t == 7) {
             j.type = DEC_SKIP;
+            kind = DEC_KIND_LIGHT;
             expect = clen ? orig : 0;
         } else {
+            if (t == 255 || t == 1 || t == 4) kind = DEC_KIND_LIGHT;
             j.type = t;
             switch (t) {
             case 255: expect = orig; break;
@@ -610,6 +619,9 @@ void walk_body(const uint8_t* body, uint64_t blen, uint64_t orig_size, const uin
             if (t == 9 && clen) {
                 const uint64_t cb = lz4_content_bound(body + pos, clen);
                 if (cb > STAGE_DEC) { j.scratch_off = w.scratch; j.scratch_cap = cb; w.scratch += (cb + 15) & ~15ull; }
+                // dec_lz4_par's domain: small output, 15-bit payload indices, no content checksum
+                else if (clen >= 7 && clen <= 0x7FFF && !((body[pos + 4] >> 2) & 1))
+                    kind = cb <= 4096 ? DEC_KIND_LZ4_4K : DEC_KIND_LZ4_8K;
             }
             if (t == 2 && clen && (uint64_t)orig + 256 > STAGE_DEC) {
                 j.scratch_off = w.scratch; j.scratch_cap = (uint64_t)orig + 256;
@@ -625,6 +637,7 @@ void walk_body(const uint8_t* body, uint64_t blen, uint64_t orig_size, const uin
             w.host.push_back(h);
         }
         w.jobs.push_back(j);
+        w.kind.push_back((uint8_t)kind);
         w.src_index.push_back(ord);
         out += expect;
         pos += clen;
@@ -662,7 +675,19 @@ static int decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t or
         HIPCHK(d.jobs.ensure((size_t)std::max<uint32_t>(nj, 1) * sizeof(DecJob)));
         HIPCHK(d.produced.ensure((size_t)std::max<uint32_t>(nj, 1) * 4));
         HIPCHK(d.scratch.ensure(w.scratch + 64));
+        // job lists per decode kernel, concatenated
+        std::vector<uint32_t> lists(nj);
+        uint32_t cnt[DEC_KINDS] = {0}, base[DEC_KINDS + 1] = {0};
+        for (uint32_t i = 0; i < nj; i++) cnt[w.kind[i]]++;
+        for (int k = 0; k < DEC_KINDS; k++) base[k + 1] = base[k] + cnt[k];
+        {
+            uint32_t fill[DEC_KINDS];
+            for (int k = 0; k < DEC_KINDS; k++) fill[k] = base[k];
+            for (uint32_t i = 0; i < nj; i++) lists[fill[w.kind[i]]++] = i;
+        }
+        HIPCHK(d.list.ensure((size_t)std::max<uint32_t>(nj, 1) * 4));
         if (nj) HIPCHK(hipMemcpyAsync(d.jobs.p, w.jobs.data(), nj * sizeof(DecJob), hipMemcpyHostToDevice, s));
+        if (nj) HIPCHK(hipMemcpyAsync(d.list.p, lists.data(), nj * 4, hipMemcpyHostToDevice, s));
         if (w.total < orig_size) HIPCHK(hipMemsetAsync(d.dout.as<uint8_t>() + w.total, 0, orig_size - w.total, s));
         DecArgs a{};
         a.body = d.body.as<uint8_t>();
@@ -672,9 +697,37 @@ static int decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t or
         a.n_jobs = nj;
         a.scratch = d.scratch.as<uint8_t>();
         a.produced = d.produced.as<uint32_t>();
+        if (getenv("AMBC_STAMPS") && nj) {
+            HIPCHK(d.seg.ensure((size_t)nj * 64));
+            HIPCHK(hipMemsetAsync(d.seg.p, 0, (size_t)nj * 64, s));
+            a.stamps = d.seg.as<unsigned long long>();
+        }
         HIPCHK(hipEventRecord(d.ev[0], s));
-        HIPCHK(launch_decode(a, s));
+        for (int k = 0; k < DEC_KINDS; k++) {
+            a.list = d.list.as<uint32_t>() + base[k];
+            a.n_list = cnt[k];
+            HIPCHK(launch_decode(k, a, s));
+        }
         HIPCHK(hipEventRecord(d.ev[1], s));
+        if (a.stamps) {
+            std::vector<unsigned long long> sv((size_t)nj * 8);
+            HIPCHK(hipMemcpyAsync(sv.data(), d.seg.p, (size_t)nj * 64, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            double sum[8] = {0};
+            uint64_t cnt = 0, tagged[16] = {0};
+            for (uint32_t i = 0; i < nj; i++) {
+                tagged[sv[i * 8 + 7] & 15]++;
+                if (sv[i * 8 + 7] != 9) continue;
+                cnt++;
+                for (int q = 0; q < 7; q++) sum[q] += (double)sv[i * 8 + q];
+            }
+            fprintf(stderr, "[ambc stamps] jobs=%u tagged9=%llu untagged=%llu\n", nj,
+                    (unsigned long long)tagged[9], (unsigned long long)tagged[0]);
+            if (cnt)
+                fprintf(stderr, "[ambc stamps] lz4 jobs=%llu cycles/job: pin %.0f parse %.0f resolve %.0f "
+                        "gather %.0f passes %.2f\n", (unsigned long long)cnt, sum[0] / cnt, sum[1] / cnt,
+                        sum[2] / cnt, sum[3] / cnt, sum[6] / cnt);
+        }
         std::vector<uint32_t> prod(nj);
         if (nj) HIPCHK(hipMemcpyAsync(prod.data(), d.produced.p, nj * 4, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));

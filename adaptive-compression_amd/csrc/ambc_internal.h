@@ -65,7 +65,14 @@ struct DecArgs {
     uint32_t n_jobs;
     uint8_t* scratch;
     uint32_t* produced;     // actual produced bytes per job
+    unsigned long long* stamps;  // diagnostic build (-DAMBC_STAMPS): per-job phase cycles
+    const uint32_t* list;   // job indices this launch decodes (nullptr = 0..n_jobs-1)
+    uint32_t n_list;
 };
+
+// decode kernels by LDS footprint (host routes each job to one of them)
+enum : int { DEC_KIND_LIGHT = 0, DEC_KIND_LZ4_4K = 1, DEC_KIND_LZ4_8K = 2, DEC_KIND_HEAVY = 3,
+             DEC_KINDS = 4 };
 
 constexpr uint32_t DEC_VERBATIM = 256;
 constexpr uint32_t DEC_SKIP = 257;
@@ -79,7 +86,7 @@ hipError_t launch_stats(const uint8_t* ids, const uint32_t* plen, uint32_t n_chu
 hipError_t scan_sizes(const uint64_t* sizes, uint64_t* off, uint32_t count, void* tmp,
                       size_t* tmp_bytes, hipStream_t s);
 hipError_t launch_copy(uint8_t* dst, const uint8_t* src, uint64_t len, hipStream_t s);
-hipError_t launch_decode(const DecArgs& a, hipStream_t s);
+hipError_t launch_decode(int kind, const DecArgs& a, hipStream_t s);
 hipError_t launch_synth(uint8_t* out, uint64_t n, const uint64_t* seg, uint32_t nseg,
                         uint64_t seed, hipStream_t s);
 

@@ -172,6 +172,7 @@ def main():
         body_total = float(body_len)
 
     verified = None
+    decode = None
     if not args.no_verify and rank == 0:
         # bit-exact round trip of the last step's body (outside the timed region)
         body_host = d_out[:body_len if world == 1 else body_len].cpu().numpy().tobytes()
@@ -179,9 +180,16 @@ def main():
             body_host += b"\xff\xff" + b"\x00" * 14
         from ambc import AdaptiveCompressor
         comp = AdaptiveCompressor(chunk_size=args.chunk, mode=args.mode, methods=methods)
+        t = time.perf_counter()
         back = comp._adaptive_decompress(body_host, n)
+        dwall = time.perf_counter() - t
         verified = back == d_in.cpu().numpy().tobytes()
-        log(f"round trip bit-exact: {verified}")
+        ds = comp._last_device_stats
+        decode = {"kernel_ms": round(ds.kernel_ns / 1e6, 3), "header_walk_ms": round(ds.walk_ns / 1e6, 3),
+                  "h2d_ms": round(ds.h2d_ns / 1e6, 3), "d2h_ms": round(ds.d2h_ns / 1e6, 3),
+                  "kernel_GBps": round(n / max(ds.kernel_ns, 1), 3),
+                  "host_api_GBps": round(n / dwall / 1e9, 3)}
+        log(f"round trip bit-exact: {verified}; decode {decode}")
 
     result = None
     if rank == 0:
@@ -201,7 +209,7 @@ def main():
                        "mode": args.mode, "methods": methods, "seed": args.seed,
                        "ratio": round(body_total / (n * world), 5),
                        "parallelism": f"chunk-shard dp{world}" if world > 1 else "single GPU",
-                       "round_trip_bit_exact": verified},
+                       "round_trip_bit_exact": verified, "decode": decode},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,

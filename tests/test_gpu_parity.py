@@ -251,3 +251,71 @@ def test_device_synth_matches_host(ctx):
     finally:
         ctx.lib.ambc_device_free(ctx.h, 0, d)
     assert bytes(got) == orc.synth(n, 99)
+
+
+# ---------------------------------------------------------------------------
+# LZ4 frames written by the system liblz4 (LZ4F_compressFrame), i.e. not by
+# this project's encoder: every frame option the decoder accepts, plus damaged
+# frames, decoded by the GPU through the plugin API and checked against the
+# oracle's decoder (advanced_compression.py:283-296 semantics: invalid -> the
+# chunk decodes to zeros; short/long content is padded/truncated)
+# ---------------------------------------------------------------------------
+class _FrameInfo(C.Structure):
+    _fields_ = [("blockSizeID", C.c_int), ("blockMode", C.c_int), ("contentChecksumFlag", C.c_int),
+                ("frameType", C.c_int), ("contentSize", C.c_ulonglong), ("dictID", C.c_uint),
+                ("blockChecksumFlag", C.c_int)]
+
+
+class _Prefs(C.Structure):
+    _fields_ = [("frameInfo", _FrameInfo), ("compressionLevel", C.c_int), ("autoFlush", C.c_uint),
+                ("favorDecSpeed", C.c_uint), ("reserved", C.c_uint * 3)]
+
+
+def _lz4f(data, bsid=4, linked=False, cck=False, bck=False, csize=True, level=0):
+    try:
+        lz = C.CDLL("liblz4.so.1")
+    except OSError:
+        pytest.skip("system liblz4 not present")
+    lz.LZ4F_compressFrameBound.restype = C.c_size_t
+    lz.LZ4F_compressFrameBound.argtypes = [C.c_size_t, C.c_void_p]
+    lz.LZ4F_compressFrame.restype = C.c_size_t
+    lz.LZ4F_compressFrame.argtypes = [C.c_void_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_void_p]
+    pr = _Prefs()
+    pr.frameInfo.blockSizeID = bsid
+    pr.frameInfo.blockMode = 0 if linked else 1
+    pr.frameInfo.contentChecksumFlag = int(cck)
+    pr.frameInfo.blockChecksumFlag = int(bck)
+    pr.frameInfo.contentSize = len(data) if csize else 0
+    pr.compressionLevel = level
+    cap = lz.LZ4F_compressFrameBound(len(data), C.byref(pr))
+    out = C.create_string_buffer(cap)
+    r = lz.LZ4F_compressFrame(out, cap, data, len(data), C.byref(pr))
+    assert r < cap
+    return out.raw[:r]
+
+
+def test_lz4_external_frames(ctx):
+    from ambc.methods import LZ4Compression
+    lz4 = LZ4Compression()
+    mixed = synth.generate(1 << 20, 21)
+    datas = [mixed[:4096], mixed[200000:208192], bytes(5000), b"xyz" * 1000, os.urandom(2000),
+             mixed[300000:300000 + 70000], mixed[600000:600000 + 200000], b"", b"q"]
+    rng = random.Random(5)
+    n_checked = 0
+    for d in datas:
+        for opts in ({}, {"linked": True}, {"cck": True}, {"bck": True}, {"csize": False},
+                     {"level": 9}, {"linked": True, "cck": True, "bck": True, "level": 12},
+                     {"bsid": 5}, {"bsid": 7, "cck": True}):
+            fr = _lz4f(d, **opts)
+            for orig in sorted({len(d), len(d) + 7, max(0, len(d) - 3)}):
+                want = orc.decode_chunk(9, fr, orig)
+                assert want[:min(orig, len(d))] == d[:orig]
+                assert lz4.decompress(fr, orig) == want, (len(d), opts, orig)
+                n_checked += 1
+            # damaged copies: flipped bytes anywhere in the frame
+            for _ in range(4):
+                bad = bytearray(fr)
+                bad[rng.randrange(len(bad))] ^= 1 << rng.randrange(8)
+                assert lz4.decompress(bytes(bad), len(d)) == orc.decode_chunk(9, bytes(bad), len(d))
+                n_checked += 1
+    assert n_checked > 200
