@@ -40,11 +40,24 @@ constexpr uint32_t LUT_BITS = 10;
     unsigned long long* _stp = A.stamps ? A.stamps + (uint64_t)blockIdx.x * 8 : nullptr;
 #define DSTAMP_PARAMS , unsigned long long* _stp, uint64_t& _st_t
 #define DSTAMP_ARGS , _stp, _st_t
+// accumulate into register sums (inside loops), flushed with DACC_FLUSH
+#define DACC(ph)                                                \
+    do {                                                        \
+        __builtin_amdgcn_s_waitcnt(0xC07F);                     \
+        const uint64_t _t = __builtin_amdgcn_s_memtime();       \
+        _acc[ph] += _t - _st_t;                                 \
+        _st_t = _t;                                             \
+    } while (0)
+#define DACC_PARAMS , uint64_t* _acc, uint64_t& _st_t
+#define DACC_ARGS , _acc, _st_t
 #else
 #define DSTAMP(ph) do {} while (0)
 #define DSTAMP_DECL
 #define DSTAMP_PARAMS
 #define DSTAMP_ARGS
+#define DACC(ph) do {} while (0)
+#define DACC_PARAMS
+#define DACC_ARGS
 #endif
 
 constexpr uint32_t SRC_LIT = 0x8000;  // LZ4 source map: payload byte (else earlier output byte)
@@ -461,11 +474,11 @@ __device__ __forceinline__ uint32_t win_byte(ByteWin& W, const uint8_t* g, uint3
     return __builtin_amdgcn_readfirstlane((readlane(W.v, r >> 2) >> ((r & 3) * 8)) & 0xFF);
 }
 
-// One sequence of an LZ4 block read speculatively from payload index x (token
-// byte tok), with dec_lz4's bounds checks: literal start y, literal length L,
-// offset position z, match length ml; returns the next token's index, TOK_END
-// (the literals reach the block end: last sequence) or TOK_ERR.
-constexpr uint32_t TOK_END = 0xFFFF, TOK_ERR = 0xFFFE;
+// One sequence of an LZ4 block parsed from payload index x (token byte tok),
+// with dec_lz4's bounds checks: literal start y, literal length L, offset
+// position z, match length ml.  Returns the next token's index, TOK_END (the
+// literals reach the block end: last sequence) or TOK_ERR.
+constexpr uint32_t TOK_END = 0xFFFFFFFFu, TOK_ERR = 0xFFFFFFFEu, TOK_SLOW = 0xFFFFFFFDu;
 
 __device__ __forceinline__ uint32_t seq_parse(const uint8_t* g, uint32_t x, uint32_t tok, uint32_t end,
                                               uint32_t& y, uint32_t& L, uint32_t& z, uint32_t& ml) {
@@ -487,6 +500,18 @@ __device__ __forceinline__ uint32_t seq_parse(const uint8_t* g, uint32_t x, uint
     }
     ml += 4;
     return w;
+}
+
+// the same without length-extension bytes (TOK_SLOW when the token has any)
+__device__ __forceinline__ uint32_t seq_next_fast(uint32_t x, uint32_t tok, uint32_t end) {
+    const uint32_t L = tok >> 4;
+    if (L == 15) return TOK_SLOW;
+    const uint32_t z = x + 1 + L;
+    if (z > end) return TOK_ERR;
+    if (z == end) return TOK_END;
+    if (z + 2 > end) return TOK_ERR;
+    if ((tok & 15) == 15) return TOK_SLOW;
+    return z + 2;
 }
 
 // source-map entries of one sequence (o = output index of its first literal).
@@ -519,108 +544,119 @@ __device__ __forceinline__ void seq_write_wave(uint16_t* src, uint32_t o, uint32
     }
 }
 
-// One compressed block [hp, end) of a frame: the wave reads 256 payload bytes
-// at a time; every lane parses the 4 positions it holds as if a sequence began
-// there, the scalar unit then follows the real token chain through the window
-// (one v_readlane per sequence), and the marked sequences are laid out in
-// parallel (wave prefix sum of their output lengths).  Returns the output
-// index after the block or -1.
+// One compressed block [hp, end) of a frame, 256 payload positions at a time
+// (lane l holds positions wlo + l + 64q, q = 0..3):
+//   1. every lane takes each of its positions as a possible token and computes
+//      where the next token would start (no extension bytes; TOK_SLOW if any);
+//   2. the scalar unit follows the real token chain through the window, one
+//      v_readlane per sequence, marking chain positions in four 64-bit masks;
+//   3. the marked sequences are decoded in parallel, laid out by wave prefix
+//      sums of their output lengths (in position order), validated, and their
+//      source-map entries written (long ones by the whole wave).
+// Returns the output index after the block or -1.
 constexpr uint32_t SEQ_LONG = 32;
 
-__device__ __forceinline__ int64_t lz4_block_par(const uint8_t* g, uint32_t hp, uint32_t end, uint32_t op, uint32_t lim,
-                                 uint32_t plen, uint16_t* src, uint32_t lane) {
+__device__ __forceinline__ int64_t lz4_block_par(const uint8_t* g, uint32_t hp, uint32_t end, uint32_t op,
+                                                 uint32_t lim, uint32_t plen, uint16_t* src,
+                                                 uint32_t lane DACC_PARAMS) {
     uint32_t x0 = hp;
     for (;;) {
         if (x0 >= end) return -1;  // a token must start inside the block
-        const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(g + x0) & 3);
-        const uint32_t wlo = __builtin_amdgcn_readfirstlane(x0 - mis);
-        const uint32_t* a = reinterpret_cast<const uint32_t*>(g + x0 - mis);
-        const uint32_t wv = (wlo + 4 * lane < plen) ? a[lane] : 0u;
-        uint32_t nx[4];
+        const uint32_t wlo = x0;
+        uint32_t tb[4], nx[4];
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint32_t pos = wlo + 4 * lane + k;
-            uint32_t y, L, z, ml;
-            nx[k] = (pos >= x0 && pos < end) ? seq_parse(g, pos, (wv >> (8 * k)) & 0xFF, end, y, L, z, ml)
-                                             : TOK_ERR;
+        for (int q = 0; q < 4; q++) {
+            const uint32_t pos = wlo + lane + 64 * q;
+            tb[q] = pos < plen ? g[pos] : 0u;
         }
-        const uint32_t nA = nx[0] | nx[1] << 16, nB = nx[2] | nx[3] << 16;
-        // the token chain through this window (scalar)
-        uint64_t mk0 = 0, mk1 = 0, mk2 = 0, mk3 = 0;
-        uint32_t s = x0;
-        bool last = false;
-        for (;;) {
-            const uint32_t r = __builtin_amdgcn_readfirstlane(s - wlo);
-            if (r >= 256) break;
-            const uint64_t bit = 1ull << (r & 63);
-            const uint32_t q = r >> 6;
-            mk0 |= q == 0 ? bit : 0;
-            mk1 |= q == 1 ? bit : 0;
-            mk2 |= q == 2 ? bit : 0;
-            mk3 |= q == 3 ? bit : 0;
-            const uint32_t v = readlane((r & 2) ? nB : nA, r >> 2);
-            const uint32_t t = (r & 1) ? v >> 16 : v & 0xFFFF;
-            if (t == TOK_ERR) return -1;
-            if (t == TOK_END) { last = true; break; }
-            s = t;
-            if (s >= end) return -1;  // the block cannot end right after a match
-        }
-        // the marked sequences this lane holds
-        const uint64_t mw = lane < 16 ? mk0 : lane < 32 ? mk1 : lane < 48 ? mk2 : mk3;
-        const uint32_t bits = (uint32_t)(mw >> ((lane & 15) * 4)) & 15;
-        uint32_t ky[4], kL[4], koff[4], kml[4], ko[4];
-        uint32_t tot = 0;
-        bool lng = false;
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            ky[k] = kL[k] = koff[k] = kml[k] = 0;
-            if ((bits >> k) & 1) {
-                const uint32_t pos = wlo + 4 * lane + k;
-                uint32_t y, L, z, ml = 0;
-                const uint32_t nt = seq_parse(g, pos, (wv >> (8 * k)) & 0xFF, end, y, L, z, ml);
-                ky[k] = y;
-                kL[k] = L;
-                if (nt != TOK_END) { koff[k] = (uint32_t)g[z] | (uint32_t)g[z + 1] << 8; kml[k] = ml; }
-                tot += L + kml[k];
-                lng |= L > SEQ_LONG || kml[k] > SEQ_LONG;
+        for (int q = 0; q < 4; q++) {
+            const uint32_t pos = wlo + lane + 64 * q;
+            nx[q] = pos < end ? seq_next_fast(pos, tb[q], end) : TOK_ERR;
+        }
+        DACC(0);
+        // the token chain through this window (scalar): the inner loop is one
+        // v_readlane and a compare per sequence; tokens with extension bytes,
+        // the last sequence and errors leave it (all codes are >= end)
+        uint64_t mk[4] = {0, 0, 0, 0};
+        uint32_t s = x0, st = 0;  // st: 0 walking, 1 last sequence, 2 invalid
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            while (st == 0) {
+                const uint32_t lim_r = 64u * (q + 1);
+                if (s - wlo >= lim_r) break;  // on to the next 64 positions
+                uint64_t m = 0;
+                uint32_t cur = s, t;
+                const uint32_t climit = min(end, wlo + lim_r);  // codes are all >= end
+                do {  // single-exit loop: keeps the scalar code branch-light
+                    const uint32_t r = cur - wlo;
+                    m |= 1ull << (r & 63);
+                    t = readlane(nx[q], r & 63);
+                    s = cur;
+                    cur = t;
+                } while (t < climit);
+                mk[q] |= m;
+                if (t < end) { s = t; break; }
+                if (t == TOK_SLOW) {
+                    uint32_t y, L, z, ml;
+                    t = __builtin_amdgcn_readfirstlane(
+                        seq_parse(g, s, readlane(tb[q], (s - wlo) & 63), end, y, L, z, ml));
+                    if (t < end) { s = t; continue; }
+                }
+                st = t == TOK_END ? 1 : 2;  // TOK_ERR, or a block ending right after a match
+                break;
             }
         }
-        const uint32_t incl = wave_incl_sum(tot);
-        const uint32_t wtot = readlane(incl, 63);
-        uint32_t o = op + incl - tot;
-        bool bad = false;
+        if (st == 2) return -1;
+        DACC(1);
+        // the marked sequences, in position order (q major, lane minor)
+        uint32_t ky[4], kL[4], koff[4], kml[4], ko[4];
+        bool lng = false, bad = false;
+        uint32_t base = op;
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            ko[k] = o;
-            if ((bits >> k) & 1) {
-                if (o + kL[k] > lim) bad = true;
-                o += kL[k];
-                if (kml[k]) {
-                    if (koff[k] == 0 || koff[k] > o || o + kml[k] > lim) bad = true;
-                    o += kml[k];
-                }
+        for (int q = 0; q < 4; q++) {
+            ky[q] = kL[q] = koff[q] = kml[q] = 0;
+            uint32_t tot = 0;
+            if ((mk[q] >> lane) & 1) {
+                const uint32_t pos = wlo + lane + 64 * q;
+                uint32_t y, L, z, ml = 0;
+                const uint32_t nt = seq_parse(g, pos, tb[q], end, y, L, z, ml);
+                ky[q] = y;
+                kL[q] = L;
+                if (nt != TOK_END) { koff[q] = (uint32_t)g[z] | (uint32_t)g[z + 1] << 8; kml[q] = ml; }
+                tot = L + kml[q];
+                lng |= L > SEQ_LONG || kml[q] > SEQ_LONG;
+            }
+            const uint32_t incl = wave_incl_sum(tot);
+            ko[q] = base + incl - tot;
+            base += readlane(incl, 63);
+            if ((mk[q] >> lane) & 1) {
+                const uint32_t o = ko[q] + kL[q];
+                if (o > lim) bad = true;
+                if (kml[q] && (koff[q] == 0 || koff[q] > o || o + kml[q] > lim)) bad = true;
             }
         }
         if (__any(bad)) return -1;
+        DACC(2);
         if (!lng) {
 #pragma unroll
-            for (int k = 0; k < 4; k++)
-                if ((bits >> k) & 1) seq_write_lane(src, ko[k], ky[k], kL[k], koff[k], kml[k]);
+            for (int q = 0; q < 4; q++)
+                if ((mk[q] >> lane) & 1) seq_write_lane(src, ko[q], ky[q], kL[q], koff[q], kml[q]);
         }
         // lanes holding a long sequence: written by the whole wave, one lane at a time
         uint64_t lm = __ballot(lng);
         while (lm) {
             const uint32_t l = (uint32_t)__builtin_ctzll(lm);
             lm &= lm - 1;
-            const uint32_t lb = readlane(bits, l);
 #pragma unroll
-            for (int k = 0; k < 4; k++)
-                if ((lb >> k) & 1)
-                    seq_write_wave(src, readlane(ko[k], l), readlane(ky[k], l), readlane(kL[k], l),
-                                   readlane(koff[k], l), readlane(kml[k], l), lane);
+            for (int q = 0; q < 4; q++)
+                if ((mk[q] >> l) & 1)
+                    seq_write_wave(src, readlane(ko[q], l), readlane(ky[q], l), readlane(kL[q], l),
+                                   readlane(koff[q], l), readlane(kml[q], l), lane);
         }
-        op += wtot;
-        if (last) return (int64_t)op;
+        DACC(3);
+        op = base;
+        if (st == 1) return (int64_t)op;
         x0 = s;
     }
 }
@@ -628,6 +664,9 @@ __device__ __forceinline__ int64_t lz4_block_par(const uint8_t* g, uint32_t hp, 
 __device__ __forceinline__ int64_t dec_lz4_par(const uint8_t* p, uint32_t plen, uint16_t* src, uint32_t cap,
                                uint32_t lane DSTAMP_PARAMS) {
     if (plen > 0x7FFF || plen < 7) return -2;
+#ifdef AMBC_STAMPS
+    uint64_t _acc[4] = {0, 0, 0, 0};
+#endif
     ByteWin W;
     win_load(W, p, 0, plen, lane);
     auto B = [&](uint32_t i) { return win_byte(W, p, i, plen, lane); };
@@ -666,7 +705,7 @@ __device__ __forceinline__ int64_t dec_lz4_par(const uint8_t* p, uint32_t plen, 
             op += sz;
         } else {
             const uint64_t lim = min((uint64_t)op + bmax, (uint64_t)cap);
-            const int64_t r = lz4_block_par(p, hp, hp + sz, op, (uint32_t)lim, plen, src, lane);
+            const int64_t r = lz4_block_par(p, hp, hp + sz, op, (uint32_t)lim, plen, src, lane DACC_ARGS);
             if (r < 0) return -1;
             op = (uint32_t)r;
         }
@@ -680,6 +719,9 @@ __device__ __forceinline__ int64_t dec_lz4_par(const uint8_t* p, uint32_t plen, 
     if (has_cs && op != csize) return -1;
     wave_sync();
     DSTAMP(1);
+#ifdef AMBC_STAMPS
+    if (lane == 0 && _stp) { _stp[1] = _acc[0]; _stp[2] = _acc[1]; _stp[3] = _acc[2]; _stp[4] = _acc[3]; }
+#endif
     uint32_t passes = 0;
     (void)passes;
     // pointer jumping: every pass at least doubles the distance each entry skips
@@ -701,10 +743,7 @@ __device__ __forceinline__ int64_t dec_lz4_par(const uint8_t* p, uint32_t plen, 
         passes++;
         if (!__any(more)) break;
     }
-    DSTAMP(2);
-#ifdef AMBC_STAMPS
-    if (lane == 0 && _stp) _stp[6] = passes;
-#endif
+    DSTAMP(5);
     return (int64_t)op;
 }
 
@@ -830,7 +869,7 @@ __global__ __launch_bounds__(64) void k_decode_lz4(DecArgs A) {
         lz4_gather(out, g, src, m, lane);
         wave_zero(out + m, orig - m, lane);
     }
-    DSTAMP(3);
+    DSTAMP(6);
 #ifdef AMBC_STAMPS
     if (lane == 0 && _stp) _stp[7] = 9;
 #endif

@@ -724,9 +724,10 @@ static int decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t or
             fprintf(stderr, "[ambc stamps] jobs=%u tagged9=%llu untagged=%llu\n", nj,
                     (unsigned long long)tagged[9], (unsigned long long)tagged[0]);
             if (cnt)
-                fprintf(stderr, "[ambc stamps] lz4 jobs=%llu cycles/job: pin %.0f parse %.0f resolve %.0f "
-                        "gather %.0f passes %.2f\n", (unsigned long long)cnt, sum[0] / cnt, sum[1] / cnt,
-                        sum[2] / cnt, sum[3] / cnt, sum[6] / cnt);
+                fprintf(stderr, "[ambc stamps] lz4 jobs=%llu cycles/job: pre %.0f spec %.0f chain %.0f "
+                        "seqs %.0f writes %.0f resolve %.0f gather %.0f\n", (unsigned long long)cnt,
+                        sum[0] / cnt, sum[1] / cnt, sum[2] / cnt, sum[3] / cnt, sum[4] / cnt, sum[5] / cnt,
+                        sum[6] / cnt);
         }
         std::vector<uint32_t> prod(nj);
         if (nj) HIPCHK(hipMemcpyAsync(prod.data(), d.produced.p, nj * 4, hipMemcpyDeviceToHost, s));
