@@ -60,7 +60,10 @@ constexpr uint32_t LUT_BITS = 10;
 #define DACC_ARGS
 #endif
 
-constexpr uint32_t SRC_LIT = 0x8000;  // LZ4 source map: payload byte (else earlier output byte)
+// LZ4 source map entry flag: payload byte (else an earlier output byte)
+template <typename T> struct SrcLit;
+template <> struct SrcLit<uint16_t> { static constexpr uint32_t v = 0x8000u; };      // LDS maps
+template <> struct SrcLit<uint32_t> { static constexpr uint32_t v = 0x80000000u; };  // global maps
 
 struct DecSmem {
     alignas(16) uint8_t pin[PIN + 64];
@@ -517,21 +520,23 @@ __device__ __forceinline__ uint32_t seq_next_fast(uint32_t x, uint32_t tok, uint
 // source-map entries of one sequence (o = output index of its first literal).
 // Overlapping matches (off < ml) point into the period before the match, so no
 // entry's source chain grows with the match length.
-__device__ __forceinline__ void seq_write_lane(uint16_t* src, uint32_t o, uint32_t y, uint32_t L,
+template <typename T>
+__device__ __forceinline__ void seq_write_lane(T* src, uint32_t o, uint32_t y, uint32_t L,
                                                uint32_t off, uint32_t ml) {
-    for (uint32_t t = 0; t < L; t++) src[o + t] = (uint16_t)(SRC_LIT | (y + t));
+    for (uint32_t t = 0; t < L; t++) src[o + t] = (T)(SrcLit<T>::v | (y + t));
     const uint32_t m0 = o + L - off;
     uint32_t c = 0;
     for (uint32_t t = 0; t < ml; t++) {
-        src[o + L + t] = (uint16_t)(m0 + c);
+        src[o + L + t] = (T)(m0 + c);
         if (++c == off) c = 0;
     }
 }
 
-__device__ __forceinline__ void seq_write_wave(uint16_t* src, uint32_t o, uint32_t y, uint32_t L,
+template <typename T>
+__device__ __forceinline__ void seq_write_wave(T* src, uint32_t o, uint32_t y, uint32_t L,
                                                uint32_t off, uint32_t ml, uint32_t lane) {
     for (uint32_t b = 0; b < L; b += 64)
-        if (b + lane < L) src[o + b + lane] = (uint16_t)(SRC_LIT | (y + b + lane));
+        if (b + lane < L) src[o + b + lane] = (T)(SrcLit<T>::v | (y + b + lane));
     if (ml == 0) return;
     const uint32_t m0 = o + L - off;
     const uint32_t lmod = lane % off;   // (b + lane) % off = (b % off + lane % off) mod off
@@ -539,7 +544,7 @@ __device__ __forceinline__ void seq_write_wave(uint16_t* src, uint32_t o, uint32
     for (uint32_t b = 0; b < ml; b += 64) {
         uint32_t c = bmod + lmod;
         if (c >= off) c -= off;
-        if (b + lane < ml) src[o + L + b + lane] = (uint16_t)(m0 + c);
+        if (b + lane < ml) src[o + L + b + lane] = (T)(m0 + c);
         bmod = (bmod + 64) % off;
     }
 }
@@ -556,8 +561,9 @@ __device__ __forceinline__ void seq_write_wave(uint16_t* src, uint32_t o, uint32
 // Returns the output index after the block or -1.
 constexpr uint32_t SEQ_LONG = 32;
 
+template <typename T>
 __device__ __forceinline__ int64_t lz4_block_par(const uint8_t* g, uint32_t hp, uint32_t end, uint32_t op,
-                                                 uint32_t lim, uint32_t plen, uint16_t* src,
+                                                 uint32_t lim, uint32_t plen, T* src,
                                                  uint32_t lane DACC_PARAMS) {
     uint32_t x0 = hp;
     for (;;) {
@@ -661,9 +667,11 @@ __device__ __forceinline__ int64_t lz4_block_par(const uint8_t* g, uint32_t hp, 
     }
 }
 
-__device__ __forceinline__ int64_t dec_lz4_par(const uint8_t* p, uint32_t plen, uint16_t* src, uint32_t cap,
+template <typename T>
+__device__ __forceinline__ int64_t dec_lz4_par(const uint8_t* p, uint32_t plen, T* src, uint32_t cap,
                                uint32_t lane DSTAMP_PARAMS) {
-    if (plen > 0x7FFF || plen < 7) return -2;
+    constexpr uint32_t SRC_LIT = SrcLit<T>::v;
+    if (plen >= SRC_LIT || cap > SRC_LIT || plen < 7) return -2;
 #ifdef AMBC_STAMPS
     uint64_t _acc[4] = {0, 0, 0, 0};
 #endif
@@ -701,7 +709,7 @@ __device__ __forceinline__ int64_t dec_lz4_par(const uint8_t* p, uint32_t plen, 
         if (sz > bmax || (uint64_t)hp + sz > plen) return -1;
         if (bs & 0x80000000u) {
             if ((uint64_t)op + sz > cap) return -1;
-            for (uint32_t t = lane; t < sz; t += 64) src[op + t] = (uint16_t)(SRC_LIT | (hp + t));
+            for (uint32_t t = lane; t < sz; t += 64) src[op + t] = (T)(SRC_LIT | (hp + t));
             op += sz;
         } else {
             const uint64_t lim = min((uint64_t)op + bmax, (uint64_t)cap);
@@ -735,7 +743,7 @@ __device__ __forceinline__ int64_t dec_lz4_par(const uint8_t* p, uint32_t plen, 
             for (int k = 0; k < 4; k++)
                 if (!(v[k] & SRC_LIT)) {
                     v[k] = src[v[k]];
-                    src[q0 + k] = (uint16_t)v[k];
+                    src[q0 + k] = (T)v[k];
                     more |= !(v[k] & SRC_LIT);
                 }
         }
@@ -748,18 +756,19 @@ __device__ __forceinline__ int64_t dec_lz4_par(const uint8_t* p, uint32_t plen, 
 }
 
 // out[0, m) = payload bytes named by the resolved source map
-__device__ void lz4_gather(uint8_t* out, const uint8_t* p, const uint16_t* src, uint32_t m,
-                           uint32_t lane) {
+template <typename T>
+__device__ void lz4_gather(uint8_t* out, const uint8_t* p, const T* src, uint32_t m, uint32_t lane) {
+    constexpr uint32_t MSK = SrcLit<T>::v - 1;
     const uint32_t head = min((uint32_t)((4 - (reinterpret_cast<uintptr_t>(out) & 3)) & 3), m);
-    if (lane < head) out[lane] = p[src[lane] & 0x7FFF];
+    if (lane < head) out[lane] = p[src[lane] & MSK];
     const uint32_t nw = (m - head) >> 2;
     uint32_t* o32 = reinterpret_cast<uint32_t*>(out + head);
     for (uint32_t w = lane; w < nw; w += 64) {
         const uint32_t q = head + 4 * w;
-        o32[w] = (uint32_t)p[src[q] & 0x7FFF] | (uint32_t)p[src[q + 1] & 0x7FFF] << 8 |
-                 (uint32_t)p[src[q + 2] & 0x7FFF] << 16 | (uint32_t)p[src[q + 3] & 0x7FFF] << 24;
+        o32[w] = (uint32_t)p[src[q] & MSK] | (uint32_t)p[src[q + 1] & MSK] << 8 |
+                 (uint32_t)p[src[q + 2] & MSK] << 16 | (uint32_t)p[src[q + 3] & MSK] << 24;
     }
-    for (uint32_t i = head + (nw << 2) + lane; i < m; i += 64) out[i] = p[src[i] & 0x7FFF];
+    for (uint32_t i = head + (nw << 2) + lane; i < m; i += 64) out[i] = p[src[i] & MSK];
 }
 
 // Dictionary (id 2): serial by lane 0 (back-references into its own output)
@@ -847,20 +856,19 @@ __global__ __launch_bounds__(64) void k_decode_light(DecArgs A) {
     put_produced(A, j, produced, lane);
 }
 
-// LZ4 frames the host routed here: content bound <= OUTMAX, payload < 32 KiB,
-// no content checksum -- so dec_lz4_par never asks for the serial decoder
-template <uint32_t OUTMAX>
-__global__ __launch_bounds__(64) void k_decode_lz4(DecArgs A) {
-    __shared__ uint16_t src[OUTMAX];
-    const uint32_t lane = threadIdx.x;
+// LZ4 frames the host routed here: no content checksum, content bound <=
+// OUTMAX and payload < 32 KiB (LDS source map of u16), or any size with the
+// map in the job's device scratch window (u32 entries, k_decode_lz4_g) -- so
+// dec_lz4_par never asks for the serial decoder
+template <typename T>
+__device__ __forceinline__ void lz4_job(const DecArgs& A, uint32_t j, const DecJob& J, T* src, uint32_t cap,
+                                        uint32_t lane) {
     DSTAMP_DECL
-    const uint32_t j = job_index(A);
-    const DecJob J = A.jobs[j];
     const uint8_t* g = A.body + J.body_off;
     uint8_t* out = A.out + J.out_off;
     const uint32_t orig = J.orig;
     DSTAMP(0);
-    const int64_t r = dec_lz4_par(g, J.clen, src, OUTMAX, lane DSTAMP_ARGS);
+    const int64_t r = dec_lz4_par(g, J.clen, src, cap, lane DSTAMP_ARGS);
     wave_sync();
     if (r < 0) {
         wave_zero(out, orig, lane);
@@ -874,6 +882,21 @@ __global__ __launch_bounds__(64) void k_decode_lz4(DecArgs A) {
     if (lane == 0 && _stp) _stp[7] = 9;
 #endif
     put_produced(A, j, r == -2 ? -1 : (int64_t)orig, lane);
+}
+
+template <uint32_t OUTMAX>
+__global__ __launch_bounds__(64) void k_decode_lz4(DecArgs A) {
+    __shared__ uint16_t src[OUTMAX];
+    const uint32_t j = job_index(A);
+    const DecJob J = A.jobs[j];
+    lz4_job(A, j, J, src, OUTMAX, threadIdx.x);
+}
+
+__global__ __launch_bounds__(64) void k_decode_lz4_g(DecArgs A) {
+    const uint32_t j = job_index(A);
+    const DecJob J = A.jobs[j];
+    lz4_job(A, j, J, reinterpret_cast<uint32_t*>(A.scratch + J.scratch_off), (uint32_t)J.scratch_cap,
+            threadIdx.x);
 }
 
 // everything else: Huffman, Dictionary, LZ4 frames that need the serial decoder
@@ -957,6 +980,8 @@ hipError_t launch_decode(int kind, const DecArgs& a, hipStream_t s) {
     case DEC_KIND_LIGHT: hipLaunchKernelGGL(k_decode_light, dim3(a.n_list), dim3(64), 0, s, a); break;
     case DEC_KIND_LZ4_4K: hipLaunchKernelGGL(k_decode_lz4<4096>, dim3(a.n_list), dim3(64), 0, s, a); break;
     case DEC_KIND_LZ4_8K: hipLaunchKernelGGL(k_decode_lz4<8192>, dim3(a.n_list), dim3(64), 0, s, a); break;
+    case DEC_KIND_LZ4_16K: hipLaunchKernelGGL(k_decode_lz4<16384>, dim3(a.n_list), dim3(64), 0, s, a); break;
+    case DEC_KIND_LZ4_G: hipLaunchKernelGGL(k_decode_lz4_g, dim3(a.n_list), dim3(64), 0, s, a); break;
     default: hipLaunchKernelGGL(k_decode, dim3(a.n_list), dim3(64), 0, s, a); break;
     }
     return hipGetLastError();

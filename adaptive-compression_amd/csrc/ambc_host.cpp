@@ -618,10 +618,20 @@ void walk_body(const uint8_t* body, uint64_t blen, uint64_t orig_size, const uin
             }
             if (t == 9 && clen) {
                 const uint64_t cb = lz4_content_bound(body + pos, clen);
-                if (cb > STAGE_DEC) { j.scratch_off = w.scratch; j.scratch_cap = cb; w.scratch += (cb + 15) & ~15ull; }
-                // dec_lz4_par's domain: small output, 15-bit payload indices, no content checksum
-                else if (clen >= 7 && clen <= 0x7FFF && !((body[pos + 4] >> 2) & 1))
-                    kind = cb <= 4096 ? DEC_KIND_LZ4_4K : DEC_KIND_LZ4_8K;
+                if (clen >= 7 && !((body[pos + 4] >> 2) & 1) && cb < 0x80000000ull) {
+                    // dec_lz4_par's domain (no content checksum): LDS source map of u16
+                    // entries for small frames, else a u32 map in device scratch
+                    if (clen <= 0x7FFF && cb <= 16384) {
+                        kind = cb <= 4096 ? DEC_KIND_LZ4_4K : cb <= 8192 ? DEC_KIND_LZ4_8K : DEC_KIND_LZ4_16K;
+                    } else {
+                        kind = DEC_KIND_LZ4_G;
+                        j.scratch_off = w.scratch;
+                        j.scratch_cap = cb;
+                        w.scratch += (4 * cb + 15) & ~15ull;
+                    }
+                } else if (cb > STAGE_DEC) {
+                    j.scratch_off = w.scratch; j.scratch_cap = cb; w.scratch += (cb + 15) & ~15ull;
+                }
             }
             if (t == 2 && clen && (uint64_t)orig + 256 > STAGE_DEC) {
                 j.scratch_off = w.scratch; j.scratch_cap = (uint64_t)orig + 256;

@@ -71,8 +71,8 @@ struct DecArgs {
 };
 
 // decode kernels by LDS footprint (host routes each job to one of them)
-enum : int { DEC_KIND_LIGHT = 0, DEC_KIND_LZ4_4K = 1, DEC_KIND_LZ4_8K = 2, DEC_KIND_HEAVY = 3,
-             DEC_KINDS = 4 };
+enum : int { DEC_KIND_LIGHT = 0, DEC_KIND_LZ4_4K = 1, DEC_KIND_LZ4_8K = 2, DEC_KIND_LZ4_16K = 3,
+             DEC_KIND_LZ4_G = 4, DEC_KIND_HEAVY = 5, DEC_KINDS = 6 };
 
 constexpr uint32_t DEC_VERBATIM = 256;
 constexpr uint32_t DEC_SKIP = 257;
