@@ -74,6 +74,8 @@ struct Dev {
     int id = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev[6] = {};
+    hipStream_t xs[2] = {};     // copy streams of the slab pipeline: H2D, D2H
+    hipEvent_t xev[6] = {};     // h2d_done[2], comp_done[2], d2h_done[2]
     Buf in, out, slots, plen, ids, sizes, off, scan_tmp, acc, ent_full, ent_tail;
     Buf body, jobs, produced, dout, scratch, seg, list;
     uint64_t t_encode = 0, t_scan = 0, t_compact = 0;
@@ -127,6 +129,8 @@ int ambc_init(const int* device_ids, int n_devices, ambc_ctx** out) {
                                            prop.gcnArchName);
         HIPCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
         for (auto& ev : d.ev) HIPCHK(hipEventCreate(&ev));
+        for (auto& x : d.xs) HIPCHK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+        for (auto& ev : d.xev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         ctx->devs.push_back(d);
     }
     *out = ctx.release();
@@ -140,9 +144,11 @@ void ambc_destroy(ambc_ctx* ctx) {
         (void)hipStreamSynchronize(d.stream);
         for (Buf* b : {&d.in, &d.out, &d.slots, &d.plen, &d.ids, &d.sizes, &d.off, &d.scan_tmp,
                        &d.acc, &d.ent_full, &d.ent_tail, &d.body, &d.jobs, &d.produced, &d.dout,
-                       &d.scratch, &d.seg})
+                       &d.scratch, &d.seg, &d.list})
             b->release();
         for (auto& ev : d.ev) (void)hipEventDestroy(ev);
+        for (auto& ev : d.xev) (void)hipEventDestroy(ev);
+        for (auto& x : d.xs) { (void)hipStreamSynchronize(x); (void)hipStreamDestroy(x); }
         (void)hipStreamDestroy(d.stream);
     }
     delete ctx;
@@ -346,6 +352,69 @@ static void add_stats(ambc_stats* a, const ambc_stats& b) {
     a->kernel_ns = std::max(a->kernel_ns, b.kernel_ns);
 }
 
+// Host buffers in, host body out, with the copies overlapped: the input goes up
+// in chunk-aligned slabs on one copy stream while the previous slab is being
+// compressed and the one before that comes back on a second copy stream
+// (double-buffered on the device).  Native mode only: slabs are independent
+// there, so their bodies simply concatenate (the last one carries the end chunk).
+// The overlap needs page-locked host buffers (ambc_host_alloc).
+static constexpr uint64_t kSlabBytes = 256ull << 20;
+
+static int compress_slabs(Dev& d, const uint8_t* in, uint64_t n, const ambc_params* p, uint8_t* out,
+                          uint64_t out_cap, uint64_t* out_len, ambc_stats* st) {
+    const uint64_t t0 = now_ns();
+    const uint32_t C = p->chunk_size;
+    const uint64_t SLAB = std::max<uint64_t>(C, kSlabBytes / C * C);
+    const uint64_t ns = (n + SLAB - 1) / SLAB;
+    const uint64_t sb = ambc_compress_bound(SLAB, C) + 64;
+    HIPCHK(hipSetDevice(d.id));
+    HIPCHK(d.in.ensure(2 * (SLAB + 64)));
+    HIPCHK(d.out.ensure(2 * sb));
+    uint8_t* din[2] = {d.in.as<uint8_t>(), d.in.as<uint8_t>() + SLAB + 64};
+    uint8_t* dout[2] = {d.out.as<uint8_t>(), d.out.as<uint8_t>() + sb};
+    hipEvent_t* h2d_done = d.xev;
+    hipEvent_t* comp_done = d.xev + 2;
+    hipEvent_t* d2h_done = d.xev + 4;
+    auto slab_len = [&](uint64_t k) { return std::min(SLAB, n - k * SLAB); };
+    auto up = [&](uint64_t k) -> int {
+        if (k >= 2) HIPCHK(hipStreamWaitEvent(d.xs[0], comp_done[k & 1], 0));  // din[k&1] free
+        HIPCHK(hipMemcpyAsync(din[k & 1], in + k * SLAB, slab_len(k), hipMemcpyHostToDevice, d.xs[0]));
+        HIPCHK(hipEventRecord(h2d_done[k & 1], d.xs[0]));
+        return AMBC_OK;
+    };
+    ambc_stats tot{};
+    uint64_t o = 0, kern = 0;
+    int rc = up(0);
+    for (uint64_t k = 0; k < ns && rc == AMBC_OK; k++) {
+        if (k + 1 < ns && (rc = up(k + 1)) != AMBC_OK) break;
+        HIPCHK(hipStreamWaitEvent(d.stream, h2d_done[k & 1], 0));
+        if (k >= 2) HIPCHK(hipStreamWaitEvent(d.stream, d2h_done[k & 1], 0));  // dout[k&1] free
+        ambc_params q = *p;
+        if (k + 1 != ns) { q.flags |= AMBC_FLAG_NO_END_CHUNK; q.ent_tail = nullptr; }
+        uint64_t len = 0;
+        ambc_stats s1{};
+        if ((rc = compress_on(d, din[k & 1], slab_len(k), &q, dout[k & 1], sb, &len, &s1)) != AMBC_OK) break;
+        HIPCHK(hipEventRecord(comp_done[k & 1], d.stream));
+        if (o + len > out_cap) { rc = fail(AMBC_E_CAPACITY, "output buffer too small for the body"); break; }
+        HIPCHK(hipStreamWaitEvent(d.xs[1], comp_done[k & 1], 0));
+        HIPCHK(hipMemcpyAsync(out + o, dout[k & 1], len, hipMemcpyDeviceToHost, d.xs[1]));
+        HIPCHK(hipEventRecord(d2h_done[k & 1], d.xs[1]));
+        o += len;
+        kern += s1.kernel_ns;
+        add_stats(&tot, s1);
+    }
+    HIPCHK(hipStreamSynchronize(d.xs[0]));
+    HIPCHK(hipStreamSynchronize(d.xs[1]));
+    if (rc != AMBC_OK) return rc;
+    *out_len = o;
+    if (st) {
+        *st = tot;
+        st->kernel_ns = kern;
+        st->total_ns = now_ns() - t0;
+    }
+    return AMBC_OK;
+}
+
 extern "C" int ambc_compress_batch(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const ambc_params* p,
                                    uint8_t* out, uint64_t out_cap, uint64_t* out_len, ambc_stats* st) {
     if (!ctx || (!in && n) || !out || !out_len) return fail(AMBC_E_INVAL, "NULL argument");
@@ -356,6 +425,8 @@ extern "C" int ambc_compress_batch(ambc_ctx* ctx, const uint8_t* in, uint64_t n,
     const uint64_t M = (n + C - 1) / C;
     int G = (int)ctx->devs.size();
     if (p->mode == AMBC_MODE_REFERENCE || M < (uint64_t)G * 4) G = 1;  // remainder rule is global
+    if (G == 1 && p->mode == AMBC_MODE_NATIVE && n > kSlabBytes)
+        return compress_slabs(ctx->devs[0], in, n, p, out, out_cap, out_len, st);
     ambc_stats total{};
     std::vector<uint64_t> lens(G, 0);
     std::vector<int> rcs(G, 0);

@@ -45,6 +45,9 @@ def parse():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--no-e2e", action="store_true", help="skip the pinned host-to-host leg")
+    ap.add_argument("--api-bytes", type=int, default=256 << 20,
+                    help="input size of the AdaptiveCompressor.compress(path, path) leg (0: skip)")
     return ap.parse_args()
 
 
@@ -73,6 +76,70 @@ def cpu_baseline(args, threads):
             "sample": f"first {n} bytes (seed {args.seed}) of the same stream, chunk "
                       f"{args.chunk}, oracle/ambc_oracle.c OpenMP restatement, "
                       f"{dt:.1f} s wall, ratio {len(body) / n:.4f}"}
+
+
+def e2e_leg(lib, ctx, d_in, d_out, body_len, n, p, reps=3):
+    """T_e2e: page-locked host input -> page-locked host body through
+    ambc_compress_batch (slab pipeline: H2D, compress and D2H overlapped).  The
+    body must equal the device-resident one byte for byte."""
+    import numpy as np
+    import torch
+    from ambc import _lib
+    cap = lib.ambc_compress_bound(n, p.chunk_size)
+    h_in = lib.ambc_host_alloc(n)
+    h_out = lib.ambc_host_alloc(cap)
+    if not h_in or not h_out:
+        return None
+    try:
+        _lib.check(lib.ambc_memcpy_d2h(ctx.h, 0, h_in, d_in.data_ptr(), n), lib)
+        olen = C.c_uint64()
+        st = _lib.Stats()
+        u8p = C.POINTER(C.c_uint8)
+        ts = []
+        for i in range(reps + 1):
+            t = time.perf_counter()
+            _lib.check(lib.ambc_compress_batch(ctx.h, C.cast(h_in, u8p), n, C.byref(p),
+                                               C.cast(h_out, u8p), cap, C.byref(olen),
+                                               C.byref(st)), lib)
+            if i:
+                ts.append(time.perf_counter() - t)
+        got = np.ctypeslib.as_array((C.c_uint8 * olen.value).from_address(h_out))
+        same = olen.value == body_len and bool(
+            torch.equal(torch.from_numpy(got).to(d_out.device), d_out[:body_len]))
+        ts.sort()
+        return {"GBps": round(n / ts[len(ts) // 2] / 1e9, 3), "ms": round(ts[len(ts) // 2] * 1e3, 3),
+                "reps": reps, "host_buffers": "pinned (ambc_host_alloc)", "body_equal_device": same,
+                "kernel_ms": round(st.kernel_ns / 1e6, 3)}
+    finally:
+        lib.ambc_host_free(h_in)
+        lib.ambc_host_free(h_out)
+
+
+def api_leg(nbytes, chunk, mode, methods, seed):
+    """T_api: AdaptiveCompressor.compress(path, path) wall time on a
+    file of the same stream (file read, MD5, compress, file write included),
+    then decompress(path, path) with its MD5 check."""
+    import tempfile
+    from ambc import AdaptiveCompressor
+    from oracle import synth
+    data = synth.generate(nbytes, seed)
+    with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
+        src, dst, back = (os.path.join(td, x) for x in ("in.bin", "out.ambc", "back.bin"))
+        with open(src, "wb") as f:
+            f.write(data)
+        comp = AdaptiveCompressor(chunk_size=chunk, mode=mode, methods=methods)
+        comp.compress(src, dst)                       # warm-up
+        t = time.perf_counter()
+        stats = comp.compress(src, dst)
+        tc = time.perf_counter() - t
+        t = time.perf_counter()
+        comp.decompress(dst, back)
+        td_ = time.perf_counter() - t
+        with open(back, "rb") as f:
+            ok = f.read() == data
+    return {"bytes": nbytes, "compress_GBps": round(nbytes / tc / 1e9, 3),
+            "decompress_GBps": round(nbytes / td_ / 1e9, 3), "round_trip_bit_exact": ok,
+            "ratio": round(stats["compressed_size"] / nbytes, 5) if "compressed_size" in stats else None}
 
 
 def pmc_traffic(workload):
@@ -191,6 +258,14 @@ def main():
                   "host_api_GBps": round(n / dwall / 1e9, 3)}
         log(f"round trip bit-exact: {verified}; decode {decode}")
 
+    e2e = api = None
+    if rank == 0 and world == 1 and not args.no_e2e:
+        e2e = e2e_leg(lib, ctx, d_in, d_out, body_len, n, p)
+        log(f"e2e: {e2e}")
+    if rank == 0 and world == 1 and args.api_bytes:
+        api = api_leg(args.api_bytes, args.chunk, args.mode, methods, args.seed)
+        log(f"api: {api}")
+
     result = None
     if rank == 0:
         total_in = n * world * args.steps
@@ -209,7 +284,8 @@ def main():
                        "mode": args.mode, "methods": methods, "seed": args.seed,
                        "ratio": round(body_total / (n * world), 5),
                        "parallelism": f"chunk-shard dp{world}" if world > 1 else "single GPU",
-                       "round_trip_bit_exact": verified, "decode": decode},
+                       "round_trip_bit_exact": verified, "decode": decode,
+                       "e2e_pinned_host": e2e, "api_file": api},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,

@@ -223,21 +223,41 @@ def test_empty_and_tiny_files(ctx):
 
 
 def test_large_roundtrip_and_checksums(ctx):
-    """Size-independent properties at 256 MiB: round trip + per-chunk decision
-    checksum against the (multi-threaded) oracle."""
+    """Size-independent properties above the 256 MiB slab size (host API ->
+    slab pipeline, two full slabs + a partial one + a short tail chunk): the
+    body hashes equal to the (multi-threaded) oracle's, the stats agree, and
+    the round trip is exact; pinned host buffers give the same body."""
     from ambc import _lib
-    n = 256 << 20
+    n = (600 << 20) + 777
     data = np.empty(n, dtype=np.uint8)
     ctx.lib.ambc_synth_fill(data.ctypes.data, n, 20250418)
     ref = orc.synth(1 << 20, 20250418)
     assert data[:1 << 20].tobytes() == ref
     comp = _compressor(chunk_size=4096)
-    body = comp._adaptive_compress(data.tobytes())
-    oref, st = orc.compress_body(data.tobytes(), orc.make_params(4096, "native", (1, 3, 4, 9),
-                                                                 n_total=n), nthreads=0)
+    raw = data.tobytes()
+    body = comp._adaptive_compress(raw)
+    oref, ost = orc.compress_body(raw, orc.make_params(4096, "native", (1, 3, 4, 9), n_total=n),
+                                  nthreads=0)
     assert hashlib.sha256(body).digest() == hashlib.sha256(oref).digest()
-    assert comp._adaptive_decompress(body, n) == data.tobytes()
-    del _lib
+    st = comp._last_device_stats
+    assert (st.total_chunks, st.compressed_chunks, st.payload_bytes, st.overhead_bytes) == \
+        (ost.total_chunks, ost.compressed_chunks, ost.payload_bytes, ost.overhead_bytes)
+    assert [st.method_usage[i] for i in (1, 3, 4, 9)] == [ost.method_usage[i] for i in (1, 3, 4, 9)]
+    assert comp._adaptive_decompress(body, n) == raw
+    # page-locked buffers (the overlapped copy path)
+    u8p = C.POINTER(C.c_uint8)
+    cap = ctx.lib.ambc_compress_bound(n, 4096)
+    h_in, h_out = ctx.lib.ambc_host_alloc(n), ctx.lib.ambc_host_alloc(cap)
+    try:
+        C.memmove(h_in, data.ctypes.data, n)
+        p, keep = comp._params(n)
+        olen = C.c_uint64()
+        _lib.check(ctx.lib.ambc_compress_batch(ctx.h, C.cast(h_in, u8p), n, C.byref(p),
+                                               C.cast(h_out, u8p), cap, C.byref(olen), None), ctx.lib)
+        assert C.string_at(h_out, olen.value) == body
+    finally:
+        ctx.lib.ambc_host_free(h_in)
+        ctx.lib.ambc_host_free(h_out)
 
 
 def test_device_synth_matches_host(ctx):
