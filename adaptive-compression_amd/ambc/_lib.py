@@ -62,7 +62,7 @@ class Stats(C.Structure):
                 ("bytes_saved", C.c_uint64), ("payload_bytes", C.c_uint64),
                 ("overhead_bytes", C.c_uint64), ("kernel_ns", C.c_uint64),
                 ("h2d_ns", C.c_uint64), ("d2h_ns", C.c_uint64), ("walk_ns", C.c_uint64),
-                ("total_ns", C.c_uint64)]
+                ("total_ns", C.c_uint64), ("host_codec_ns", C.c_uint64)]
 
 
 class HostChunk(C.Structure):

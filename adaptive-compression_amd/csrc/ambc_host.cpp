@@ -18,6 +18,8 @@
 #include <thread>
 #include <vector>
 
+#include <zlib.h>
+
 #include "../../include/ambc.h"
 #include "ambc_internal.h"
 
@@ -640,7 +642,8 @@ struct Walk {
     std::vector<DecJob> jobs;
     std::vector<uint32_t> src_index;   // job -> package ordinal
     std::vector<uint8_t> kind;         // job -> DEC_KIND_* kernel
-    std::vector<ambc_host_chunk> host;
+    std::vector<ambc_host_chunk> host;    // decoded by the caller (ids 6, 7)
+    std::vector<ambc_host_chunk> zlib;    // id 5: inflated here on host threads
     uint64_t total = 0;
     uint64_t scratch = 0;
     bool marker_error = false;
@@ -715,7 +718,8 @@ void walk_body(const uint8_t* body, uint64_t blen, uint64_t orig_size, const uin
         j.out_off = out;
         if (j.type == DEC_SKIP) {
             ambc_host_chunk h{pos, out, clen, orig, t, 0};
-            w.host.push_back(h);
+            if (t == 5) { if (clen) w.zlib.push_back(h); }
+            else w.host.push_back(h);
         }
         w.jobs.push_back(j);
         w.kind.push_back((uint8_t)kind);
@@ -729,6 +733,67 @@ void walk_body(const uint8_t* body, uint64_t blen, uint64_t orig_size, const uin
 }
 
 }  // namespace
+
+// DeflateCompression.decompress (advanced_compression.py:83-96): zlib.decompress
+// of the payload (zlib wrapper, Adler-32 checked, bytes after the end of the
+// stream ignored, an unfinished stream is an error), then pad / truncate to
+// orig; any error -> orig zero bytes.
+static void inflate_chunk(const uint8_t* in, uint32_t n, uint8_t* out, uint32_t orig) {
+    z_stream zs{};
+    bool ok = inflateInit(&zs) == Z_OK;
+    uint64_t produced = 0;
+    if (ok) {
+        uint8_t discard[16384];
+        zs.next_in = const_cast<Bytef*>(in);
+        zs.avail_in = n;
+        for (;;) {
+            const bool spill = produced >= orig;
+            zs.next_out = spill ? discard : out + produced;
+            zs.avail_out = spill ? (uInt)sizeof discard : (uInt)(orig - produced);
+            const uInt room = zs.avail_out;
+            const int rc = inflate(&zs, Z_NO_FLUSH);
+            produced += room - zs.avail_out;
+            if (rc == Z_STREAM_END) break;
+            if (rc == Z_OK && zs.avail_out == 0) continue;         // output full: keep going
+            if (rc == Z_OK || rc == Z_BUF_ERROR) {
+                if (zs.avail_in == 0) { ok = false; break; }        // truncated stream
+                if (rc == Z_OK) continue;
+            }
+            ok = false;                                             // data / header / checksum error
+            break;
+        }
+        inflateEnd(&zs);
+    }
+    if (!ok) std::memset(out, 0, orig);
+    else if (produced < orig) std::memset(out + produced, 0, orig - produced);
+}
+
+static void inflate_all(const uint8_t* body, const std::vector<ambc_host_chunk>& jobs, uint8_t* out,
+                        uint64_t orig_size) {
+    if (jobs.empty()) return;
+    const char* e = getenv("AMBC_HOST_THREADS");
+    unsigned nt = e ? (unsigned)std::max(1, atoi(e)) : std::min(16u, std::thread::hardware_concurrency());
+    nt = std::max(1u, std::min<unsigned>(nt, (unsigned)((jobs.size() + 63) / 64)));
+    auto run = [&](unsigned w) {
+        std::vector<uint8_t> tmp;
+        for (size_t i = w; i < jobs.size(); i += nt) {
+            const ambc_host_chunk& h = jobs[i];
+            if (h.out_off >= orig_size) continue;
+            // the last chunk may run past orig_size (the final truncate): decode aside
+            if (h.out_off + h.orig <= orig_size) {
+                inflate_chunk(body + h.body_off, h.clen, out + h.out_off, h.orig);
+            } else {
+                tmp.resize(h.orig);
+                inflate_chunk(body + h.body_off, h.clen, tmp.data(), h.orig);
+                std::memcpy(out + h.out_off, tmp.data(), orig_size - h.out_off);
+            }
+        }
+    };
+    if (nt == 1) { run(0); return; }
+    std::vector<std::thread> th;
+    for (unsigned w = 0; w < nt; w++) th.emplace_back(run, w);
+    for (auto& t : th) t.join();
+}
 
 static int decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t orig_size,
                          const uint64_t reg[4], uint8_t* out, std::vector<ambc_host_chunk>& host,
@@ -826,15 +891,20 @@ static int decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t or
     t = now_ns();
     HIPCHK(hipMemcpyAsync(out, d.dout.p, orig_size, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    const uint64_t d2h_ns = now_ns() - t;
+    const uint64_t t_inf = now_ns();
+    inflate_all(body, w.zlib, out, orig_size);
+    const uint64_t inflate_ns = now_ns() - t_inf;
     host = w.host;
     if (st) {
         std::memset(st, 0, sizeof *st);
         st->total_chunks = w.jobs.size();
         st->payload_bytes = w.total;   // bytes the chunks produced before the final pad/truncate
         st->h2d_ns = h2d;
-        st->d2h_ns = now_ns() - t;
+        st->d2h_ns = d2h_ns;
         st->walk_ns = walk_ns;
         st->kernel_ns = kern_ns;
+        st->host_codec_ns = inflate_ns;
         st->total_ns = now_ns() - t0;
     }
     return AMBC_OK;
@@ -854,7 +924,7 @@ extern "C" int ambc_decompress_ex(ambc_ctx* ctx, const uint8_t* body, uint64_t b
     if (rc) return rc;
     if (n_host) *n_host = (uint32_t)host.size();
     if (host.size() > host_cap) {
-        if (!host_chunks && !n_host) return fail(AMBC_E_HOSTCODEC, "body has zlib/bz2/lzma chunks");
+        if (!host_chunks && !n_host) return fail(AMBC_E_HOSTCODEC, "body has bz2/lzma chunks");
         if (host.size() > host_cap) return fail(AMBC_E_CAPACITY, "host_chunks capacity too small");
     }
     for (size_t i = 0; i < host.size(); i++) host_chunks[i] = host[i];
@@ -865,7 +935,7 @@ extern "C" int ambc_decompress_batch(ambc_ctx* ctx, const uint8_t* body, uint64_
                                      uint64_t orig_size, uint8_t* out, ambc_stats* st) {
     uint32_t nh = 0;
     int rc = ambc_decompress_ex(ctx, body, body_len, orig_size, nullptr, out, nullptr, 0, &nh, st);
-    if (rc == AMBC_E_CAPACITY && nh) return fail(AMBC_E_HOSTCODEC, "body has zlib/bz2/lzma chunks: use ambc_decompress_ex");
+    if (rc == AMBC_E_CAPACITY && nh) return fail(AMBC_E_HOSTCODEC, "body has bz2/lzma chunks: use ambc_decompress_ex");
     return rc;
 }
 

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define AMBC_ABI_VERSION 1
+#define AMBC_ABI_VERSION 2
 
 #define AMBC_OK 0
 #define AMBC_E_INVAL (-1)     /* bad argument */
@@ -47,7 +47,7 @@ extern "C" {
 #define AMBC_E_RANGE (-4)     /* a u32 chunk field would overflow (reference: struct.error) */
 #define AMBC_E_MARKER (-5)    /* "Marker mismatch in chunk header." (reference ValueError) */
 #define AMBC_E_CAPACITY (-6)  /* output buffer too small */
-#define AMBC_E_HOSTCODEC (-7) /* body holds ids 5/6/7 chunks: use ambc_decompress_ex */
+#define AMBC_E_HOSTCODEC (-7) /* body holds ids 6/7 chunks: use ambc_decompress_ex */
 #define AMBC_E_CODEC (-8)     /* the codec raises in the reference (e.g. Huffman on 1 or 256 symbols) */
 
 #define AMBC_MODE_NATIVE 0    /* every C-byte chunk decided independently */
@@ -88,9 +88,11 @@ typedef struct {
     uint64_t bytes_saved, payload_bytes, overhead_bytes;
     uint64_t kernel_ns;  /* device time of the kernels (hipEvents) */
     uint64_t h2d_ns, d2h_ns, walk_ns, total_ns;
+    uint64_t host_codec_ns; /* decode: id-5 (zlib) chunks inflated on host threads */
 } ambc_stats;
 
-/* A chunk the GPU leaves to the host (ids 5/6/7: zlib/bz2/lzma). */
+/* A chunk the library leaves to the caller (ids 6/7: bz2/lzma; id 5 zlib chunks
+ * are inflated inside the library on host threads). */
 typedef struct {
     uint64_t body_off; /* payload offset in the body */
     uint64_t out_off;  /* where its decoded bytes go in the output */
@@ -116,7 +118,7 @@ int ambc_compress_batch(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const ambc
 int ambc_decompress_batch(ambc_ctx* ctx, const uint8_t* body, uint64_t body_len,
                           uint64_t orig_size, uint8_t* out, ambc_stats* st);
 
-/* As ambc_decompress_batch; ids 5/6/7 chunks are not decoded but listed in
+/* As ambc_decompress_batch; ids 6/7 chunks are not decoded but listed in
  * host_chunks (capacity host_cap, count in *n_host) for the caller to fill.
  * registered[id>>6] bit (id&63) marks ids with a registered method
  * (method_lookup); an unregistered id's payload is copied verbatim

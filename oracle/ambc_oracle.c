@@ -20,6 +20,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+
+#include <zlib.h>
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -576,6 +578,29 @@ done:
 }
 
 /* ------------------------------------------------------------------------ */
+/* DEFLATE (id 5)   advanced_compression.py:71-107                           */
+/* compress = zlib.compress(data, level=9) (CPython: deflateInit(level),     */
+/* i.e. compress2), should_use = n >= 64 and calculate_entropy < 8.0 (:48-57,*/
+/* :98-107; H reaches 8.0 only for an exactly uniform histogram).            */
+/* ------------------------------------------------------------------------ */
+EXPORT int64_t orc_deflate_encode(const uint8_t* d, uint32_t n, uint8_t* out) {
+    if (n == 0) return 0;
+    uLongf cap = compressBound(n);
+    uint8_t* tmp = out ? NULL : (uint8_t*)malloc(cap);
+    int rc = compress2(out ? out : tmp, &cap, d, n, 9);
+    free(tmp);
+    return rc == Z_OK ? (int64_t)cap : -1;
+}
+
+EXPORT int orc_deflate_should_use(const uint8_t* d, uint32_t n) {
+    if (n < 64) return 0;
+    uint32_t h[256] = {0};
+    for (uint32_t i = 0; i < n; i++) h[d[i]]++;
+    for (int s = 1; s < 256; s++) if (h[s] != h[0]) return 1;
+    return 0;   /* exactly uniform: entropy == 8.0 */
+}
+
+/* ------------------------------------------------------------------------ */
 /* per-chunk selection   adaptive_compressor.py:537-590 (single candidate)  */
 /* + _process_chunk :631-700                                                 */
 /* ------------------------------------------------------------------------ */
@@ -619,6 +644,10 @@ EXPORT int orc_select(const uint8_t* d, uint32_t n, const orc_params* p, const d
         if (l >= 0 && l + 18 < best) { best = l + 18; win = 3; wl = l; }
     }
     /* id 4 (Delta): payload length == n, can never satisfy len+18 < n */
+    if (pref_ok(p, 5, n) && orc_deflate_should_use(d, n)) {
+        int64_t l = orc_deflate_encode(d, n, NULL);
+        if (l >= 0 && l + 18 < best) { best = l + 18; win = 5; wl = l; }
+    }
     if (pref_ok(p, 9, n) && n >= 1024) {          /* LZ4 should_use :298-307 */
         int64_t l = orc_lz4_frame_encode(d, n, NULL);
         if (l + 18 < best) { best = l + 18; win = 9; wl = l; }
@@ -642,6 +671,7 @@ static int64_t encode_payload(int id, const uint8_t* d, uint32_t n, uint8_t* out
     case 1: return orc_rle_encode(d, n, out);
     case 2: return orc_dict_encode(d, n, out);
     case 3: return orc_huff_encode(d, n, out);
+    case 5: return orc_deflate_encode(d, n, out);
     case 9: return orc_lz4_frame_encode(d, n, out);
     default: memcpy(out, d, n); return n;
     }

@@ -47,14 +47,15 @@ def lib():
         _lib = C.CDLL(LIB_PATH)
         u8p, i64, u32 = C.c_void_p, C.c_int64, C.c_uint32
         for name in ("orc_rle_encode", "orc_huff_encode", "orc_dict_encode",
-                     "orc_lz4_frame_encode", "orc_lz4_block_encode"):
+                     "orc_lz4_frame_encode", "orc_lz4_block_encode", "orc_deflate_encode"):
             getattr(_lib, name).argtypes = [u8p, u32, u8p]
             getattr(_lib, name).restype = i64
         for name in ("orc_rle_decode", "orc_huff_decode", "orc_delta_decode", "orc_dict_decode",
                      "orc_lz4_frame_decode"):
             getattr(_lib, name).argtypes = [u8p, u32, u32, u8p]
             getattr(_lib, name).restype = i64
-        for name in ("orc_rle_should_use", "orc_delta_should_use", "orc_dict_should_use"):
+        for name in ("orc_rle_should_use", "orc_delta_should_use", "orc_dict_should_use",
+                     "orc_deflate_should_use"):
             getattr(_lib, name).argtypes = [u8p, u32]
             getattr(_lib, name).restype = C.c_int
         _lib.orc_huff_should_use.argtypes = [u8p, u32, u8p]
@@ -129,6 +130,11 @@ def lz4_frame_encode(d):
     return _call_enc("orc_lz4_frame_encode", d, len(d) + len(d) // 255 + 64)
 
 
+def deflate_encode(d):
+    """zlib.compress(d, level=9) through the same system zlib CPython links."""
+    return _call_enc("orc_deflate_encode", d, len(d) + len(d) // 1000 + 64)
+
+
 def lz4_block_encode(d):
     return _call_enc("orc_lz4_block_encode", d, len(d) + len(d) // 255 + 64)
 
@@ -141,6 +147,8 @@ def should_use(mid, d, tab=None):
         return bool(L.orc_dict_should_use(C.addressof(src), len(d)))
     if mid == 4:
         return bool(L.orc_delta_should_use(C.addressof(src), len(d)))
+    if mid == 5:
+        return bool(L.orc_deflate_should_use(C.addressof(src), len(d)))
     if mid == 3:
         t = entropy_table(len(d)) if (tab is None and len(d) > 0) else tab
         return bool(L.orc_huff_should_use(C.addressof(src), len(d),

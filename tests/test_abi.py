@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
 def test_abi_version_and_bound():
     from ambc import _lib
     lib = _lib.load()
-    assert lib.ambc_abi_version() == 1
+    assert lib.ambc_abi_version() == 2
     assert lib.ambc_compress_bound(0, 4096) == 16
     assert lib.ambc_compress_bound(4096, 4096) == 4096 + 18 + 16
     assert lib.ambc_compress_bound(4097, 4096) == 4097 + 36 + 16

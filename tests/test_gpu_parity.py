@@ -339,3 +339,48 @@ def test_lz4_external_frames(ctx):
                 assert lz4.decompress(bytes(bad), len(d)) == orc.decode_chunk(9, bytes(bad), len(d))
                 n_checked += 1
     assert n_checked > 200
+
+
+# ---------------------------------------------------------------------------
+# id 5 (zlib DEFLATE) chunks: inflated by the library on host threads with
+# zlib.decompress semantics (advanced_compression.py:83-96) -- bodies from the
+# oracle's zlib-9 selector, plus damaged / truncated / trailing-garbage payloads
+# ---------------------------------------------------------------------------
+def _chunk(t, payload, orig):
+    import struct
+    return b"\xff\xff\x00\x00" + struct.pack("<BBIII", t, 0, orig, orig, len(payload)) + payload
+
+
+def test_deflate_chunks_decode(ctx):
+    import zlib
+    n = (2 << 20) + 333
+    data = orc.synth(n, 31)
+    p = orc.make_params(4096, "native", (1, 3, 5), n_total=n)
+    body, st = orc.compress_body(data, p, nthreads=0)
+    assert st.method_usage[5] > 100
+    comp = _compressor()
+    assert comp._adaptive_decompress(body, n) == data
+    # hand-made bodies: valid, damaged, truncated, trailing bytes, empty, over/under-long
+    rng = random.Random(3)
+    parts, orig_total = [], 0
+    for i in range(60):
+        src = data[i * 3000:i * 3000 + 4096]
+        z = zlib.compress(src, 9)
+        kind = i % 6
+        if kind == 1:
+            z = bytearray(z); z[rng.randrange(len(z))] ^= 0x10; z = bytes(z)
+        elif kind == 2:
+            z = z[:rng.randrange(1, len(z))]
+        elif kind == 3:
+            z = z + b"tail-garbage"
+        elif kind == 4:
+            src = src + src[:100]                      # decodes longer than orig -> truncated
+            z = zlib.compress(src, 9)
+        orig = 4096 if kind != 5 else 5000             # kind 5: shorter than orig -> zero pad
+        parts.append(_chunk(5, z, orig))
+        orig_total += orig
+    parts.append(_chunk(5, b"", 10))                   # empty payload: produces nothing
+    orig_total += 10
+    body = b"".join(parts) + b"\xff\xff\x00\x00\x00\x00" + bytes(10)
+    want = orc.decompress_body(body, orig_total)
+    assert comp._adaptive_decompress(body, orig_total) == want
