@@ -182,13 +182,17 @@ class AdaptiveCompressor:
         return bytes(memoryview(out)[:olen.value])
 
     def _adaptive_decompress(self, data, orig_size):
-        """One C-ABI call for every GPU-routable chunk; ids 5/6/7 through the
+        """One C-ABI call: GPU kernels for ids 1/2/3/4/9/255 and unregistered ids,
+        host zlib threads inside the library for id 5; ids 6/7 through the
         reference's library wrappers."""
         if self.marker_bytes_aligned not in (b"", MARKER_BYTES):
             raise NotImplementedError("only the reference's constant 32-bit marker is supported")
         ctx = self._ctx()
         data = bytes(data)
-        out = bytearray(max(orig_size, 1))
+        # large outputs: decode straight into a fresh (calloc'd, lazily zeroed)
+        # bytes object that nothing else references yet -- saves a full copy
+        direct = orig_size >= (1 << 16)
+        out = bytes(orig_size) if direct else bytearray(max(orig_size, 1))
         reg = (C.c_uint64 * 4)()
         for t in self.method_lookup:
             reg[t >> 6] |= 1 << (t & 63)
@@ -197,8 +201,9 @@ class AdaptiveCompressor:
             hc = (_lib.HostChunk * cap)()
             nh = C.c_uint32()
             st = _lib.Stats()
+            optr = C.cast(C.c_char_p(out), C.POINTER(C.c_uint8)) if direct else _lib.addr(out)
             rc = ctx.lib.ambc_decompress_ex(ctx.h, _lib.addr(data), len(data), orig_size, reg,
-                                            _lib.addr(out), hc, cap, C.byref(nh), C.byref(st))
+                                            optr, hc, cap, C.byref(nh), C.byref(st))
             if rc == _lib.AMBC_E_CAPACITY and nh.value > cap:
                 cap = nh.value
                 continue
@@ -206,15 +211,20 @@ class AdaptiveCompressor:
                 raise ValueError("Marker mismatch in chunk header.")
             _lib.check(rc, ctx.lib)
             break
-        for i in range(nh.value):
+        if nh.value and direct:
+            optr = C.cast(C.c_char_p(out), C.c_void_p).value
+        for i in range(nh.value):                # ids 6/7: the reference's library wrappers
             h = hc[i]
             payload = data[h.body_off:h.body_off + h.clen]
             dec = self.method_lookup[h.type].decompress(payload, h.orig)
             end = min(h.out_off + len(dec), orig_size)
             if end > h.out_off:
-                out[h.out_off:end] = dec[:end - h.out_off]
+                if direct:
+                    C.memmove(optr + h.out_off, dec, end - h.out_off)
+                else:
+                    out[h.out_off:end] = dec[:end - h.out_off]
         self._last_device_stats = st
-        return bytes(memoryview(out)[:orig_size])
+        return out if direct else bytes(memoryview(out)[:orig_size])
 
     # -- stats (adaptive_compressor.py:257-284,482-532) ---------------------------
     def _build_stats_raw(self, original_size, elapsed):
