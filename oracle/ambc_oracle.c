@@ -601,6 +601,285 @@ EXPORT int orc_deflate_should_use(const uint8_t* d, uint32_t n) {
 }
 
 /* ------------------------------------------------------------------------ */
+/* "ambc-deflate v1": this project's DEFLATE (id 5) encoder, the GPU's       */
+/* definition (the reference calls zlib.compress(level=9); any valid zlib    */
+/* stream decodes there, and bytes are only round-trip tested).              */
+/*  parse : h(i) = (u32le(d+i) * 2654435761) >> 21 for i <= n-4;             */
+/*          cand(i) = last j < i with h(j) == h(i); match at p iff           */
+/*          u32le(d+cand) == u32le(d+p) and p - cand <= 32768; greedy, the   */
+/*          match taken at its full length capped at 258 and at n - p.       */
+/*  codes : one final block, the smallest of dynamic / fixed / stored        */
+/*          (ties in that order); Huffman lengths from the two-queue          */
+/*          construction over (freq, symbol)-sorted leaves, limited to 15    */
+/*          (7 for the code-length code) by the bl_count fix-up, assigned     */
+/*          shortest-first from the most frequent (ties: higher symbol);     */
+/*          code lengths run-length coded with 16/17/18 (rule in gd_rle).     */
+/*  frame : zlib header 78 DA, the block, Adler-32 big-endian.               */
+/* ------------------------------------------------------------------------ */
+static const uint16_t GD_LBASE[29] = {3, 4, 5, 6, 7, 8, 9, 10, 11, 13, 15, 17, 19, 23, 27,
+                                      31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+static const uint8_t GD_LEXT[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2,
+                                    2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+static const uint16_t GD_DBASE[30] = {1, 2, 3, 4, 5, 7, 9, 13, 17, 25, 33, 49, 65, 97, 129,
+                                      193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097,
+                                      6145, 8193, 12289, 16385, 24577};
+static const uint8_t GD_DEXT[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6,
+                                    6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+static const uint8_t GD_CLORD[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+static int gd_lcode(uint32_t L) { int k = 28; while (GD_LBASE[k] > L) k--; return k; }
+static int gd_dcode(uint32_t D) { int k = 29; while (GD_DBASE[k] > D) k--; return k; }
+
+typedef struct { uint32_t pos, len, dist; } gd_seq;
+
+EXPORT uint32_t orc_gd_parse(const uint8_t* d, uint32_t n, uint32_t* out3) {
+    int32_t last[2048];
+    for (int i = 0; i < 2048; i++) last[i] = -1;
+    int32_t* cand = (int32_t*)malloc((size_t)(n ? n : 1) * 4);
+    for (uint32_t i = 0; i < n; i++) cand[i] = -1;
+    for (uint32_t i = 0; i + 4 <= n; i++) {
+        uint32_t h = (rd32(d + i) * 2654435761u) >> 21;
+        cand[i] = last[h];
+        last[h] = (int32_t)i;
+    }
+    uint32_t ns = 0, p = 0;
+    while (p < n) {
+        int32_t c = cand[p];
+        if (p + 4 <= n && c >= 0 && p - (uint32_t)c <= 32768 && rd32(d + c) == rd32(d + p)) {
+            uint32_t L = 4;
+            while (L < 258 && p + L < n && d[c + L] == d[p + L]) L++;
+            if (out3) { out3[3 * ns] = p; out3[3 * ns + 1] = L; out3[3 * ns + 2] = p - (uint32_t)c; }
+            ns++;
+            p += L;
+        } else {
+            p++;
+        }
+    }
+    free(cand);
+    return ns;
+}
+
+/* Huffman code lengths, see the header comment */
+EXPORT void orc_gd_lengths(const uint32_t* freq, int nsym, int maxbits, uint8_t* len) {
+    int syms[320], k = 0;
+    memset(len, 0, (size_t)nsym);
+    for (int s = 0; s < nsym; s++) if (freq[s]) syms[k++] = s;
+    if (k == 0) return;
+    if (k == 1) { len[syms[0]] = 1; return; }
+    /* sort by (freq, sym) ascending (insertion sort: k <= 320) */
+    for (int i = 1; i < k; i++) {
+        int s = syms[i], j = i - 1;
+        while (j >= 0 && (freq[syms[j]] > freq[s] || (freq[syms[j]] == freq[s] && syms[j] > s))) {
+            syms[j + 1] = syms[j];
+            j--;
+        }
+        syms[j + 1] = s;
+    }
+    /* two-queue construction: leaves 0..k-1, internal nodes k..2k-2 */
+    uint64_t w[640];
+    int parent[640];
+    for (int i = 0; i < k; i++) w[i] = freq[syms[i]];
+    int a = 0, b = k, nb = k;   /* fronts of the leaf and internal queues, next internal id */
+    for (int m = 0; m < k - 1; m++) {
+        int pick[2];
+        for (int t = 0; t < 2; t++) {
+            if (a < k && (b >= nb || w[a] <= w[b])) pick[t] = a++;
+            else pick[t] = b++;
+        }
+        w[nb] = w[pick[0]] + w[pick[1]];
+        parent[pick[0]] = parent[pick[1]] = nb;
+        nb++;
+    }
+    int depth[640];
+    depth[nb - 1] = 0;
+    for (int i = nb - 2; i >= 0; i--) depth[i] = depth[parent[i]] + 1;
+    uint32_t blc[64] = {0};
+    for (int i = 0; i < k; i++) blc[depth[i] > 63 ? 63 : depth[i]]++;
+    /* limit to maxbits */
+    for (int d2 = maxbits + 1; d2 < 64; d2++) { blc[maxbits] += blc[d2]; blc[d2] = 0; }
+    uint64_t total = 0;
+    for (int d2 = 1; d2 <= maxbits; d2++) total += (uint64_t)blc[d2] << (maxbits - d2);
+    while (total > (1ull << maxbits)) {
+        blc[maxbits]--;
+        for (int d2 = maxbits - 1; d2 > 0; d2--)
+            if (blc[d2]) { blc[d2]--; blc[d2 + 1] += 2; break; }
+        total--;
+    }
+    /* shortest lengths to the most frequent symbols */
+    int j = k;
+    for (int d2 = 1; d2 <= maxbits; d2++)
+        for (uint32_t c = blc[d2]; c > 0; c--) len[syms[--j]] = (uint8_t)d2;
+}
+
+/* canonical codes (RFC 1951 3.2.2), bit-reversed for LSB-first emission */
+static void gd_codes(const uint8_t* len, int nsym, uint16_t* rcode) {
+    uint32_t blc[16] = {0}, next[16];
+    for (int s = 0; s < nsym; s++) blc[len[s]]++;
+    blc[0] = 0;
+    uint32_t c = 0;
+    for (int b = 1; b < 16; b++) { c = (c + blc[b - 1]) << 1; next[b] = c; }
+    for (int s = 0; s < nsym; s++) {
+        if (!len[s]) { rcode[s] = 0; continue; }
+        uint32_t v = next[len[s]]++, r = 0;
+        for (int b = 0; b < len[s]; b++) r |= ((v >> b) & 1) << (len[s] - 1 - b);
+        rcode[s] = (uint16_t)r;
+    }
+}
+
+/* code-length RLE over the HLIT + HDIST lengths: (symbol, extra value) pairs.
+ * run of zeros r: 18 x min(r,138) while r >= 11, then 17 x r if r >= 3, else
+ * literal zeros; run of v != 0: v once, then 16 x min(r,6) while r >= 3, then
+ * literal v for the rest. */
+static int gd_rle(const uint8_t* L, int cnt, uint8_t* sym, uint8_t* ext) {
+    int ns = 0, i = 0;
+    while (i < cnt) {
+        int v = L[i], r = 1;
+        while (i + r < cnt && L[i + r] == v) r++;
+        i += r;
+        if (v == 0) {
+            while (r >= 11) { int t = r < 138 ? r : 138; sym[ns] = 18; ext[ns++] = (uint8_t)(t - 11); r -= t; }
+            if (r >= 3) { sym[ns] = 17; ext[ns++] = (uint8_t)(r - 3); r = 0; }
+            while (r-- > 0) { sym[ns] = 0; ext[ns++] = 0; }
+        } else {
+            sym[ns] = (uint8_t)v; ext[ns++] = 0; r--;
+            while (r >= 3) { int t = r < 6 ? r : 6; sym[ns] = 16; ext[ns++] = (uint8_t)(t - 3); r -= t; }
+            while (r-- > 0) { sym[ns] = (uint8_t)v; ext[ns++] = 0; }
+        }
+    }
+    return ns;
+}
+
+typedef struct { uint8_t* p; uint64_t bit; } gd_bits;
+static void gd_put(gd_bits* o, uint32_t v, int nb) {
+    for (int i = 0; i < nb; i++) {
+        if ((v >> i) & 1) o->p[(o->bit + i) >> 3] |= (uint8_t)(1u << ((o->bit + i) & 7));
+    }
+    o->bit += nb;
+}
+
+static uint32_t gd_adler(const uint8_t* d, uint32_t n) {
+    uint32_t a = 1, b = 0;
+    for (uint32_t i = 0; i < n; i++) { a = (a + d[i]) % 65521; b = (b + a) % 65521; }
+    return b << 16 | a;
+}
+
+/* returns the zlib stream length; writes it to out when out != NULL
+ * (out must hold n + 5 * (n / 65535 + 1) + 6 bytes) */
+EXPORT int64_t orc_gd_encode(const uint8_t* d, uint32_t n, uint8_t* out) {
+    uint32_t* sq = (uint32_t*)malloc(((size_t)n / 4 + 2) * 12);
+    uint32_t ns = orc_gd_parse(d, n, sq);
+    uint32_t lf[286] = {0}, df[30] = {0};
+    uint64_t extra = 0;
+    uint32_t p = 0;
+    for (uint32_t s = 0; s <= ns; s++) {
+        uint32_t mp = s < ns ? sq[3 * s] : n;
+        for (; p < mp; p++) lf[d[p]]++;
+        if (s < ns) {
+            int lc = gd_lcode(sq[3 * s + 1]), dc = gd_dcode(sq[3 * s + 2]);
+            lf[257 + lc]++; df[dc]++;
+            extra += GD_LEXT[lc] + GD_DEXT[dc];
+            p += sq[3 * s + 1];
+        }
+    }
+    lf[256] = 1;
+    /* dynamic: at least two distance codes carry a length (zlib's convention) */
+    uint32_t dfx[30];
+    memcpy(dfx, df, sizeof dfx);
+    { int used = 0; for (int i = 0; i < 30; i++) used += dfx[i] != 0;
+      for (int i = 0; used < 2 && i < 2; i++) if (!dfx[i]) { dfx[i] = 1; used++; } }
+    uint8_t ll[286], dl[30];
+    orc_gd_lengths(lf, 286, 15, ll);
+    orc_gd_lengths(dfx, 30, 15, dl);
+    int hlit = 286; while (hlit > 257 && !ll[hlit - 1]) hlit--;
+    int hdist = 30; while (hdist > 1 && !dl[hdist - 1]) hdist--;
+    uint8_t cat[316], rs[316], re[316];
+    memcpy(cat, ll, (size_t)hlit);
+    memcpy(cat + hlit, dl, (size_t)hdist);
+    int nr = gd_rle(cat, hlit + hdist, rs, re);
+    uint32_t cf[19] = {0};
+    for (int i = 0; i < nr; i++) cf[rs[i]]++;
+    uint8_t cl[19];
+    orc_gd_lengths(cf, 19, 7, cl);
+    int hclen = 19; while (hclen > 4 && !cl[GD_CLORD[hclen - 1]]) hclen--;
+    uint64_t dyn = 3 + 5 + 5 + 4 + 3ull * hclen;
+    for (int i = 0; i < nr; i++) dyn += cl[rs[i]] + (rs[i] == 16 ? 2 : rs[i] == 17 ? 3 : rs[i] == 18 ? 7 : 0);
+    uint64_t fix = 3;
+    for (int s = 0; s < 286; s++) {
+        dyn += (uint64_t)lf[s] * ll[s];
+        fix += (uint64_t)lf[s] * (s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8);
+    }
+    for (int s = 0; s < 30; s++) { dyn += (uint64_t)df[s] * dl[s]; fix += (uint64_t)df[s] * 5; }
+    dyn += extra; fix += extra;
+    uint64_t nblk = n ? (n + 65534) / 65535 : 1;
+    uint64_t by_dyn = (dyn + 7) / 8, by_fix = (fix + 7) / 8, by_sto = (uint64_t)n + 5 * nblk;
+    int kind = by_dyn <= by_fix && by_dyn <= by_sto ? 2 : by_fix <= by_sto ? 1 : 0;
+    uint64_t body = kind == 2 ? by_dyn : kind == 1 ? by_fix : by_sto;
+    int64_t total = (int64_t)(2 + body + 4);
+    if (out) {
+        memset(out, 0, (size_t)total);
+        out[0] = 0x78; out[1] = 0xDA;
+        gd_bits o = {out + 2, 0};
+        if (kind == 0) {
+            uint8_t* q = out + 2;
+            for (uint64_t b = 0, pos = 0; b < nblk; b++) {
+                uint32_t L = (uint32_t)((n - pos) < 65535 ? (n - pos) : 65535);
+                *q++ = b + 1 == nblk ? 1 : 0;
+                q[0] = (uint8_t)L; q[1] = (uint8_t)(L >> 8); q[2] = (uint8_t)~L; q[3] = (uint8_t)(~L >> 8);
+                q += 4;
+                memcpy(q, d + pos, L); q += L; pos += L;
+            }
+        } else {
+            uint8_t fl[288], fd[30];
+            const uint8_t* LL = ll;
+            const uint8_t* DL = dl;
+            uint16_t lc[288], dcd[30];
+            gd_put(&o, 1, 1);
+            gd_put(&o, (uint32_t)kind, 2);
+            if (kind == 1) {
+                for (int s = 0; s < 288; s++) fl[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
+                for (int s = 0; s < 30; s++) fd[s] = 5;
+                LL = fl; DL = fd;
+                gd_codes(fl, 288, lc);
+                gd_codes(fd, 30, dcd);
+            } else {
+                gd_codes(ll, 286, lc);
+                gd_codes(dl, 30, dcd);
+                uint16_t cc[19];
+                gd_codes(cl, 19, cc);
+                gd_put(&o, (uint32_t)(hlit - 257), 5);
+                gd_put(&o, (uint32_t)(hdist - 1), 5);
+                gd_put(&o, (uint32_t)(hclen - 4), 4);
+                for (int i = 0; i < hclen; i++) gd_put(&o, cl[GD_CLORD[i]], 3);
+                for (int i = 0; i < nr; i++) {
+                    gd_put(&o, cc[rs[i]], cl[rs[i]]);
+                    if (rs[i] >= 16) gd_put(&o, re[i], rs[i] == 16 ? 2 : rs[i] == 17 ? 3 : 7);
+                }
+            }
+            p = 0;
+            for (uint32_t s = 0; s <= ns; s++) {
+                uint32_t mp = s < ns ? sq[3 * s] : n;
+                for (; p < mp; p++) gd_put(&o, lc[d[p]], LL[d[p]]);
+                if (s < ns) {
+                    uint32_t L = sq[3 * s + 1], D = sq[3 * s + 2];
+                    int lcd = gd_lcode(L), dcc = gd_dcode(D);
+                    gd_put(&o, lc[257 + lcd], LL[257 + lcd]);
+                    gd_put(&o, L - GD_LBASE[lcd], GD_LEXT[lcd]);
+                    gd_put(&o, dcd[dcc], DL[dcc]);
+                    gd_put(&o, D - GD_DBASE[dcc], GD_DEXT[dcc]);
+                    p += L;
+                }
+            }
+            gd_put(&o, lc[256], LL[256]);
+        }
+        uint32_t ad = gd_adler(d, n);
+        uint8_t* t = out + total - 4;
+        t[0] = (uint8_t)(ad >> 24); t[1] = (uint8_t)(ad >> 16); t[2] = (uint8_t)(ad >> 8); t[3] = (uint8_t)ad;
+    }
+    free(sq);
+    return total;
+}
+
+/* ------------------------------------------------------------------------ */
 /* per-chunk selection   adaptive_compressor.py:537-590 (single candidate)  */
 /* + _process_chunk :631-700                                                 */
 /* ------------------------------------------------------------------------ */
@@ -608,12 +887,14 @@ typedef struct {
     uint32_t chunk_size;
     uint32_t mode;          /* 0 native (per-chunk), 1 reference (remainder-raw) */
     uint32_t method_mask;   /* bit i -> method id i enabled (ids 1..15) */
-    uint32_t reserved;
+    uint32_t flags;         /* ORC_GDEFLATE: id 5 = "ambc-deflate v1" (GPU engine), else zlib-9 */
     uint32_t pref_min[16];
     uint32_t pref_max[16];
     const double* ent_full; /* optional numpy entropy terms for n == chunk_size */
     const double* ent_tail; /* optional numpy entropy terms for n == N % chunk_size */
 } orc_params;
+
+#define ORC_GDEFLATE 1u
 
 typedef struct {
     uint64_t method_usage[256];
@@ -645,7 +926,7 @@ EXPORT int orc_select(const uint8_t* d, uint32_t n, const orc_params* p, const d
     }
     /* id 4 (Delta): payload length == n, can never satisfy len+18 < n */
     if (pref_ok(p, 5, n) && orc_deflate_should_use(d, n)) {
-        int64_t l = orc_deflate_encode(d, n, NULL);
+        int64_t l = (p->flags & ORC_GDEFLATE) ? orc_gd_encode(d, n, NULL) : orc_deflate_encode(d, n, NULL);
         if (l >= 0 && l + 18 < best) { best = l + 18; win = 5; wl = l; }
     }
     if (pref_ok(p, 9, n) && n >= 1024) {          /* LZ4 should_use :298-307 */
@@ -666,7 +947,8 @@ static void put_hdr(uint8_t* o, int type, uint32_t used, uint32_t orig, uint32_t
     }
 }
 
-static int64_t encode_payload(int id, const uint8_t* d, uint32_t n, uint8_t* out) {
+static int64_t encode_payload(int id, const uint8_t* d, uint32_t n, uint8_t* out, uint32_t flags) {
+    if (id == 5 && (flags & ORC_GDEFLATE)) return orc_gd_encode(d, n, out);
     switch (id) {
     case 1: return orc_rle_encode(d, n, out);
     case 2: return orc_dict_encode(d, n, out);
@@ -732,7 +1014,7 @@ EXPORT int64_t orc_compress_body(const uint8_t* in, uint64_t n, const orc_params
         int id = ids[k];
         uint32_t clen = id == 255 ? len : pl[k];
         put_hdr(o, id, len, len, clen);
-        encode_payload(id, in + pos, len, o + 18);
+        encode_payload(id, in + pos, len, o + 18, p->flags);
     }
     for (uint64_t k = 0; k < (R < M ? R : M); k++) {
         uint64_t len = n - k * C < C ? n - k * C : C;

@@ -47,7 +47,8 @@ def lib():
         _lib = C.CDLL(LIB_PATH)
         u8p, i64, u32 = C.c_void_p, C.c_int64, C.c_uint32
         for name in ("orc_rle_encode", "orc_huff_encode", "orc_dict_encode",
-                     "orc_lz4_frame_encode", "orc_lz4_block_encode", "orc_deflate_encode"):
+                     "orc_lz4_frame_encode", "orc_lz4_block_encode", "orc_deflate_encode",
+                     "orc_gd_encode"):
             getattr(_lib, name).argtypes = [u8p, u32, u8p]
             getattr(_lib, name).restype = i64
         for name in ("orc_rle_decode", "orc_huff_decode", "orc_delta_decode", "orc_dict_decode",
@@ -59,6 +60,8 @@ def lib():
             getattr(_lib, name).argtypes = [u8p, u32]
             getattr(_lib, name).restype = C.c_int
         _lib.orc_huff_should_use.argtypes = [u8p, u32, u8p]
+        _lib.orc_gd_parse.argtypes = [u8p, u32, u8p]
+        _lib.orc_gd_parse.restype = u32
         _lib.orc_huff_should_use.restype = C.c_int
         _lib.orc_huff_entropy.argtypes = [u8p, u32, u8p]
         _lib.orc_huff_entropy.restype = C.c_double
@@ -79,7 +82,7 @@ def lib():
 
 class Params(C.Structure):
     _fields_ = [("chunk_size", C.c_uint32), ("mode", C.c_uint32), ("method_mask", C.c_uint32),
-                ("reserved", C.c_uint32), ("pref_min", C.c_uint32 * 16),
+                ("flags", C.c_uint32), ("pref_min", C.c_uint32 * 16),
                 ("pref_max", C.c_uint32 * 16), ("ent_full", C.c_void_p),
                 ("ent_tail", C.c_void_p)]
 
@@ -133,6 +136,20 @@ def lz4_frame_encode(d):
 def deflate_encode(d):
     """zlib.compress(d, level=9) through the same system zlib CPython links."""
     return _call_enc("orc_deflate_encode", d, len(d) + len(d) // 1000 + 64)
+
+
+def gdeflate_encode(d):
+    """"ambc-deflate v1" (the GPU engine's id-5 encoder) -> zlib stream."""
+    return _call_enc("orc_gd_encode", d, len(d) + 5 * (len(d) // 65535 + 1) + 64)
+
+
+def gd_parse(d):
+    """"ambc-deflate v1" greedy parse -> list of (pos, length, distance)."""
+    L = lib()
+    src = _buf(d)
+    out = (C.c_uint32 * (3 * (len(d) // 4 + 2)))()
+    ns = L.orc_gd_parse(C.addressof(src), len(d), C.addressof(out))
+    return [tuple(out[3 * i:3 * i + 3]) for i in range(ns)]
 
 
 def lz4_block_encode(d):
@@ -192,12 +209,18 @@ def random_bytes(n, seed):
     return bytes(out[:n])
 
 
+ORC_GDEFLATE = 1
+
+
 def make_params(chunk, mode="native", methods=(1, 3, 4, 255), prefs=None, n_total=None,
-                exact_entropy=True):
+                exact_entropy=True, deflate="zlib"):
+    """deflate: which id-5 encoder -- "zlib" (zlib.compress level 9, the
+    reference's) or "gd" ("ambc-deflate v1", the GPU engine's)."""
     prefs = PREFS if prefs is None else prefs
     p = Params()
     p.chunk_size = chunk
     p.mode = 1 if mode == "reference" else 0
+    p.flags = ORC_GDEFLATE if deflate == "gd" else 0
     mask = 0
     for m in methods:
         if m < 16:
