@@ -9,8 +9,11 @@ exceptions raised like the reference's.
   libambc_hip (single-chunk calls of the same kernels the batched path uses);
 * id 2 (Dictionary) decodes on the GPU; its encoder is SURVEY §8(f) "next";
 * ids 5, 6, 7 are the reference's own stdlib library wrappers
-  (advanced_compression.py:71-213) -- the selector never routes to them, they
-  are registered so that reference-produced files holding such chunks decode.
+  (advanced_compression.py:71-213), registered so that reference-produced files
+  holding such chunks decode.  When id 5 is among ``methods`` the batched engine
+  selects and encodes it on the GPU with "ambc-deflate v1" (k_deflate: a valid
+  zlib stream that this wrapper and the reference decode, not zlib level-9
+  bytes); the per-chunk plugin itself keeps the reference's zlib.compress.
 
 The batched engine (compressor.py) does not call these per chunk: it makes one
 C-ABI call for the whole body.
@@ -276,7 +279,8 @@ class LZMACompression(CompressionMethod):
             return bytes(original_length)
 
 
-GPU_METHODS = {1: RLECompression, 3: HuffmanCompression, 4: DeltaCompression, 9: LZ4Compression}
+GPU_METHODS = {1: RLECompression, 3: HuffmanCompression, 4: DeltaCompression,
+               5: DeflateCompression, 9: LZ4Compression}
 DECODE_METHODS = {1: RLECompression, 2: DictionaryCompression, 3: HuffmanCompression,
                   4: DeltaCompression, 5: DeflateCompression, 6: Bzip2Compression,
                   7: LZMACompression, 9: LZ4Compression, 255: NoCompression}

@@ -79,7 +79,7 @@ struct Dev {
     hipStream_t xs[2] = {};     // copy streams of the slab pipeline: H2D, D2H
     hipEvent_t xev[6] = {};     // h2d_done[2], comp_done[2], d2h_done[2]
     Buf in, out, slots, plen, ids, sizes, off, scan_tmp, acc, ent_full, ent_tail;
-    Buf body, jobs, produced, dout, scratch, seg, list;
+    Buf body, jobs, produced, dout, scratch, seg, list, bestpre;
     uint64_t t_encode = 0, t_scan = 0, t_compact = 0;
 };
 
@@ -146,7 +146,7 @@ void ambc_destroy(ambc_ctx* ctx) {
         (void)hipStreamSynchronize(d.stream);
         for (Buf* b : {&d.in, &d.out, &d.slots, &d.plen, &d.ids, &d.sizes, &d.off, &d.scan_tmp,
                        &d.acc, &d.ent_full, &d.ent_tail, &d.body, &d.jobs, &d.produced, &d.dout,
-                       &d.scratch, &d.seg, &d.list})
+                       &d.scratch, &d.seg, &d.list, &d.bestpre})
             b->release();
         for (auto& ev : d.ev) (void)hipEventDestroy(ev);
         for (auto& ev : d.xev) (void)hipEventDestroy(ev);
@@ -173,9 +173,11 @@ static int check_params(const ambc_params* p) {
         return fail(AMBC_E_INVAL, "chunk_size must be a multiple of 16 in [16, 65536]");
     if (p->mode > 1) return fail(AMBC_E_INVAL, "mode must be AMBC_MODE_NATIVE or AMBC_MODE_REFERENCE");
     const uint32_t allowed = (1u << AMBC_M_RLE) | (1u << AMBC_M_HUFFMAN) | (1u << AMBC_M_DELTA) |
-                             (1u << AMBC_M_LZ4);
+                             (1u << AMBC_M_DEFLATE) | (1u << AMBC_M_LZ4);
     if (p->method_mask & ~allowed)
-        return fail(AMBC_E_INVAL, "method_mask holds ids without a GPU encoder (allowed: 1, 3, 4, 9)");
+        return fail(AMBC_E_INVAL, "method_mask holds ids without a GPU encoder (allowed: 1, 3, 4, 5, 9)");
+    if (((p->method_mask >> AMBC_M_DEFLATE) & 1) && C > 16384)
+        return fail(AMBC_E_INVAL, "the GPU DEFLATE encoder supports chunk_size <= 16384");
     return AMBC_OK;
 }
 
@@ -236,8 +238,14 @@ static int compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_param
         HIPCHK(hipMemsetAsync(d.seg.p, 0, (size_t)M * 64, s));
         ea.stamps = d.seg.as<unsigned long long>();
     }
+    const bool deflate = (p->method_mask >> AMBC_M_DEFLATE) & 1;
+    if (deflate) {
+        HIPCHK(d.bestpre.ensure((size_t)std::max<uint32_t>(M, 1) * 4));
+        ea.bestpre = d.bestpre.as<uint32_t>();
+    }
     HIPCHK(hipEventRecord(d.ev[0], s));
     HIPCHK(launch_encode(ea, s));
+    if (deflate) HIPCHK(launch_deflate(ea, s));   // id 5 after 1/3/4, against LZ4 (ties -> 5)
     HIPCHK(hipEventRecord(d.ev[1], s));
     if (ea.stamps) {
         stamps.resize((size_t)M * 8);

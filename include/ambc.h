@@ -60,6 +60,7 @@ extern "C" {
 #define AMBC_M_DICT 2  /* decode only (encoder: SURVEY §8(f) next) */
 #define AMBC_M_HUFFMAN 3
 #define AMBC_M_DELTA 4 /* never selected: payload length == n (compression_methods.py:598-608) */
+#define AMBC_M_DEFLATE 5 /* GPU encoder "ambc-deflate v1" (chunk_size <= 16384); decode: host zlib */
 #define AMBC_M_LZ4 9
 #define AMBC_M_RAW 255
 

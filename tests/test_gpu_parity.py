@@ -384,3 +384,56 @@ def test_deflate_chunks_decode(ctx):
     body = b"".join(parts) + b"\xff\xff\x00\x00\x00\x00" + bytes(10)
     want = orc.decompress_body(body, orig_total)
     assert comp._adaptive_decompress(body, orig_total) == want
+
+
+# ---------------------------------------------------------------------------
+# id 5 on the GPU: "ambc-deflate v1" (k_deflate) against the oracle's
+# restatement, byte for byte, inside the whole selector; every stream inflates
+# with zlib (what the reference's DeflateCompression.decompress calls)
+# ---------------------------------------------------------------------------
+GD_CASES = [((1 << 20) + 77, 20250418, 4096, (1, 3, 4, 5, 9)), ((1 << 20) + 5, 3, 1024, (1, 3, 5)),
+            (600000, 8, 8192, (5,)), (700001, 9, 16384, (1, 3, 4, 5, 9)), (300000, 10, 2048, (3, 5, 9)),
+            (250000, 12, 4096, (5, 9))]
+
+
+@pytest.mark.parametrize("n,seed,chunk,methods", GD_CASES)
+def test_gdeflate_bodies_match_oracle(ctx, n, seed, chunk, methods):
+    import zlib
+    data = synth.generate(n, seed)
+    for mode in ("native", "reference"):
+        comp = _compressor(chunk_size=chunk, mode=mode, methods=methods)
+        body = comp._adaptive_compress(data)
+        p = orc.make_params(chunk, mode, methods, n_total=n, deflate="gd")
+        ref, st = orc.compress_body(data, p, nthreads=0)
+        assert body == ref, (mode, n, chunk, methods)
+        gst = comp._last_device_stats
+        assert [gst.method_usage[i] for i in (1, 3, 5, 9)] == [st.method_usage[i] for i in (1, 3, 5, 9)]
+        assert comp._adaptive_decompress(body, n) == data
+    # every id-5 package is a valid zlib stream of its chunk
+    pos = off = 0
+    seen = 0
+    while pos + 18 <= len(body) and body[pos + 4] != 0:
+        t = body[pos + 4]
+        orig = int.from_bytes(body[pos + 10:pos + 14], "little")
+        clen = int.from_bytes(body[pos + 14:pos + 18], "little")
+        if t == 5:
+            assert zlib.decompress(body[pos + 18:pos + 18 + clen]) == data[off:off + orig]
+            seen += 1
+        pos += 18 + clen
+        off += orig
+    assert seen > 0
+
+
+def test_gdeflate_edge_chunks(ctx):
+    """zero runs (258-splits), periodic data with overlapping matches, 1-symbol
+    and uniform histograms (should_use False), tiny tails below 64 bytes."""
+    edge = [bytes(16384), b"ab" * 8192, bytes(range(256)) * 64, b"\x07" * 5000 + bytes(range(256)) * 8,
+            synth.random_bytes(20000, 4) + bytes(3000) + b"xyz" * 2000, b"q" * 4159]
+    for d in edge:
+        for chunk in (1024, 4096):
+            comp = _compressor(chunk_size=chunk, methods=(1, 3, 5, 9))
+            body = comp._adaptive_compress(d)
+            ref, _ = orc.compress_body(d, orc.make_params(chunk, "native", (1, 3, 5, 9), n_total=len(d),
+                                                           deflate="gd"), nthreads=0)
+            assert body == ref, (len(d), chunk)
+            assert comp._adaptive_decompress(body, len(d)) == d
