@@ -42,6 +42,31 @@ __constant__ uint8_t c_dext[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6,
                                    6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
 __constant__ uint8_t c_clord[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
+#ifdef AMBC_STAMPS
+// diagnostic build only: per-chunk phase cycles in A.stamps[(M + k) * 8 + phase]
+#define GSTAMP_DECL uint64_t _st_t = __builtin_amdgcn_s_memtime(); uint64_t _acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define GSTAMP(ph)                                                 \
+    do {                                                           \
+        __builtin_amdgcn_s_waitcnt(0xC07F);                        \
+        const uint64_t _t = __builtin_amdgcn_s_memtime();          \
+        _acc[ph] += _t - _st_t;                                    \
+        _st_t = _t;                                                \
+    } while (0)
+#define GSTAMP_FLUSH                                               \
+    if (lane == 0 && A.stamps)                                     \
+        for (int _p = 0; _p < 8; _p++) A.stamps[((uint64_t)A.n_chunks + k) * 8 + _p] = _acc[_p];
+#else
+#define GSTAMP_DECL
+#define GSTAMP(ph) do {} while (0)
+#define GSTAMP_FLUSH
+#endif
+
+#define GRET             \
+    do {                 \
+        GSTAMP_FLUSH;    \
+        return;          \
+    } while (0)
+
 constexpr uint32_t GD_LCAP = 32;  // per-lane precomputed match length; longer ones extend in the walk
 
 // length symbol index (0..28) of a match length 3..258
@@ -68,6 +93,11 @@ __device__ __forceinline__ uint32_t ld32(const uint8_t* base, uint32_t i) {
     return __builtin_amdgcn_alignbyte(w[a + 1], w[a], i & 3);
 }
 
+// v_writelane stand-in: lane `idx` (uniform) takes `val`
+__device__ __forceinline__ uint32_t wlane(uint32_t old, uint32_t idx, uint32_t val, uint32_t lane) {
+    return lane == idx ? val : old;
+}
+
 // OR nb (<= 32) bits of v into an LSB-first bit stream of u32 words at bit b
 __device__ __forceinline__ void put_bits_atomic(uint32_t* words, uint32_t b, uint32_t v, uint32_t nb) {
     if (!nb) return;
@@ -85,7 +115,7 @@ __device__ __forceinline__ void put_bits_plain(uint32_t* words, uint32_t b, uint
 
 template <int CMAX>
 struct GdSmem {
-    static constexpr int REGION = (CMAX > 4608 ? CMAX : 4608) + 64;
+    static constexpr int REGION = (CMAX > 5120 ? CMAX : 5120) + 64;
     static constexpr int MAXSEQ = CMAX / 4 + 2;
     static constexpr int ROUNDS = (CMAX + 63) / 64;
     alignas(16) uint8_t chunk[CMAX + 64];  // zero padded
@@ -100,16 +130,19 @@ struct GdSmem {
     uint8_t rs[320], re[320];              // code-length RLE: symbols, extra values
     uint32_t blc[24];
     uint32_t misc[8];
+    unsigned long long bk[256];            // parse: lane masks per 8-bit hash bucket
 };
 
 // Huffman code lengths of freq[0..nsym) limited to maxbits (see the file
-// header), on one wave.  scratch: >= 4608 bytes of LDS.
-__device__ void gd_lengths(const uint32_t* freq, int nsym, int maxbits, uint8_t* len, uint32_t* scratch,
-                           uint32_t* blc, uint32_t lane) {
+// header), on one wave.  scratch: >= 5120 bytes of LDS.
+template <int NSYM>
+__device__ __forceinline__ void gd_lengths(const uint32_t* freq, int maxbits, uint8_t* len, uint32_t* scratch,
+                                           uint32_t* blc, uint32_t lane) {
+    constexpr int nsym = NSYM;
     uint16_t* sorted = reinterpret_cast<uint16_t*>(scratch);       // 320 x u16
     uint32_t* w = scratch + 160;                                   // 640 x u32
     uint16_t* parent = reinterpret_cast<uint16_t*>(scratch + 800); // 640 x u16
-    constexpr int J = 5;  // symbols lane + 64 j, nsym <= 320
+    constexpr int J = (NSYM + 63) / 64;  // symbols lane + 64 j
     uint32_t f[J];
     uint32_t used = 0;
 #pragma unroll
@@ -127,49 +160,98 @@ __device__ void gd_lengths(const uint32_t* freq, int nsym, int maxbits, uint8_t*
             if (f[j]) len[lane + 64 * j] = 1;
         return;
     }
-    // rank of every used symbol among (freq, symbol)
+    // used symbols compacted as (freq << 9 | symbol) keys, then ranked
+    uint32_t* keys = scratch + 960;  // 320 x u32 (after parent[])
+    {
+        const uint64_t lt = (1ull << lane) - 1;
+        uint32_t base = 0;
+#pragma unroll
+        for (int j = 0; j < J; j++) {
+            const uint64_t m = __ballot(f[j] != 0);
+            if (f[j]) keys[base + (uint32_t)__popcll(m & lt)] = f[j] << 9 | (uint32_t)(lane + 64 * j);
+            base += (uint32_t)__popcll(m);
+        }
+    }
+    wave_sync();
 #pragma unroll
     for (int j = 0; j < J; j++) {
-        const uint32_t s = lane + 64 * j;
         if (f[j]) {
+            const uint32_t key = f[j] << 9 | (uint32_t)(lane + 64 * j);
             uint32_t r = 0;
-            for (int t = 0; t < nsym; t++) {
-                const uint32_t ft = freq[t];
-                r += ft && (ft < f[j] || (ft == f[j] && (uint32_t)t < s));
-            }
-            sorted[r] = (uint16_t)s;
+#pragma unroll 4
+            for (uint32_t t = 0; t < k; t++) r += keys[t] < key;
+            sorted[r] = (uint16_t)(lane + 64 * j);
             w[r] = f[j];
         }
     }
     wave_sync();
-    // two-queue construction (serial): leaves 0..k-1, internal k..2k-2
-    if (lane == 0) {
-        uint32_t a = 0, b = k, nb = k;
+    for (int i = lane; i < 24; i += 64) blc[i] = 0;
+    bool deep = true;  // a leaf deeper than maxbits: the bl_count fix-up runs
+    if (k <= 64) {
+        // two-queue construction in registers: leaf i and internal node t live
+        // in lane i / lane t; the fronts are read with v_readlane, new nodes
+        // written with lane selects (no LDS round trips on the serial chain)
+        const uint32_t INF = 0xFFFFFFFFu;
+        const uint32_t wl = lane < k ? w[lane] : INF;
+        uint32_t wi = INF, pl = 0, pi = 0, di = 0;
+        uint32_t a = 0, b = 0, nb = 0;
         for (uint32_t m = 0; m + 1 < k; m++) {
-            uint32_t pick[2];
+            uint32_t sum = 0;
 #pragma unroll
             for (int t = 0; t < 2; t++) {
-                const bool leaf = a < k && (b >= nb || w[a] <= w[b]);
-                pick[t] = leaf ? a++ : b++;
+                const uint32_t va = a < k ? readlane(wl, a) : INF;
+                const uint32_t vb = b < nb ? readlane(wi, b) : INF;
+                if (a < k && (b >= nb || va <= vb)) {
+                    pl = wlane(pl, a, nb, lane);
+                    sum += va;
+                    a++;
+                } else {
+                    pi = wlane(pi, b, nb, lane);
+                    sum += vb;
+                    b++;
+                }
             }
-            w[nb] = w[pick[0]] + w[pick[1]];
-            parent[pick[0]] = (uint16_t)nb;
-            parent[pick[1]] = (uint16_t)nb;
+            wi = wlane(wi, nb, sum, lane);
             nb++;
         }
-        // depths of the internal nodes, root first (stored in w[], reused)
-        w[nb - 1] = 0;
-        for (int i = (int)nb - 2; i >= (int)k; i--) w[i] = w[parent[i]] + 1;
+        // depths of the internal nodes from the root (node nb - 1) down
+        di = wlane(di, nb - 1, 0u, lane);
+        for (int t = (int)nb - 2; t >= 0; t--) {
+            const uint32_t d = readlane(di, readlane(pi, (uint32_t)t)) + 1;
+            di = wlane(di, (uint32_t)t, d, lane);
+        }
+        const uint32_t dleaf = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pl << 2), (int)di) + 1;
+        wave_sync();
+        if (lane < k) atomicAdd(&blc[dleaf > 23 ? 23 : dleaf], 1u);
+        deep = wave_max_i32(lane < k ? (int)dleaf : 0) > maxbits;
+    } else {
+        // two-queue construction (serial, LDS): leaves 0..k-1, internal k..2k-2
+        if (lane == 0) {
+            uint32_t a = 0, b = k, nb = k;
+            for (uint32_t m = 0; m + 1 < k; m++) {
+                uint32_t pick[2];
+#pragma unroll
+                for (int t = 0; t < 2; t++) {
+                    const bool leaf = a < k && (b >= nb || w[a] <= w[b]);
+                    pick[t] = leaf ? a++ : b++;
+                }
+                w[nb] = w[pick[0]] + w[pick[1]];
+                parent[pick[0]] = (uint16_t)nb;
+                parent[pick[1]] = (uint16_t)nb;
+                nb++;
+            }
+            // depths of the internal nodes, root first (stored in w[], reused)
+            w[nb - 1] = 0;
+            for (int i = (int)nb - 2; i >= (int)k; i--) w[i] = w[parent[i]] + 1;
+        }
+        wave_sync();
+        for (uint32_t i = lane; i < k; i += 64) {
+            const uint32_t d = w[parent[i]] + 1;
+            atomicAdd(&blc[d > 23 ? 23 : d], 1u);
+        }
     }
     wave_sync();
-    for (int i = lane; i < 24; i += 64) blc[i] = 0;
-    wave_sync();
-    for (uint32_t i = lane; i < k; i += 64) {
-        const uint32_t d = w[parent[i]] + 1;
-        atomicAdd(&blc[d > 23 ? 23 : d], 1u);
-    }
-    wave_sync();
-    if (lane == 0) {
+    if (deep && lane == 0) {
         for (int d = maxbits + 1; d < 24; d++) { blc[maxbits] += blc[d]; blc[d] = 0; }
         uint64_t total = 0;
         for (int d = 1; d <= maxbits; d++) total += (uint64_t)blc[d] << (maxbits - d);
@@ -196,8 +278,10 @@ __device__ void gd_lengths(const uint32_t* freq, int nsym, int maxbits, uint8_t*
 }
 
 // canonical codes of len[0..nsym) (RFC 1951 3.2.2), bit-reversed
-__device__ void gd_codes(const uint8_t* len, int nsym, uint16_t* rcode, uint32_t* blc, uint32_t lane) {
-    constexpr int J = 5;
+template <int NSYM>
+__device__ __forceinline__ void gd_codes(const uint8_t* len, uint16_t* rcode, uint32_t* blc, uint32_t lane) {
+    constexpr int nsym = NSYM;
+    constexpr int J = (NSYM + 63) / 64;
     for (int i = lane; i < 24; i += 64) blc[i] = 0;
     wave_sync();
     uint32_t l[J];
@@ -221,19 +305,60 @@ __device__ void gd_codes(const uint8_t* len, int nsym, uint16_t* rcode, uint32_t
 #pragma unroll
     for (int b = 0; b < 16; b++) seen[b] = 0;
     const uint64_t lt = (1ull << lane) - 1;
+    uint32_t lmax = 0;
+#pragma unroll
+    for (int j = 0; j < J; j++) lmax = max(lmax, l[j]);
+    lmax = (uint32_t)wave_max_i32((int)lmax);
 #pragma unroll
     for (int j = 0; j < J; j++) {
         const int s = lane + 64 * j;
         uint32_t code = 0;
 #pragma unroll
         for (int b = 1; b < 16; b++) {
-            const uint64_t m = __ballot(l[j] == (uint32_t)b);
-            if (l[j] == (uint32_t)b) code = blc[b] + seen[b] + (uint32_t)__popcll(m & lt);
-            seen[b] += (uint32_t)__popcll(m);
+            if ((uint32_t)b <= lmax) {  // uniform
+                const uint64_t m = __ballot(l[j] == (uint32_t)b);
+                if (l[j] == (uint32_t)b) code = blc[b] + seen[b] + (uint32_t)__popcll(m & lt);
+                seen[b] += (uint32_t)__popcll(m);
+            }
         }
         if (s < nsym) rcode[s] = l[j] ? (uint16_t)(__builtin_bitreverse32(code) >> (32 - l[j])) : 0;
     }
     wave_sync();
+}
+
+// one run of rr equal code lengths v -> code-length symbols at rs/re[o..];
+// returns the new count (the rule of the file header / orc_gd: gd_rle)
+__device__ __forceinline__ uint32_t rle_flush(uint8_t* rs, uint8_t* re, uint32_t o, uint32_t v, uint32_t rr,
+                                              uint32_t lane) {
+    const bool w = lane == 0;
+    if (v == 0) {
+        while (rr >= 11) {
+            const uint32_t t = min(rr, 138u);
+            if (w) { rs[o] = 18; re[o] = (uint8_t)(t - 11); }
+            o++;
+            rr -= t;
+        }
+        if (rr >= 3) {
+            if (w) { rs[o] = 17; re[o] = (uint8_t)(rr - 3); }
+            o++;
+            rr = 0;
+        }
+        for (; rr > 0; rr--, o++)
+            if (w) { rs[o] = 0; re[o] = 0; }
+    } else {
+        if (w) { rs[o] = (uint8_t)v; re[o] = 0; }
+        o++;
+        rr--;
+        while (rr >= 3) {
+            const uint32_t t = min(rr, 6u);
+            if (w) { rs[o] = 16; re[o] = (uint8_t)(t - 3); }
+            o++;
+            rr -= t;
+        }
+        for (; rr > 0; rr--, o++)
+            if (w) { rs[o] = (uint8_t)v; re[o] = 0; }
+    }
+    return o;
 }
 
 template <int CMAX>
@@ -244,17 +369,20 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     const uint32_t k = blockIdx.x;
     const uint64_t pos0 = (uint64_t)k * A.chunk_size;
     const uint32_t n = (uint32_t)min((uint64_t)A.chunk_size, A.n_total - pos0);
+    GSTAMP_DECL
     // prefs gate (adaptive_compressor.py:565-567) and should_use's n >= 64
-    if (!((A.method_mask >> 5) & 1) || n < A.pref_min[5] || n > A.pref_max[5] || n < 64) return;
+    if (!((A.method_mask >> 5) & 1) || n < A.pref_min[5] || n > A.pref_max[5] || n < 64) GRET;
     const uint32_t w0 = A.ids[k];
-    const uint32_t bestpre = A.bestpre[k];
+    const uint32_t bp0 = A.bestpre[k];
+    if (bp0 >> 31) GRET;  // calculate_entropy == 8.0: should_use is False (k_encode's histogram)
+    const uint32_t bestpre = bp0;
     // id 5 wins iff len + 18 < T (ties against an LZ4 winner go to id 5)
     const uint32_t T = w0 == 9 ? min(bestpre, A.plen[k] + 18 + 1) : bestpre;
-    if (T <= 18 + 6) return;
+    if (T <= 18 + 6) GRET;
     const uint8_t* src = A.in + pos0;
     uint8_t* slot = A.slots + (uint64_t)k * A.slot_stride;
 
-    // ---- stage, byte histogram (should_use: entropy < 8.0 <=> not exactly uniform) ----
+    // ---- stage the chunk in LDS ----
     {
         const uint32_t nv = n >> 4;
         if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
@@ -266,31 +394,12 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
         }
         for (uint32_t i = n + lane; i < (uint32_t)CMAX + 64; i += 64) S.chunk[i] = 0;
     }
-    uint32_t* hist = S.region;
-    for (uint32_t i = lane; i < 256; i += 64) hist[i] = 0;
     wave_sync();
-    uint64_t asum = 0, bsum = 0;  // Adler-32 partial sums
-    for (uint32_t i = lane; i < n; i += 64) {
-        const uint32_t c = S.chunk[i];
-        atomicAdd(&hist[c], 1u);
-        asum += c;
-        bsum += (uint64_t)(n - i) * c;
-    }
-    wave_sync();
-    {
-        const uint32_t h0 = hist[0];
-        bool diff = false;
-        for (uint32_t i = lane; i < 256; i += 64) diff |= hist[i] != h0;
-        if (!__any(diff)) return;  // calculate_entropy == 8.0: should_use is False
-    }
-    asum = wave_sum<uint64_t>(asum);
-    bsum = wave_sum<uint64_t>(bsum);
-    const uint32_t adler = (uint32_t)(((n + bsum) % 65521) << 16 | ((1 + asum) % 65521));
-    wave_sync();
-
+    GSTAMP(0);
     // ---- parse ----
     uint16_t* last = reinterpret_cast<uint16_t*>(S.region);
     for (uint32_t i = lane; i < 2048; i += 64) last[i] = 0xFFFF;
+    for (uint32_t i = lane; i < 256; i += 64) S.bk[i] = 0;
     wave_sync();
     const int hl = (int)n - 4;  // last hashable position
     uint32_t p = 0, ns = 0;
@@ -302,11 +411,23 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
         const bool act = i <= hl;
         const uint32_t v = act ? ld32(S.chunk, (uint32_t)i) : 0u;
         const uint32_t h = (v * 2654435761u) >> 21;
-        uint64_t peers = __ballot(act);
+        // lanes with my 11-bit hash: an order-free LDS OR per 8-bit bucket, then
+        // the remaining 3 bits by ballots (one shared hash: the active mask)
+        const uint64_t actm = __ballot(act);
+        uint64_t peers;
+        if (__all(!act || h == __builtin_amdgcn_readfirstlane(h))) {
+            peers = act ? actm : 0ull;
+        } else {
+            if (act) atomicOr(&S.bk[h & 255], 1ull << lane);
+            wave_sync();
+            peers = act ? S.bk[h & 255] : 0ull;
 #pragma unroll
-        for (int b = 0; b < 11; b++) {
-            const uint64_t m = __ballot((h >> b) & 1u);
-            peers &= ((h >> b) & 1u) ? m : ~m;
+            for (int b = 8; b < 11; b++) {
+                const uint64_t m = __ballot((h >> b) & 1u);
+                peers &= ((h >> b) & 1u) ? m : ~m;
+            }
+            wave_sync();
+            if (act) S.bk[h & 255] = 0;
         }
         const uint64_t lower = lane ? (peers & ((1ull << lane) - 1)) : 0ull;
         int cand;
@@ -320,7 +441,7 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
         wave_sync();
         if (act && (peers >> lane) == 1ull) last[h] = (uint16_t)i;
         uint32_t L = 0;
-        if (valid) {
+        if (valid && (uint32_t)i >= p) {  // the walk never looks below p
             const uint32_t lim = min(258u, n - (uint32_t)i);
             L = 4;
             while (L < GD_LCAP && L < lim) {
@@ -334,42 +455,51 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
         uint64_t selm = 0;
         const uint32_t ns0 = ns;
         if (p < (uint32_t)base + 64) {
-            // scalar greedy walk over this round's positions
+            // scalar greedy walk over this round's positions: one v_readlane per
+            // match; a match longer than GD_LCAP is extended by the whole wave
             while (p < (uint32_t)base + 64 && p < n) {
                 const uint64_t m = vm >> (p - (uint32_t)base);
                 if (!m) { p = (uint32_t)base + 64; break; }
                 p += (uint32_t)__builtin_ctzll(m);
                 const uint32_t l = p - (uint32_t)base;
                 uint32_t Lp = readlane(L, l);
-                const uint32_t c = readlane((uint32_t)cand, l);
-                const uint32_t lim = min(258u, n - p);
-                if (Lp >= GD_LCAP && Lp < lim) {
-                    // extend with the whole wave: 64 dwords per step
-                    for (;;) {
-                        const uint32_t off = Lp + 4 * lane;
-                        const uint32_t x = off < lim ? (ld32(S.chunk, c + off) ^ ld32(S.chunk, p + off)) : 1u;
-                        const uint64_t mm = __ballot(x != 0);
-                        if (mm) {
-                            const uint32_t f = (uint32_t)__builtin_ctzll(mm);
-                            const uint32_t xf = readlane(x, f);
-                            Lp += 4 * f + ((uint32_t)__builtin_ctz(xf) >> 3);
-                            break;
+                if (Lp >= GD_LCAP) {
+                    const uint32_t lim = min(258u, n - p);
+                    if (Lp < lim) {
+                        const uint32_t c = readlane((uint32_t)cand, l);
+                        for (;;) {
+                            const uint32_t off = Lp + 4 * lane;
+                            const uint32_t x = off < lim ? (ld32(S.chunk, c + off) ^ ld32(S.chunk, p + off)) : 1u;
+                            const uint64_t mm = __ballot(x != 0);
+                            if (mm) {
+                                const uint32_t f = (uint32_t)__builtin_ctzll(mm);
+                                const uint32_t xf = readlane(x, f);
+                                Lp += 4 * f + ((uint32_t)__builtin_ctz(xf) >> 3);
+                                break;
+                            }
+                            Lp += 256;
                         }
-                        Lp += 256;
+                        Lp = min(Lp, lim);
+                        L = wlane(L, l, Lp, lane);
                     }
-                    Lp = min(Lp, lim);
                 }
-                if (lane == 0) { S.slen[ns] = (uint16_t)Lp; S.sdist[ns] = (uint16_t)(p - c); }
                 selm |= 1ull << l;
-                ns++;
                 p += Lp;
             }
         }
+        // the selected matches record themselves, in position order
+        if ((selm >> lane) & 1) {
+            const uint32_t si = ns0 + (uint32_t)__popcll(selm & ((1ull << lane) - 1));
+            S.slen[si] = (uint16_t)L;
+            S.sdist[si] = (uint16_t)(i - cand);
+        }
+        ns = ns0 + (uint32_t)__popcll(selm);
         if (lane == 0) { S.sel[r] = selm; S.sbase[r] = (uint16_t)ns0; }
     }
     const uint32_t nrounds = (n + 63) / 64;
     wave_sync();
 
+    GSTAMP(1);
     // ---- symbol frequencies ----
     for (uint32_t i = lane; i < 288; i += 64) S.lf[i] = 0;
     if (lane < 32) S.df[lane] = 0;
@@ -382,6 +512,7 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
         for (uint32_t r = 0; r < nrounds; r++) {
             const uint32_t i = r * 64 + lane;
             const uint64_t sm = S.sel[r];
+            if (!sm && carry >= (int)(r * 64 + 64)) continue;  // inside one match
             const bool st = (sm >> lane) & 1;
             int e = 0;
             if (st) {
@@ -402,6 +533,7 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     if (lane == 0) S.lf[256] = 1;
     wave_sync();
 
+    GSTAMP(2);
     // ---- fixed size and the dynamic lower bound ----
     uint64_t fixb = 0;
     double ent = 0.0;
@@ -423,8 +555,9 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     const uint32_t nblk = (n + 65534) / 65535;
     const uint32_t sto_bytes = n + 5 * nblk;
     const bool dyn_possible = lb_bytes + 6 + 18 < T;
-    if (!dyn_possible && fix_bytes + 6 + 18 >= T) return;  // cannot win
+    if (!dyn_possible && fix_bytes + 6 + 18 >= T) GRET;  // cannot win
 
+    GSTAMP(3);
     // ---- dynamic code ----
     uint32_t dyn_bytes = 0xFFFFFFFFu;
     uint32_t hlit = 257, hdist = 1, hclen = 4, nr = 0;
@@ -438,8 +571,10 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
                 if (!S.df[i]) { S.df[i] = 1; S.misc[i] = 1; used++; }
         }
         wave_sync();
-        gd_lengths(S.lf, 286, 15, S.ll, S.region, S.blc, lane);
-        gd_lengths(S.df, 30, 15, S.dl, S.region, S.blc, lane);
+        GSTAMP(4);
+        gd_lengths<286>(S.lf, 15, S.ll, S.region, S.blc, lane);
+        gd_lengths<30>(S.df, 15, S.dl, S.region, S.blc, lane);
+        GSTAMP(6);
         if (lane == 0) {  // the forced distance frequencies do not count as symbols
             for (int i = 0; i < 2; i++) if (S.misc[i] == 1) S.df[i] = 0;
         }
@@ -453,33 +588,49 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
             if (lane < 30 && S.dl[lane]) hd = (int)lane + 1;
             hdist = (uint32_t)max(1, wave_max_i32(hd));
         }
-        // code-length RLE (serial, lane 0)
-        if (lane == 0) {
+        // code-length RLE: the HLIT + HDIST lengths held 5 per lane (entry
+        // e = 64 j + lane), walked on the scalar unit with v_readlane
+        {
             const uint32_t cnt = hlit + hdist;
-            auto L = [&](uint32_t q) { return q < hlit ? S.ll[q] : S.dl[q - hlit]; };
-            uint32_t q = 0, o = 0;
-            while (q < cnt) {
-                const uint32_t v = L(q);
-                uint32_t rr = 1;
-                while (q + rr < cnt && L(q + rr) == v) rr++;
-                q += rr;
-                if (v == 0) {
-                    while (rr >= 11) { const uint32_t t = min(rr, 138u); S.rs[o] = 18; S.re[o++] = (uint8_t)(t - 11); rr -= t; }
-                    if (rr >= 3) { S.rs[o] = 17; S.re[o++] = (uint8_t)(rr - 3); rr = 0; }
-                    while (rr > 0) { S.rs[o] = 0; S.re[o++] = 0; rr--; }
-                } else {
-                    S.rs[o] = (uint8_t)v; S.re[o++] = 0; rr--;
-                    while (rr >= 3) { const uint32_t t = min(rr, 6u); S.rs[o] = 16; S.re[o++] = (uint8_t)(t - 3); rr -= t; }
-                    while (rr > 0) { S.rs[o] = (uint8_t)v; S.re[o++] = 0; rr--; }
+            uint32_t val[5];
+#pragma unroll
+            for (int j = 0; j < 5; j++) {
+                const uint32_t e = 64 * j + lane;
+                val[j] = e < hlit ? S.ll[e] : (e < cnt ? S.dl[e - hlit] : 0u);
+            }
+            // run starts by ballot (entry e differs from e - 1), then one
+            // scalar step per run
+            uint64_t bnd[5];
+#pragma unroll
+            for (int j = 0; j < 5; j++) {
+                const uint32_t e = 64 * j + lane;
+                uint32_t prev = __shfl_up(val[j], 1);
+                if (lane == 0) prev = j ? readlane(val[j > 0 ? j - 1 : 0], 63) : 0xFFu;
+                bnd[j] = __ballot(e < cnt && val[j] != prev);
+            }
+            uint32_t o = 0, cur = readlane(val[0], 0), start = 0;
+#pragma unroll
+            for (int j = 0; j < 5; j++) {
+                uint64_t m = bnd[j];
+                while (m) {
+                    const uint32_t l = (uint32_t)__builtin_ctzll(m);
+                    m &= m - 1;
+                    const uint32_t e = 64 * j + l;
+                    if (e) o = rle_flush(S.rs, S.re, o, cur, e - start, lane);
+                    cur = readlane(val[j], l);
+                    start = e;
                 }
             }
-            S.misc[2] = o;
-            for (int i = 0; i < 19; i++) S.cf[i] = 0;
-            for (uint32_t i = 0; i < o; i++) S.cf[S.rs[i]]++;
+            o = rle_flush(S.rs, S.re, o, cur, cnt - start, lane);
+            if (lane == 0) S.misc[2] = o;
+            if (lane < 20) S.cf[lane] = 0;
+            wave_sync();
+            for (uint32_t i = lane; i < o; i += 64) atomicAdd(&S.cf[S.rs[i]], 1u);
         }
         wave_sync();
+        GSTAMP(7);
         nr = S.misc[2];
-        gd_lengths(S.cf, 19, 7, S.cl, S.region, S.blc, lane);
+        gd_lengths<19>(S.cf, 7, S.cl, S.region, S.blc, lane);
         {
             int hc = 4;
             if (lane < 19 && S.cl[c_clord[lane]]) hc = (int)lane + 1;
@@ -495,22 +646,23 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
         dynb = wave_sum<uint64_t>(dynb) + 17 + 3ull * hclen + extra;
         dyn_bytes = (uint32_t)((dynb + 7) / 8);
     }
+    GSTAMP(4);
     const int kind = (dyn_bytes <= fix_bytes && dyn_bytes <= sto_bytes) ? 2 : (fix_bytes <= sto_bytes ? 1 : 0);
     const uint32_t body = kind == 2 ? dyn_bytes : kind == 1 ? fix_bytes : sto_bytes;
     const uint32_t total = 2 + body + 4;
-    if (kind == 0 || total + 18 >= T) return;  // a stored block never beats raw
+    if (kind == 0 || total + 18 >= T) GRET;  // a stored block never beats raw
 
     // ---- emission (this chunk's winner) ----
     if (kind == 1) {  // fixed tables
         for (uint32_t s = lane; s < 288; s += 64) S.ll[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
         if (lane < 30) S.dl[lane] = 5;
         wave_sync();
-        gd_codes(S.ll, 288, S.lc, S.blc, lane);
-        gd_codes(S.dl, 30, S.dc, S.blc, lane);
+        gd_codes<288>(S.ll, S.lc, S.blc, lane);
+        gd_codes<30>(S.dl, S.dc, S.blc, lane);
     } else {
-        gd_codes(S.ll, 286, S.lc, S.blc, lane);
-        gd_codes(S.dl, 30, S.dc, S.blc, lane);
-        gd_codes(S.cl, 19, S.cc, S.blc, lane);
+        gd_codes<286>(S.ll, S.lc, S.blc, lane);
+        gd_codes<30>(S.dl, S.dc, S.blc, lane);
+        gd_codes<19>(S.cl, S.cc, S.blc, lane);
     }
     uint32_t* bits = S.region;
     const uint32_t nwords = (body + 8) / 4 + 1;
@@ -542,6 +694,7 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
         for (uint32_t r = 0; r < nrounds; r++) {
             const uint32_t i = r * 64 + lane;
             const uint64_t sm = S.sel[r];
+            if (!sm && carry >= (int)(r * 64 + 64)) continue;  // inside one match
             const bool st = (sm >> lane) & 1;
             int e = 0;
             uint32_t Lx = 0, Dx = 0, lcd = 0, dcd = 0, cost = 0;
@@ -564,10 +717,10 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
             if (lit) {
                 put_bits_atomic(bits, b, S.lc[c], S.ll[c]);
             } else if (st) {
-                put_bits_atomic(bits, b, S.lc[257 + lcd], S.ll[257 + lcd]); b += S.ll[257 + lcd];
-                put_bits_atomic(bits, b, Lx - c_lbase[lcd], c_lext[lcd]); b += c_lext[lcd];
-                put_bits_atomic(bits, b, S.dc[dcd], S.dl[dcd]); b += S.dl[dcd];
-                put_bits_atomic(bits, b, Dx - c_dbase[dcd], c_dext[dcd]);
+                const uint32_t l1 = S.ll[257 + lcd], l2 = S.dl[dcd];
+                put_bits_atomic(bits, b, S.lc[257 + lcd] | (Lx - c_lbase[lcd]) << l1, l1 + c_lext[lcd]);
+                b += l1 + c_lext[lcd];
+                put_bits_atomic(bits, b, S.dc[dcd] | (Dx - c_dbase[dcd]) << l2, l2 + c_dext[dcd]);
             }
             bp += readlane(incl, 63);
         }
@@ -575,6 +728,19 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     wave_sync();
     if (lane == 0) put_bits_plain(bits, bp, S.lc[256], S.ll[256]);
     wave_sync();
+    // ---- Adler-32 of the chunk ----
+    uint32_t adler;
+    {
+        uint64_t asum = 0, bsum = 0;
+        for (uint32_t i = lane; i < n; i += 64) {
+            const uint32_t c = S.chunk[i];
+            asum += c;
+            bsum += (uint64_t)(n - i) * c;
+        }
+        asum = wave_sum<uint64_t>(asum);
+        bsum = wave_sum<uint64_t>(bsum);
+        adler = (uint32_t)(((n + bsum) % 65521) << 16 | ((1 + asum) % 65521));
+    }
     // ---- the zlib stream into the slot ----
     const uint8_t* bb = reinterpret_cast<const uint8_t*>(bits);
     for (uint32_t i = lane; i < total; i += 64) {
@@ -590,6 +756,8 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
         A.plen[k] = total;
         A.sizes[k] = 18ull + total;
     }
+    GSTAMP(5);
+    GSTAMP_FLUSH;
 }
 
 template <int CMAX>

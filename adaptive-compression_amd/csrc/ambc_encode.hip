@@ -351,7 +351,16 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
     // "ambc-lz4 greedy v1": cand(i) = last j < i with the same 12-bit hash, valid
     // iff the 4 bytes match; greedy from the first valid position; matches start
     // at i <= n-12 and end by n-5 (LZ4 block end rules).
-    if (A.bestpre && lane == 0) A.bestpre[k] = best;
+    if (A.bestpre) {
+        // for k_deflate: the best (len + 18) before LZ4, and bit 31 = DEFLATE's
+        // should_use is False (calculate_entropy == 8.0: an exactly uniform histogram)
+        const uint32_t h0 = S.hist[0];
+        bool diff = false;
+#pragma unroll
+        for (int j = 0; j < 4; j++) diff |= S.hist[lane + 64 * j] != h0;
+        const bool uniform = !__any(diff);
+        if (lane == 0) A.bestpre[k] = best | (uniform ? 0x80000000u : 0u);
+    }
     if (eligible(9) && (force || n >= 1024) && best > 42) {
         uint16_t* last = reinterpret_cast<uint16_t*>(S.region);
         for (uint32_t i = lane; i < (1u << LZ4_HASH_BITS); i += 64) last[i] = 0xFFFF;

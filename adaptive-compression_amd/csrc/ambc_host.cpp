@@ -233,9 +233,9 @@ static int compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_param
 
     TRACE("compress_on n=%llu M=%u C=%u", (unsigned long long)n, M, C);
     std::vector<unsigned long long> stamps;
-    if (getenv("AMBC_STAMPS")) {
-        HIPCHK(d.seg.ensure((size_t)std::max<uint32_t>(M, 1) * 64));
-        HIPCHK(hipMemsetAsync(d.seg.p, 0, (size_t)M * 64, s));
+    if (getenv("AMBC_STAMPS")) {   // k_encode: M x 8 records, k_deflate: the next M x 8
+        HIPCHK(d.seg.ensure((size_t)std::max<uint32_t>(M, 1) * 128));
+        HIPCHK(hipMemsetAsync(d.seg.p, 0, (size_t)M * 128, s));
         ea.stamps = d.seg.as<unsigned long long>();
     }
     const bool deflate = (p->method_mask >> AMBC_M_DEFLATE) & 1;
@@ -256,6 +256,17 @@ static int compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_param
         fprintf(stderr, "[ambc stamps] M=%u cycles/chunk: passA %.0f huff %.0f lz4hash %.0f lz4len %.0f "
                 "lz4walk %.0f lz4tail+emit %.0f final %.0f lz4emit %.0f\n", M, sum[0] / M, sum[1] / M,
                 sum[2] / M, sum[3] / M, sum[4] / M, sum[5] / M, sum[6] / M, sum[7] / M);
+        if (deflate) {
+            std::vector<unsigned long long> g((size_t)M * 8);
+            HIPCHK(hipMemcpyAsync(g.data(), d.seg.as<unsigned long long>() + (size_t)M * 8, (size_t)M * 64,
+                                  hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            double gs[8] = {0};
+            for (size_t q = 0; q < g.size(); q++) gs[q & 7] += (double)g[q];
+            fprintf(stderr, "[ambc stamps] deflate cycles/chunk: stage %.0f parse %.0f freq %.0f "
+                    "bound %.0f trees(rest) %.0f emit %.0f lengths %.0f rle %.0f\n", gs[0] / M, gs[1] / M,
+                    gs[2] / M, gs[3] / M, gs[4] / M, gs[5] / M, gs[6] / M, gs[7] / M);
+        }
     }
 
     // reference mode: the first chunk with no winner swallows the remainder

@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--chunk", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--msets", default="-;1;3;9;1,3,4,9",
+                    help="method sets, ';'-separated ('-' = none)")
     args = ap.parse_args()
     ctx = _lib.Context()
     lib = ctx.lib
@@ -54,7 +56,8 @@ def main():
     inputs = make_inputs(n)
     for name, arr in inputs.items():
         _lib.check(lib.ambc_memcpy_h2d(ctx.h, 0, d_in, arr.ctypes.data, n), lib)
-        for mset in ((), (1,), (3,), (9,), (1, 3, 4, 9)):
+        msets = [() if m == "-" else tuple(int(x) for x in m.split(",")) for m in args.msets.split(";")]
+        for mset in msets:
             p = _lib.Params()
             p.chunk_size = args.chunk
             p.method_mask = method_mask(mset)
@@ -74,7 +77,7 @@ def main():
             ms = min(ts)
             r = {"input": name, "methods": list(mset), "encode_ms": round(ms, 3),
                  "GBps": round(n / ms / 1e6, 1), "ratio": round(olen.value / n, 4),
-                 "usage": {k: int(st.method_usage[k]) for k in (1, 3, 9) if st.method_usage[k]}}
+                 "usage": {k: int(st.method_usage[k]) for k in (1, 3, 5, 9) if st.method_usage[k]}}
             res.append(r)
             print(json.dumps(r), flush=True)
     if args.out:
