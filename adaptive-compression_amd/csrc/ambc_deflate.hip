@@ -100,6 +100,9 @@ __device__ __forceinline__ uint32_t wlane(uint32_t old, uint32_t idx, uint32_t v
 
 // OR nb (<= 32) bits of v into an LSB-first bit stream of u32 words at bit b
 __device__ __forceinline__ void put_bits_atomic(uint32_t* words, uint32_t b, uint32_t v, uint32_t nb) {
+#ifdef GD_NOATOMIC
+    return;
+#endif
     if (!nb) return;
     const uint32_t w = b >> 5, o = b & 31;
     atomicOr(&words[w], v << o);
@@ -115,13 +118,12 @@ __device__ __forceinline__ void put_bits_plain(uint32_t* words, uint32_t b, uint
 
 template <int CMAX>
 struct GdSmem {
-    static constexpr int REGION = (CMAX > 5120 ? CMAX : 5120) + 64;
-    static constexpr int MAXSEQ = CMAX / 4 + 2;
+    // parse: last[] (4 KB) + bucket masks (2 KB); trees: 5 KB; emit: bit staging
+    static constexpr int REGION = (CMAX > 6144 ? CMAX : 6144) + 64;
     static constexpr int ROUNDS = (CMAX + 63) / 64;
     alignas(16) uint8_t chunk[CMAX + 64];  // zero padded
     // parse: last[] (u16 x 2048) | trees: sorted/weights/parents | emit: bit staging
     alignas(16) uint32_t region[REGION / 4];
-    uint16_t slen[MAXSEQ], sdist[MAXSEQ];  // the parse's matches, in order
     uint64_t sel[ROUNDS];                  // match-start positions, per 64-position round
     uint16_t sbase[ROUNDS + 1];            // first match index of every round
     uint32_t lf[288], df[32], cf[20];      // symbol frequencies
@@ -130,7 +132,6 @@ struct GdSmem {
     uint8_t rs[320], re[320];              // code-length RLE: symbols, extra values
     uint32_t blc[24];
     uint32_t misc[8];
-    unsigned long long bk[256];            // parse: lane masks per 8-bit hash bucket
 };
 
 // Huffman code lengths of freq[0..nsym) limited to maxbits (see the file
@@ -173,15 +174,31 @@ __device__ __forceinline__ void gd_lengths(const uint32_t* freq, int maxbits, ui
         }
     }
     wave_sync();
+    if (k <= 64) {
+        // ranks against the k keys held one per lane (v_readlane, no LDS)
+        const uint32_t kreg = lane < k ? keys[lane] : 0u;
+        uint32_t r[J];
 #pragma unroll
-    for (int j = 0; j < J; j++) {
-        if (f[j]) {
-            const uint32_t key = f[j] << 9 | (uint32_t)(lane + 64 * j);
-            uint32_t r = 0;
+        for (int j = 0; j < J; j++) r[j] = 0;
+        for (uint32_t t = 0; t < k; t++) {
+            const uint32_t kt = readlane(kreg, t);
+#pragma unroll
+            for (int j = 0; j < J; j++) r[j] += kt < (f[j] << 9 | (uint32_t)(lane + 64 * j));
+        }
+#pragma unroll
+        for (int j = 0; j < J; j++)
+            if (f[j]) { sorted[r[j]] = (uint16_t)(lane + 64 * j); w[r[j]] = f[j]; }
+    } else {
+#pragma unroll
+        for (int j = 0; j < J; j++) {
+            if (f[j]) {
+                const uint32_t key = f[j] << 9 | (uint32_t)(lane + 64 * j);
+                uint32_t r = 0;
 #pragma unroll 4
-            for (uint32_t t = 0; t < k; t++) r += keys[t] < key;
-            sorted[r] = (uint16_t)(lane + 64 * j);
-            w[r] = f[j];
+                for (uint32_t t = 0; t < k; t++) r += keys[t] < key;
+                sorted[r] = (uint16_t)(lane + 64 * j);
+                w[r] = f[j];
+            }
         }
     }
     wave_sync();
@@ -221,9 +238,27 @@ __device__ __forceinline__ void gd_lengths(const uint32_t* freq, int maxbits, ui
             di = wlane(di, (uint32_t)t, d, lane);
         }
         const uint32_t dleaf = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(pl << 2), (int)di) + 1;
+        deep = wave_max_i32(lane < k ? (int)dleaf : 0) > maxbits;
+        if (!deep) {
+            // no length limit to enforce: bl_count by ballots, cumulative counts in
+            // registers, leaf (rank) i takes the smallest d with cum[d] > k - 1 - i
+            uint32_t cum[16];
+            uint32_t c = 0;
+#pragma unroll
+            for (int d = 1; d < 16; d++) {
+                if (d <= maxbits) c += (uint32_t)__popcll(__ballot(lane < k && dleaf == (uint32_t)d));
+                cum[d] = c;
+            }
+            const uint32_t e = k - 1 - lane;
+            uint32_t d = 1;
+#pragma unroll
+            for (int t = 1; t < 16; t++) d += (t <= maxbits && cum[t] <= e) ? 1u : 0u;
+            if (lane < k) len[sorted[lane]] = (uint8_t)d;
+            wave_sync();
+            return;
+        }
         wave_sync();
         if (lane < k) atomicAdd(&blc[dleaf > 23 ? 23 : dleaf], 1u);
-        deep = wave_max_i32(lane < k ? (int)dleaf : 0) > maxbits;
     } else {
         // two-queue construction (serial, LDS): leaves 0..k-1, internal k..2k-2
         if (lane == 0) {
@@ -280,48 +315,39 @@ __device__ __forceinline__ void gd_lengths(const uint32_t* freq, int maxbits, ui
 // canonical codes of len[0..nsym) (RFC 1951 3.2.2), bit-reversed
 template <int NSYM>
 __device__ __forceinline__ void gd_codes(const uint8_t* len, uint16_t* rcode, uint32_t* blc, uint32_t lane) {
+    // canonical assignment with ballots only: for each length b (ascending) the
+    // first code follows from the previous length's first code and count, and a
+    // symbol's code adds the number of same-length symbols below it
+    (void)blc;
     constexpr int nsym = NSYM;
     constexpr int J = (NSYM + 63) / 64;
-    for (int i = lane; i < 24; i += 64) blc[i] = 0;
-    wave_sync();
-    uint32_t l[J];
+    uint32_t l[J], code[J];
+    uint32_t lmax = 0;
 #pragma unroll
     for (int j = 0; j < J; j++) {
         const int s = lane + 64 * j;
         l[j] = s < nsym ? len[s] : 0u;
-        if (l[j]) atomicAdd(&blc[l[j]], 1u);
+        code[j] = 0;
+        lmax = max(lmax, l[j]);
     }
-    wave_sync();
-    if (lane == 0) {  // next_code per length in blc[16 + ..] -- kept in registers below
-        uint32_t c = 0, prev = 0;
-        for (int b = 1; b < 16; b++) {
-            c = (c + prev) << 1;
-            prev = blc[b];
-            blc[b] = c;  // first code of length b
-        }
-    }
-    wave_sync();
-    uint32_t seen[16];
-#pragma unroll
-    for (int b = 0; b < 16; b++) seen[b] = 0;
-    const uint64_t lt = (1ull << lane) - 1;
-    uint32_t lmax = 0;
-#pragma unroll
-    for (int j = 0; j < J; j++) lmax = max(lmax, l[j]);
     lmax = (uint32_t)wave_max_i32((int)lmax);
+    const uint64_t lt = (1ull << lane) - 1;
+    uint32_t first = 0, prevcnt = 0;
+    for (uint32_t b = 1; b <= lmax; b++) {
+        first = (first + prevcnt) << 1;
+        uint32_t seen = 0;
+#pragma unroll
+        for (int j = 0; j < J; j++) {
+            const uint64_t m = __ballot(l[j] == b);
+            if (l[j] == b) code[j] = first + seen + (uint32_t)__popcll(m & lt);
+            seen += (uint32_t)__popcll(m);
+        }
+        prevcnt = seen;
+    }
 #pragma unroll
     for (int j = 0; j < J; j++) {
         const int s = lane + 64 * j;
-        uint32_t code = 0;
-#pragma unroll
-        for (int b = 1; b < 16; b++) {
-            if ((uint32_t)b <= lmax) {  // uniform
-                const uint64_t m = __ballot(l[j] == (uint32_t)b);
-                if (l[j] == (uint32_t)b) code = blc[b] + seen[b] + (uint32_t)__popcll(m & lt);
-                seen[b] += (uint32_t)__popcll(m);
-            }
-        }
-        if (s < nsym) rcode[s] = l[j] ? (uint16_t)(__builtin_bitreverse32(code) >> (32 - l[j])) : 0;
+        if (s < nsym) rcode[s] = l[j] ? (uint16_t)(__builtin_bitreverse32(code[j]) >> (32 - l[j])) : 0;
     }
     wave_sync();
 }
@@ -375,7 +401,8 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     const uint32_t w0 = A.ids[k];
     const uint32_t bp0 = A.bestpre[k];
     if (bp0 >> 31) GRET;  // calculate_entropy == 8.0: should_use is False (k_encode's histogram)
-    const uint32_t bestpre = bp0;
+    const bool single = (bp0 >> 30) & 1;   // one byte value throughout
+    const uint32_t bestpre = bp0 & 0x3FFFFFFFu;
     // id 5 wins iff len + 18 < T (ties against an LZ4 winner go to id 5)
     const uint32_t T = w0 == 9 ? min(bestpre, A.plen[k] + 18 + 1) : bestpre;
     if (T <= 18 + 6) GRET;
@@ -397,12 +424,33 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     wave_sync();
     GSTAMP(0);
     // ---- parse ----
+    // the parse's matches, in order, as (length | distance << 16) in the chunk's
+    // window of the device scratch A.gdseq (CMAX bytes: at most n/4 matches)
+    uint32_t* seq = reinterpret_cast<uint32_t*>(A.gdseq + (uint64_t)k * CMAX);
+    unsigned long long* bk = reinterpret_cast<unsigned long long*>(S.region + 1024);  // after last[]
+    uint32_t ns = 0;
+    if (single) {
+        // one byte value: the greedy parse is a literal at 0, then distance-1
+        // matches of min(258, n - p) at p = 1 + 258 j while p + 4 <= n
+        const uint32_t M = n >= 5 ? (n - 5) / 258 + 1 : 0;
+        for (uint32_t r = lane; r < (n + 63) / 64; r += 64) {
+            S.sel[r] = 0;
+            S.sbase[r] = (uint16_t)(64 * r <= 1 ? 0u : min(M, (64 * r - 2) / 258 + 1));
+        }
+        wave_sync();
+        for (uint32_t j = lane; j < M; j += 64) {
+            const uint32_t pj = 1 + 258 * j;
+            seq[j] = min(258u, n - pj) | 1u << 16;
+            atomicOr(&S.sel[pj >> 6], 1ull << (pj & 63));
+        }
+        ns = M;
+    } else {
     uint16_t* last = reinterpret_cast<uint16_t*>(S.region);
     for (uint32_t i = lane; i < 2048; i += 64) last[i] = 0xFFFF;
-    for (uint32_t i = lane; i < 256; i += 64) S.bk[i] = 0;
+    for (uint32_t i = lane; i < 256; i += 64) bk[i] = 0;
     wave_sync();
     const int hl = (int)n - 4;  // last hashable position
-    uint32_t p = 0, ns = 0;
+    uint32_t p = 0;
 #pragma unroll 1
     for (int r = 0; r < ROUNDS; r++) {
         const int base = r * 64;
@@ -418,16 +466,16 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
         if (__all(!act || h == __builtin_amdgcn_readfirstlane(h))) {
             peers = act ? actm : 0ull;
         } else {
-            if (act) atomicOr(&S.bk[h & 255], 1ull << lane);
+            if (act) atomicOr(&bk[h & 255], 1ull << lane);
             wave_sync();
-            peers = act ? S.bk[h & 255] : 0ull;
+            peers = act ? bk[h & 255] : 0ull;
 #pragma unroll
             for (int b = 8; b < 11; b++) {
                 const uint64_t m = __ballot((h >> b) & 1u);
                 peers &= ((h >> b) & 1u) ? m : ~m;
             }
             wave_sync();
-            if (act) S.bk[h & 255] = 0;
+            if (act) bk[h & 255] = 0;
         }
         const uint64_t lower = lane ? (peers & ((1ull << lane) - 1)) : 0ull;
         int cand;
@@ -490,13 +538,14 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
         // the selected matches record themselves, in position order
         if ((selm >> lane) & 1) {
             const uint32_t si = ns0 + (uint32_t)__popcll(selm & ((1ull << lane) - 1));
-            S.slen[si] = (uint16_t)L;
-            S.sdist[si] = (uint16_t)(i - cand);
+            seq[si] = L | (uint32_t)(i - cand) << 16;
         }
         ns = ns0 + (uint32_t)__popcll(selm);
         if (lane == 0) { S.sel[r] = selm; S.sbase[r] = (uint16_t)ns0; }
     }
+    }
     const uint32_t nrounds = (n + 63) / 64;
+    __threadfence_block();  // the match records (global) are read back by other lanes
     wave_sync();
 
     GSTAMP(1);
@@ -517,7 +566,8 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
             int e = 0;
             if (st) {
                 const uint32_t si = S.sbase[r] + (uint32_t)__popcll(sm & lt);
-                const uint32_t Lx = S.slen[si], Dx = S.sdist[si];
+                const uint32_t sq = seq[si];
+                const uint32_t Lx = sq & 0xFFFF, Dx = sq >> 16;
                 e = (int)(i + Lx);
                 const uint32_t lcd = gd_lcode(Lx), dcd = gd_dcode(Dx);
                 atomicAdd(&S.lf[257 + lcd], 1u);
@@ -700,8 +750,9 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
             uint32_t Lx = 0, Dx = 0, lcd = 0, dcd = 0, cost = 0;
             if (st) {
                 const uint32_t si = S.sbase[r] + (uint32_t)__popcll(sm & lt);
-                Lx = S.slen[si];
-                Dx = S.sdist[si];
+                const uint32_t sq = seq[si];
+                Lx = sq & 0xFFFF;
+                Dx = sq >> 16;
                 e = (int)(i + Lx);
                 lcd = gd_lcode(Lx);
                 dcd = gd_dcode(Dx);

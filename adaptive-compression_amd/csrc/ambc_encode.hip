@@ -354,12 +354,18 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
     if (A.bestpre) {
         // for k_deflate: the best (len + 18) before LZ4, and bit 31 = DEFLATE's
         // should_use is False (calculate_entropy == 8.0: an exactly uniform histogram)
+        // bit 30 = a single byte value (k_deflate builds that parse directly)
         const uint32_t h0 = S.hist[0];
         bool diff = false;
+        uint32_t nz = 0;
 #pragma unroll
-        for (int j = 0; j < 4; j++) diff |= S.hist[lane + 64 * j] != h0;
+        for (int j = 0; j < 4; j++) {
+            diff |= S.hist[lane + 64 * j] != h0;
+            nz += S.hist[lane + 64 * j] != 0;
+        }
         const bool uniform = !__any(diff);
-        if (lane == 0) A.bestpre[k] = best | (uniform ? 0x80000000u : 0u);
+        const bool single = wave_sum_u32(nz) == 1;
+        if (lane == 0) A.bestpre[k] = best | (uniform ? 0x80000000u : 0u) | (single ? 0x40000000u : 0u);
     }
     if (eligible(9) && (force || n >= 1024) && best > 42) {
         uint16_t* last = reinterpret_cast<uint16_t*>(S.region);

@@ -79,7 +79,7 @@ struct Dev {
     hipStream_t xs[2] = {};     // copy streams of the slab pipeline: H2D, D2H
     hipEvent_t xev[6] = {};     // h2d_done[2], comp_done[2], d2h_done[2]
     Buf in, out, slots, plen, ids, sizes, off, scan_tmp, acc, ent_full, ent_tail;
-    Buf body, jobs, produced, dout, scratch, seg, list, bestpre;
+    Buf body, jobs, produced, dout, scratch, seg, list, bestpre, gdseq;
     uint64_t t_encode = 0, t_scan = 0, t_compact = 0;
 };
 
@@ -146,7 +146,7 @@ void ambc_destroy(ambc_ctx* ctx) {
         (void)hipStreamSynchronize(d.stream);
         for (Buf* b : {&d.in, &d.out, &d.slots, &d.plen, &d.ids, &d.sizes, &d.off, &d.scan_tmp,
                        &d.acc, &d.ent_full, &d.ent_tail, &d.body, &d.jobs, &d.produced, &d.dout,
-                       &d.scratch, &d.seg, &d.list, &d.bestpre})
+                       &d.scratch, &d.seg, &d.list, &d.bestpre, &d.gdseq})
             b->release();
         for (auto& ev : d.ev) (void)hipEventDestroy(ev);
         for (auto& ev : d.xev) (void)hipEventDestroy(ev);
@@ -242,6 +242,10 @@ static int compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_param
     if (deflate) {
         HIPCHK(d.bestpre.ensure((size_t)std::max<uint32_t>(M, 1) * 4));
         ea.bestpre = d.bestpre.as<uint32_t>();
+        uint32_t cmax = 1024;                 // launch_deflate's template bucket
+        while (cmax < C) cmax <<= 1;
+        HIPCHK(d.gdseq.ensure((size_t)std::max<uint32_t>(M, 1) * cmax));
+        ea.gdseq = d.gdseq.as<uint8_t>();
     }
     HIPCHK(hipEventRecord(d.ev[0], s));
     HIPCHK(launch_encode(ea, s));

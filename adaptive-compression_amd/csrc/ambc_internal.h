@@ -29,6 +29,7 @@ struct EncArgs {
     uint32_t flags;          // ENC_FORCE: encode with the single enabled method, no gates
     unsigned long long* stamps;  // diagnostic build (-DAMBC_STAMPS): per-phase cycle sums
     uint32_t* bestpre;       // optional: best (len + 18) before LZ4 (k_deflate's threshold)
+    uint8_t* gdseq;          // k_deflate: n_chunks x chunk-size scratch for the parse's matches
     uint32_t pref_min[16];
     uint32_t pref_max[16];
 };
