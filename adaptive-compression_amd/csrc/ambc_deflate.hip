@@ -429,6 +429,9 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     uint32_t* seq = reinterpret_cast<uint32_t*>(A.gdseq + (uint64_t)k * CMAX);
     unsigned long long* bk = reinterpret_cast<unsigned long long*>(S.region + 1024);  // after last[]
     uint32_t ns = 0;
+    uint32_t extra = 0;  // extra bits of the length / distance codes
+    for (uint32_t i = lane; i < 288; i += 64) S.lf[i] = 0;
+    if (lane < 32) S.df[lane] = 0;
     if (single) {
         // one byte value: the greedy parse is a literal at 0, then distance-1
         // matches of min(258, n - p) at p = 1 + 258 j while p + 4 <= n
@@ -451,6 +454,7 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     wave_sync();
     const int hl = (int)n - 4;  // last hashable position
     uint32_t p = 0;
+    int fcarry = 0;  // max match end so far (frequency count)
 #pragma unroll 1
     for (int r = 0; r < ROUNDS; r++) {
         const int base = r * 64;
@@ -535,10 +539,24 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
                 p += Lp;
             }
         }
-        // the selected matches record themselves, in position order
-        if ((selm >> lane) & 1) {
-            const uint32_t si = ns0 + (uint32_t)__popcll(selm & ((1ull << lane) - 1));
-            seq[si] = L | (uint32_t)(i - cand) << 16;
+        // the selected matches record themselves, in position order, and the
+        // round's symbol frequencies are counted (literals: positions no match covers)
+        if (selm || fcarry < base + 64) {
+            const bool st = (selm >> lane) & 1;
+            int e = 0;
+            if (st) {
+                const uint32_t si = ns0 + (uint32_t)__popcll(selm & ((1ull << lane) - 1));
+                const uint32_t D = (uint32_t)(i - cand);
+                seq[si] = L | D << 16;
+                e = i + (int)L;
+                const uint32_t lcd = gd_lcode(L), dcd = gd_dcode(D);
+                atomicAdd(&S.lf[257 + lcd], 1u);
+                atomicAdd(&S.df[dcd], 1u);
+                extra += c_lext[lcd] + c_dext[dcd];
+            }
+            const int E = max(fcarry, wave_incl_max_i32(e));
+            fcarry = max(fcarry, wave_max_i32(e));
+            if (i < (int)n && E <= i) atomicAdd(&S.lf[S.chunk[i]], 1u);
         }
         ns = ns0 + (uint32_t)__popcll(selm);
         if (lane == 0) { S.sel[r] = selm; S.sbase[r] = (uint16_t)ns0; }
@@ -549,12 +567,8 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     wave_sync();
 
     GSTAMP(1);
-    // ---- symbol frequencies ----
-    for (uint32_t i = lane; i < 288; i += 64) S.lf[i] = 0;
-    if (lane < 32) S.df[lane] = 0;
-    wave_sync();
-    uint32_t extra = 0;
-    {
+    // ---- symbol frequencies (the general parse counted them as it went) ----
+    if (single) {
         int carry = 0;  // max match end so far
         const uint64_t lt = (1ull << lane) - 1;
 #pragma unroll 1
