@@ -424,9 +424,11 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     wave_sync();
     GSTAMP(0);
     // ---- parse ----
-    // the parse's matches, in order, as (length | distance << 16) in the chunk's
-    // window of the device scratch A.gdseq (CMAX bytes: at most n/4 matches)
-    uint32_t* seq = reinterpret_cast<uint32_t*>(A.gdseq + (uint64_t)k * CMAX);
+    // the parse's matches, in order, as (position | length << 16 | distance << 32)
+    // in the chunk's window of the device scratch A.gdseq (2 CMAX bytes: at most
+    // n/4 matches)
+    uint64_t* seq = reinterpret_cast<uint64_t*>(A.gdseq + (uint64_t)k * 2 * CMAX);
+    uint32_t mcov = 0;  // bytes the matches cover
     unsigned long long* bk = reinterpret_cast<unsigned long long*>(S.region + 1024);  // after last[]
     uint32_t ns = 0;
     uint32_t extra = 0;  // extra bits of the length / distance codes
@@ -443,10 +445,13 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
         wave_sync();
         for (uint32_t j = lane; j < M; j += 64) {
             const uint32_t pj = 1 + 258 * j;
-            seq[j] = min(258u, n - pj) | 1u << 16;
+            const uint32_t Lj = min(258u, n - pj);
+            seq[j] = pj | (uint64_t)Lj << 16 | 1ull << 32;
+            mcov += Lj;
             atomicOr(&S.sel[pj >> 6], 1ull << (pj & 63));
         }
         ns = M;
+        mcov = wave_sum_u32(mcov);
     } else {
     uint16_t* last = reinterpret_cast<uint16_t*>(S.region);
     for (uint32_t i = lane; i < 2048; i += 64) last[i] = 0xFFFF;
@@ -547,7 +552,7 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
             if (st) {
                 const uint32_t si = ns0 + (uint32_t)__popcll(selm & ((1ull << lane) - 1));
                 const uint32_t D = (uint32_t)(i - cand);
-                seq[si] = L | D << 16;
+                seq[si] = (uint64_t)i | (uint64_t)L << 16 | (uint64_t)D << 32;
                 e = i + (int)L;
                 const uint32_t lcd = gd_lcode(L), dcd = gd_dcode(D);
                 atomicAdd(&S.lf[257 + lcd], 1u);
@@ -557,6 +562,7 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
             const int E = max(fcarry, wave_incl_max_i32(e));
             fcarry = max(fcarry, wave_max_i32(e));
             if (i < (int)n && E <= i) atomicAdd(&S.lf[S.chunk[i]], 1u);
+            mcov += wave_sum_u32(st ? L : 0u);
         }
         ns = ns0 + (uint32_t)__popcll(selm);
         if (lane == 0) { S.sel[r] = selm; S.sbase[r] = (uint16_t)ns0; }
@@ -580,8 +586,8 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
             int e = 0;
             if (st) {
                 const uint32_t si = S.sbase[r] + (uint32_t)__popcll(sm & lt);
-                const uint32_t sq = seq[si];
-                const uint32_t Lx = sq & 0xFFFF, Dx = sq >> 16;
+                const uint64_t sq = seq[si];
+                const uint32_t Lx = (uint32_t)(sq >> 16) & 0xFFFF, Dx = (uint32_t)(sq >> 32);
                 e = (int)(i + Lx);
                 const uint32_t lcd = gd_lcode(Lx), dcd = gd_dcode(Dx);
                 atomicAdd(&S.lf[257 + lcd], 1u);
@@ -751,7 +757,49 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     }
     bp = readlane(bp, 0);
     wave_sync();
-    {
+    if (n - mcov <= 8 * (ns + 1)) {
+        // match-major: lane e emits the literal run before match e and the
+        // match (element ns: the literals after the last match); 64 matches per
+        // step instead of 64 positions
+        uint32_t pe_carry = 0;
+#pragma unroll 1
+        for (uint32_t b0 = 0; b0 <= ns; b0 += 64) {
+            const uint32_t e = b0 + lane;
+            const bool has = e <= ns, mt = e < ns;
+            const uint64_t sq = mt ? seq[e] : 0ull;
+            const uint32_t pos = mt ? (uint32_t)(sq & 0xFFFF) : n;
+            const uint32_t Lx = (uint32_t)(sq >> 16) & 0xFFFF, Dx = (uint32_t)(sq >> 32);
+            const uint32_t myend = mt ? pos + Lx : n;
+            uint32_t pe = __shfl_up(myend, 1);
+            if (lane == 0) pe = pe_carry;
+            uint32_t cost = 0, lcd = 0, dcd = 0;
+            if (has)
+                for (uint32_t q = pe; q < pos; q++) cost += S.ll[S.chunk[q]];
+            if (mt) {
+                lcd = gd_lcode(Lx);
+                dcd = gd_dcode(Dx);
+                cost += S.ll[257 + lcd] + c_lext[lcd] + S.dl[dcd] + c_dext[dcd];
+            }
+            const uint32_t incl = wave_incl_sum(cost);
+            uint32_t b = bp + incl - cost;
+            if (has) {
+                for (uint32_t q = pe; q < pos; q++) {
+                    const uint32_t c = S.chunk[q];
+                    put_bits_atomic(bits, b, S.lc[c], S.ll[c]);
+                    b += S.ll[c];
+                }
+            }
+            if (mt) {
+                const uint32_t l1 = S.ll[257 + lcd], l2 = S.dl[dcd];
+                put_bits_atomic(bits, b, S.lc[257 + lcd] | (Lx - c_lbase[lcd]) << l1, l1 + c_lext[lcd]);
+                b += l1 + c_lext[lcd];
+                put_bits_atomic(bits, b, S.dc[dcd] | (Dx - c_dbase[dcd]) << l2, l2 + c_dext[dcd]);
+            }
+            bp += readlane(incl, 63);
+            pe_carry = readlane(myend, 63);
+        }
+    } else {
+        // position-major (literal-heavy chunks)
         int carry = 0;
         const uint64_t lt = (1ull << lane) - 1;
 #pragma unroll 1
@@ -764,9 +812,9 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
             uint32_t Lx = 0, Dx = 0, lcd = 0, dcd = 0, cost = 0;
             if (st) {
                 const uint32_t si = S.sbase[r] + (uint32_t)__popcll(sm & lt);
-                const uint32_t sq = seq[si];
-                Lx = sq & 0xFFFF;
-                Dx = sq >> 16;
+                const uint64_t sq = seq[si];
+                Lx = (uint32_t)(sq >> 16) & 0xFFFF;
+                Dx = (uint32_t)(sq >> 32);
                 e = (int)(i + Lx);
                 lcd = gd_lcode(Lx);
                 dcd = gd_dcode(Dx);

@@ -244,7 +244,7 @@ static int compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_param
         ea.bestpre = d.bestpre.as<uint32_t>();
         uint32_t cmax = 1024;                 // launch_deflate's template bucket
         while (cmax < C) cmax <<= 1;
-        HIPCHK(d.gdseq.ensure((size_t)std::max<uint32_t>(M, 1) * cmax));
+        HIPCHK(d.gdseq.ensure((size_t)std::max<uint32_t>(M, 1) * 2 * cmax));
         ea.gdseq = d.gdseq.as<uint8_t>();
     }
     HIPCHK(hipEventRecord(d.ev[0], s));
