@@ -575,28 +575,15 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     GSTAMP(1);
     // ---- symbol frequencies (the general parse counted them as it went) ----
     if (single) {
-        int carry = 0;  // max match end so far
-        const uint64_t lt = (1ull << lane) - 1;
-#pragma unroll 1
-        for (uint32_t r = 0; r < nrounds; r++) {
-            const uint32_t i = r * 64 + lane;
-            const uint64_t sm = S.sel[r];
-            if (!sm && carry >= (int)(r * 64 + 64)) continue;  // inside one match
-            const bool st = (sm >> lane) & 1;
-            int e = 0;
-            if (st) {
-                const uint32_t si = S.sbase[r] + (uint32_t)__popcll(sm & lt);
-                const uint64_t sq = seq[si];
-                const uint32_t Lx = (uint32_t)(sq >> 16) & 0xFFFF, Dx = (uint32_t)(sq >> 32);
-                e = (int)(i + Lx);
-                const uint32_t lcd = gd_lcode(Lx), dcd = gd_dcode(Dx);
-                atomicAdd(&S.lf[257 + lcd], 1u);
-                atomicAdd(&S.df[dcd], 1u);
-                extra += c_lext[lcd] + c_dext[dcd];
-            }
-            const int E = max(carry, wave_incl_max_i32(e));
-            carry = max(carry, wave_max_i32(e));
-            if (i < n && E <= (int)i) atomicAdd(&S.lf[S.chunk[i]], 1u);
+        // a literal at 0 and after the last match, then the matches of seq[]
+        if (lane == 0) S.lf[S.chunk[0]] += n - mcov;
+        wave_sync();
+        for (uint32_t j = lane; j < ns; j += 64) {
+            const uint32_t Lj = (uint32_t)(seq[j] >> 16) & 0xFFFF;
+            const uint32_t lcd = gd_lcode(Lj);
+            atomicAdd(&S.lf[257 + lcd], 1u);
+            atomicAdd(&S.df[0], 1u);
+            extra += c_lext[lcd];
         }
     }
     extra = wave_sum_u32(extra);

@@ -46,6 +46,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-e2e", action="store_true", help="skip the pinned host-to-host leg")
+    ap.add_argument("--alt-methods", default="1,3,4,5",
+                    help="second method set reported beside the headline ('' to skip): "
+                         "1,3,4,5 = RLE/Huffman/Delta/DEFLATE (every package decodable by the "
+                         "stdlib-only reference)")
     ap.add_argument("--api-bytes", type=int, default=256 << 20,
                     help="input size of the AdaptiveCompressor.compress(path, path) leg (0: skip)")
     return ap.parse_args()
@@ -140,6 +144,61 @@ def api_leg(nbytes, chunk, mode, methods, seed):
     return {"bytes": nbytes, "compress_GBps": round(nbytes / tc / 1e9, 3),
             "decompress_GBps": round(nbytes / td_ / 1e9, 3), "round_trip_bit_exact": ok,
             "ratio": round(stats["compressed_size"] / nbytes, 5) if "compressed_size" in stats else None}
+
+
+def alt_leg(lib, ctx, d_in, n, args, methods, steps):
+    """The same input under another method set (device-resident, same clock
+    discipline as the headline), its ratio and a bit-exact decode."""
+    import torch
+    from ambc import _lib, AdaptiveCompressor
+    from ambc.compressor import entropy_terms
+    from ambc.registry import METHOD_CHUNK_PREFS, method_mask
+    p = _lib.Params()
+    p.chunk_size = args.chunk
+    p.mode = _lib.MODE_REFERENCE if args.mode == "reference" else _lib.MODE_NATIVE
+    p.method_mask = method_mask(methods)
+    for i in range(16):
+        lo, hi = METHOD_CHUNK_PREFS.get(i, (1, 0))
+        p.pref_min[i], p.pref_max[i] = lo, min(hi, 0xFFFFFFFF)
+    tabs = [entropy_terms(args.chunk)]
+    p.ent_full = tabs[0].ctypes.data
+    if n % args.chunk:
+        tabs.append(entropy_terms(n % args.chunk))
+        p.ent_tail = tabs[1].ctypes.data
+    cap = lib.ambc_compress_bound(n, args.chunk)
+    d_out = torch.empty(cap + 64, dtype=torch.uint8, device=d_in.device)
+    olen = C.c_uint64()
+    st = _lib.Stats()
+    enc = []
+
+    def once():
+        _lib.check(lib.ambc_compress_device(ctx.h, 0, d_in.data_ptr(), n, C.byref(p), d_out.data_ptr(),
+                                            cap, C.byref(olen), C.byref(st), None), lib)
+        e = C.c_uint64()
+        lib.ambc_last_kernel_times(ctx.h, 0, C.byref(e), None, None)
+        enc.append(e.value)
+
+    once()
+    enc.clear()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        once()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    body = d_out[:olen.value].cpu().numpy().tobytes()
+    comp = AdaptiveCompressor(chunk_size=args.chunk, mode=args.mode, methods=methods)
+    t = time.perf_counter()
+    back = comp._adaptive_decompress(body, n)
+    dwall = time.perf_counter() - t
+    ok = back == d_in.cpu().numpy().tobytes()
+    ds = comp._last_device_stats
+    usage = {i: int(st.method_usage[i]) for i in range(256) if st.method_usage[i]}
+    return {"methods": methods, "GBps": round(n / dt / 1e9, 3), "ms_per_step": round(dt * 1e3, 3),
+            "steps": steps, "ratio": round(olen.value / n, 5), "method_usage": usage,
+            "kernels_ms": round(sum(enc) / len(enc) / 1e6, 3), "round_trip_bit_exact": ok,
+            "decode": {"kernel_ms": round(ds.kernel_ns / 1e6, 3), "host_zlib_ms": round(ds.host_codec_ns / 1e6, 3),
+                       "header_walk_ms": round(ds.walk_ns / 1e6, 3), "host_api_GBps": round(n / dwall / 1e9, 3)}}
 
 
 def pmc_traffic(workload):
@@ -262,6 +321,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_e2e:
         e2e = e2e_leg(lib, ctx, d_in, d_out, body_len, n, p)
         log(f"e2e: {e2e}")
+    alt = None
+    if rank == 0 and world == 1 and args.alt_methods:
+        alt = alt_leg(lib, ctx, d_in, n, args, [int(x) for x in args.alt_methods.split(",")], args.steps)
+        log(f"alt: {alt}")
     if rank == 0 and world == 1 and args.api_bytes:
         api = api_leg(args.api_bytes, args.chunk, args.mode, methods, args.seed)
         log(f"api: {api}")
@@ -285,7 +348,7 @@ def main():
                        "ratio": round(body_total / (n * world), 5),
                        "parallelism": f"chunk-shard dp{world}" if world > 1 else "single GPU",
                        "round_trip_bit_exact": verified, "decode": decode,
-                       "e2e_pinned_host": e2e, "api_file": api},
+                       "e2e_pinned_host": e2e, "api_file": api, "alt_method_set": alt},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
