@@ -26,7 +26,7 @@ def counter(d, name, kernel="k_encode"):
         if f.endswith("counter_collection.csv"):
             with open(os.path.join(d, f)) as fh:
                 for r in csv.DictReader(fh):
-                    if r["Counter_Name"] == name and r["Kernel_Name"].startswith(kernel):
+                    if r["Counter_Name"] == name and kernel + "<" in r["Kernel_Name"]:
                         vals.append(float(r["Counter_Value"]))
     return vals
 
