@@ -982,6 +982,9 @@ hipError_t launch_decode(int kind, const DecArgs& a, hipStream_t s) {
     case DEC_KIND_LZ4_8K: hipLaunchKernelGGL(k_decode_lz4<8192>, dim3(a.n_list), dim3(64), 0, s, a); break;
     case DEC_KIND_LZ4_16K: hipLaunchKernelGGL(k_decode_lz4<16384>, dim3(a.n_list), dim3(64), 0, s, a); break;
     case DEC_KIND_LZ4_G: hipLaunchKernelGGL(k_decode_lz4_g, dim3(a.n_list), dim3(64), 0, s, a); break;
+    case DEC_KIND_INFLATE_4K:
+    case DEC_KIND_INFLATE_8K:
+    case DEC_KIND_INFLATE_16K: return launch_inflate(kind, a, s);
     default: hipLaunchKernelGGL(k_decode, dim3(a.n_list), dim3(64), 0, s, a); break;
     }
     return hipGetLastError();

@@ -701,6 +701,11 @@ void walk_body(const uint8_t* body, uint64_t blen, uint64_t orig_size, const uin
             j.type = DEC_VERBATIM;
             kind = DEC_KIND_LIGHT;
             expect = clen;
+        } else if (t == 5 && clen && orig <= 16384) {
+            // zlib payload: inflated on the GPU (host zlib if it decodes past the map)
+            j.type = 5;
+            kind = orig <= 4096 ? DEC_KIND_INFLATE_4K : orig <= 8192 ? DEC_KIND_INFLATE_8K : DEC_KIND_INFLATE_16K;
+            expect = orig;
         } else if (t == 5 || t == 6 || t == 7) {
             j.type = DEC_SKIP;
             kind = DEC_KIND_LIGHT;
@@ -831,6 +836,7 @@ static int decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t or
     const uint64_t h2d = now_ns() - t;
     std::map<uint32_t, uint64_t> known;
     Walk w;
+    std::vector<ambc_host_chunk> hostinf;   // id-5 packages the GPU handed back
     uint64_t walk_ns = 0, kern_ns = 0;
     for (int iter = 0; iter < 64; iter++) {
         w = Walk();
@@ -905,7 +911,13 @@ static int decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t or
         HIPCHK(hipEventElapsedTime(&ms, d.ev[0], d.ev[1]));
         kern_ns += (uint64_t)(ms * 1e6);
         bool redo = false;
+        hostinf.clear();
         for (uint32_t i = 0; i < nj; i++) {
+            if (prod[i] == DEC_PRODUCED_HOST) {   // inflate on host after the copy back
+                const DecJob& jb = w.jobs[i];
+                hostinf.push_back(ambc_host_chunk{jb.body_off, jb.out_off, jb.clen, jb.orig, 5, 0});
+                continue;
+            }
             if (prod[i] == 0xFFFFFFFFu) return fail(AMBC_E_DEVICE, "decode job failed");
             if (prod[i] != w.jobs[i].expect) { known[w.src_index[i]] = prod[i]; redo = true; }
         }
@@ -917,6 +929,7 @@ static int decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t or
     const uint64_t d2h_ns = now_ns() - t;
     const uint64_t t_inf = now_ns();
     inflate_all(body, w.zlib, out, orig_size);
+    inflate_all(body, hostinf, out, orig_size);
     const uint64_t inflate_ns = now_ns() - t_inf;
     host = w.host;
     if (st) {

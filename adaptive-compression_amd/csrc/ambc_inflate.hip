@@ -1,0 +1,455 @@
+// ambc_inflate.hip -- zlib inflate (id 5 payloads) on gfx950, one wavefront per
+// package.  Semantics are DeflateCompression.decompress's
+// (advanced_compression.py:83-96): zlib.decompress(payload) with the default
+// window, i.e. zlib's inflate() checks -- header (CM 8, window <= 32 KiB, FCHECK,
+// no preset dictionary), block types, code-length sets (over-subscribed or
+// incomplete sets are errors except a single 1-bit literal/distance code),
+// "invalid bit length repeat", missing end-of-block code, invalid codes,
+// distances too far back, an unfinished stream and the Adler-32 check -- then
+// pad / truncate to orig; any error decodes the package to orig zero bytes.
+// Bytes after the stream's end are ignored.
+//
+// Layout: the payload is read through a 256-byte register window (4 bytes per
+// lane, fetched with v_readlane) into a 64-bit bit buffer on the scalar unit;
+// Huffman codes resolve through 10-bit LDS lookup tables (longer codes by the
+// canonical first-code search).  Output bytes are produced as a source map in
+// LDS (u16 per byte: 0x8000 | value for a literal, else the earlier output
+// index it copies), match copies written by the whole wave; pointer jumping
+// resolves the map, which then yields the Adler-32 and the output.  Output
+// larger than the map (OUTMAX) is handed back to the host zlib path.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ambc_internal.h"
+#include "ambc_wave.h"
+
+namespace ambc {
+namespace {
+
+constexpr uint32_t IN_LIT = 0x8000u;
+constexpr int LUTB = 10;            // primary lookup bits
+// lookup entries: symbol << 5 | length << 1 | 1; 0 = no code, 2 = a code
+// longer than LUTB bits (canonical search)
+constexpr uint16_t LUT_BAD = 0;
+constexpr uint16_t LUT_LONG = 2;
+
+__constant__ uint8_t c_clord2[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+template <uint32_t OUTMAX>
+struct InfSmem {
+    uint16_t src[OUTMAX];             // output source map
+    uint16_t lut[2][1 << LUTB];       // [0] literal/length (or code lengths), [1] distance
+    uint16_t sorted[2][288];          // symbols in canonical (length, symbol) order
+    uint16_t first[2][16], cnt[2][16], offs[2][16];
+    uint8_t lens[320];                // code lengths of the current dynamic block
+};
+
+// payload byte stream through a 256-byte register window
+struct InBits {
+    const uint8_t* g;
+    uint32_t plen;
+    uint32_t win;      // 4 payload bytes per lane
+    uint32_t wlo;      // payload index of the window's first byte (multiple of 4 from g)
+    uint64_t buf;      // bit buffer (LSB = next bit)
+    uint32_t cnt;      // bits in buf
+    uint32_t pos;      // next payload byte to load into buf
+    uint32_t lane;
+};
+
+__device__ __forceinline__ void in_window(InBits& I, uint32_t at) {
+    I.wlo = __builtin_amdgcn_readfirstlane(at & ~3u);
+    const uint32_t q = I.wlo + 4 * I.lane;
+    uint32_t x = 0;
+    if (q + 4 <= I.plen) {
+        x = (uint32_t)I.g[q] | (uint32_t)I.g[q + 1] << 8 | (uint32_t)I.g[q + 2] << 16 | (uint32_t)I.g[q + 3] << 24;
+    } else {
+#pragma unroll
+        for (int b = 0; b < 4; b++)
+            if (q + b < I.plen) x |= (uint32_t)I.g[q + b] << (8 * b);
+    }
+    I.win = x;
+}
+
+__device__ __forceinline__ uint32_t in_byte(InBits& I, uint32_t at) {
+    uint32_t r = __builtin_amdgcn_readfirstlane(at - I.wlo);
+    if (r >= 256) {  // uniform
+        in_window(I, at);
+        r = __builtin_amdgcn_readfirstlane(at - I.wlo);
+    }
+    return __builtin_amdgcn_readfirstlane((readlane(I.win, r >> 2) >> ((r & 3) * 8)) & 0xFF);
+}
+
+// keep >= 32 bits in the buffer while payload bytes remain (missing bits read as
+// zero; the caller checks I.cnt against what it consumes)
+__device__ __forceinline__ void in_fill(InBits& I) {
+    while (I.cnt <= 56 && I.pos < I.plen) {
+        I.buf |= (uint64_t)in_byte(I, I.pos) << I.cnt;
+        I.cnt += 8;
+        I.pos++;
+        if (I.cnt >= 32) break;
+    }
+}
+
+// take n bits (n <= 32); false when the payload is exhausted
+__device__ __forceinline__ bool in_take(InBits& I, uint32_t n, uint32_t& v) {
+    if (I.cnt < n) in_fill(I);
+    if (I.cnt < n) {
+        in_fill(I);
+        if (I.cnt < n) return false;
+    }
+    v = (uint32_t)(I.buf & ((n >= 32) ? 0xFFFFFFFFull : ((1ull << n) - 1)));
+    I.buf >>= n;
+    I.cnt -= n;
+    return true;
+}
+
+// Build the decode tables of code lengths len[0..nsym) into table t.
+// kind: 0 = code-length code (incomplete sets are errors), 1 = literal/length
+// or distance (a single 1-bit code may be incomplete).  Returns false on an
+// over-subscribed or invalid incomplete set (zlib inflate_table's -1).
+template <uint32_t OUTMAX>
+__device__ bool inf_build(InfSmem<OUTMAX>& S, int t, const uint8_t* len, int nsym, int kind, uint32_t lane) {
+    constexpr int J = 5;
+    uint32_t l[J];
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        const int s = lane + 64 * j;
+        l[j] = s < nsym ? len[s] : 0u;
+    }
+    uint32_t count[16];
+    uint32_t maxl = 0;
+#pragma unroll
+    for (int b = 1; b < 16; b++) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int j = 0; j < J; j++) c += (uint32_t)__popcll(__ballot(l[j] == (uint32_t)b));
+        count[b] = c;
+        if (c) maxl = b;
+    }
+    // table fill: every entry "no code" first
+    for (uint32_t i = lane; i < (1u << LUTB); i += 64) S.lut[t][i] = LUT_BAD;
+    if (maxl == 0) {  // no symbols: decoding any code is an error (zlib: valid table)
+        if (lane < 16) { S.cnt[t][lane] = 0; S.first[t][lane] = 0; S.offs[t][lane] = 0; }
+        wave_sync();
+        return true;
+    }
+    int left = 1;
+#pragma unroll
+    for (int b = 1; b < 16; b++) {
+        left <<= 1;
+        left -= (int)count[b];
+        if (left < 0) return false;  // over-subscribed
+    }
+    if (left > 0 && (kind == 0 || maxl != 1)) return false;  // incomplete
+    // canonical codes; sorted order (length, symbol)
+    uint32_t first = 0, prev = 0, off = 0;
+    uint32_t code[J];
+    const uint64_t lt = (1ull << lane) - 1;
+#pragma unroll
+    for (int b = 1; b < 16; b++) {
+        first = (first + prev) << 1;
+        if (lane == (uint32_t)b) {
+            S.first[t][b] = (uint16_t)first;
+            S.cnt[t][b] = (uint16_t)count[b];
+            S.offs[t][b] = (uint16_t)off;
+        }
+        uint32_t seen = 0;
+#pragma unroll
+        for (int j = 0; j < J; j++) {
+            const uint64_t m = __ballot(l[j] == (uint32_t)b);
+            if (l[j] == (uint32_t)b) {
+                const uint32_t r = seen + (uint32_t)__popcll(m & lt);
+                code[j] = first + r;
+                S.sorted[t][off + r] = (uint16_t)(lane + 64 * j);
+            }
+            seen += (uint32_t)__popcll(m);
+        }
+        prev = count[b];
+        off += count[b];
+    }
+    wave_sync();
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+        if (!l[j]) continue;
+        const uint32_t L = l[j];
+        const uint32_t rc = __builtin_bitreverse32(code[j]) >> (32 - L);  // LSB-first index
+        const uint32_t sym = lane + 64 * j;
+        if (L <= (uint32_t)LUTB) {
+            const uint16_t e = (uint16_t)(sym << 5 | L << 1 | 1);  // sym 0..319, len 1..10
+            for (uint32_t k = 0; k < (1u << (LUTB - L)); k++) S.lut[t][rc | k << L] = e;
+        } else {
+            S.lut[t][rc & ((1u << LUTB) - 1)] = LUT_LONG;
+        }
+    }
+    wave_sync();
+    return true;
+}
+
+// decode one symbol of table t; -1 = invalid / truncated
+template <uint32_t OUTMAX>
+__device__ __forceinline__ int inf_sym(InfSmem<OUTMAX>& S, int t, InBits& I) {
+    if (I.cnt < 15) in_fill(I);
+    const uint16_t e = S.lut[t][I.buf & ((1u << LUTB) - 1)];
+    if (e & 1) {
+        const uint32_t L = (e >> 1) & 15;
+        if (L > I.cnt) return -1;
+        I.buf >>= L;
+        I.cnt -= L;
+        return e >> 5;
+    }
+    if (e == LUT_BAD) return -1;
+    // canonical search for a code of 11..15 bits
+    uint32_t c = 0;
+    for (uint32_t L = 1; L <= 15; L++) {
+        if (L > I.cnt) return -1;
+        c = c << 1 | (uint32_t)((I.buf >> (L - 1)) & 1);
+        if (L <= (uint32_t)LUTB) continue;
+        const uint32_t cnt = S.cnt[t][L], f = S.first[t][L];
+        if (c - f < cnt && c >= f) {
+            I.buf >>= L;
+            I.cnt -= L;
+            return S.sorted[t][S.offs[t][L] + (c - f)];
+        }
+    }
+    return -1;
+}
+
+// the whole zlib stream; returns the decoded length, -1 invalid, -2 output
+// larger than OUTMAX (host path)
+template <uint32_t OUTMAX>
+__device__ int64_t inflate_stream(InfSmem<OUTMAX>& S, const uint8_t* g, uint32_t plen, uint32_t lane) {
+    InBits I;
+    I.g = g;
+    I.plen = plen;
+    I.buf = 0;
+    I.cnt = 0;
+    I.pos = 0;
+    I.lane = lane;
+    in_window(I, 0);
+    uint32_t v;
+    if (!in_take(I, 16, v)) return -1;
+    const uint32_t cmf = v & 0xFF, flg = v >> 8;
+    if (((cmf << 8) | flg) % 31) return -1;            // incorrect header check
+    if ((cmf & 15) != 8) return -1;                    // unknown compression method
+    if ((cmf >> 4) + 8 > 15) return -1;                // invalid window size
+    if (flg & 0x20) return -1;                         // preset dictionary: zlib.decompress raises
+    uint32_t op = 0;
+    for (;;) {
+        uint32_t hdr;
+        if (!in_take(I, 3, hdr)) return -1;
+        const uint32_t bfinal = hdr & 1, btype = hdr >> 1;
+        if (btype == 0) {
+            // stored: to the byte boundary, LEN, NLEN
+            I.buf >>= (I.cnt & 7);
+            I.cnt -= (I.cnt & 7);
+            uint32_t ln, nl;
+            if (!in_take(I, 16, ln) || !in_take(I, 16, nl)) return -1;
+            if (ln != (~nl & 0xFFFF)) return -1;
+            if (op + ln > OUTMAX) return -2;
+            // the buffered bytes first, then straight from the payload
+            uint32_t k = 0;
+            while (k < ln && I.cnt >= 8) {
+                if (lane == 0) S.src[op + k] = (uint16_t)(IN_LIT | (I.buf & 0xFF));
+                I.buf >>= 8;
+                I.cnt -= 8;
+                k++;
+            }
+            if (I.pos + (ln - k) > plen) return -1;
+            for (uint32_t b = 0; b < ln - k; b += 64)
+                if (b + lane < ln - k) S.src[op + k + b + lane] = (uint16_t)(IN_LIT | g[I.pos + b + lane]);
+            I.pos += ln - k;
+            op += ln;
+        } else if (btype == 1 || btype == 2) {
+            if (btype == 1) {
+                for (uint32_t s = lane; s < 320; s += 64)
+                    S.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : (s < 320 ? 5 : 0);
+                wave_sync();
+                // literal/length 0..287, distance 0..29 (+30, 31: codes that decode as invalid)
+                if (!inf_build(S, 0, S.lens, 288, 1, lane)) return -1;
+                if (!inf_build(S, 1, S.lens + 288, 32, 1, lane)) return -1;
+            } else {
+                uint32_t h;
+                if (!in_take(I, 14, h)) return -1;
+                const uint32_t nlen = 257 + (h & 31), ndist = 1 + ((h >> 5) & 31), ncode = 4 + (h >> 10);
+                if (nlen > 286 || ndist > 30) return -1;
+                for (uint32_t s = lane; s < 320; s += 64) S.lens[s] = 0;
+                wave_sync();
+                for (uint32_t i = 0; i < ncode; i++) {
+                    uint32_t c;
+                    if (!in_take(I, 3, c)) return -1;
+                    if (lane == 0) S.lens[c_clord2[i]] = (uint8_t)c;
+                }
+                wave_sync();
+                if (!inf_build(S, 0, S.lens, 19, 0, lane)) return -1;
+                uint32_t have = 0;
+                const uint32_t tot = nlen + ndist;
+                uint32_t lastlen = 0;
+                while (have < tot) {
+                    const int sy = inf_sym(S, 0, I);
+                    if (sy < 0) return -1;
+                    uint32_t ln = 0, copy = 1;
+                    if (sy < 16) {
+                        ln = (uint32_t)sy;
+                    } else {
+                        uint32_t x;
+                        if (sy == 16) {
+                            if (have == 0) return -1;
+                            ln = lastlen;
+                            if (!in_take(I, 2, x)) return -1;
+                            copy = 3 + x;
+                        } else if (sy == 17) {
+                            if (!in_take(I, 3, x)) return -1;
+                            copy = 3 + x;
+                        } else {
+                            if (!in_take(I, 7, x)) return -1;
+                            copy = 11 + x;
+                        }
+                        if (have + copy > tot) return -1;
+                    }
+                    // code lengths into the literal/length (0..) and distance (288..) halves
+                    for (uint32_t c = lane; c < copy; c += 64) {
+                        const uint32_t q = have + c;
+                        S.lens[q < nlen ? q : 288 + (q - nlen)] = (uint8_t)ln;
+                    }
+                    lastlen = ln;
+                    have += copy;
+                }
+                wave_sync();
+                // literal/length lengths live at [0, nlen) (rest 0 up to 288), distances at [288, 288+ndist)
+                for (uint32_t s = nlen + lane; s < 288; s += 64) S.lens[s] = 0;
+                for (uint32_t s = 288 + ndist + lane; s < 320; s += 64) S.lens[s] = 0;
+                wave_sync();
+                if (S.lens[256] == 0) return -1;  // missing end-of-block code
+                if (!inf_build(S, 0, S.lens, 288, 1, lane)) return -1;
+                if (!inf_build(S, 1, S.lens + 288, 32, 1, lane)) return -1;
+            }
+            // symbols
+            for (;;) {
+                const int sy = inf_sym(S, 0, I);
+                if (sy < 0) return -1;
+                if (sy < 256) {
+                    if (op >= OUTMAX) return -2;
+                    if (lane == 0) S.src[op] = (uint16_t)(IN_LIT | (uint32_t)sy);
+                    op++;
+                    continue;
+                }
+                if (sy == 256) break;
+                const uint32_t k = (uint32_t)sy - 257;
+                if (k >= 29) return -1;  // 286, 287
+                uint32_t L;
+                if (k < 8) {
+                    L = 3 + k;
+                } else if (k == 28) {
+                    L = 258;
+                } else {
+                    const uint32_t eb = (k >> 2) - 1, base = ((4u | (k & 3)) << eb) + 3;
+                    uint32_t x;
+                    if (!in_take(I, eb, x)) return -1;
+                    L = base + x;
+                }
+                const int ds = inf_sym(S, 1, I);
+                if (ds < 0 || ds >= 30) return -1;
+                uint32_t D;
+                if (ds < 4) {
+                    D = (uint32_t)ds + 1;
+                } else {
+                    const uint32_t eb = ((uint32_t)ds >> 1) - 1, base = ((2u | ((uint32_t)ds & 1)) << eb) + 1;
+                    uint32_t x;
+                    if (!in_take(I, eb, x)) return -1;
+                    D = base + x;
+                }
+                if (D > op) return -1;  // invalid distance too far back
+                if (op + L > OUTMAX) return -2;
+                // entries point into the period before the match (chains stay short)
+                const uint32_t m0 = op - D;
+                const uint32_t lmod = lane % D;
+                uint32_t bmod = 0;
+                for (uint32_t b = 0; b < L; b += 64) {
+                    uint32_t c = bmod + lmod;
+                    if (c >= D) c -= D;
+                    if (b + lane < L) S.src[op + b + lane] = (uint16_t)(m0 + c);
+                    bmod = (bmod + 64) % D;
+                }
+                op += L;
+            }
+        } else {
+            return -1;  // invalid block type
+        }
+        if (bfinal) break;
+    }
+    // Adler-32, big-endian, after the byte boundary
+    I.buf >>= (I.cnt & 7);
+    I.cnt -= (I.cnt & 7);
+    uint32_t a0, a1;
+    if (!in_take(I, 16, a0) || !in_take(I, 16, a1)) return -1;
+    const uint32_t want = ((a0 & 0xFF) << 24) | ((a0 >> 8) << 16) | ((a1 & 0xFF) << 8) | (a1 >> 8);
+    wave_sync();
+    // resolve the map (pointer jumping)
+    for (;;) {
+        bool more = false;
+        for (uint32_t q0 = lane * 4; q0 < op; q0 += 256) {
+            uint32_t w[4];
+#pragma unroll
+            for (int t = 0; t < 4; t++) w[t] = q0 + t < op ? S.src[q0 + t] : IN_LIT;
+#pragma unroll
+            for (int t = 0; t < 4; t++)
+                if (!(w[t] & IN_LIT)) {
+                    w[t] = S.src[w[t]];
+                    S.src[q0 + t] = (uint16_t)w[t];
+                    more |= !(w[t] & IN_LIT);
+                }
+        }
+        wave_sync();
+        if (!__any(more)) break;
+    }
+    uint64_t asum = 0, bsum = 0;
+    for (uint32_t q = lane; q < op; q += 64) {
+        const uint32_t c = S.src[q] & 0xFF;
+        asum += c;
+        bsum += (uint64_t)(op - q) * c;
+    }
+    asum = wave_sum<uint64_t>(asum);
+    bsum = wave_sum<uint64_t>(bsum);
+    const uint32_t adler = (uint32_t)(((op + bsum) % 65521) << 16 | ((1 + asum) % 65521));
+    if (adler != want) return -1;
+    return (int64_t)op;
+}
+
+template <uint32_t OUTMAX>
+__global__ __launch_bounds__(64) void k_decode_inflate(DecArgs A) {
+    __shared__ InfSmem<OUTMAX> S;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t j = A.list ? A.list[blockIdx.x] : blockIdx.x;
+    const DecJob J = A.jobs[j];
+    uint8_t* out = A.out + J.out_off;
+    const uint32_t orig = J.orig;
+    const int64_t r = inflate_stream(S, A.body + J.body_off, J.clen, lane);
+    wave_sync();
+    if (r == -2) {  // larger than the map: the host inflates it
+        if (lane == 0) A.produced[j] = 0xFFFFFFFEu;
+        return;
+    }
+    if (r < 0) {
+        for (uint32_t q = lane; q < orig; q += 64) out[q] = 0;
+    } else {
+        const uint32_t m = min((uint32_t)r, orig);
+        for (uint32_t q = lane; q < m; q += 64) out[q] = (uint8_t)(S.src[q] & 0xFF);
+        for (uint32_t q = m + lane; q < orig; q += 64) out[q] = 0;
+    }
+    if (lane == 0) A.produced[j] = orig;
+}
+
+}  // namespace
+
+hipError_t launch_inflate(int kind, const DecArgs& a, hipStream_t s) {
+    if (a.n_list == 0) return hipSuccess;
+    if (kind == DEC_KIND_INFLATE_4K)
+        hipLaunchKernelGGL(k_decode_inflate<4096>, dim3(a.n_list), dim3(64), 0, s, a);
+    else if (kind == DEC_KIND_INFLATE_8K)
+        hipLaunchKernelGGL(k_decode_inflate<8192>, dim3(a.n_list), dim3(64), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_decode_inflate<16384>, dim3(a.n_list), dim3(64), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace ambc

@@ -74,7 +74,9 @@ struct DecArgs {
 
 // decode kernels by LDS footprint (host routes each job to one of them)
 enum : int { DEC_KIND_LIGHT = 0, DEC_KIND_LZ4_4K = 1, DEC_KIND_LZ4_8K = 2, DEC_KIND_LZ4_16K = 3,
-             DEC_KIND_LZ4_G = 4, DEC_KIND_HEAVY = 5, DEC_KINDS = 6 };
+             DEC_KIND_LZ4_G = 4, DEC_KIND_INFLATE_4K = 5, DEC_KIND_INFLATE_8K = 6,
+             DEC_KIND_INFLATE_16K = 7, DEC_KIND_HEAVY = 8, DEC_KINDS = 9 };
+constexpr uint32_t DEC_PRODUCED_HOST = 0xFFFFFFFEu;  // k_decode_inflate: output too large, inflate on host
 
 constexpr uint32_t DEC_VERBATIM = 256;
 constexpr uint32_t DEC_SKIP = 257;
@@ -90,6 +92,7 @@ hipError_t scan_sizes(const uint64_t* sizes, uint64_t* off, uint32_t count, void
                       size_t* tmp_bytes, hipStream_t s);
 hipError_t launch_copy(uint8_t* dst, const uint8_t* src, uint64_t len, hipStream_t s);
 hipError_t launch_decode(int kind, const DecArgs& a, hipStream_t s);
+hipError_t launch_inflate(int kind, const DecArgs& a, hipStream_t s);   // ambc_inflate.hip
 hipError_t launch_synth(uint8_t* out, uint64_t n, const uint64_t* seg, uint32_t nseg,
                         uint64_t seed, hipStream_t s);
 

@@ -437,3 +437,38 @@ def test_gdeflate_edge_chunks(ctx):
                                                            deflate="gd"), nthreads=0)
             assert body == ref, (len(d), chunk)
             assert comp._adaptive_decompress(body, len(d)) == d
+
+
+def test_gpu_inflate_zlib_corpus(ctx):
+    """k_decode_inflate against zlib.decompress semantics on streams the
+    reference's zlib writes: levels 0-9 (stored / fixed / dynamic blocks),
+    multi-block streams (compressobj with full flushes), streams that decode
+    past the chunk, bad headers (CM, FCHECK, window, preset dictionary) and a
+    truncation at every byte of a short stream."""
+    import zlib
+    mixed = synth.generate(1 << 20, 41)
+    payloads = []
+    for lvl in range(10):
+        for o, n in ((0, 4096), (70000, 3000), (140000, 4096), (5000, 100), (200000, 16384)):
+            payloads.append((zlib.compress(mixed[o:o + n], lvl), n))
+    co = zlib.compressobj(6)
+    parts = b""
+    for q in range(0, 4096, 512):
+        parts += co.compress(mixed[300000 + q:300512 + q]) + co.flush(zlib.Z_FULL_FLUSH)
+    payloads.append((parts + co.flush(), 4096))
+    payloads.append((zlib.compress(bytes(9000), 9), 4096))          # decodes past the chunk
+    good = zlib.compress(mixed[9000:9400], 9)
+    payloads += [(bytes([0x79]) + good[1:], 400), (bytes([0x88, 0x1C]) + good[2:], 400),
+                 (bytes([0x78, 0x9D]) + good[2:], 400), (bytes([0x78, 0xBB]) + good[2:], 400)]
+    for cut in range(1, len(good)):
+        payloads.append((good[:cut], 400))
+    parts, orig_total = [], 0
+    for z, n in payloads:
+        parts.append(_chunk(5, z, n))
+        orig_total += n
+    body = b"".join(parts) + b"\xff\xff\x00\x00\x00\x00" + bytes(10)
+    want = orc.decompress_body(body, orig_total)
+    comp = _compressor()
+    assert comp._adaptive_decompress(body, orig_total) == want
+    st = comp._last_device_stats
+    assert st.kernel_ns > 0
