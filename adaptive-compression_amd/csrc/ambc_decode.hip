@@ -539,6 +539,11 @@ __device__ __forceinline__ void seq_write_wave(T* src, uint32_t o, uint32_t y, u
         if (b + lane < L) src[o + b + lane] = (T)(SrcLit<T>::v | (y + b + lane));
     if (ml == 0) return;
     const uint32_t m0 = o + L - off;
+    if (off >= ml) {  // no overlap: a plain copy
+        for (uint32_t b = 0; b < ml; b += 64)
+            if (b + lane < ml) src[o + L + b + lane] = (T)(m0 + b + lane);
+        return;
+    }
     const uint32_t lmod = lane % off;   // (b + lane) % off = (b % off + lane % off) mod off
     uint32_t bmod = 0;
     for (uint32_t b = 0; b < ml; b += 64) {
@@ -838,7 +843,7 @@ __device__ __forceinline__ bool decode_light(const DecJob& J, const uint8_t* p, 
 }
 
 __device__ __forceinline__ uint32_t job_index(const DecArgs& A) {
-    return A.list ? A.list[blockIdx.x] : blockIdx.x;
+    return uniform_u32(A.list ? A.list[blockIdx.x] : blockIdx.x);
 }
 
 __device__ __forceinline__ void put_produced(const DecArgs& A, uint32_t j, int64_t produced,
@@ -864,11 +869,11 @@ template <typename T>
 __device__ __forceinline__ void lz4_job(const DecArgs& A, uint32_t j, const DecJob& J, T* src, uint32_t cap,
                                         uint32_t lane) {
     DSTAMP_DECL
-    const uint8_t* g = A.body + J.body_off;
-    uint8_t* out = A.out + J.out_off;
-    const uint32_t orig = J.orig;
+    const uint8_t* g = uniform_ptr(A.body + J.body_off);
+    uint8_t* out = uniform_ptr(A.out + J.out_off);
+    const uint32_t orig = uniform_u32(J.orig);
     DSTAMP(0);
-    const int64_t r = dec_lz4_par(g, J.clen, src, cap, lane DSTAMP_ARGS);
+    const int64_t r = dec_lz4_par(g, uniform_u32(J.clen), src, uniform_u32(cap), lane DSTAMP_ARGS);
     wave_sync();
     if (r < 0) {
         wave_zero(out, orig, lane);

@@ -898,6 +898,14 @@ static int decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t or
             }
             fprintf(stderr, "[ambc stamps] jobs=%u tagged9=%llu untagged=%llu\n", nj,
                     (unsigned long long)tagged[9], (unsigned long long)tagged[0]);
+            if (tagged[5]) {
+                double g5[4] = {0};
+                for (uint32_t i = 0; i < nj; i++)
+                    if (sv[i * 8 + 7] == 5) for (int q = 0; q < 4; q++) g5[q] += (double)sv[i * 8 + q];
+                const double c5 = (double)tagged[5];
+                fprintf(stderr, "[ambc stamps] inflate jobs=%.0f cycles/job: tables %.0f symbols %.0f "
+                        "resolve %.0f adler+out %.0f\n", c5, g5[0] / c5, g5[1] / c5, g5[2] / c5, g5[3] / c5);
+            }
             if (cnt)
                 fprintf(stderr, "[ambc stamps] lz4 jobs=%llu cycles/job: pre %.0f spec %.0f chain %.0f "
                         "seqs %.0f writes %.0f resolve %.0f gather %.0f\n", (unsigned long long)cnt,

@@ -26,6 +26,18 @@
 namespace ambc {
 namespace {
 
+#ifdef AMBC_STAMPS
+#define ISTAMP(ph)                                              \
+    do {                                                        \
+        __builtin_amdgcn_s_waitcnt(0xC07F);                     \
+        const uint64_t _t = __builtin_amdgcn_s_memtime();       \
+        _acc[ph] += _t - _st_t;                                 \
+        _st_t = _t;                                             \
+    } while (0)
+#else
+#define ISTAMP(ph) do {} while (0)
+#endif
+
 constexpr uint32_t IN_LIT = 0x8000u;
 constexpr int LUTB = 10;            // primary lookup bits
 // lookup entries: symbol << 5 | length << 1 | 1; 0 = no code, 2 = a code
@@ -56,43 +68,48 @@ struct InBits {
     uint32_t lane;
 };
 
-__device__ __forceinline__ void in_window(InBits& I, uint32_t at) {
-    I.wlo = __builtin_amdgcn_readfirstlane(at & ~3u);
-    const uint32_t q = I.wlo + 4 * I.lane;
+// 4 payload bytes per lane starting at the 4-aligned index wlo; zeros past plen
+__device__ __noinline__ uint32_t in_load(const uint8_t* g, uint32_t plen, uint32_t wlo, uint32_t lane) {
+    const uint32_t q = wlo + 4 * lane;
     uint32_t x = 0;
-    if (q + 4 <= I.plen) {
-        x = (uint32_t)I.g[q] | (uint32_t)I.g[q + 1] << 8 | (uint32_t)I.g[q + 2] << 16 | (uint32_t)I.g[q + 3] << 24;
+    if (q + 4 <= plen) {
+        x = (uint32_t)g[q] | (uint32_t)g[q + 1] << 8 | (uint32_t)g[q + 2] << 16 | (uint32_t)g[q + 3] << 24;
     } else {
 #pragma unroll
         for (int b = 0; b < 4; b++)
-            if (q + b < I.plen) x |= (uint32_t)I.g[q + b] << (8 * b);
+            if (q + b < plen) x |= (uint32_t)g[q + b] << (8 * b);
     }
-    I.win = x;
+    return x;
 }
 
-__device__ __forceinline__ uint32_t in_byte(InBits& I, uint32_t at) {
+__device__ __forceinline__ void in_window(InBits& I, uint32_t at) {
+    I.wlo = __builtin_amdgcn_readfirstlane(at & ~3u);
+    I.win = in_load(I.g, I.plen, I.wlo, I.lane);
+}
+
+// 4 payload bytes from the window (little-endian; zeros past the payload)
+__device__ __forceinline__ uint32_t in_word(InBits& I, uint32_t at) {
     uint32_t r = __builtin_amdgcn_readfirstlane(at - I.wlo);
-    if (r >= 256) {  // uniform
+    if (r > 248) {  // uniform: keep lane (r >> 2) + 1 inside the window
         in_window(I, at);
         r = __builtin_amdgcn_readfirstlane(at - I.wlo);
     }
-    return __builtin_amdgcn_readfirstlane((readlane(I.win, r >> 2) >> ((r & 3) * 8)) & 0xFF);
+    const uint32_t lo = readlane(I.win, r >> 2), hi = readlane(I.win, (r >> 2) + 1);
+    return __builtin_amdgcn_readfirstlane(__builtin_amdgcn_alignbyte(hi, lo, r & 3));
 }
 
-// keep >= 32 bits in the buffer while payload bytes remain (missing bits read as
-// zero; the caller checks I.cnt against what it consumes)
+// top the bit buffer up with the next (at most 4) payload bytes when it holds
+// 32 bits or fewer; the caller checks I.cnt against what it consumes
 __device__ __forceinline__ void in_fill(InBits& I) {
-    while (I.cnt <= 56 && I.pos < I.plen) {
-        I.buf |= (uint64_t)in_byte(I, I.pos) << I.cnt;
-        I.cnt += 8;
-        I.pos++;
-        if (I.cnt >= 32) break;
-    }
+    if (I.cnt > 32 || I.pos >= I.plen) return;
+    const uint32_t avail = min(4u, I.plen - I.pos);
+    I.buf |= (uint64_t)in_word(I, I.pos) << I.cnt;
+    I.cnt += 8 * avail;
+    I.pos += avail;
 }
 
 // take n bits (n <= 32); false when the payload is exhausted
 __device__ __forceinline__ bool in_take(InBits& I, uint32_t n, uint32_t& v) {
-    if (I.cnt < n) in_fill(I);
     if (I.cnt < n) {
         in_fill(I);
         if (I.cnt < n) return false;
@@ -168,19 +185,26 @@ __device__ bool inf_build(InfSmem<OUTMAX>& S, int t, const uint8_t* len, int nsy
         off += count[b];
     }
     wave_sync();
+    // lookup entries: entry x holds the code whose bits (read LSB first) prefix x
+    const uint32_t first10 = (uint32_t)S.first[t][LUTB], cnt10 = count[LUTB];
+    (void)first10;
+    for (uint32_t x = lane; x < (1u << LUTB); x += 64) {
+        const uint32_t v = __builtin_bitreverse32(x) >> (32 - LUTB);  // MSB-first 10-bit window
+        uint16_t e = LUT_BAD;
+        uint32_t f = 0, pv = 0, of = 0;
 #pragma unroll
-    for (int j = 0; j < J; j++) {
-        if (!l[j]) continue;
-        const uint32_t L = l[j];
-        const uint32_t rc = __builtin_bitreverse32(code[j]) >> (32 - L);  // LSB-first index
-        const uint32_t sym = lane + 64 * j;
-        if (L <= (uint32_t)LUTB) {
-            const uint16_t e = (uint16_t)(sym << 5 | L << 1 | 1);  // sym 0..319, len 1..10
-            for (uint32_t k = 0; k < (1u << (LUTB - L)); k++) S.lut[t][rc | k << L] = e;
-        } else {
-            S.lut[t][rc & ((1u << LUTB) - 1)] = LUT_LONG;
+        for (int L = 1; L <= LUTB; L++) {
+            f = (f + pv) << 1;                 // first code of length L (same recurrence)
+            const uint32_t c = v >> (LUTB - L);
+            if (e == LUT_BAD && count[L] && c >= f && c - f < count[L])
+                e = (uint16_t)(S.sorted[t][of + (c - f)] << 5 | (uint32_t)L << 1 | 1);
+            pv = count[L];
+            of += count[L];
         }
+        if (e == LUT_BAD && maxl > (uint32_t)LUTB && v >= f + cnt10) e = LUT_LONG;
+        S.lut[t][x] = e;
     }
+    (void)code;
     wave_sync();
     return true;
 }
@@ -189,7 +213,9 @@ __device__ bool inf_build(InfSmem<OUTMAX>& S, int t, const uint8_t* len, int nsy
 template <uint32_t OUTMAX>
 __device__ __forceinline__ int inf_sym(InfSmem<OUTMAX>& S, int t, InBits& I) {
     if (I.cnt < 15) in_fill(I);
-    const uint16_t e = S.lut[t][I.buf & ((1u << LUTB) - 1)];
+    // (LDS values are not known to be wave-uniform: readfirstlane keeps the
+    // decode loop on the scalar unit)
+    const uint32_t e = __builtin_amdgcn_readfirstlane(S.lut[t][I.buf & ((1u << LUTB) - 1)]);
     if (e & 1) {
         const uint32_t L = (e >> 1) & 15;
         if (L > I.cnt) return -1;
@@ -204,11 +230,12 @@ __device__ __forceinline__ int inf_sym(InfSmem<OUTMAX>& S, int t, InBits& I) {
         if (L > I.cnt) return -1;
         c = c << 1 | (uint32_t)((I.buf >> (L - 1)) & 1);
         if (L <= (uint32_t)LUTB) continue;
-        const uint32_t cnt = S.cnt[t][L], f = S.first[t][L];
+        const uint32_t cnt = __builtin_amdgcn_readfirstlane(S.cnt[t][L]);
+        const uint32_t f = __builtin_amdgcn_readfirstlane(S.first[t][L]);
         if (c - f < cnt && c >= f) {
             I.buf >>= L;
             I.cnt -= L;
-            return S.sorted[t][S.offs[t][L] + (c - f)];
+            return (int)__builtin_amdgcn_readfirstlane(S.sorted[t][__builtin_amdgcn_readfirstlane(S.offs[t][L]) + (c - f)]);
         }
     }
     return -1;
@@ -216,8 +243,15 @@ __device__ __forceinline__ int inf_sym(InfSmem<OUTMAX>& S, int t, InBits& I) {
 
 // the whole zlib stream; returns the decoded length, -1 invalid, -2 output
 // larger than OUTMAX (host path)
+#ifdef AMBC_STAMPS
+#define ISTAMP_PARAMS , uint64_t* _acc, uint64_t& _st_t
+#define ISTAMP_ARGS , _acc, _st_t
+#else
+#define ISTAMP_PARAMS
+#define ISTAMP_ARGS
+#endif
 template <uint32_t OUTMAX>
-__device__ int64_t inflate_stream(InfSmem<OUTMAX>& S, const uint8_t* g, uint32_t plen, uint32_t lane) {
+__device__ int64_t inflate_stream(InfSmem<OUTMAX>& S, const uint8_t* g, uint32_t plen, uint32_t lane ISTAMP_PARAMS) {
     InBits I;
     I.g = g;
     I.plen = plen;
@@ -265,8 +299,8 @@ __device__ int64_t inflate_stream(InfSmem<OUTMAX>& S, const uint8_t* g, uint32_t
                     S.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : (s < 320 ? 5 : 0);
                 wave_sync();
                 // literal/length 0..287, distance 0..29 (+30, 31: codes that decode as invalid)
-                if (!inf_build(S, 0, S.lens, 288, 1, lane)) return -1;
-                if (!inf_build(S, 1, S.lens + 288, 32, 1, lane)) return -1;
+                if (!uniform_u32(inf_build(S, 0, S.lens, 288, 1, lane))) return -1;
+                if (!uniform_u32(inf_build(S, 1, S.lens + 288, 32, 1, lane))) return -1;
             } else {
                 uint32_t h;
                 if (!in_take(I, 14, h)) return -1;
@@ -280,7 +314,7 @@ __device__ int64_t inflate_stream(InfSmem<OUTMAX>& S, const uint8_t* g, uint32_t
                     if (lane == 0) S.lens[c_clord2[i]] = (uint8_t)c;
                 }
                 wave_sync();
-                if (!inf_build(S, 0, S.lens, 19, 0, lane)) return -1;
+                if (!uniform_u32(inf_build(S, 0, S.lens, 19, 0, lane))) return -1;
                 uint32_t have = 0;
                 const uint32_t tot = nlen + ndist;
                 uint32_t lastlen = 0;
@@ -319,10 +353,11 @@ __device__ int64_t inflate_stream(InfSmem<OUTMAX>& S, const uint8_t* g, uint32_t
                 for (uint32_t s = nlen + lane; s < 288; s += 64) S.lens[s] = 0;
                 for (uint32_t s = 288 + ndist + lane; s < 320; s += 64) S.lens[s] = 0;
                 wave_sync();
-                if (S.lens[256] == 0) return -1;  // missing end-of-block code
-                if (!inf_build(S, 0, S.lens, 288, 1, lane)) return -1;
-                if (!inf_build(S, 1, S.lens + 288, 32, 1, lane)) return -1;
+                if (__builtin_amdgcn_readfirstlane(S.lens[256]) == 0) return -1;  // missing end-of-block code
+                if (!uniform_u32(inf_build(S, 0, S.lens, 288, 1, lane))) return -1;
+                if (!uniform_u32(inf_build(S, 1, S.lens + 288, 32, 1, lane))) return -1;
             }
+            ISTAMP(0);
             // symbols
             for (;;) {
                 const int sy = inf_sym(S, 0, I);
@@ -362,16 +397,23 @@ __device__ int64_t inflate_stream(InfSmem<OUTMAX>& S, const uint8_t* g, uint32_t
                 if (op + L > OUTMAX) return -2;
                 // entries point into the period before the match (chains stay short)
                 const uint32_t m0 = op - D;
-                const uint32_t lmod = lane % D;
-                uint32_t bmod = 0;
-                for (uint32_t b = 0; b < L; b += 64) {
-                    uint32_t c = bmod + lmod;
-                    if (c >= D) c -= D;
-                    if (b + lane < L) S.src[op + b + lane] = (uint16_t)(m0 + c);
-                    bmod = (bmod + 64) % D;
+                if (D >= L) {
+                    if (lane < L) S.src[op + lane] = (uint16_t)(m0 + lane);
+                    for (uint32_t b = 64; b < L; b += 64)
+                        if (b + lane < L) S.src[op + b + lane] = (uint16_t)(m0 + b + lane);
+                } else {
+                    const uint32_t lmod = lane % D;
+                    uint32_t bmod = 0;
+                    for (uint32_t b = 0; b < L; b += 64) {
+                        uint32_t c = bmod + lmod;
+                        if (c >= D) c -= D;
+                        if (b + lane < L) S.src[op + b + lane] = (uint16_t)(m0 + c);
+                        bmod = (bmod + 64) % D;
+                    }
                 }
                 op += L;
             }
+            ISTAMP(1);
         } else {
             return -1;  // invalid block type
         }
@@ -408,6 +450,7 @@ __device__ int64_t inflate_stream(InfSmem<OUTMAX>& S, const uint8_t* g, uint32_t
         asum += c;
         bsum += (uint64_t)(op - q) * c;
     }
+    ISTAMP(2);
     asum = wave_sum<uint64_t>(asum);
     bsum = wave_sum<uint64_t>(bsum);
     const uint32_t adler = (uint32_t)(((op + bsum) % 65521) << 16 | ((1 + asum) % 65521));
@@ -419,11 +462,15 @@ template <uint32_t OUTMAX>
 __global__ __launch_bounds__(64) void k_decode_inflate(DecArgs A) {
     __shared__ InfSmem<OUTMAX> S;
     const uint32_t lane = threadIdx.x;
-    const uint32_t j = A.list ? A.list[blockIdx.x] : blockIdx.x;
+    const uint32_t j = uniform_u32(A.list ? A.list[blockIdx.x] : blockIdx.x);
     const DecJob J = A.jobs[j];
-    uint8_t* out = A.out + J.out_off;
-    const uint32_t orig = J.orig;
-    const int64_t r = inflate_stream(S, A.body + J.body_off, J.clen, lane);
+    uint8_t* out = uniform_ptr(A.out + J.out_off);
+    const uint32_t orig = uniform_u32(J.orig);
+#ifdef AMBC_STAMPS
+    uint64_t _st_t = __builtin_amdgcn_s_memtime();
+    uint64_t _acc[4] = {0, 0, 0, 0};
+#endif
+    const int64_t r = inflate_stream(S, uniform_ptr(A.body + J.body_off), uniform_u32(J.clen), lane ISTAMP_ARGS);
     wave_sync();
     if (r == -2) {  // larger than the map: the host inflates it
         if (lane == 0) A.produced[j] = 0xFFFFFFFEu;
@@ -433,10 +480,26 @@ __global__ __launch_bounds__(64) void k_decode_inflate(DecArgs A) {
         for (uint32_t q = lane; q < orig; q += 64) out[q] = 0;
     } else {
         const uint32_t m = min((uint32_t)r, orig);
-        for (uint32_t q = lane; q < m; q += 64) out[q] = (uint8_t)(S.src[q] & 0xFF);
+        const uint32_t head = min((uint32_t)((4 - (reinterpret_cast<uintptr_t>(out) & 3)) & 3), m);
+        if (lane < head) out[lane] = (uint8_t)(S.src[lane] & 0xFF);
+        const uint32_t nw = (m - head) >> 2;
+        uint32_t* o32 = reinterpret_cast<uint32_t*>(out + head);
+        for (uint32_t w = lane; w < nw; w += 64) {
+            const uint32_t q = head + 4 * w;
+            o32[w] = (S.src[q] & 0xFFu) | (S.src[q + 1] & 0xFFu) << 8 | (S.src[q + 2] & 0xFFu) << 16 |
+                     (S.src[q + 3] & 0xFFu) << 24;
+        }
+        for (uint32_t q = head + (nw << 2) + lane; q < m; q += 64) out[q] = (uint8_t)(S.src[q] & 0xFF);
         for (uint32_t q = m + lane; q < orig; q += 64) out[q] = 0;
     }
     if (lane == 0) A.produced[j] = orig;
+#ifdef AMBC_STAMPS
+    ISTAMP(3);
+    if (lane == 0 && A.stamps) {
+        for (int q = 0; q < 4; q++) A.stamps[(uint64_t)j * 8 + q] = _acc[q];
+        A.stamps[(uint64_t)j * 8 + 7] = 5;
+    }
+#endif
 }
 
 }  // namespace

@@ -136,4 +136,17 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 
 __device__ __forceinline__ uint32_t bcast0(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// Values loaded from memory are not known to be wave-uniform even when every
+// lane loaded the same address; these make that explicit so that the code
+// depending on them stays on the scalar unit.
+// (the builtin returns int: go through uint32_t so that nothing sign-extends)
+__device__ __forceinline__ uint32_t uniform_u32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
+    return (uint64_t)uniform_u32((uint32_t)v) | (uint64_t)uniform_u32((uint32_t)(v >> 32)) << 32;
+}
+template <typename T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {
+    return reinterpret_cast<T*>(uniform_u64(reinterpret_cast<uint64_t>(p)));
+}
+
 }  // namespace ambc

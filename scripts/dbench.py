@@ -20,9 +20,10 @@ def main():
     ap.add_argument("--size", type=int, default=256 << 20)
     ap.add_argument("--chunk", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--methods", default="1,3,4,9")
     args = ap.parse_args()
     from ambc import AdaptiveCompressor
-    comp = AdaptiveCompressor(chunk_size=args.chunk, methods=(1, 3, 4, 9))
+    comp = AdaptiveCompressor(chunk_size=args.chunk, methods=[int(x) for x in args.methods.split(",")])
     for name, a in make_inputs(args.size).items():
         data = a.tobytes()
         body = comp._adaptive_compress(data)
