@@ -252,6 +252,63 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
     };
 
     uint32_t kdist = 0;
+    // Huffman code lengths/codes into clen[]/code[] from hist[] (kdist >= 2 symbols)
+    auto huff_tree = [&](uint32_t& nb, uint32_t& maxlen) {
+        // tree: slot s holds the active node whose first symbol is s; merge the two
+        // smallest (weight, first symbol) keys (heapq order, :482-494)
+        uint32_t key[4];
+        uint32_t nid[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t s = lane + 64 * j, c = S.hist[s];
+            key[j] = c ? (c << 8 | s) : 0xFFFFFFFFu;
+            nid[j] = s;
+        }
+#pragma unroll 1
+        for (uint32_t m = 0; m + 1 < kdist; m++) {
+            uint32_t lm = min(min(key[0], key[1]), min(key[2], key[3]));
+            const uint32_t k1 = wave_min_u32(lm);
+            uint32_t lm2 = 0xFFFFFFFFu;
+#pragma unroll
+            for (int j = 0; j < 4; j++) if (key[j] != k1) lm2 = min(lm2, key[j]);
+            const uint32_t k2 = wave_min_u32(lm2);
+            const uint32_t s1 = k1 & 255u, s2 = k2 & 255u;
+            const uint32_t merged = ((k1 >> 8) + (k2 >> 8)) << 8 | s1;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                if (lane + 64 * j == s1) {
+                    S.parent()[nid[j]] = (uint16_t)(256 + m); S.pbit()[nid[j]] = 0;
+                    key[j] = merged; nid[j] = 256 + m;
+                } else if (lane + 64 * j == s2) {
+                    S.parent()[nid[j]] = (uint16_t)(256 + m); S.pbit()[nid[j]] = 1;
+                    key[j] = 0xFFFFFFFFu;
+                }
+            }
+        }
+        wave_sync();
+        const uint32_t root = 256 + kdist - 2;
+        nb = 0; maxlen = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t s = lane + 64 * j, c = S.hist[s];
+            if (c) {
+                uint32_t nd = s, len = 0, code = 0;
+                while (nd != root) {
+                    if (len < 32) code |= (uint32_t)S.pbit()[nd] << len;
+                    len++;
+                    nd = S.parent()[nd];
+                }
+                S.clen[s] = (uint8_t)min(len, 255u);
+                S.code[s] = code;
+                nb += c * len;
+                maxlen = max(maxlen, len);
+            }
+        }
+        nb = wave_sum_u32(nb);
+        maxlen = (uint32_t)wave_max_i32((int)maxlen);
+        wave_sync();
+    };
+
     bool huff_su = false;
     if ((eligible(3) || analyze) && (n >= 100 || force)) {
         double part = 0.0;
@@ -286,59 +343,8 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         }
         huff_su = n >= 100 && H < 7.0;
         if (eligible(3) && (force || huff_su) && kdist >= 2 && kdist <= 255) {
-            // tree: slot s holds the active node whose first symbol is s; merge the two
-            // smallest (weight, first symbol) keys (heapq order, :482-494)
-            uint32_t key[4];
-            uint32_t nid[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint32_t s = lane + 64 * j, c = S.hist[s];
-                key[j] = c ? (c << 8 | s) : 0xFFFFFFFFu;
-                nid[j] = s;
-            }
-#pragma unroll 1
-            for (uint32_t m = 0; m + 1 < kdist; m++) {
-                uint32_t lm = min(min(key[0], key[1]), min(key[2], key[3]));
-                const uint32_t k1 = wave_min_u32(lm);
-                uint32_t lm2 = 0xFFFFFFFFu;
-#pragma unroll
-                for (int j = 0; j < 4; j++) if (key[j] != k1) lm2 = min(lm2, key[j]);
-                const uint32_t k2 = wave_min_u32(lm2);
-                const uint32_t s1 = k1 & 255u, s2 = k2 & 255u;
-                const uint32_t merged = ((k1 >> 8) + (k2 >> 8)) << 8 | s1;
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    if (lane + 64 * j == s1) {
-                        S.parent()[nid[j]] = (uint16_t)(256 + m); S.pbit()[nid[j]] = 0;
-                        key[j] = merged; nid[j] = 256 + m;
-                    } else if (lane + 64 * j == s2) {
-                        S.parent()[nid[j]] = (uint16_t)(256 + m); S.pbit()[nid[j]] = 1;
-                        key[j] = 0xFFFFFFFFu;
-                    }
-                }
-            }
-            wave_sync();
-            const uint32_t root = 256 + kdist - 2;
-            uint32_t nb = 0, maxlen = 0;
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint32_t s = lane + 64 * j, c = S.hist[s];
-                if (c) {
-                    uint32_t nd = s, len = 0, code = 0;
-                    while (nd != root) {
-                        if (len < 32) code |= (uint32_t)S.pbit()[nd] << len;
-                        len++;
-                        nd = S.parent()[nd];
-                    }
-                    S.clen[s] = (uint8_t)min(len, 255u);
-                    S.code[s] = code;
-                    nb += c * len;
-                    maxlen = max(maxlen, len);
-                }
-            }
-            nb = wave_sum_u32(nb);
-            maxlen = (uint32_t)wave_max_i32((int)maxlen);
-            wave_sync();
+            uint32_t nb, maxlen;
+            huff_tree(nb, maxlen);
             if (maxlen <= 32) {
                 const uint32_t l = 1 + 5 * kdist + 4 + (nb + 7) / 8;
                 if (l + HDR < best) { best = l + HDR; win = 3; wlen = l; }
@@ -367,9 +373,13 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         const bool single = wave_sum_u32(nz) == 1;
         if (lane == 0) A.bestpre[k] = best | (uniform ? 0x80000000u : 0u) | (single ? 0x40000000u : 0u);
     }
+    bool lz4_ran = false;   // the LZ4 walk reuses hist[]/code[] for its bucket masks
     if (eligible(9) && (force || n >= 1024) && best > 42) {
+        lz4_ran = true;
         uint16_t* last = reinterpret_cast<uint16_t*>(S.region);
+        uint64_t* bk = reinterpret_cast<uint64_t*>(S.hist);   // 256 x 8 B over hist + code
         for (uint32_t i = lane; i < (1u << LZ4_HASH_BITS); i += 64) last[i] = 0xFFFF;
+        for (uint32_t i = lane; i < 256; i += 64) bk[i] = 0;
         wave_sync();
         // LZ4 wins iff block < budget; forced (single-method) encodes fall back to a
         // stored block once the compressed block would reach n (LZ4F rule)
@@ -378,20 +388,34 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         uint8_t* blk = slot + 19;
         uint32_t emitted = 0, anchor = 0, nextp = 0;
         bool alive = true;
-        constexpr uint32_t LCAP = 64;       // per-lane precomputed match length cap
+        constexpr uint32_t LCAP = 32;       // per-lane precomputed match length cap
 #pragma unroll 1
         for (int base = 0; base <= mlim && alive; base += 64) {
             const int i = base + (int)lane;
             const bool act = i <= mlim;
             const uint32_t v = act ? lds_rd32(S.chunk, (uint32_t)i) : 0u;
             const uint32_t h = (v * 2654435761u) >> (32 - LZ4_HASH_BITS);
-            uint64_t peers = __ballot(act);
+            // lanes with my hash: one shared hash (runs) is the active mask; else an
+            // order-free LDS OR per 8-bit bucket, then 3 ballots for the top bits
+            const uint64_t actm = __ballot(act);
+            const uint32_t h0 = __builtin_amdgcn_readfirstlane(h);
+            uint64_t peers;
+            if (__ballot(act && h != h0) == 0ull) {
+                peers = act ? actm : 0ull;
+            } else {
+                if (act) atomicOr(reinterpret_cast<unsigned long long*>(&bk[h & 255u]), 1ull << lane);
+                wave_sync();
+                peers = act ? bk[h & 255u] : 0ull;
 #pragma unroll
-            for (int b = 0; b < (int)LZ4_HASH_BITS; b++) {
-                const uint64_t m = __ballot((h >> b) & 1u);
-                peers &= ((h >> b) & 1u) ? m : ~m;
+                for (int b = 8; b < (int)LZ4_HASH_BITS; b++) {
+                    const uint64_t m = __ballot((h >> b) & 1u);
+                    const uint64_t flip = 0ull - (uint64_t)((h >> b) & 1u);
+                    peers &= ~(m ^ flip);
+                }
+                wave_sync();
+                if (act) bk[h & 255u] = 0ull;
             }
-            const uint64_t lower = lane ? (peers & ((1ull << lane) - 1)) : 0ull;
+            const uint64_t lower = peers & ((1ull << lane) - 1ull);
             int cand;
             if (lower) cand = base + 63 - (int)__clzll((long long)lower);
             else {
@@ -404,42 +428,56 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
             if (act && (peers >> lane) == 1ull) last[h] = (uint16_t)i;
             STAMP(2);
             if (base + 63 < (int)nextp) continue;   // round lies inside the previous match
-            // per-lane match length, dword compares, capped at LCAP
+            // per-lane match length: 16 bytes per step (five aligned dwords per side
+            // issued together), capped at LCAP; the walk extends longer ones
             uint32_t L = 0;
-            if (valid && (uint32_t)i >= nextp) {
-                const uint32_t lim = n - 5 - (uint32_t)i;
-                const uint32_t cap = min(lim, LCAP);
-                L = 4;
-                while (L < cap) {
-                    const uint32_t x = lds_rd32(S.chunk, (uint32_t)i + L) ^ lds_rd32(S.chunk, (uint32_t)cand + L);
-                    if (x) { L += (uint32_t)__builtin_ctz(x) >> 3; break; }
-                    L += 4;
+            bool run = valid && (uint32_t)i >= nextp;
+            const uint32_t lim = run ? n - 5 - (uint32_t)i : 0u;
+            const uint32_t cap = min(lim, LCAP);
+            if (run) L = 4;
+            const uint32_t* c32 = reinterpret_cast<const uint32_t*>(S.chunk);
+            const uint32_t si = (uint32_t)i & 3u, sc = (uint32_t)cand & 3u;
+#pragma unroll 1
+            while (__ballot(run && L < cap)) {
+                if (run && L < cap) {
+                    const uint32_t ai = ((uint32_t)i + L) >> 2, ac = ((uint32_t)cand + L) >> 2;
+                    uint32_t wi[5], wc[5];
+#pragma unroll
+                    for (int t = 0; t < 5; t++) { wi[t] = c32[ai + t]; wc[t] = c32[ac + t]; }
+                    uint32_t add = 16;
+#pragma unroll
+                    for (int t = 3; t >= 0; t--) {
+                        const uint32_t x = __builtin_amdgcn_alignbyte(wi[t + 1], wi[t], si) ^
+                                           __builtin_amdgcn_alignbyte(wc[t + 1], wc[t], sc);
+                        if (x) add = 4 * t + ((uint32_t)__builtin_ctz(x) >> 3);
+                    }
+                    L += add;
+                    if (add < 16) run = false;
                 }
-                L = min(L, lim);
             }
+            L = min(L, lim);
             STAMP(3);
             // (1) scalar greedy walk: select this round's match starts (one bit per
             // lane).  p = next undecided position relative to base; everything here
             // is wave-uniform (SALU + v_readlane).
             uint64_t sel = 0;
-            uint32_t p = (int)nextp > base ? nextp - (uint32_t)base : 0u;
+            uint32_t p = __builtin_amdgcn_readfirstlane((int)nextp > base ? nextp - (uint32_t)base : 0u);
             while (p < 64) {
-                p = __builtin_amdgcn_readfirstlane(p);
                 const uint64_t m = vm & (~0ull << p);
                 if (!m) break;
                 const uint32_t L0 = (uint32_t)__builtin_ctzll(m);
                 uint32_t Lj = readlane(L, L0);
                 if (Lj >= LCAP) {
                     const uint32_t j = (uint32_t)base + L0;
-                    const uint32_t lim = n - 5 - j;
-                    if (Lj < lim) {
+                    const uint32_t lj = n - 5 - j;
+                    if (Lj < lj) {
                         // long match: extend cooperatively, 256 bytes per step
                         const uint32_t c = readlane((uint32_t)cand, L0);
-                        while (Lj < lim) {
+                        while (Lj < lj) {
                             const uint32_t q = Lj + 4 * lane;
                             uint32_t fd = 0;
                             bool eq = false;
-                            if (q < lim) {
+                            if (q < lj) {
                                 const uint32_t x = lds_rd32(S.chunk, j + q) ^ lds_rd32(S.chunk, c + q);
                                 eq = x == 0;
                                 fd = x ? (uint32_t)__builtin_ctz(x) >> 3 : 4;
@@ -452,8 +490,8 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                             }
                             Lj += 256;
                         }
-                        Lj = __builtin_amdgcn_readfirstlane(min(Lj, lim));
-                        if (lane == L0) L = Lj;
+                        Lj = __builtin_amdgcn_readfirstlane(min(Lj, lj));
+                        L = lane == L0 ? Lj : L;
                     }
                 }
                 sel |= 1ull << L0;
@@ -482,7 +520,15 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                     uint32_t q = 1;
                     for (uint32_t t = 0; t < xl; t++) o[q + t] = (uint8_t)ext_byte(lit, xl, t);
                     q += xl;
-                    for (uint32_t t = 0; t < lit; t++) o[q + t] = S.chunk[(uint32_t)pe + t];
+                    // literals: 8 bytes per step from two unaligned LDS dwords
+#pragma unroll 1
+                    for (uint32_t t = 0; t < lit; t += 8) {
+                        const uint32_t w0 = lds_rd32(S.chunk, (uint32_t)pe + t);
+                        const uint32_t w1 = lds_rd32(S.chunk, (uint32_t)pe + t + 4);
+#pragma unroll
+                        for (uint32_t b = 0; b < 8; b++)
+                            if (t + b < lit) o[q + t + b] = (uint8_t)((b < 4 ? w0 : w1) >> (8 * (b & 3)));
+                    }
                     q += lit;
                     const uint32_t offv = (uint32_t)(i - cand);
                     o[q] = (uint8_t)offv;
@@ -596,6 +642,26 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
             wave_sync();
         }
     } else if (win == 3) {
+        if (lz4_ran) {
+            // the LZ4 walk overwrote hist[]/code[]: count again, rebuild the same tree
+            for (uint32_t i = lane; i < 256; i += 64) S.hist[i] = 0;
+            wave_sync();
+#pragma unroll 1
+            for (int r = 0; r < ROUNDS; r++) {
+                const uint32_t b0 = (uint32_t)(r * 64 + lane) * BS;
+                uint32_t cur = S.chunk[b0], rc = 0;
+                for_block_bytes<BS>(S.chunk, b0, [&](uint32_t p, uint32_t c, uint32_t) {
+                    if (p < n) {
+                        if (c == cur) rc++;
+                        else { atomicAdd(&S.hist[cur], rc); cur = c; rc = 1; }
+                    }
+                });
+                if (rc) atomicAdd(&S.hist[cur], rc);
+            }
+            wave_sync();
+            uint32_t nb2, ml2;
+            huff_tree(nb2, ml2);
+        }
         compute_first();   // (the LZ4 table may have overwritten an earlier order[])
         uint32_t* bits = S.region;
         const uint32_t kk = kdist;
