@@ -428,10 +428,13 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
             if (act && (peers >> lane) == 1ull) last[h] = (uint16_t)i;
             STAMP(2);
             if (base + 63 < (int)nextp) continue;   // round lies inside the previous match
+            uint32_t p = __builtin_amdgcn_readfirstlane((int)nextp > base ? nextp - (uint32_t)base : 0u);
+            if ((vm & (~0ull << p)) == 0ull) continue;   // no match starts here: all literals
             // per-lane match length: 16 bytes per step (five aligned dwords per side
             // issued together), capped at LCAP; the walk extends longer ones
             uint32_t L = 0;
-            bool run = valid && (uint32_t)i >= nextp;
+            const bool run_l = valid && (uint32_t)i >= nextp;
+            bool run = run_l;
             const uint32_t lim = run ? n - 5 - (uint32_t)i : 0u;
             const uint32_t cap = min(lim, LCAP);
             if (run) L = 4;
@@ -457,45 +460,73 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
             }
             L = min(L, lim);
             STAMP(3);
-            // (1) scalar greedy walk: select this round's match starts (one bit per
-            // lane).  p = next undecided position relative to base; everything here
-            // is wave-uniform (SALU + v_readlane).
+            // (1) greedy walk over this round's positions.  Every lane first links
+            // itself to the next match start the greedy parse would take after it
+            // (first valid position >= its match end; 64 = leaves the round, 65 =
+            // its match needs extending beyond LCAP), and two bpermutes extend the
+            // link to the next four starts, packed 7 bits each.  The scalar walk
+            // then consumes four matches per v_readlane.
+            const bool longl = run_l && L >= LCAP && L < lim;
+            const uint32_t E = lane + L;    // match end relative to base (lanes with L)
+            uint32_t nx1;
+            {
+                const uint64_t mm = E < 64 ? (vm & (~0ull << E)) : 0ull;
+                nx1 = longl ? 65u : (mm ? (uint32_t)__builtin_ctzll(mm) : 64u);
+            }
+            uint32_t nx2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(min(nx1, 63u) << 2), (int)nx1);
+            if (nx1 >= 64) nx2 = nx1;
+            const uint32_t pr = nx1 | nx2 << 7;
+            uint32_t pr2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(min(nx2, 63u) << 2), (int)pr);
+            if (nx2 >= 64) pr2 = nx2 | nx2 << 7;
+            const uint32_t pack = pr | pr2 << 14;
             uint64_t sel = 0;
-            uint32_t p = __builtin_amdgcn_readfirstlane((int)nextp > base ? nextp - (uint32_t)base : 0u);
-            while (p < 64) {
-                const uint64_t m = vm & (~0ull << p);
-                if (!m) break;
-                const uint32_t L0 = (uint32_t)__builtin_ctzll(m);
-                uint32_t Lj = readlane(L, L0);
-                if (Lj >= LCAP) {
-                    const uint32_t j = (uint32_t)base + L0;
-                    const uint32_t lj = n - 5 - j;
-                    if (Lj < lj) {
-                        // long match: extend cooperatively, 256 bytes per step
-                        const uint32_t c = readlane((uint32_t)cand, L0);
-                        while (Lj < lj) {
-                            const uint32_t q = Lj + 4 * lane;
-                            uint32_t fd = 0;
-                            bool eq = false;
-                            if (q < lj) {
-                                const uint32_t x = lds_rd32(S.chunk, j + q) ^ lds_rd32(S.chunk, c + q);
-                                eq = x == 0;
-                                fd = x ? (uint32_t)__builtin_ctz(x) >> 3 : 4;
-                            }
-                            const uint64_t ne = __ballot(!eq);
-                            if (ne) {
-                                const uint32_t lk = (uint32_t)__builtin_ctzll(ne);
-                                Lj += 4 * lk + readlane(fd, lk);
-                                break;
-                            }
-                            Lj += 256;
-                        }
-                        Lj = __builtin_amdgcn_readfirstlane(min(Lj, lj));
-                        L = lane == L0 ? Lj : L;
+            {
+                const uint64_t m0 = vm & (~0ull << p);
+                uint32_t cur = m0 ? (uint32_t)__builtin_ctzll(m0) : 64u;
+                while (cur < 64) {
+                    sel |= 1ull << cur;
+                    const uint32_t pk = readlane(pack, cur);
+                    uint32_t x = pk & 127u, f = 1;
+                    while (x < 64) {
+                        sel |= 1ull << x;
+                        cur = x;
+                        if (f == 4) break;
+                        x = (pk >> (7 * f)) & 127u;
+                        f++;
                     }
+                    if (x < 64) continue;          // four more starts taken; go on from cur
+                    if (x == 64) {                 // cur's match is the round's last
+                        p = readlane(E, cur);
+                        break;
+                    }
+                    // x == 65: cur's match reaches LCAP: extend cooperatively, 256 B per step
+                    const uint32_t j = (uint32_t)base + cur;
+                    const uint32_t lj = n - 5 - j;
+                    uint32_t Lj = readlane(L, cur);
+                    const uint32_t c = readlane((uint32_t)cand, cur);
+                    while (Lj < lj) {
+                        const uint32_t q = Lj + 4 * lane;
+                        uint32_t fd = 0;
+                        bool eq = false;
+                        if (q < lj) {
+                            const uint32_t xx = lds_rd32(S.chunk, j + q) ^ lds_rd32(S.chunk, c + q);
+                            eq = xx == 0;
+                            fd = xx ? (uint32_t)__builtin_ctz(xx) >> 3 : 4;
+                        }
+                        const uint64_t ne = __ballot(!eq);
+                        if (ne) {
+                            const uint32_t lk = (uint32_t)__builtin_ctzll(ne);
+                            Lj += 4 * lk + readlane(fd, lk);
+                            break;
+                        }
+                        Lj += 256;
+                    }
+                    Lj = __builtin_amdgcn_readfirstlane(min(Lj, lj));
+                    L = lane == cur ? Lj : L;
+                    p = cur + Lj;
+                    const uint64_t mn = p < 64 ? (vm & (~0ull << p)) : 0ull;
+                    cur = mn ? (uint32_t)__builtin_ctzll(mn) : 64u;
                 }
-                sel |= 1ull << L0;
-                p = L0 + Lj;
             }
             const uint32_t np = (uint32_t)base + p;
             STAMP(4);

@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--chunk", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--inputs", default="zero,random,ascii,mixed")
     ap.add_argument("--msets", default="-;1;3;9;1,3,4,9",
                     help="method sets, ';'-separated ('-' = none)")
     args = ap.parse_args()
@@ -55,6 +56,8 @@ def main():
     res = []
     inputs = make_inputs(n)
     for name, arr in inputs.items():
+        if name not in args.inputs.split(","):
+            continue
         _lib.check(lib.ambc_memcpy_h2d(ctx.h, 0, d_in, arr.ctypes.data, n), lib)
         msets = [() if m == "-" else tuple(int(x) for x in m.split(",")) for m in args.msets.split(";")]
         for mset in msets:
