@@ -538,34 +538,47 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                 const int pe = wave_excl_max(me ? i + (int)L : -1, (int)anchor);
                 const uint32_t lit = me ? (uint32_t)(i - pe) : 0u;
                 const uint32_t ml = me ? L - 4 : 0u;
-                const uint32_t xl = ext_len(lit), xm = ext_len(ml);
-                const uint32_t sz = me ? 1 + xl + lit + 2 + xm : 0u;
+                // length extension bytes only when some sequence needs them
+                const bool ext = __ballot(lit >= 15 || ml >= 15) != 0ull;
+                const uint32_t xl = ext ? ext_len(lit) : 0u, xm = ext ? ext_len(ml) : 0u;
+                const uint32_t sz = me ? 3 + xl + lit + xm : 0u;
                 const uint32_t incl = wave_incl_sum(sz);
                 const uint32_t tot = readlane(incl, 63);
                 // the sequential walk gives up at the first sequence that makes
                 // block + 1 >= budget; the round total decides the same way
                 if (emitted + tot + 1 >= budget) { alive = false; break; }
+                // 32-bit offsets from the (uniform) block pointer: saddr stores
+                const uint32_t q0 = emitted + incl - sz;     // token
+                const uint32_t ql = q0 + 1 + xl;             // first literal
                 if (me) {
-                    uint8_t* o = blk + emitted + incl - sz;
-                    o[0] = (uint8_t)((lit >= 15 ? 15 : lit) << 4 | (ml >= 15 ? 15 : ml));
-                    uint32_t q = 1;
-                    for (uint32_t t = 0; t < xl; t++) o[q + t] = (uint8_t)ext_byte(lit, xl, t);
-                    q += xl;
-                    // literals: 8 bytes per step from two unaligned LDS dwords
+                    blk[q0] = (uint8_t)((lit >= 15 ? 15 : lit) << 4 | (ml >= 15 ? 15 : ml));
+                    const uint32_t offv = (uint32_t)(i - cand);
+                    blk[ql + lit] = (uint8_t)offv;
+                    blk[ql + lit + 1] = (uint8_t)(offv >> 8);
+                }
+                if (ext && me) {
+                    for (uint32_t t = 0; t < xl; t++) blk[q0 + 1 + t] = (uint8_t)ext_byte(lit, xl, t);
+                    for (uint32_t t = 0; t < xm; t++) blk[ql + lit + 2 + t] = (uint8_t)ext_byte(ml, xm, t);
+                }
+                // literals: short runs per lane (8 bytes per step from two unaligned
+                // LDS dwords), long runs by the whole wave (one byte per lane)
+                if (me && lit && lit < 32) {
 #pragma unroll 1
                     for (uint32_t t = 0; t < lit; t += 8) {
                         const uint32_t w0 = lds_rd32(S.chunk, (uint32_t)pe + t);
                         const uint32_t w1 = lds_rd32(S.chunk, (uint32_t)pe + t + 4);
 #pragma unroll
                         for (uint32_t b = 0; b < 8; b++)
-                            if (t + b < lit) o[q + t + b] = (uint8_t)((b < 4 ? w0 : w1) >> (8 * (b & 3)));
+                            if (t + b < lit) blk[ql + t + b] = (uint8_t)((b < 4 ? w0 : w1) >> (8 * (b & 3)));
                     }
-                    q += lit;
-                    const uint32_t offv = (uint32_t)(i - cand);
-                    o[q] = (uint8_t)offv;
-                    o[q + 1] = (uint8_t)(offv >> 8);
-                    q += 2;
-                    for (uint32_t t = 0; t < xm; t++) o[q + t] = (uint8_t)ext_byte(ml, xm, t);
+                }
+                uint64_t lmask = __ballot(lit >= 32);
+                while (lmask) {
+                    const uint32_t j = (uint32_t)__builtin_ctzll(lmask);
+                    lmask &= lmask - 1;
+                    const uint32_t src = readlane((uint32_t)pe, j), dst = readlane(ql, j),
+                                   len = readlane(lit, j);
+                    for (uint32_t t = lane; t < len; t += 64) blk[dst + t] = S.chunk[src + t];
                 }
                 emitted = __builtin_amdgcn_readfirstlane(emitted + tot);
                 anchor = np;
