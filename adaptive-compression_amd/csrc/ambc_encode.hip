@@ -391,21 +391,27 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         constexpr uint32_t LCAP = 32;       // per-lane precomputed match length cap
 #pragma unroll 1
         for (int base = 0; base <= mlim && alive; base += 64) {
+            // control state is wave-uniform: keep it in SGPRs
+            nextp = __builtin_amdgcn_readfirstlane(nextp);
+            anchor = __builtin_amdgcn_readfirstlane(anchor);
+            emitted = __builtin_amdgcn_readfirstlane(emitted);
             const int i = base + (int)lane;
             const bool act = i <= mlim;
-            const uint32_t v = act ? lds_rd32(S.chunk, (uint32_t)i) : 0u;
+            // loads run for every lane (the chunk is zero padded past n + 63)
+            const uint32_t v = lds_rd32(S.chunk, (uint32_t)i);
             const uint32_t h = (v * 2654435761u) >> (32 - LZ4_HASH_BITS);
+            const uint32_t c16 = last[h];
             // lanes with my hash: one shared hash (runs) is the active mask; else an
             // order-free LDS OR per 8-bit bucket, then 3 ballots for the top bits
-            const uint64_t actm = __ballot(act);
+            const uint64_t actm = base + 63 <= mlim ? ~0ull : __ballot(act);
             const uint32_t h0 = __builtin_amdgcn_readfirstlane(h);
             uint64_t peers;
-            if (__ballot(act && h != h0) == 0ull) {
-                peers = act ? actm : 0ull;
+            if (__ballot(h != h0) == 0ull) {
+                peers = actm;
             } else {
-                if (act) atomicOr(reinterpret_cast<unsigned long long*>(&bk[h & 255u]), 1ull << lane);
+                atomicOr(reinterpret_cast<unsigned long long*>(&bk[h & 255u]), act ? 1ull << lane : 0ull);
                 wave_sync();
-                peers = act ? bk[h & 255u] : 0ull;
+                peers = bk[h & 255u] & actm;
 #pragma unroll
                 for (int b = 8; b < (int)LZ4_HASH_BITS; b++) {
                     const uint64_t m = __ballot((h >> b) & 1u);
@@ -413,16 +419,13 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                     peers &= ~(m ^ flip);
                 }
                 wave_sync();
-                if (act) bk[h & 255u] = 0ull;
+                bk[h & 255u] = 0ull;
             }
             const uint64_t lower = peers & ((1ull << lane) - 1ull);
-            int cand;
-            if (lower) cand = base + 63 - (int)__clzll((long long)lower);
-            else {
-                const uint16_t c = act ? last[h] : (uint16_t)0xFFFF;
-                cand = c == 0xFFFF ? -1 : (int)c;
-            }
-            const bool valid = act && cand >= 0 && lds_rd32(S.chunk, (uint32_t)cand) == v;
+            const int cand = lower ? base + 63 - (int)__clzll((long long)lower)
+                                   : (c16 == 0xFFFFu ? -1 : (int)c16);
+            const uint32_t cv = lds_rd32(S.chunk, (uint32_t)max(cand, 0));
+            const bool valid = act && cand >= 0 && cv == v;
             const uint64_t vm = __ballot(valid);
             wave_sync();
             if (act && (peers >> lane) == 1ull) last[h] = (uint16_t)i;
@@ -581,9 +584,9 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                     for (uint32_t t = lane; t < len; t += 64) blk[dst + t] = S.chunk[src + t];
                 }
                 emitted = __builtin_amdgcn_readfirstlane(emitted + tot);
-                anchor = np;
+                anchor = __builtin_amdgcn_readfirstlane(np);
             }
-            nextp = np;
+            nextp = __builtin_amdgcn_readfirstlane(np);
             STAMP(7);
         }
         uint32_t fin = 0, flit = 0, fxl = 0;
