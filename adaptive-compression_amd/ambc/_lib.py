@@ -34,7 +34,7 @@ EXPORTS = (
     "ambc_compress_device", "ambc_encode_method", "ambc_analyze", "ambc_host_alloc",
     "ambc_host_free", "ambc_device_alloc", "ambc_device_free", "ambc_memcpy_h2d",
     "ambc_memcpy_d2h", "ambc_synchronize", "ambc_synth_fill", "ambc_synth_device",
-    "ambc_last_kernel_times",
+    "ambc_last_kernel_times", "ambc_split_body", "ambc_decompress_device",
 )
 
 
@@ -102,6 +102,8 @@ def _declare(lib):
         "ambc_synth_fill": ([u8p, u64, u64], None),
         "ambc_synth_device": ([vp, i32, vp, u64, u64], i32),
         "ambc_last_kernel_times": ([vp, i32, C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)], i32),
+        "ambc_split_body": ([u8p, u64, u64, C.POINTER(u64), u32, C.POINTER(u64), C.POINTER(u64)], i32),
+        "ambc_decompress_device": ([vp, i32, u8p, u64, u64, C.POINTER(u64), vp, C.POINTER(Stats)], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

@@ -672,6 +672,17 @@ struct Walk {
     bool marker_error = false;
 };
 
+// bytes the reference's decode of one package appends when its codec behaves
+// (adaptive_compressor.py:426-442): unregistered ids copy the payload, raw
+// pads/truncates to orig, Delta yields min(clen, orig), codecs yield orig
+// (an empty payload decodes to nothing)
+uint64_t expect_len(uint32_t t, uint32_t clen, uint32_t orig, const uint64_t reg[4]) {
+    if (!registered_id(reg, t)) return clen;
+    if (t == 255) return orig;
+    if (t == 4) return clen ? std::min(clen, orig) : 0;
+    return clen ? orig : 0;
+}
+
 // _adaptive_decompress header walk (adaptive_compressor.py:399-445)
 void walk_body(const uint8_t* body, uint64_t blen, uint64_t orig_size, const uint64_t reg[4],
                const std::map<uint32_t, uint64_t>& known, Walk& w) {
@@ -825,7 +836,7 @@ static void inflate_all(const uint8_t* body, const std::vector<ambc_host_chunk>&
 
 static int decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t orig_size,
                          const uint64_t reg[4], uint8_t* out, std::vector<ambc_host_chunk>& host,
-                         ambc_stats* st) {
+                         ambc_stats* st, uint8_t* d_out_ext = nullptr) {
     const uint64_t t0 = now_ns();
     HIPCHK(hipSetDevice(d.id));
     hipStream_t s = d.stream;
@@ -931,8 +942,14 @@ static int decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t or
         }
         if (!redo) break;
     }
+    if (d_out_ext && (!w.zlib.empty() || !hostinf.empty() || !w.host.empty()))
+        return fail(AMBC_E_HOSTCODEC, "body has packages decoded by host codecs: use ambc_decompress_ex");
     t = now_ns();
-    HIPCHK(hipMemcpyAsync(out, d.dout.p, orig_size, hipMemcpyDeviceToHost, s));
+    if (d_out_ext) {   // device-resident output (multi-GPU decode): no copy back
+        if (orig_size) HIPCHK(hipMemcpyAsync(d_out_ext, d.dout.p, orig_size, hipMemcpyDeviceToDevice, s));
+    } else {
+        HIPCHK(hipMemcpyAsync(out, d.dout.p, orig_size, hipMemcpyDeviceToHost, s));
+    }
     HIPCHK(hipStreamSynchronize(s));
     const uint64_t d2h_ns = now_ns() - t;
     const uint64_t t_inf = now_ns();
@@ -981,6 +998,62 @@ extern "C" int ambc_decompress_batch(ambc_ctx* ctx, const uint8_t* body, uint64_
     int rc = ambc_decompress_ex(ctx, body, body_len, orig_size, nullptr, out, nullptr, 0, &nh, st);
     if (rc == AMBC_E_CAPACITY && nh) return fail(AMBC_E_HOSTCODEC, "body has bz2/lzma chunks: use ambc_decompress_ex");
     return rc;
+}
+
+extern "C" int ambc_decompress_device(ambc_ctx* ctx, int dev, const uint8_t* body, uint64_t body_len,
+                                      uint64_t orig_size, const uint64_t registered[4], void* d_out,
+                                      ambc_stats* st) {
+    if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || (!body && body_len) || (!d_out && orig_size))
+        return fail(AMBC_E_INVAL, "bad argument");
+    uint64_t reg[4] = {0, 0, 0, 0};
+    if (registered) std::memcpy(reg, registered, sizeof reg);
+    else for (uint32_t t : {1u, 2u, 3u, 4u, 5u, 6u, 7u, 9u, 255u}) reg[t >> 6] |= 1ull << (t & 63);
+    std::vector<ambc_host_chunk> host;
+    return decompress_on(ctx->devs[dev], body, body_len, orig_size, reg, nullptr, host, st,
+                         static_cast<uint8_t*>(d_out));
+}
+
+// Multi-GPU decode split: the reference's header walk with the
+// expected package sizes, cut at package boundaries into nparts ranges of
+// about orig_size / nparts output bytes each.  Part r = body bytes
+// [body_off[r], body_off[r+1]) decoding to [out_off[r], out_off[r+1]); the last
+// non-empty part runs to the end of the body (end chunk included) so that its
+// own walk stops where the whole-body walk stops.  Host code only.
+extern "C" int ambc_split_body(const uint8_t* body, uint64_t blen, uint64_t orig_size,
+                               const uint64_t registered[4], uint32_t nparts, uint64_t* body_off,
+                               uint64_t* out_off) {
+    if ((!body && blen) || nparts == 0 || !body_off || !out_off) return fail(AMBC_E_INVAL, "bad argument");
+    uint64_t reg[4] = {0, 0, 0, 0};
+    if (registered) std::memcpy(reg, registered, sizeof reg);
+    else for (uint32_t t : {1u, 2u, 3u, 4u, 5u, 6u, 7u, 9u, 255u}) reg[t >> 6] |= 1ull << (t & 63);
+    auto target = [&](uint32_t r) {
+        return (uint64_t)(((unsigned __int128)orig_size * r) / nparts);
+    };
+    body_off[0] = 0;
+    out_off[0] = 0;
+    uint32_t next = 1;
+    uint64_t pos = 0, out = 0;
+    while (pos < blen) {
+        if (pos + HDR > blen) break;
+        if (!(body[pos] == 0xFF && body[pos + 1] == 0xFF && body[pos + 2] == 0 && body[pos + 3] == 0))
+            return fail(AMBC_E_MARKER, "Marker mismatch in chunk header.");
+        const uint32_t t = body[pos + 4];
+        const uint32_t orig = rd32le(body + pos + 10);
+        const uint32_t clen = rd32le(body + pos + 14);
+        if (t == 0 || pos + HDR + clen > blen) break;
+        while (next < nparts && out >= target(next)) {
+            body_off[next] = pos;
+            out_off[next] = out;
+            next++;
+        }
+        out += expect_len(t, clen, orig, reg);
+        pos += HDR + (uint64_t)clen;
+        if (out >= orig_size) break;
+    }
+    for (; next < nparts; next++) { body_off[next] = blen; out_off[next] = orig_size; }
+    body_off[nparts] = blen;
+    out_off[nparts] = orig_size;
+    return AMBC_OK;
 }
 
 // ---------------------------------------------------------------------------

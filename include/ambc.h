@@ -128,6 +128,24 @@ int ambc_decompress_ex(ambc_ctx* ctx, const uint8_t* body, uint64_t body_len, ui
                        const uint64_t registered[4], uint8_t* out, ambc_host_chunk* host_chunks,
                        uint32_t host_cap, uint32_t* n_host, ambc_stats* st);
 
+/* Multi-GPU decode: cut the body at package boundaries into
+ * nparts ranges of about orig_size / nparts decoded bytes (the reference's
+ * header walk with each package's expected length, adaptive_compressor.py:
+ * 396-454).  body_off / out_off hold nparts + 1 entries; part r is body bytes
+ * [body_off[r], body_off[r+1]) decoding to output bytes [out_off[r],
+ * out_off[r+1]); empty parts have equal offsets.  Host code only (no device). */
+int ambc_split_body(const uint8_t* body, uint64_t body_len, uint64_t orig_size,
+                    const uint64_t registered[4], uint32_t nparts, uint64_t* body_off,
+                    uint64_t* out_off);
+
+/* As ambc_decompress_ex, but the decoded bytes stay in device memory d_out
+ * (orig_size bytes on device dev); AMBC_E_HOSTCODEC if any package needs a host
+ * codec.  stats->payload_bytes = bytes the packages produced before the final
+ * pad / truncate (equal to orig_size for a well-formed body). */
+int ambc_decompress_device(ambc_ctx* ctx, int dev, const uint8_t* body, uint64_t body_len,
+                           uint64_t orig_size, const uint64_t registered[4], void* d_out,
+                           ambc_stats* st);
+
 /* Device-resident variants (inputs already in HBM; used by bench.py and the
  * multi-GPU path).  dev = index into the ctx's device list; stream may be NULL. */
 int ambc_compress_device(ambc_ctx* ctx, int dev, const void* d_in, uint64_t n,

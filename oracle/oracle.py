@@ -376,8 +376,11 @@ def decode_chunk(mid, payload, orig):
     return None
 
 
-def decompress_body(body, orig_size, registered=(1, 2, 3, 4, 5, 6, 7, 9, 255)):
-    """_adaptive_decompress (adaptive_compressor.py:396-454)."""
+def decompress_body(body, orig_size, registered=(1, 2, 3, 4, 5, 6, 7, 9, 255),
+                    return_produced=False):
+    """_adaptive_decompress (adaptive_compressor.py:396-454).  With
+    ``return_produced``: (output, bytes the packages produced before the final
+    pad/truncate)."""
     out = bytearray()
     pos = 0
     n = len(body)
@@ -399,6 +402,8 @@ def decompress_body(body, orig_size, registered=(1, 2, 3, 4, 5, 6, 7, 9, 255)):
         out += payload if r is None else r
         if len(out) >= orig_size:
             break
+    if return_produced:
+        return _pad_trunc(bytes(out), orig_size), len(out)
     return _pad_trunc(bytes(out), orig_size)
 
 
