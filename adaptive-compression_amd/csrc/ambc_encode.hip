@@ -31,21 +31,28 @@ namespace ambc {
 
 template <int CMAX>
 struct EncSmem {
-    // region = union, by lifetime: Huffman tree build (parent/pbit) + first
-    // occurrences (first/order) | LZ4 last[] hash table | RLE pair starts |
-    // Huffman bit staging.  Keeping it small keeps ~15 workgroups per CU.
-    static constexpr int REGION = (CMAX > 4096 ? CMAX : 4096) + 64;
+    // work = union, by lifetime.  Selection: hist | code | clen | Huffman tree
+    // (parent/pbit) | first occurrences (first/order).  LZ4: last[] hash table +
+    // 128 bucket masks.  Emit: RLE pair starts | Huffman bit staging behind
+    // hist/code/clen.  9.3 KB per workgroup at C = 4096 -> 17 workgroups per CU.
+    static constexpr int WORK = CMAX <= 4096 ? 5120 : 2304 + CMAX + 64;
+    static constexpr int STAGE_OFF = 2304;                  // Huffman bit staging
+    static constexpr int STAGE = WORK - STAGE_OFF;
     alignas(16) uint8_t chunk[CMAX + 64];      // zero padded
-    alignas(16) uint32_t region[REGION / 4];
-    uint32_t hist[256];
-    uint32_t code[256];
-    uint8_t clen[256];
-    __device__ __forceinline__ uint16_t* parent() { return reinterpret_cast<uint16_t*>(region); }
-    __device__ __forceinline__ uint8_t* pbit() { return reinterpret_cast<uint8_t*>(region) + 1024; }
-    __device__ __forceinline__ uint32_t* first() { return region + 384; }              // +1536 B
-    __device__ __forceinline__ uint8_t* order() { return reinterpret_cast<uint8_t*>(region) + 2560; }
+    alignas(16) uint32_t work[WORK / 4];
+    __device__ __forceinline__ uint8_t* wb() { return reinterpret_cast<uint8_t*>(work); }
+    __device__ __forceinline__ uint32_t* hist() { return work; }
+    __device__ __forceinline__ uint32_t* code() { return work + 256; }
+    __device__ __forceinline__ uint8_t* clen() { return wb() + 2048; }
+    __device__ __forceinline__ uint16_t* parent() { return reinterpret_cast<uint16_t*>(wb() + 2304); }
+    __device__ __forceinline__ uint8_t* pbit() { return wb() + 3328; }
+    __device__ __forceinline__ uint32_t* first() { return reinterpret_cast<uint32_t*>(wb() + 3840); }
+    __device__ __forceinline__ uint8_t* order() { return wb() + 4864; }
+    __device__ __forceinline__ uint16_t* last() { return reinterpret_cast<uint16_t*>(work); }
+    __device__ __forceinline__ uint64_t* bk() { return reinterpret_cast<uint64_t*>(wb() + 4096); }
+    __device__ __forceinline__ uint32_t* stage() { return reinterpret_cast<uint32_t*>(wb() + STAGE_OFF); }
 };
-static_assert((1u << LZ4_HASH_BITS) * 2 <= 4096, "LZ4 table must fit the region");
+static_assert((1u << LZ4_HASH_BITS) * 2 <= 4096, "LZ4 table must fit the work area");
 
 // Visit the bytes of a lane's block [b0, b0+BS) 16 at a time (one ds_read_b128
 // per step; the 16-byte body is unrolled, the sub-block loop is not, which
@@ -152,7 +159,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
             for (uint32_t i = lane; i < n; i += 64) S.chunk[i] = src[i];
         }
         for (uint32_t i = n + lane; i < (uint32_t)CMAX + 64; i += 64) S.chunk[i] = 0;
-        for (uint32_t i = lane; i < 256; i += 64) S.hist[i] = 0;
+        for (uint32_t i = lane; i < 256; i += 64) S.hist()[i] = 0;
     }
     wave_sync();
 
@@ -189,11 +196,11 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
             ph = ph + 1 == step ? 0u : ph + 1;
             if (valid) {
                 if (c == cur) rc++;
-                else { atomicAdd(&S.hist[cur], rc); cur = c; rc = 1; }
+                else { atomicAdd(&S.hist()[cur], rc); cur = c; rc = 1; }
             }
             prev = c;
         });
-        if (rc) atomicAdd(&S.hist[cur], rc);
+        if (rc) atomicAdd(&S.hist()[cur], rc);
     }
     pairs = wave_sum_u32(pairs);
     samp = wave_sum_u32(samp);
@@ -260,7 +267,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         uint32_t nid[4];
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            const uint32_t s = lane + 64 * j, c = S.hist[s];
+            const uint32_t s = lane + 64 * j, c = S.hist()[s];
             key[j] = c ? (c << 8 | s) : 0xFFFFFFFFu;
             nid[j] = s;
         }
@@ -290,7 +297,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         nb = 0; maxlen = 0;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            const uint32_t s = lane + 64 * j, c = S.hist[s];
+            const uint32_t s = lane + 64 * j, c = S.hist()[s];
             if (c) {
                 uint32_t nd = s, len = 0, code = 0;
                 while (nd != root) {
@@ -298,8 +305,8 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                     len++;
                     nd = S.parent()[nd];
                 }
-                S.clen[s] = (uint8_t)min(len, 255u);
-                S.code[s] = code;
+                S.clen()[s] = (uint8_t)min(len, 255u);
+                S.code()[s] = code;
                 nb += c * len;
                 maxlen = max(maxlen, len);
             }
@@ -315,7 +322,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         uint32_t kc = 0;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            const uint32_t c = S.hist[lane + 64 * j];
+            const uint32_t c = S.hist()[lane + 64 * j];
             if (c) {
                 kc++;
                 const double p = (double)c / (double)n;
@@ -332,7 +339,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
             double e = 0.0;
             if (lane == 0) {
                 for (uint32_t q = 0; q < kdist; q++) {
-                    const uint32_t c = S.hist[S.order()[q]];
+                    const uint32_t c = S.hist()[S.order()[q]];
                     double t;
                     if (tab) t = tab[c];
                     else { const double p = (double)c / (double)n; t = p * log2(p); }
@@ -361,13 +368,13 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         // for k_deflate: the best (len + 18) before LZ4, and bit 31 = DEFLATE's
         // should_use is False (calculate_entropy == 8.0: an exactly uniform histogram)
         // bit 30 = a single byte value (k_deflate builds that parse directly)
-        const uint32_t h0 = S.hist[0];
+        const uint32_t h0 = S.hist()[0];
         bool diff = false;
         uint32_t nz = 0;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            diff |= S.hist[lane + 64 * j] != h0;
-            nz += S.hist[lane + 64 * j] != 0;
+            diff |= S.hist()[lane + 64 * j] != h0;
+            nz += S.hist()[lane + 64 * j] != 0;
         }
         const bool uniform = !__any(diff);
         const bool single = wave_sum_u32(nz) == 1;
@@ -376,10 +383,10 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
     bool lz4_ran = false;   // the LZ4 walk reuses hist[]/code[] for its bucket masks
     if (eligible(9) && (force || n >= 1024) && best > 42) {
         lz4_ran = true;
-        uint16_t* last = reinterpret_cast<uint16_t*>(S.region);
-        uint64_t* bk = reinterpret_cast<uint64_t*>(S.hist);   // 256 x 8 B over hist + code
+        uint16_t* last = S.last();
+        uint64_t* bk = S.bk();
         for (uint32_t i = lane; i < (1u << LZ4_HASH_BITS); i += 64) last[i] = 0xFFFF;
-        for (uint32_t i = lane; i < 256; i += 64) bk[i] = 0;
+        for (uint32_t i = lane; i < 128; i += 64) bk[i] = 0;
         wave_sync();
         // LZ4 wins iff block < budget; forced (single-method) encodes fall back to a
         // stored block once the compressed block would reach n (LZ4F rule)
@@ -402,24 +409,24 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
             const uint32_t h = (v * 2654435761u) >> (32 - LZ4_HASH_BITS);
             const uint32_t c16 = last[h];
             // lanes with my hash: one shared hash (runs) is the active mask; else an
-            // order-free LDS OR per 8-bit bucket, then 3 ballots for the top bits
+            // order-free LDS OR per 7-bit bucket, then 4 ballots for the top bits
             const uint64_t actm = base + 63 <= mlim ? ~0ull : __ballot(act);
             const uint32_t h0 = __builtin_amdgcn_readfirstlane(h);
             uint64_t peers;
             if (__ballot(h != h0) == 0ull) {
                 peers = actm;
             } else {
-                atomicOr(reinterpret_cast<unsigned long long*>(&bk[h & 255u]), act ? 1ull << lane : 0ull);
+                atomicOr(reinterpret_cast<unsigned long long*>(&bk[h & 127u]), act ? 1ull << lane : 0ull);
                 wave_sync();
-                peers = bk[h & 255u] & actm;
+                peers = bk[h & 127u] & actm;
 #pragma unroll
-                for (int b = 8; b < (int)LZ4_HASH_BITS; b++) {
+                for (int b = 7; b < (int)LZ4_HASH_BITS; b++) {
                     const uint64_t m = __ballot((h >> b) & 1u);
                     const uint64_t flip = 0ull - (uint64_t)((h >> b) & 1u);
                     peers &= ~(m ^ flip);
                 }
                 wave_sync();
-                bk[h & 255u] = 0ull;
+                bk[h & 127u] = 0ull;
             }
             const uint64_t lower = peers & ((1ull << lane) - 1ull);
             const int cand = lower ? base + 63 - (int)__clzll((long long)lower)
@@ -637,8 +644,8 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
     } else if (win == 1) {
         // pair starts -> region (u16) in windows of CAPP entries (a forced RLE on
         // incompressible data has up to n pairs), then (byte, count) pairs
-        uint16_t* ps = reinterpret_cast<uint16_t*>(S.region);
-        constexpr uint32_t CAPP = EncSmem<CMAX>::REGION / 2;
+        uint16_t* ps = reinterpret_cast<uint16_t*>(S.work);
+        constexpr uint32_t CAPP = EncSmem<CMAX>::WORK / 2;
 #pragma unroll 1
         for (uint32_t wb = 0; wb < pairs; wb += CAPP - 1) {
             uint32_t base_idx = 0;
@@ -691,7 +698,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
     } else if (win == 3) {
         if (lz4_ran) {
             // the LZ4 walk overwrote hist[]/code[]: count again, rebuild the same tree
-            for (uint32_t i = lane; i < 256; i += 64) S.hist[i] = 0;
+            for (uint32_t i = lane; i < 256; i += 64) S.hist()[i] = 0;
             wave_sync();
 #pragma unroll 1
             for (int r = 0; r < ROUNDS; r++) {
@@ -700,22 +707,22 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                 for_block_bytes<BS>(S.chunk, b0, [&](uint32_t p, uint32_t c, uint32_t) {
                     if (p < n) {
                         if (c == cur) rc++;
-                        else { atomicAdd(&S.hist[cur], rc); cur = c; rc = 1; }
+                        else { atomicAdd(&S.hist()[cur], rc); cur = c; rc = 1; }
                     }
                 });
-                if (rc) atomicAdd(&S.hist[cur], rc);
+                if (rc) atomicAdd(&S.hist()[cur], rc);
             }
             wave_sync();
             uint32_t nb2, ml2;
             huff_tree(nb2, ml2);
         }
         compute_first();   // (the LZ4 table may have overwritten an earlier order[])
-        uint32_t* bits = S.region;
+        uint32_t* bits = S.stage();
         const uint32_t kk = kdist;
         // table: [k][sym, count u32le] x k (first-occurrence order) [nbits u32le]
         if (lane == 0) slot[0] = (uint8_t)kk;
         for (uint32_t q = lane; q < kk; q += 64) {
-            const uint32_t s = S.order()[q], c = S.hist[s];
+            const uint32_t s = S.order()[q], c = S.hist()[s];
             uint8_t* e = slot + 1 + 5 * q;
             e[0] = (uint8_t)s; e[1] = (uint8_t)c; e[2] = (uint8_t)(c >> 8);
             e[3] = (uint8_t)(c >> 16); e[4] = (uint8_t)(c >> 24);
@@ -725,7 +732,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         const uint32_t nwords = (nbytes + 3) >> 2;
         // forced encodes of high-entropy data can outgrow the LDS region: stage the
         // bit words in the slot behind the payload instead (slot holds 3C + 1344 B)
-        const bool gstage = (nwords + 1) * 4 > (uint32_t)EncSmem<CMAX>::REGION;
+        const bool gstage = (nwords + 1) * 4 > (uint32_t)EncSmem<CMAX>::STAGE;
         if (gstage) bits = reinterpret_cast<uint32_t*>(slot + ((wlen + 15) & ~15u));
         for (uint32_t w = lane; w < nwords + 1; w += 64) bits[w] = 0;
         if (gstage) __threadfence();
@@ -736,14 +743,14 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
             const uint32_t b0 = (uint32_t)(r * 64 + lane) * BS;
             uint32_t my = 0;
             for_block_bytes<BS>(S.chunk, b0, [&](uint32_t p, uint32_t c, uint32_t) {
-                if (p < n) my += S.clen[c];
+                if (p < n) my += S.clen()[c];
             });
             const uint32_t incl = wave_incl_sum(my);
             uint32_t bp = bitbase + incl - my;
             uint32_t cw = bp >> 5, acc = 0;
             for_block_bytes<BS>(S.chunk, b0, [&](uint32_t p, uint32_t s, uint32_t) {
                 if (p < n) {
-                    const uint32_t L = S.clen[s], cd = S.code[s];
+                    const uint32_t L = S.clen()[s], cd = S.code()[s];
                     const uint32_t o = bp & 31, w = bp >> 5;
                     if (w != cw) { if (acc) atomicOr(&bits[cw], acc); cw = w; acc = 0; }
                     if (o + L <= 32) {
