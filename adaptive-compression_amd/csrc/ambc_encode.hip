@@ -164,43 +164,80 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
     wave_sync();
 
     // ---- pass A: histogram, RLE pairs, RLE / Delta should_use samples ----
+    // Word-parallel: per dword, the bytes that differ from their predecessor (a
+    // run starts there) as bit 8j+7 of chg.  RLE pairs = run starts + the
+    // 255-byte splits of the run carried into the lane (a run that starts inside
+    // a lane is shorter than 255 there); the should_use samples at step 4 are
+    // byte 0 against byte 1 of each dword; the histogram adds whole runs.
     const uint32_t ss = n < 1000 ? n : 1000;
     const uint32_t step = max(1u, n / ss);
+    const bool fast_samples = step == 4;
     uint32_t pairs = 0, samp = 0, dsamp = 0;
     int rs_carry = -1;
+    const uint32_t* c32 = reinterpret_cast<const uint32_t*>(S.chunk);
 #pragma unroll 1
     for (int r = 0; r < ROUNDS; r++) {
         const uint32_t b0 = (uint32_t)(r * 64 + lane) * BS;
-        const uint32_t prevb = b0 ? S.chunk[b0 - 1] : 0x100u;
-        int lb = -1;
-        {
-            uint32_t prev = prevb;
-            for_block_bytes<BS>(S.chunk, b0, [&](uint32_t p, uint32_t c, uint32_t) {
-                if (p < n && c != prev) lb = (int)p;
-                prev = c;
-            });
+        // previous byte; position 0 always starts a run (the reference's prev = None)
+        uint32_t pw = b0 ? c32[(b0 >> 2) - 1] : ~((uint32_t)S.chunk[0] << 24);
+        int lb = -1, fc = -1;
+        uint32_t starts = 0, cur = S.chunk[b0], rc = 0;
+#pragma unroll 1
+        for (int q = 0; q < BS / 16; q++) {
+            const uint4 v4 = *reinterpret_cast<const uint4*>(S.chunk + b0 + 16 * q);
+            const uint32_t wv[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const uint32_t w = wv[e];
+                const uint32_t p = b0 + 16 * q + 4 * e;
+                const uint32_t x = w ^ __builtin_amdgcn_alignbyte(w, pw, 3);
+                const uint32_t nv = p < n ? min(n - p, 4u) : 0u;       // valid bytes
+                const uint32_t vmask = nv >= 4 ? 0xFFFFFFFFu : (1u << (8 * nv)) - 1u;
+                const uint32_t chg = (x | ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu)) & 0x80808080u & vmask;
+                starts += __builtin_popcount(chg);
+                if (chg) {
+                    lb = (int)(p + ((31 - __builtin_clz(chg)) >> 3));
+                    if (fc < 0) fc = (int)(p + ((uint32_t)__builtin_ctz(chg) >> 3));
+                }
+                if (fast_samples && p + 1 < n) {      // sample p: byte 0 against byte 1
+                    const uint32_t a0 = w & 0xFFu, a1 = (w >> 8) & 0xFFu;
+                    samp += (chg & 0x8000u) == 0;
+                    dsamp += (a0 > a1 ? a0 - a1 : a1 - a0) < 32u;
+                }
+                if (chg == 0) {
+                    rc += nv;                         // the current run goes on
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        if ((uint32_t)j < nv) {
+                            if ((chg >> (8 * j + 7)) & 1u) {
+                                if (rc) atomicAdd(&S.hist()[cur], rc);
+                                cur = (w >> (8 * j)) & 0xFFu;
+                                rc = 0;
+                            }
+                            rc++;
+                        }
+                    }
+                }
+                pw = w;
+            }
         }
+        if (rc) atomicAdd(&S.hist()[cur], rc);
         const int rs = wave_excl_max(lb, rs_carry);  // run start of position b0-1
         rs_carry = max(rs_carry, wave_max_i32(lb));
-        uint32_t off = b0 == 0 ? 254u : (uint32_t)((int)(b0 - 1) - rs) % 255u;
-        uint32_t ph = b0 % step;
-        uint32_t prev = prevb, cur = S.chunk[b0], rc = 0;
-        for_block_bytes<BS>(S.chunk, b0, [&](uint32_t p, uint32_t c, uint32_t nx) {
-            const bool valid = p < n;
-            off = c != prev ? 0u : (off == 254u ? 0u : off + 1u);
-            if (valid && off == 0) pairs++;
-            if (valid && ph == 0 && p + 1 < n) {
+        // 255-byte splits of the carried-in run inside [b0, first run start)
+        const int end = fc >= 0 ? fc : (int)min(b0 + BS, n);
+        if (b0 && end > (int)b0) starts += (uint32_t)((end - 1 - rs) / 255 - ((int)b0 - 1 - rs) / 255);
+        pairs += starts;
+        if (!fast_samples) {
+            // other steps: positions p = step * i in the lane's block
+#pragma unroll 1
+            for (uint32_t p = (b0 + step - 1) / step * step; p < b0 + BS && p + 1 < n; p += step) {
+                const uint32_t c = S.chunk[p], nx = S.chunk[p + 1];
                 samp += c == nx;
                 dsamp += (c > nx ? c - nx : nx - c) < 32u;
             }
-            ph = ph + 1 == step ? 0u : ph + 1;
-            if (valid) {
-                if (c == cur) rc++;
-                else { atomicAdd(&S.hist()[cur], rc); cur = c; rc = 1; }
-            }
-            prev = c;
-        });
-        if (rc) atomicAdd(&S.hist()[cur], rc);
+        }
     }
     pairs = wave_sum_u32(pairs);
     samp = wave_sum_u32(samp);
@@ -316,6 +353,37 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         wave_sync();
     };
 
+    // Huffman payload bits without the tree: every merge of the heapq order
+    // (:482-494) adds its weight once per level below it, so the encoded length
+    // is the sum of the merged weights
+    auto huff_bits = [&]() -> uint32_t {
+        uint32_t key[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t s = lane + 64 * j, c = S.hist()[s];
+            key[j] = c ? (c << 8 | s) : 0xFFFFFFFFu;
+        }
+        uint32_t nb = 0;
+#pragma unroll 1
+        for (uint32_t m = 0; m + 1 < kdist; m++) {
+            const uint32_t lm = min(min(key[0], key[1]), min(key[2], key[3]));
+            const uint32_t k1 = wave_min_u32(lm);
+            uint32_t lm2 = 0xFFFFFFFFu;
+#pragma unroll
+            for (int j = 0; j < 4; j++) if (key[j] != k1) lm2 = min(lm2, key[j]);
+            const uint32_t k2 = wave_min_u32(lm2);
+            const uint32_t s1 = k1 & 255u, s2 = k2 & 255u;
+            const uint32_t wsum = (k1 >> 8) + (k2 >> 8);
+            nb += wsum;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                if (lane + 64 * j == s1) key[j] = wsum << 8 | s1;
+                else if (lane + 64 * j == s2) key[j] = 0xFFFFFFFFu;
+            }
+        }
+        return nb;
+    };
+
     bool huff_su = false;
     if ((eligible(3) || analyze) && (n >= 100 || force)) {
         double part = 0.0;
@@ -350,12 +418,10 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         }
         huff_su = n >= 100 && H < 7.0;
         if (eligible(3) && (force || huff_su) && kdist >= 2 && kdist <= 255) {
-            uint32_t nb, maxlen;
-            huff_tree(nb, maxlen);
-            if (maxlen <= 32) {
-                const uint32_t l = 1 + 5 * kdist + 4 + (nb + 7) / 8;
-                if (l + HDR < best) { best = l + HDR; win = 3; wlen = l; }
-            }
+            // (code lengths stay <= 23 for n <= 65536: a Fibonacci-weighted tree)
+            const uint32_t nb = huff_bits();
+            const uint32_t l = 1 + 5 * kdist + 4 + (nb + 7) / 8;
+            if (l + HDR < best) { best = l + HDR; win = 3; wlen = l; }
         }
     }
 
@@ -381,7 +447,10 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         if (lane == 0) A.bestpre[k] = best | (uniform ? 0x80000000u : 0u) | (single ? 0x40000000u : 0u);
     }
     bool lz4_ran = false;   // the LZ4 walk reuses hist[]/code[] for its bucket masks
-    if (eligible(9) && (force || n >= 1024) && best > 42) {
+    // LZ4's frame is at least 23 + 10 + ext(n - 10) bytes: a literal at 0 (no
+    // candidate), one match up to n - 5, the last five bytes literal; with the
+    // 18-B header it cannot win unless best > 51 + ext(n - 10) (zero runs: RLE 52)
+    if (eligible(9) && (force || (n >= 1024 && best > 51 + ext_len(n - 10)))) {
         lz4_ran = true;
         uint16_t* last = S.last();
         uint64_t* bk = S.bk();
@@ -641,6 +710,13 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         const uint32_t nv = (n + 15) >> 4;
         for (uint32_t v = lane; v < nv; v += 64)
             reinterpret_cast<uint4*>(slot)[v] = reinterpret_cast<const uint4*>(S.chunk)[v];
+    } else if (win == 1 && S.hist()[S.chunk[0]] == n && !lz4_ran) {
+        // one byte value: (c, 255) pairs and the remainder (compression_methods.py:95-109)
+        const uint32_t c = S.chunk[0];
+        for (uint32_t j = lane; j < pairs; j += 64) {
+            slot[2 * j] = (uint8_t)c;
+            slot[2 * j + 1] = (uint8_t)(j + 1 < pairs ? 255u : n - 255u * (pairs - 1));
+        }
     } else if (win == 1) {
         // pair starts -> region (u16) in windows of CAPP entries (a forced RLE on
         // incompressible data has up to n pairs), then (byte, count) pairs
@@ -697,7 +773,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         }
     } else if (win == 3) {
         if (lz4_ran) {
-            // the LZ4 walk overwrote hist[]/code[]: count again, rebuild the same tree
+            // the LZ4 walk overwrote hist[]: count again
             for (uint32_t i = lane; i < 256; i += 64) S.hist()[i] = 0;
             wave_sync();
 #pragma unroll 1
@@ -713,8 +789,10 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                 if (rc) atomicAdd(&S.hist()[cur], rc);
             }
             wave_sync();
+        }
+        {
             uint32_t nb2, ml2;
-            huff_tree(nb2, ml2);
+            huff_tree(nb2, ml2);   // codes and lengths of the winner's tree
         }
         compute_first();   // (the LZ4 table may have overwritten an earlier order[])
         uint32_t* bits = S.stage();

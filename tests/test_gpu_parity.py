@@ -214,6 +214,31 @@ def test_random_edge_inputs(ctx):
         assert comp._adaptive_decompress(body, len(data)) == data
 
 
+def test_huffman_winner_staging_paths(ctx):
+    """Huffman winners of every payload size: alphabets of 12..127 symbols give
+    payloads from ~1.9 KB (bits staged in LDS) to ~3.9 KB per 4 KiB chunk (bits
+    staged behind the payload in the chunk's slot), next to zero runs and random
+    chunks, for the reference's {1,3,4} set and with LZ4 competing."""
+    rng = np.random.default_rng(77)
+    parts = []
+    for k in (12, 30, 64, 90, 110, 127):
+        for _ in range(3):
+            parts.append((rng.integers(0, k, 4096) + 40).astype(np.uint8).tobytes())
+    parts += [bytes(4096), rng.integers(0, 256, 4096).astype(np.uint8).tobytes()]
+    order = rng.permutation(len(parts))
+    data = b"".join(parts[i] for i in order) + parts[0][:1234]
+    for chunk in (1024, 2048, 4096, 8192):
+        for methods in ((1, 3, 4), (1, 3, 4, 9)):
+            comp = _compressor(chunk_size=chunk, methods=methods)
+            body = comp._adaptive_compress(data)
+            ref, st = orc.compress_body(data, orc.make_params(chunk, "native", methods,
+                                                              n_total=len(data)))
+            assert body == ref, (chunk, methods)
+            if methods == (1, 3, 4) and chunk == 4096:
+                assert st.method_usage[3] >= 12
+            assert comp._adaptive_decompress(body, len(data)) == data
+
+
 def test_empty_and_tiny_files(ctx):
     for data in (b"", b"a", b"ab" * 8, bytes(47)):
         comp = _compressor(chunk_size=4096)
