@@ -460,89 +460,138 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     const int hl = (int)n - 4;  // last hashable position
     uint32_t p = 0;
     int fcarry = 0;  // max match end so far (frequency count)
+    const uint32_t* c32 = reinterpret_cast<const uint32_t*>(S.chunk);
 #pragma unroll 1
     for (int r = 0; r < ROUNDS; r++) {
         const int base = r * 64;
         if (base >= (int)n) break;
+        // control state is wave-uniform: keep it in SGPRs
+        p = __builtin_amdgcn_readfirstlane(p);
+        fcarry = (int)__builtin_amdgcn_readfirstlane((uint32_t)fcarry);
+        ns = __builtin_amdgcn_readfirstlane(ns);
         const int i = base + (int)lane;
         const bool act = i <= hl;
-        const uint32_t v = act ? ld32(S.chunk, (uint32_t)i) : 0u;
+        // loads run for every lane (the chunk is zero padded past n + 63)
+        const uint32_t v = ld32(S.chunk, (uint32_t)i);
         const uint32_t h = (v * 2654435761u) >> 21;
-        // lanes with my 11-bit hash: an order-free LDS OR per 8-bit bucket, then
-        // the remaining 3 bits by ballots (one shared hash: the active mask)
-        const uint64_t actm = __ballot(act);
+        const uint32_t c16 = last[h];
+        // lanes with my 11-bit hash: one shared hash (runs) is the active mask; else
+        // an order-free LDS OR per 8-bit bucket, then 3 ballots for the top bits
+        const uint64_t actm = base + 63 <= hl ? ~0ull : __ballot(act);
+        const uint32_t h0 = __builtin_amdgcn_readfirstlane(h);
         uint64_t peers;
-        if (__all(!act || h == __builtin_amdgcn_readfirstlane(h))) {
-            peers = act ? actm : 0ull;
+        if (__ballot(h != h0) == 0ull) {
+            peers = actm;
         } else {
-            if (act) atomicOr(&bk[h & 255], 1ull << lane);
+            atomicOr(&bk[h & 255], act ? 1ull << lane : 0ull);
             wave_sync();
-            peers = act ? bk[h & 255] : 0ull;
+            peers = bk[h & 255] & actm;
 #pragma unroll
             for (int b = 8; b < 11; b++) {
                 const uint64_t m = __ballot((h >> b) & 1u);
-                peers &= ((h >> b) & 1u) ? m : ~m;
+                const uint64_t flip = 0ull - (uint64_t)((h >> b) & 1u);
+                peers &= ~(m ^ flip);
             }
             wave_sync();
-            if (act) bk[h & 255] = 0;
+            bk[h & 255] = 0;
         }
-        const uint64_t lower = lane ? (peers & ((1ull << lane) - 1)) : 0ull;
-        int cand;
-        if (lower) {
-            cand = base + 63 - (int)__clzll((long long)lower);
-        } else {
-            const uint16_t c = act ? last[h] : (uint16_t)0xFFFF;
-            cand = c == 0xFFFF ? -1 : (int)c;
-        }
-        const bool valid = act && cand >= 0 && i - cand <= 32768 && ld32(S.chunk, (uint32_t)cand) == v;
+        const uint64_t lower = peers & ((1ull << lane) - 1ull);
+        const int cand = lower ? base + 63 - (int)__clzll((long long)lower)
+                               : (c16 == 0xFFFFu ? -1 : (int)c16);
+        const uint32_t cv = ld32(S.chunk, (uint32_t)max(cand, 0));
+        const bool valid = act && cand >= 0 && i - cand <= 32768 && cv == v;
+        const uint64_t vm = __ballot(valid);
         wave_sync();
         if (act && (peers >> lane) == 1ull) last[h] = (uint16_t)i;
         uint32_t L = 0;
-        if (valid && (uint32_t)i >= p) {  // the walk never looks below p
-            const uint32_t lim = min(258u, n - (uint32_t)i);
-            L = 4;
-            while (L < GD_LCAP && L < lim) {
-                const uint32_t x = ld32(S.chunk, (uint32_t)cand + L) ^ ld32(S.chunk, (uint32_t)i + L);
-                if (x) { L += (uint32_t)__builtin_ctz(x) >> 3; break; }
-                L += 4;
-            }
-            L = min(L, lim);
-        }
-        const uint64_t vm = __ballot(valid);
         uint64_t selm = 0;
         const uint32_t ns0 = ns;
-        if (p < (uint32_t)base + 64) {
-            // scalar greedy walk over this round's positions: one v_readlane per
-            // match; a match longer than GD_LCAP is extended by the whole wave
-            while (p < (uint32_t)base + 64 && p < n) {
-                const uint64_t m = vm >> (p - (uint32_t)base);
-                if (!m) { p = (uint32_t)base + 64; break; }
-                p += (uint32_t)__builtin_ctzll(m);
-                const uint32_t l = p - (uint32_t)base;
-                uint32_t Lp = readlane(L, l);
-                if (Lp >= GD_LCAP) {
-                    const uint32_t lim = min(258u, n - p);
-                    if (Lp < lim) {
-                        const uint32_t c = readlane((uint32_t)cand, l);
-                        for (;;) {
-                            const uint32_t off = Lp + 4 * lane;
-                            const uint32_t x = off < lim ? (ld32(S.chunk, c + off) ^ ld32(S.chunk, p + off)) : 1u;
-                            const uint64_t mm = __ballot(x != 0);
-                            if (mm) {
-                                const uint32_t f = (uint32_t)__builtin_ctzll(mm);
-                                const uint32_t xf = readlane(x, f);
-                                Lp += 4 * f + ((uint32_t)__builtin_ctz(xf) >> 3);
-                                break;
-                            }
-                            Lp += 256;
-                        }
-                        Lp = min(Lp, lim);
-                        L = wlane(L, l, Lp, lane);
+        const uint32_t pr = p - (uint32_t)base;   // p >= base
+        if (pr < 64 && (vm & (~0ull << pr)) == 0ull) {
+            p = (uint32_t)base + 64;               // no match starts here: literals
+        } else if (pr < 64) {
+            // per-lane match length: 16 bytes per step (five aligned dwords per side
+            // in flight), capped at GD_LCAP; the walk extends longer ones
+            const bool run_l = valid && (uint32_t)i >= p;
+            bool run = run_l;
+            const uint32_t lim = run ? min(258u, n - (uint32_t)i) : 0u;
+            const uint32_t cap = min(lim, GD_LCAP);
+            if (run) L = 4;
+            const uint32_t si = (uint32_t)i & 3u, sc = (uint32_t)cand & 3u;
+#pragma unroll 1
+            while (__ballot(run && L < cap)) {
+                if (run && L < cap) {
+                    const uint32_t ai = ((uint32_t)i + L) >> 2, ac = ((uint32_t)cand + L) >> 2;
+                    uint32_t wi[5], wc[5];
+#pragma unroll
+                    for (int t = 0; t < 5; t++) { wi[t] = c32[ai + t]; wc[t] = c32[ac + t]; }
+                    uint32_t add = 16;
+#pragma unroll
+                    for (int t = 3; t >= 0; t--) {
+                        const uint32_t x = __builtin_amdgcn_alignbyte(wi[t + 1], wi[t], si) ^
+                                           __builtin_amdgcn_alignbyte(wc[t + 1], wc[t], sc);
+                        if (x) add = 4 * t + ((uint32_t)__builtin_ctz(x) >> 3);
                     }
+                    L += add;
+                    if (add < 16) run = false;
                 }
-                selm |= 1ull << l;
-                p += Lp;
             }
+            L = min(L, lim);
+            // greedy walk: every lane links to the next match start the parse takes
+            // after its match (64 = none in this round, 65 = extend past GD_LCAP);
+            // two bpermutes extend the link four deep, one v_readlane per four matches
+            const bool longl = run_l && L >= GD_LCAP && L < lim;
+            const uint32_t E = lane + L;
+            uint32_t nx1;
+            {
+                const uint64_t mm = E < 64 ? (vm & (~0ull << E)) : 0ull;
+                nx1 = longl ? 65u : (mm ? (uint32_t)__builtin_ctzll(mm) : 64u);
+            }
+            uint32_t nx2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(min(nx1, 63u) << 2), (int)nx1);
+            if (nx1 >= 64) nx2 = nx1;
+            const uint32_t pk1 = nx1 | nx2 << 7;
+            uint32_t pk2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(min(nx2, 63u) << 2), (int)pk1);
+            if (nx2 >= 64) pk2 = nx2 | nx2 << 7;
+            const uint32_t pack = pk1 | pk2 << 14;
+            uint32_t cur = (uint32_t)__builtin_ctzll(vm & (~0ull << pr));
+            uint32_t endrel = 64;
+            while (cur < 64) {
+                selm |= 1ull << cur;
+                const uint32_t pk = readlane(pack, cur);
+                uint32_t x = pk & 127u, f = 1;
+                while (x < 64) {
+                    selm |= 1ull << x;
+                    cur = x;
+                    if (f == 4) break;
+                    x = (pk >> (7 * f)) & 127u;
+                    f++;
+                }
+                if (x < 64) continue;
+                if (x == 64) { endrel = readlane(E, cur); break; }
+                // x == 65: cur's match reaches GD_LCAP: the whole wave extends it
+                const uint32_t pj = (uint32_t)base + cur;
+                const uint32_t lj = min(258u, n - pj);
+                uint32_t Lp = readlane(L, cur);
+                const uint32_t c = readlane((uint32_t)cand, cur);
+                for (;;) {
+                    const uint32_t off = Lp + 4 * lane;
+                    const uint32_t xx = off < lj ? (ld32(S.chunk, c + off) ^ ld32(S.chunk, pj + off)) : 1u;
+                    const uint64_t mm = __ballot(xx != 0);
+                    if (mm) {
+                        const uint32_t fl = (uint32_t)__builtin_ctzll(mm);
+                        const uint32_t xf = readlane(xx, fl);
+                        Lp += 4 * fl + ((uint32_t)__builtin_ctz(xf) >> 3);
+                        break;
+                    }
+                    Lp += 256;
+                }
+                Lp = __builtin_amdgcn_readfirstlane(min(Lp, lj));
+                L = wlane(L, cur, Lp, lane);
+                endrel = cur + Lp;
+                const uint64_t mn = endrel < 64 ? (vm & (~0ull << endrel)) : 0ull;
+                cur = mn ? (uint32_t)__builtin_ctzll(mn) : 64u;
+            }
+            p = (uint32_t)base + max(endrel, 64u);
         }
         // the selected matches record themselves, in position order, and the
         // round's symbol frequencies are counted (literals: positions no match covers)
