@@ -146,6 +146,8 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
     const uint32_t n = (uint32_t)min((uint64_t)A.chunk_size, A.n_total - pos0);
     const uint8_t* src = A.in + pos0;
     uint8_t* slot = A.slots + (uint64_t)k * A.slot_stride;
+    // second pass after k_deflate: only the deferred chunks id 5 did not take
+    if ((A.flags & ENC_EMIT_PENDING) && (!A.pending[k] || A.ids[k] == 5)) return;
     STAMP_DECL
 
     // ---- stage the chunk in LDS (16 B per lane per load, coalesced) ----
@@ -703,7 +705,13 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
     if (force && ((mm >> 4) & 1u)) { win = 4; wlen = n; }
 
     // ---- emit the winner's payload into the slot ----
-    if (win == 4) {
+    // With DEFLATE enabled an RLE/Huffman payload waits for k_deflate's verdict:
+    // id 5 wins most such chunks, and the few it does not are emitted by a second
+    // launch (ENC_EMIT_PENDING) that repeats this chunk's selection
+    const bool defer = A.pending && !(A.flags & ENC_EMIT_PENDING) && (win == 1 || win == 3);
+    if (A.pending && !(A.flags & ENC_EMIT_PENDING) && lane == 0) A.pending[k] = defer ? 1 : 0;
+    if (defer) {
+    } else if (win == 4) {
         for (uint32_t i = lane; i < n; i += 64)
             slot[i] = i ? (uint8_t)(S.chunk[i] - S.chunk[i - 1]) : S.chunk[0];
     } else if (win == 255) {

@@ -79,7 +79,7 @@ struct Dev {
     hipStream_t xs[2] = {};     // copy streams of the slab pipeline: H2D, D2H
     hipEvent_t xev[6] = {};     // h2d_done[2], comp_done[2], d2h_done[2]
     Buf in, out, slots, plen, ids, sizes, off, scan_tmp, acc, ent_full, ent_tail;
-    Buf body, jobs, produced, dout, scratch, seg, list, bestpre, gdseq;
+    Buf body, jobs, produced, dout, scratch, seg, list, bestpre, gdseq, pending;
     uint64_t t_encode = 0, t_scan = 0, t_compact = 0;
 };
 
@@ -148,7 +148,7 @@ void ambc_destroy(ambc_ctx* ctx) {
         (void)hipStreamSynchronize(d.stream);
         for (Buf* b : {&d.in, &d.out, &d.slots, &d.plen, &d.ids, &d.sizes, &d.off, &d.scan_tmp,
                        &d.acc, &d.ent_full, &d.ent_tail, &d.body, &d.jobs, &d.produced, &d.dout,
-                       &d.scratch, &d.seg, &d.list, &d.bestpre, &d.gdseq})
+                       &d.scratch, &d.seg, &d.list, &d.bestpre, &d.gdseq, &d.pending})
             b->release();
         for (auto& ev : d.ev) (void)hipEventDestroy(ev);
         for (auto& ev : d.xev) (void)hipEventDestroy(ev);
@@ -248,10 +248,19 @@ static int compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_param
         while (cmax < C) cmax <<= 1;
         HIPCHK(d.gdseq.ensure((size_t)std::max<uint32_t>(M, 1) * 2 * cmax));
         ea.gdseq = d.gdseq.as<uint8_t>();
+        HIPCHK(d.pending.ensure((size_t)std::max<uint32_t>(M, 1)));
+        ea.pending = d.pending.as<uint8_t>();
     }
     HIPCHK(hipEventRecord(d.ev[0], s));
     HIPCHK(launch_encode(ea, s));
-    if (deflate) HIPCHK(launch_deflate(ea, s));   // id 5 after 1/3/4, against LZ4 (ties -> 5)
+    if (deflate) {
+        HIPCHK(launch_deflate(ea, s));   // id 5 after 1/3/4, against LZ4 (ties -> 5)
+        EncArgs ep = ea;                 // RLE/Huffman payloads id 5 did not replace
+        ep.flags |= ENC_EMIT_PENDING;
+        ep.bestpre = nullptr;
+        ep.stamps = nullptr;
+        HIPCHK(launch_encode(ep, s));
+    }
     HIPCHK(hipEventRecord(d.ev[1], s));
     if (ea.stamps) {
         stamps.resize((size_t)M * 8);

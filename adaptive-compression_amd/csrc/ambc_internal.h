@@ -10,6 +10,7 @@ constexpr uint32_t END_CHUNK = 16; // _create_end_chunk (u16 used field)
 constexpr uint32_t LZ4_HASH_BITS = 11;   // "ambc-lz4 greedy v1" hash width
 constexpr uint32_t ENC_FORCE = 1;    // CompressionMethod.compress(chunk) semantics
 constexpr uint32_t ENC_ANALYZE = 2;  // also evaluate every should_use
+constexpr uint32_t ENC_EMIT_PENDING = 4;  // emit only the chunks the first pass deferred and id 5 did not take
 
 // per-chunk encode: one 64-lane workgroup per chunk
 struct EncArgs {
@@ -30,6 +31,7 @@ struct EncArgs {
     unsigned long long* stamps;  // diagnostic build (-DAMBC_STAMPS): per-phase cycle sums
     uint32_t* bestpre;       // optional: best (len + 18) before LZ4 (k_deflate's threshold)
     uint8_t* gdseq;          // k_deflate: n_chunks x chunk-size scratch for the parse's matches
+    uint8_t* pending;        // with k_deflate: 1 = the RLE/Huffman payload was not emitted (id 5 may win)
     uint32_t pref_min[16];
     uint32_t pref_max[16];
 };
