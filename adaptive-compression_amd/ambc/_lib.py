@@ -155,9 +155,11 @@ def addr(buf):
         return buf
     mv = memoryview(buf)
     if mv.readonly:
-        # ctypes cannot take a pointer to read-only memory; read-only inputs
-        # (bytes) are passed via c_char_p, which points at the object's storage
-        return C.cast(C.c_char_p(bytes(mv) if not isinstance(buf, bytes) else buf), C.c_void_p).value
+        # ctypes cannot take a pointer to read-only memory: numpy's view of the
+        # caller's own buffer gives its address without a copy (valid while the
+        # caller holds the object)
+        import numpy as np
+        return np.frombuffer(mv, dtype=np.uint8).ctypes.data if mv.nbytes else None
     return C.addressof(C.c_char.from_buffer(mv))
 
 

@@ -19,11 +19,15 @@ engine runs a single chunk size C (``chunk_size=``, default 4096), i.e.
   ``CHUNK_SIZE_CANDIDATES=[C]``, including its remainder-raw rule (the first
   chunk nothing compresses swallows the rest of the file as one raw chunk).
 
-The multi-size adaptive search is SURVEY §8(f) "next".
+With several ``CHUNK_SIZE_CANDIDATES`` (e.g. the reference's default
+``REFERENCE_CHUNK_SIZE_CANDIDATES``) the reference's serial multi-size walk runs
+instead: at every position each candidate size is encoded on the GPU as one
+chunk and the sizes compare by their fp64 ratio (``_adaptive_compress_multisize``).
 """
 import ctypes as C
 import hashlib
 import os
+import struct
 import threading
 import time
 
@@ -35,7 +39,7 @@ from .container import (FORMAT_VERSION, MAGIC_NUMBER, MARKER_BYTES, MARKER_LENGT
                         update_compressed_size)
 from .methods import DECODE_METHODS, GPU_METHODS, NoCompression
 from .registry import (DEFAULT_CHUNK_SIZE, DEFAULT_METHODS, HOST_LIBRARY_IDS, METHOD_CHUNK_PREFS,
-                       METHOD_NAMES, method_mask)
+                       METHOD_NAMES, REFERENCE_CHUNK_SIZE_CANDIDATES, method_mask)
 
 _TERMS = {}
 
@@ -61,6 +65,9 @@ class AdaptiveCompressor:
     MAGIC_NUMBER = MAGIC_NUMBER
     FORMAT_VERSION = FORMAT_VERSION
     CHUNK_SIZE_CANDIDATES = [DEFAULT_CHUNK_SIZE]
+    # the reference's default list (adaptive_compressor.py:61-62): set
+    # CHUNK_SIZE_CANDIDATES to it for the reference's multi-size walk
+    REFERENCE_CHUNK_SIZE_CANDIDATES = list(REFERENCE_CHUNK_SIZE_CANDIDATES)
 
     def __init__(self, marker_max_length=32, sample_size=10000, *, chunk_size=None,
                  mode="native", methods=None, devices=None):
@@ -126,9 +133,8 @@ class AdaptiveCompressor:
     def chunk_size(self):
         cands = list(self.CHUNK_SIZE_CANDIDATES)
         if len(cands) != 1:
-            raise NotImplementedError(
-                "multi-size CHUNK_SIZE_CANDIDATES search is SURVEY §8(f) 'next'; "
-                "set chunk_size=C (CHUNK_SIZE_CANDIDATES=[C])")
+            raise ValueError("several CHUNK_SIZE_CANDIDATES: no single chunk size "
+                             "(the multi-size walk runs in _adaptive_compress)")
         return int(cands[0])
 
     def _params(self, n):
@@ -150,8 +156,103 @@ class AdaptiveCompressor:
     def _ctx(self):
         return _lib.default_context(self.devices)
 
+    def _encode_one(self, ctx, chunk, ids):
+        """One chunk of len(chunk) bytes through ambc_compress_batch: the package
+        of the reference's per-size method loop (adaptive_compressor.py:559-579 +
+        _process_chunk :631-700), or None when no method beats raw."""
+        s = len(chunk)
+        elig = [i for i in ids if self.method_chunk_prefs.get(i, (1, 999999999))[0] <= s
+                <= self.method_chunk_prefs.get(i, (1, 999999999))[1]]
+        if not elig:
+            return None
+        if s > _lib.MAX_CHUNK or (5 in elig and s > 16384):
+            raise NotImplementedError(
+                f"a {s}-byte candidate chunk with methods {elig}: the GPU encoders take chunks "
+                f"up to {_lib.MAX_CHUNK} bytes (DEFLATE up to 16384)")
+        C_ = (s + 15) & ~15
+        p = _lib.Params()
+        p.chunk_size = C_
+        p.mode = _lib.MODE_NATIVE
+        p.flags = _lib.FLAG_NO_END_CHUNK
+        p.method_mask = method_mask(elig)
+        for i in range(16):
+            lo, hi = self.method_chunk_prefs.get(i, (1, 0))
+            p.pref_min[i], p.pref_max[i] = max(0, lo), min(hi, 0xFFFFFFFF)
+        tab = entropy_terms(s)
+        if s == C_:
+            p.ent_full = tab.ctypes.data
+        else:
+            p.ent_tail = tab.ctypes.data
+        cap = ctx.lib.ambc_compress_bound(s, C_)
+        out = bytearray(cap)
+        olen = C.c_uint64()
+        src = bytes(chunk)                  # held for the call: addr() does not own it
+        _lib.check(ctx.lib.ambc_compress_batch(ctx.h, _lib.addr(src), s, C.byref(p),
+                                               _lib.addr(out), cap, C.byref(olen), None), ctx.lib)
+        pkg = bytes(memoryview(out)[:olen.value])
+        return None if pkg[4] == 255 else pkg
+
+    def _adaptive_compress_multisize(self, file_data):
+        """_adaptive_compress (adaptive_compressor.py:363-394) with several
+        CHUNK_SIZE_CANDIDATES: at every position each candidate size, clamped to
+        the remainder, is encoded as one chunk on the GPU (its in-size winner in id
+        order); sizes compare by (len + 18) / size in fp64, strictly, in list
+        order (:548-584); a position where no size beats raw stores the whole
+        remainder raw (:586-588)."""
+        n = len(file_data)
+        ctx = self._ctx()
+        ids = [m.type_id for m in self.compression_methods if m.type_id != 255]
+        cands = [int(c) for c in self.CHUNK_SIZE_CANDIDATES]
+        mv = memoryview(file_data)
+        usage = {m.type_id: 0 for m in self.compression_methods}
+        total = comp = raw = saved = payload = overhead = 0
+        out = bytearray()
+        pos = 0
+        while pos < n:
+            remain = n - pos
+            best_ratio, best_s, best_pkg = 1.0, remain, None
+            tried = {}
+            for cand in cands:
+                s = min(cand, remain)
+                if s <= 0:
+                    break
+                if s not in tried:
+                    tried[s] = self._encode_one(ctx, mv[pos:pos + s], ids)
+                pkg = tried[s]
+                if pkg is not None:
+                    ratio = len(pkg) / s          # (len(cdata) + overhead) / len(chunk)
+                    if ratio < best_ratio:
+                        best_ratio, best_s, best_pkg = ratio, s, pkg
+            total += 1
+            if best_pkg is None:                  # (remain, 255): the rest, raw
+                if remain > 0xFFFFFFFF:
+                    raise struct.error("argument out of range")
+                out += MARKER_BYTES + bytes((255, 0)) + struct.pack("<III", remain, remain, remain)
+                out += mv[pos:]
+                raw += 1
+                break
+            mid, pl = best_pkg[4], len(best_pkg) - 18
+            out += best_pkg
+            comp += 1
+            usage[mid] = usage.get(mid, 0) + 1
+            payload += pl
+            overhead += 18
+            saved += best_s - (pl + 18)
+            pos += best_s
+        out += MARKER_BYTES + bytes(12)           # _create_end_chunk (:595-607)
+        overhead += 16
+        self._last_device_stats = None
+        self.chunk_stats = {"total_chunks": total, "compressed_chunks": comp, "raw_chunks": raw,
+                            "method_usage": usage, "bytes_saved": saved, "original_size": n,
+                            "compressed_size_without_overhead": payload,
+                            "overhead_bytes": overhead}
+        self.method_usage_ids = [m.type_id for m in self.compression_methods]
+        return bytes(out)
+
     def _adaptive_compress(self, file_data):
         """One C-ABI call: input bytes -> .ambc body (packages + end chunk)."""
+        if len(self.CHUNK_SIZE_CANDIDATES) != 1:
+            return self._adaptive_compress_multisize(file_data)
         n = len(file_data)
         p, keep = self._params(n)
         ctx = self._ctx()

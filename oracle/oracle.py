@@ -280,6 +280,121 @@ def compress_body(data, params, nthreads=0):
     return bytes(out[:r]), st
 
 
+def np_entropy(d):
+    """calculate_entropy (advanced_compression.py:48-57), numpy as the reference."""
+    if not d:
+        return 0.0
+    counts = np.bincount(np.frombuffer(bytes(d), dtype=np.uint8), minlength=256)
+    probs = counts / len(d)
+    probs = probs[probs > 0]
+    return -np.sum(probs * np.log2(probs))
+
+
+def _lzma_xz(d):
+    """LZMACompression.compress (advanced_compression.py:163-185)."""
+    c = lzma.LZMACompressor(format=lzma.FORMAT_XZ, check=lzma.CHECK_CRC64,
+                            filters=[{"id": lzma.FILTER_LZMA2, "dict_size": 1 << 24}])
+    return c.compress(d) + c.flush()
+
+
+def select_reference_set(chunk, ids, prefs=None):
+    """_pick_best_chunk_and_method's per-size method loop (adaptive_compressor.py:
+    559-579) over the reference's stdlib set {1..7}: should_use, compress, keep the
+    strict minimum of len + 18 in id order.  ids 1/2/3/5 through the C restatement,
+    6/7 (bz2 / lzma) through the same stdlib calls as advanced_compression.py:112-213."""
+    prefs = PREFS if prefs is None else prefs
+    n = len(chunk)
+    best, win, wl = n, 255, n
+    for mid in sorted(i for i in ids if i != 255):
+        lo, hi = prefs.get(mid, (1, 999999999))
+        if not lo <= n <= hi:
+            continue
+        if mid in (1, 2, 3, 4, 5):
+            if not should_use(mid, chunk):
+                continue
+            if mid == 4:
+                continue                      # Delta: len == n never beats raw
+            payload = {1: rle_encode, 2: dict_encode, 3: huff_encode, 5: deflate_encode}[mid](chunk)
+            if payload is None:
+                continue                      # Huffman raises on 1 or 256 symbols
+        elif mid == 6:
+            if n < 1024 or np_entropy(chunk) >= 7.7:
+                continue
+            payload = bz2.compress(chunk, compresslevel=9)
+        elif mid == 7:
+            if n < 8192 or np_entropy(chunk) >= 8.0:
+                continue
+            payload = _lzma_xz(chunk)
+        else:
+            raise ValueError(mid)
+        if len(payload) + 18 < best:
+            best, win, wl = len(payload) + 18, mid, len(payload)
+    return win, wl
+
+
+def _encode_reference_set(mid, chunk):
+    return {1: rle_encode, 2: dict_encode, 3: huff_encode, 5: deflate_encode,
+            6: lambda d: bz2.compress(d, compresslevel=9), 7: _lzma_xz}[mid](chunk)
+
+
+def compress_body_multisize(data, sizes, methods=(1, 3, 4, 255), prefs=None, deflate="gd",
+                            reference_set=False):
+    """_adaptive_compress with several CHUNK_SIZE_CANDIDATES
+    (adaptive_compressor.py:363-394 with _pick_best_chunk_and_method :537-590):
+    at every position each candidate size clamped to the remainder, its in-size
+    winner by orc_select (ids ascending, strict '<'), sizes compared by the fp64
+    ratio (len + 18) / size, strictly, in list order; a position where no size
+    beats raw stores the remainder raw.  Returns (body, chunk_stats dict)."""
+    n = len(data)
+    enc = {1: rle_encode, 3: huff_encode, 9: lz4_frame_encode,
+           5: gdeflate_encode if deflate == "gd" else deflate_encode}
+    st = {"total_chunks": 0, "compressed_chunks": 0, "raw_chunks": 0,
+          "method_usage": {m: 0 for m in methods}, "bytes_saved": 0, "original_size": n,
+          "compressed_size_without_overhead": 0, "overhead_bytes": 0}
+    out = bytearray()
+    pos = 0
+    while pos < n:
+        remain = n - pos
+        best = (1.0, remain, 255, 0)
+        tried = {}
+        for c in sizes:
+            s = min(c, remain)
+            if s <= 0:
+                break
+            if s not in tried:
+                if reference_set:
+                    tried[s] = select_reference_set(data[pos:pos + s], methods, prefs)
+                else:
+                    p = make_params(s, "native", methods, prefs, exact_entropy=False,
+                                    deflate=deflate)
+                    tried[s] = select(data[pos:pos + s], p, tab=entropy_table(s))
+            mid, pl = tried[s]
+            if mid != 255 and (pl + 18) / s < best[0]:
+                best = ((pl + 18) / s, s, mid, pl)
+        st["total_chunks"] += 1
+        _, s, mid, pl = best
+        if mid == 255:
+            if remain > 0xFFFFFFFF:
+                raise struct.error("argument out of range")
+            out += MARKER + bytes((255, 0)) + struct.pack("<III", remain, remain, remain)
+            out += data[pos:]
+            st["raw_chunks"] += 1
+            break
+        chunk = data[pos:pos + s]
+        payload = _encode_reference_set(mid, chunk) if reference_set else enc[mid](chunk)
+        assert len(payload) == pl
+        out += MARKER + bytes((mid, 0)) + struct.pack("<III", s, s, pl) + payload
+        st["compressed_chunks"] += 1
+        st["method_usage"][mid] += 1
+        st["compressed_size_without_overhead"] += pl
+        st["overhead_bytes"] += 18
+        st["bytes_saved"] += s - (pl + 18)
+        pos += s
+    out += MARKER + bytes(12)
+    st["overhead_bytes"] += 16
+    return bytes(out), st
+
+
 def build_header(data):
     """_build_header (adaptive_compressor.py:312-325) with the constant marker."""
     hdr = bytearray(b"AMBC")

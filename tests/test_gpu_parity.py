@@ -497,3 +497,40 @@ def test_gpu_inflate_zlib_corpus(ctx):
     assert comp._adaptive_decompress(body, orig_total) == want
     st = comp._last_device_stats
     assert st.kernel_ns > 0
+
+
+# ---------------------------------------------------------------------------
+# the reference's multi-size walk (several CHUNK_SIZE_CANDIDATES)
+# ---------------------------------------------------------------------------
+REF_CANDS = [131072, 65536, 32768, 16384, 8192, 4096, 2048, 1024]
+
+
+def _zero_then_random():
+    rnd = random.Random(4242)
+    return bytes(20000) + bytes(rnd.randrange(256) for _ in range(30000))
+
+
+@pytest.mark.parametrize("methods,cands", [((1, 3, 4), REF_CANDS), ((1, 3, 4, 9), REF_CANDS),
+                                           ((1, 3, 4, 5), [16384, 8192, 4096, 2048, 1024])])
+def test_multisize_walk_matches_oracle(ctx, methods, cands):
+    inputs = [synth.generate(12288, 3), synth.generate(65536, 21), synth.generate(200000, 22),
+              _zero_then_random(), bytes(7)]
+    for data in inputs:
+        comp = _compressor(methods=methods)
+        comp.CHUNK_SIZE_CANDIDATES = list(cands)
+        body = comp._adaptive_compress(data)
+        ref, st = orc.compress_body_multisize(data, cands, tuple(methods) + (255,))
+        assert body == ref, (methods, len(data))
+        for k in ("total_chunks", "compressed_chunks", "raw_chunks", "bytes_saved",
+                  "compressed_size_without_overhead", "overhead_bytes"):
+            assert comp.chunk_stats[k] == st[k], k
+        assert comp._adaptive_decompress(body, len(data)) == data
+        blob, stats = comp.compress_bytes(data)           # header, MD5, raw fallback
+        assert comp.decompress_bytes(blob) == data if blob[:4] == b"AMBC" else blob == data
+
+
+def test_multisize_rejects_oversize_gpu_chunks(ctx):
+    comp = _compressor(methods=(1, 3, 4, 5))
+    comp.CHUNK_SIZE_CANDIDATES = list(REF_CANDS)
+    with pytest.raises(NotImplementedError):
+        comp._adaptive_compress(synth.generate(100000, 5))

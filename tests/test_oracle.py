@@ -6,6 +6,7 @@ Every vector here was produced by importing the reference
 import ctypes as C
 import hashlib
 import os
+import random
 
 import numpy as np
 import pytest
@@ -201,3 +202,33 @@ def test_gdeflate_streams_are_valid_zlib():
         tot += len(z)
         ztot += len(zlib.compress(d, 9))
     assert tot < 1.15 * ztot      # within 15 % of zlib level 9 on these inputs
+
+
+def test_multisize_walk_matches_reference_golden():
+    """The oracle's multi-size walk (adaptive_compressor.py:363-394,537-590, the
+    reference's default eight CHUNK_SIZE_CANDIDATES, its stdlib method set
+    {1..7}) reproduces the reference-generated default-candidates container."""
+    from conftest import GOLDEN, load_golden
+    rec = [r for r in load_golden("files.json") if r["name"] == "default_s3_n12288"][0]
+    data = synth.generate(rec["size"], rec["seed"])
+    with open(os.path.join(GOLDEN, rec["file"]), "rb") as f:
+        blob = f.read()
+    body, st = orc.compress_body_multisize(
+        data, [131072, 65536, 32768, 16384, 8192, 4096, 2048, 1024], (1, 2, 3, 4, 5, 6, 7, 255),
+        reference_set=True)
+    assert body == blob[47:]
+    cs = rec["stats"]["chunk_stats"]
+    for k in ("total_chunks", "compressed_chunks", "raw_chunks", "bytes_saved",
+              "compressed_size_without_overhead", "overhead_bytes"):
+        assert st[k] == cs[k], k
+    assert {str(k): v for k, v in st["method_usage"].items()} == cs["method_usage"]
+
+
+def test_multisize_walk_remainder_raw():
+    """No size beats raw at a position: the whole remainder becomes one raw
+    package (adaptive_compressor.py:586-588), after the compressible head."""
+    rnd = random.Random(4242)
+    data = bytes(20000) + bytes(rnd.randrange(256) for _ in range(30000))
+    body, st = orc.compress_body_multisize(data, [16384, 8192, 4096, 2048, 1024], (1, 3, 4, 255))
+    assert st["raw_chunks"] == 1 and st["compressed_chunks"] >= 5
+    assert orc.decompress_body(body, len(data)) == data
