@@ -34,8 +34,9 @@ struct EncSmem {
     // work = union, by lifetime.  Selection: hist | code | clen | Huffman tree
     // (parent/pbit) | first occurrences (first/order).  LZ4: last[] hash table +
     // 128 bucket masks.  Emit: RLE pair starts | Huffman bit staging behind
-    // hist/code/clen.  9.3 KB per workgroup at C = 4096 -> 17 workgroups per CU.
-    static constexpr int WORK = CMAX <= 4096 ? 5120 : 2304 + CMAX + 64;
+    // hist/code/clen.  9.3 KB per workgroup at C = 4096 -> 17 workgroups per CU
+    // (13.4 KB / 12 at 8192, 21.6 KB / 7 at 16384).
+    static constexpr int WORK = 5120;   // every chunk size; larger Huffman payloads stage in the slot
     static constexpr int STAGE_OFF = 2304;                  // Huffman bit staging
     static constexpr int STAGE = WORK - STAGE_OFF;
     alignas(16) uint8_t chunk[CMAX + 64];      // zero padded

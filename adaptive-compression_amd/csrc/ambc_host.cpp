@@ -91,11 +91,11 @@ struct ambc_ctx {
 
 // a chunk's scratch slot: winners are < n bytes; forced single-method encodes
 // (ambc_encode_method) can reach 2n (RLE) or ~1.13n + 1284 (Huffman), plus the
-// Huffman bit staging area behind the payload.  Up to C = 4096 a Huffman winner
-// of more than 2812 bytes stages its bits behind the payload too (k_encode's LDS
-// staging holds 2816 B), hence 2C there.
+// Huffman bit staging area behind the payload.  A Huffman winner of more than
+// 2812 bytes stages its bits behind the payload too (k_encode's LDS staging
+// holds 2816 B), hence 2C.
 static uint32_t slot_stride_for(uint32_t C, bool forced = false) {
-    const uint32_t need = forced ? 3 * C + 1344 : (C <= 4096 ? 2 * C + 64 : C + 64);
+    const uint32_t need = forced ? 3 * C + 1344 : 2 * C + 64;
     return (need + 15) & ~15u;
 }
 
