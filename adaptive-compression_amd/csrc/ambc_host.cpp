@@ -18,6 +18,7 @@
 #include <thread>
 #include <vector>
 
+#include <sys/mman.h>
 #include <zlib.h>
 
 #include "../../include/ambc.h"
@@ -81,6 +82,10 @@ struct Dev {
     Buf in, out, slots, plen, ids, sizes, off, scan_tmp, acc, ent_full, ent_tail;
     Buf body, jobs, produced, dout, scratch, seg, list, bestpre, gdseq, pending;
     uint64_t t_encode = 0, t_scan = 0, t_compact = 0;
+    // pinned staging for large pageable copies: 2 buffers + 2 events per copy thread
+    std::vector<void*> stage;
+    std::vector<hipStream_t> stage_st;
+    std::vector<hipEvent_t> stage_ev;
 };
 
 }  // namespace
@@ -150,6 +155,9 @@ void ambc_destroy(ambc_ctx* ctx) {
                        &d.acc, &d.ent_full, &d.ent_tail, &d.body, &d.jobs, &d.produced, &d.dout,
                        &d.scratch, &d.seg, &d.list, &d.bestpre, &d.gdseq, &d.pending})
             b->release();
+        for (void* b : d.stage) (void)hipHostFree(b);
+        for (auto& ev : d.stage_ev) (void)hipEventDestroy(ev);
+        for (auto& x : d.stage_st) (void)hipStreamDestroy(x);
         for (auto& ev : d.ev) (void)hipEventDestroy(ev);
         for (auto& ev : d.xev) (void)hipEventDestroy(ev);
         for (auto& x : d.xs) { (void)hipStreamSynchronize(x); (void)hipStreamDestroy(x); }
@@ -845,6 +853,99 @@ static void inflate_all(const uint8_t* body, const std::vector<ambc_host_chunk>&
     for (auto& t : th) t.join();
 }
 
+// Large copies between pageable host memory and the device: T threads, each
+// owning a contiguous range and two pinned buffers, overlap their own DMA with
+// the CPU copy of the previous piece; the host side (memcpy, and the first-touch
+// page faults of a freshly allocated output) runs on all T threads at once.
+constexpr size_t kStagePiece = 8u << 20;
+constexpr uint64_t kStageMin = 64ull << 20;   // below this the runtime's own path
+
+static int ensure_stage(Dev& d, unsigned T) {
+    if (d.stage_st.size() >= T) return AMBC_OK;
+    HIPCHK(hipSetDevice(d.id));
+    while (d.stage_st.size() < T) {
+        void* b[2] = {nullptr, nullptr};
+        hipStream_t st;
+        hipEvent_t ev[2];
+        HIPCHK(hipHostMalloc(&b[0], kStagePiece, hipHostMallocDefault));
+        HIPCHK(hipHostMalloc(&b[1], kStagePiece, hipHostMallocDefault));
+        HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
+        d.stage.push_back(b[0]); d.stage.push_back(b[1]);
+        d.stage_st.push_back(st);
+        d.stage_ev.push_back(ev[0]); d.stage_ev.push_back(ev[1]);
+    }
+    return AMBC_OK;
+}
+
+static unsigned stage_threads(uint64_t n) {
+    const char* e = getenv("AMBC_HOST_THREADS");
+    unsigned t = e ? (unsigned)std::max(1, atoi(e)) : std::min(16u, std::thread::hardware_concurrency());
+    return std::max(1u, std::min<unsigned>(t, (unsigned)(n / kStagePiece) + 1));
+}
+
+// to_dev: host src -> device dst; else device src -> host dst
+static int copy_staged(Dev& d, void* dst, const void* src, uint64_t n, bool to_dev) {
+    const unsigned T = stage_threads(n);
+    int rc = ensure_stage(d, T);
+    if (rc) return rc;
+    if (!to_dev) {
+        // a fresh output (calloc'd bytes) is faulted in on first touch: ask for 2 MiB
+        // pages so that 4 GiB is 2048 faults, not a million (advice only)
+        const uintptr_t lo = ((uintptr_t)dst + (2u << 20) - 1) & ~(uintptr_t)((2u << 20) - 1);
+        const uintptr_t hi = ((uintptr_t)dst + n) & ~(uintptr_t)((2u << 20) - 1);
+        if (hi > lo) (void)madvise((void*)lo, hi - lo, MADV_HUGEPAGE);
+    }
+    std::vector<int> err(T, 0);
+    auto run = [&](unsigned t) {
+        if (hipSetDevice(d.id) != hipSuccess) { err[t] = 1; return; }
+        const uint64_t a = n * t / T, b = n * (t + 1) / T;
+        uint8_t* pb[2] = {static_cast<uint8_t*>(d.stage[2 * t]), static_cast<uint8_t*>(d.stage[2 * t + 1])};
+        hipEvent_t* ev = &d.stage_ev[2 * t];
+        hipStream_t st = d.stage_st[t];
+        const uint8_t* s8 = static_cast<const uint8_t*>(src);
+        uint8_t* d8 = static_cast<uint8_t*>(dst);
+        if (to_dev) {
+            // memcpy piece k into buffer k%2 (after its previous DMA finished), then DMA it
+            int cur = 0;
+            for (uint64_t off = a; off < b; off += kStagePiece, cur ^= 1) {
+                const size_t len = (size_t)std::min<uint64_t>(kStagePiece, b - off);
+                if (off >= a + 2 * kStagePiece && hipEventSynchronize(ev[cur]) != hipSuccess) { err[t] = 1; return; }
+                std::memcpy(pb[cur], s8 + off, len);
+                if (hipMemcpyAsync(d8 + off, pb[cur], len, hipMemcpyHostToDevice, st) != hipSuccess ||
+                    hipEventRecord(ev[cur], st) != hipSuccess) { err[t] = 1; return; }
+            }
+            if (hipStreamSynchronize(st) != hipSuccess) err[t] = 1;
+        } else {
+            // DMA piece k+1 while piece k is copied out of its buffer
+            int cur = 0;
+            if (a < b) {
+                const size_t len0 = (size_t)std::min<uint64_t>(kStagePiece, b - a);
+                if (hipMemcpyAsync(pb[0], s8 + a, len0, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                    hipEventRecord(ev[0], st) != hipSuccess) { err[t] = 1; return; }
+            }
+            for (uint64_t off = a; off < b; off += kStagePiece, cur ^= 1) {
+                const size_t len = (size_t)std::min<uint64_t>(kStagePiece, b - off);
+                const uint64_t nx = off + kStagePiece;
+                if (nx < b) {
+                    const size_t ln = (size_t)std::min<uint64_t>(kStagePiece, b - nx);
+                    if (hipMemcpyAsync(pb[cur ^ 1], s8 + nx, ln, hipMemcpyDeviceToHost, st) != hipSuccess ||
+                        hipEventRecord(ev[cur ^ 1], st) != hipSuccess) { err[t] = 1; return; }
+                }
+                if (hipEventSynchronize(ev[cur]) != hipSuccess) { err[t] = 1; return; }
+                std::memcpy(d8 + off, pb[cur], len);
+            }
+        }
+    };
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < T; t++) th.emplace_back(run, t);
+    run(0);
+    for (auto& x : th) x.join();
+    for (int e : err) if (e) return fail(AMBC_E_DEVICE, "staged copy failed");
+    return AMBC_OK;
+}
+
 static int decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t orig_size,
                          const uint64_t reg[4], uint8_t* out, std::vector<ambc_host_chunk>& host,
                          ambc_stats* st, uint8_t* d_out_ext = nullptr) {
@@ -853,7 +954,12 @@ static int decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t or
     hipStream_t s = d.stream;
     HIPCHK(d.body.ensure(blen + 64));
     uint64_t t = now_ns();
-    if (blen) HIPCHK(hipMemcpyAsync(d.body.p, body, blen, hipMemcpyHostToDevice, s));
+    if (blen >= kStageMin) {
+        int rc = copy_staged(d, d.body.p, body, blen, true);
+        if (rc) return rc;
+    } else if (blen) {
+        HIPCHK(hipMemcpyAsync(d.body.p, body, blen, hipMemcpyHostToDevice, s));
+    }
     HIPCHK(hipStreamSynchronize(s));
     const uint64_t h2d = now_ns() - t;
     std::map<uint32_t, uint64_t> known;
@@ -958,6 +1064,10 @@ static int decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t or
     t = now_ns();
     if (d_out_ext) {   // device-resident output (multi-GPU decode): no copy back
         if (orig_size) HIPCHK(hipMemcpyAsync(d_out_ext, d.dout.p, orig_size, hipMemcpyDeviceToDevice, s));
+    } else if (orig_size >= kStageMin) {
+        HIPCHK(hipStreamSynchronize(s));
+        int rc = copy_staged(d, out, d.dout.p, orig_size, false);
+        if (rc) return rc;
     } else {
         HIPCHK(hipMemcpyAsync(out, d.dout.p, orig_size, hipMemcpyDeviceToHost, s));
     }
