@@ -702,92 +702,252 @@ uint64_t expect_len(uint32_t t, uint32_t clen, uint32_t orig, const uint64_t reg
     return clen ? orig : 0;
 }
 
+// One package of the _adaptive_decompress walk (adaptive_compressor.py:399-445)
+// whose 18-B header starts at hp: its decode job (offsets left to the caller),
+// decode kernel, expected output length and device scratch reservation.
+// Returns false where the walk stops at this header (type 0, payload overrun).
+bool make_job(const uint8_t* body, uint64_t blen, uint64_t hp, uint32_t ord, const uint64_t reg[4],
+              const std::map<uint32_t, uint64_t>& known, DecJob& j, int& kind, uint64_t& expect,
+              uint64_t& sneed) {
+    const uint32_t t = body[hp + 4];
+    const uint32_t orig = rd32le(body + hp + 10);
+    const uint32_t clen = rd32le(body + hp + 14);
+    const uint64_t pos = hp + HDR;
+    if (t == 0 || pos + clen > blen) return false;
+    j = DecJob{};
+    kind = DEC_KIND_HEAVY;
+    sneed = 0;
+    j.body_off = pos;
+    j.clen = clen;
+    j.orig = orig;
+    j.scratch_off = ~0ull;
+    j.scratch_cap = 0;
+    if (!registered_id(reg, t)) {
+        j.type = DEC_VERBATIM;
+        kind = DEC_KIND_LIGHT;
+    } else if (t == 5 && clen && orig <= 16384) {
+        // zlib payload: inflated on the GPU (host zlib if it decodes past the map)
+        j.type = 5;
+        kind = orig <= 4096 ? DEC_KIND_INFLATE_4K : orig <= 8192 ? DEC_KIND_INFLATE_8K : DEC_KIND_INFLATE_16K;
+    } else if (t == 5 || t == 6 || t == 7) {
+        j.type = DEC_SKIP;
+        kind = DEC_KIND_LIGHT;
+    } else {
+        if (t == 255 || t == 1 || t == 4) kind = DEC_KIND_LIGHT;
+        j.type = t;
+        if (t == 9 && clen) {
+            const uint64_t cb = lz4_content_bound(body + pos, clen);
+            if (clen >= 7 && !((body[pos + 4] >> 2) & 1) && cb < 0x80000000ull) {
+                // dec_lz4_par's domain (no content checksum): LDS source map of u16
+                // entries for small frames, else a u32 map in device scratch
+                if (clen <= 0x7FFF && cb <= 16384) {
+                    kind = cb <= 4096 ? DEC_KIND_LZ4_4K : cb <= 8192 ? DEC_KIND_LZ4_8K : DEC_KIND_LZ4_16K;
+                } else {
+                    kind = DEC_KIND_LZ4_G;
+                    j.scratch_cap = cb;
+                    sneed = (4 * cb + 15) & ~15ull;
+                }
+            } else if (cb > STAGE_DEC) {
+                j.scratch_cap = cb;
+                sneed = (cb + 15) & ~15ull;
+            }
+        }
+        if (t == 2 && clen && (uint64_t)orig + 256 > STAGE_DEC) {
+            j.scratch_cap = (uint64_t)orig + 256;
+            sneed = (j.scratch_cap + 15) & ~15ull;
+        }
+    }
+    expect = expect_len(t, clen, orig, reg);
+    auto it = known.find(ord);
+    if (it != known.end()) expect = it->second;
+    j.expect = (uint32_t)std::min<uint64_t>(expect, 0xFFFFFFFFull);
+    return true;
+}
+
+inline bool is_marker(const uint8_t* p) { return p[0] == 0xFF && p[1] == 0xFF && p[2] == 0 && p[3] == 0; }
+
+// append package j at output offset out (scratch and host-codec lists in walk order)
+void push_job(Walk& w, DecJob j, int kind, uint64_t expect, uint64_t sneed, uint32_t ord, uint64_t out,
+              const uint8_t* body) {
+    if (sneed) { j.scratch_off = w.scratch; w.scratch += sneed; }
+    j.out_off = out;
+    if (j.type == DEC_SKIP) {
+        const uint32_t t = body[j.body_off - HDR + 4];
+        ambc_host_chunk h{j.body_off, out, j.clen, j.orig, t, 0};
+        if (t == 5) { if (j.clen) w.zlib.push_back(h); }
+        else w.host.push_back(h);
+    }
+    w.jobs.push_back(j);
+    w.kind.push_back((uint8_t)kind);
+    w.src_index.push_back(ord);
+    (void)expect;
+}
+
 // _adaptive_decompress header walk (adaptive_compressor.py:399-445)
-void walk_body(const uint8_t* body, uint64_t blen, uint64_t orig_size, const uint64_t reg[4],
-               const std::map<uint32_t, uint64_t>& known, Walk& w) {
+void walk_body_serial(const uint8_t* body, uint64_t blen, uint64_t orig_size, const uint64_t reg[4],
+                      const std::map<uint32_t, uint64_t>& known, Walk& w) {
     uint64_t pos = 0, out = 0;
     uint32_t ord = 0;
     while (pos < blen) {
         if (pos + HDR > blen) break;
-        if (!(body[pos] == 0xFF && body[pos + 1] == 0xFF && body[pos + 2] == 0 && body[pos + 3] == 0)) {
-            w.marker_error = true;
-            return;
-        }
-        const uint32_t t = body[pos + 4];
-        const uint32_t orig = rd32le(body + pos + 10);
-        const uint32_t clen = rd32le(body + pos + 14);
-        pos += HDR;
-        if (t == 0) break;
-        if (pos + clen > blen) break;
-        DecJob j{};
-        int kind = DEC_KIND_HEAVY;
-        j.body_off = pos;
-        j.clen = clen;
-        j.orig = orig;
-        j.scratch_off = ~0ull;
-        j.scratch_cap = 0;
-        uint64_t expect;
-        if (!registered_id(reg, t)) {
-            j.type = DEC_VERBATIM;
-            kind = DEC_KIND_LIGHT;
-            expect = clen;
-        } else if (t == 5 && clen && orig <= 16384) {
-            // zlib payload: inflated on the GPU (host zlib if it decodes past the map)
-            j.type = 5;
-            kind = orig <= 4096 ? DEC_KIND_INFLATE_4K : orig <= 8192 ? DEC_KIND_INFLATE_8K : DEC_KIND_INFLATE_16K;
-            expect = orig;
-        } else if (t == 5 || t == 6 || t == 7) {
-            j.type = DEC_SKIP;
-            kind = DEC_KIND_LIGHT;
-            expect = clen ? orig : 0;
-        } else {
-            if (t == 255 || t == 1 || t == 4) kind = DEC_KIND_LIGHT;
-            j.type = t;
-            switch (t) {
-            case 255: expect = orig; break;
-            case 4: expect = clen ? std::min(clen, orig) : 0; break;
-            default: expect = clen ? orig : 0; break;
-            }
-            if (t == 9 && clen) {
-                const uint64_t cb = lz4_content_bound(body + pos, clen);
-                if (clen >= 7 && !((body[pos + 4] >> 2) & 1) && cb < 0x80000000ull) {
-                    // dec_lz4_par's domain (no content checksum): LDS source map of u16
-                    // entries for small frames, else a u32 map in device scratch
-                    if (clen <= 0x7FFF && cb <= 16384) {
-                        kind = cb <= 4096 ? DEC_KIND_LZ4_4K : cb <= 8192 ? DEC_KIND_LZ4_8K : DEC_KIND_LZ4_16K;
-                    } else {
-                        kind = DEC_KIND_LZ4_G;
-                        j.scratch_off = w.scratch;
-                        j.scratch_cap = cb;
-                        w.scratch += (4 * cb + 15) & ~15ull;
-                    }
-                } else if (cb > STAGE_DEC) {
-                    j.scratch_off = w.scratch; j.scratch_cap = cb; w.scratch += (cb + 15) & ~15ull;
-                }
-            }
-            if (t == 2 && clen && (uint64_t)orig + 256 > STAGE_DEC) {
-                j.scratch_off = w.scratch; j.scratch_cap = (uint64_t)orig + 256;
-                w.scratch += (j.scratch_cap + 15) & ~15ull;
-            }
-        }
-        auto it = known.find(ord);
-        if (it != known.end()) expect = it->second;
-        j.expect = (uint32_t)std::min<uint64_t>(expect, 0xFFFFFFFFull);
-        j.out_off = out;
-        if (j.type == DEC_SKIP) {
-            ambc_host_chunk h{pos, out, clen, orig, t, 0};
-            if (t == 5) { if (clen) w.zlib.push_back(h); }
-            else w.host.push_back(h);
-        }
-        w.jobs.push_back(j);
-        w.kind.push_back((uint8_t)kind);
-        w.src_index.push_back(ord);
+        if (!is_marker(body + pos)) { w.marker_error = true; return; }
+        DecJob j;
+        int kind;
+        uint64_t expect, sneed;
+        if (!make_job(body, blen, pos, ord, reg, known, j, kind, expect, sneed)) break;
+        push_job(w, j, kind, expect, sneed, ord, out, body);
         out += expect;
-        pos += clen;
+        pos = j.body_off + j.clen;
         ord++;
         if (out >= orig_size) break;
     }
     w.total = out;
+}
+
+// Follow the header chain from `start` while positions stay below `limit`:
+// header positions go to `hp`; returns 1 at a marker mismatch (position in
+// *exit), 0 otherwise with *exit = the first header position >= limit, or
+// UINT64_MAX where the chain ends (truncated header, type 0, payload overrun --
+// that last header is listed).
+int follow_chain(const uint8_t* body, uint64_t blen, uint64_t start, uint64_t limit,
+                 std::vector<uint64_t>& hp, uint64_t* exit) {
+    uint64_t pos = start;
+    while (pos < limit) {
+        if (pos + HDR > blen) { *exit = UINT64_MAX; return 0; }
+        if (!is_marker(body + pos)) { *exit = pos; return 1; }
+        hp.push_back(pos);
+        const uint32_t t = body[pos + 4];
+        const uint64_t clen = rd32le(body + pos + 14);
+        if (t == 0 || pos + HDR + clen > blen) { *exit = UINT64_MAX; return 0; }
+        pos += HDR + clen;
+    }
+    *exit = pos;
+    return 0;
+}
+
+// The same walk for large bodies on host threads.  Every thread follows the
+// chain from the first marker in its segment that leads consistently to the
+// segment's end; the true chain (from offset 0) is stitched segment by segment --
+// where it enters a segment at a position of that thread's chain, the rest of
+// the chain is the thread's (the walk is deterministic), else it is walked there.
+// Jobs are built in parallel; offsets by one serial prefix pass.
+void walk_body(const uint8_t* body, uint64_t blen, uint64_t orig_size, const uint64_t reg[4],
+               const std::map<uint32_t, uint64_t>& known, Walk& w) {
+    const unsigned T = std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    if (blen < (32ull << 20) || T < 2) { walk_body_serial(body, blen, orig_size, reg, known, w); return; }
+    std::vector<std::vector<uint64_t>> seg(T);
+    std::vector<uint64_t> sexit(T, UINT64_MAX);
+    std::vector<int> sstat(T, 0);
+    std::vector<uint64_t> s0(T + 1);
+    for (unsigned t = 0; t <= T; t++) s0[t] = blen * t / T;
+    auto discover = [&](unsigned t) {
+        if (t == 0) { sstat[0] = follow_chain(body, blen, 0, s0[1], seg[0], &sexit[0]); return; }
+        uint64_t c = s0[t];
+        for (int tries = 0; tries < 256 && c < s0[t + 1]; tries++) {
+            const void* f = memchr(body + c, 0xFF, s0[t + 1] - c);
+            if (!f) break;
+            c = (uint64_t)((const uint8_t*)f - body);
+            if (c + HDR <= blen && is_marker(body + c)) {
+                seg[t].clear();
+                uint64_t ex;
+                if (follow_chain(body, blen, c, s0[t + 1], seg[t], &ex) == 0) { sexit[t] = ex; return; }
+            }
+            c++;
+        }
+        seg[t].clear();
+        sstat[t] = -1;   // nothing consistent found: walked when the chain gets here
+    };
+    {
+        std::vector<std::thread> th;
+        for (unsigned t = 1; t < T; t++) th.emplace_back(discover, t);
+        discover(0);
+        for (auto& x : th) x.join();
+    }
+    // stitch the true chain
+    std::vector<uint64_t> H(seg[0]);
+    uint64_t q = sexit[0];
+    int status = sstat[0];
+    for (unsigned t = 1; t < T && status == 0 && q != UINT64_MAX; t++) {
+        if (q >= s0[t + 1]) continue;               // one package spans this segment
+        auto it = sstat[t] == 0 ? std::lower_bound(seg[t].begin(), seg[t].end(), q) : seg[t].end();
+        if (it != seg[t].end() && *it == q) {
+            H.insert(H.end(), it, seg[t].end());
+            q = sexit[t];
+        } else {
+            status = follow_chain(body, blen, q, s0[t + 1], H, &q);
+        }
+    }
+    // jobs in parallel, then offsets and the out >= orig_size stop in order
+    const size_t K = H.size();
+    std::vector<DecJob> J(K);
+    std::vector<int> kinds(K);
+    std::vector<uint64_t> ex(K), sn(K);
+    std::vector<uint8_t> ok(K);
+    {
+        auto build = [&](unsigned t) {
+            for (size_t k = K * t / T; k < K * (t + 1) / T; k++)
+                ok[k] = make_job(body, blen, H[k], (uint32_t)k, reg, known, J[k], kinds[k], ex[k], sn[k]);
+        };
+        std::vector<std::thread> th;
+        for (unsigned t = 1; t < T; t++) th.emplace_back(build, t);
+        build(0);
+        for (auto& x : th) x.join();
+    }
+    // offsets: per-block sums, a prefix over the blocks, then each block finds its
+    // own stop (a header that ends the walk, or out reaching orig_size) and fills
+    // in its offsets; the walk stops at the first block's stop
+    std::vector<uint64_t> bo(T + 1, 0), bs(T + 1, 0);
+    std::vector<size_t> stop(T, SIZE_MAX);
+    auto bsum = [&](unsigned t) {
+        uint64_t a = 0, b = 0;
+        for (size_t k = K * t / T; k < K * (t + 1) / T; k++) { a += ex[k]; b += sn[k]; }
+        bo[t + 1] = a;
+        bs[t + 1] = b;
+    };
+    auto fill = [&](unsigned t) {
+        uint64_t out = bo[t], scr = bs[t];
+        for (size_t k = K * t / T; k < K * (t + 1) / T; k++) {
+            if (!ok[k]) { stop[t] = k; return; }        // walk ends before this header
+            J[k].out_off = out;
+            if (sn[k]) { J[k].scratch_off = scr; scr += sn[k]; }
+            out += ex[k];
+            if (out >= orig_size) { stop[t] = k + 1; return; }
+        }
+    };
+    auto par = [&](auto&& f) {
+        std::vector<std::thread> th;
+        for (unsigned t = 1; t < T; t++) th.emplace_back(f, t);
+        f(0);
+        for (auto& x : th) x.join();
+    };
+    par(bsum);
+    for (unsigned t = 0; t < T; t++) { bo[t + 1] += bo[t]; bs[t + 1] += bs[t]; }
+    par(fill);
+    size_t nj = K;
+    bool stopped = false;
+    for (unsigned t = 0; t < T; t++)
+        if (stop[t] != SIZE_MAX) { nj = stop[t]; stopped = true; break; }
+    if (!stopped && status == 1) { w.marker_error = true; return; }
+    J.resize(nj);
+    w.jobs = std::move(J);
+    w.kind.resize(nj);
+    w.src_index.resize(nj);
+    uint64_t total = 0, scr = 0;
+    for (size_t k = 0; k < nj; k++) {
+        w.kind[k] = (uint8_t)kinds[k];
+        w.src_index[k] = (uint32_t)k;
+        total += ex[k];
+        scr += sn[k];
+        const DecJob& j = w.jobs[k];
+        if (j.type == DEC_SKIP) {
+            const uint32_t t = body[j.body_off - HDR + 4];
+            ambc_host_chunk h{j.body_off, j.out_off, j.clen, j.orig, t, 0};
+            if (t == 5) { if (j.clen) w.zlib.push_back(h); }
+            else w.host.push_back(h);
+        }
+    }
+    w.scratch = scr;
+    w.total = total;
 }
 
 }  // namespace

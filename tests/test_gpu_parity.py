@@ -534,3 +534,43 @@ def test_multisize_rejects_oversize_gpu_chunks(ctx):
     comp.CHUNK_SIZE_CANDIDATES = list(REF_CANDS)
     with pytest.raises(NotImplementedError):
         comp._adaptive_compress(synth.generate(100000, 5))
+
+
+def _pkg(t, orig, payload):
+    import struct
+    return b"\xff\xff\x00\x00" + bytes((t, 0)) + struct.pack("<III", orig, orig, len(payload)) + payload
+
+
+def test_parallel_header_walk_large_bodies(ctx):
+    """Bodies above 32 MiB take the threaded header walk: payloads full of fake
+    headers (the speculative segment chains must not be trusted), unregistered
+    ids, a short Huffman package (re-walk with known lengths), a marker mismatch
+    after the out >= orig_size stop (ignored) and one before it (raises)."""
+    rng = np.random.default_rng(5)
+    fake = _pkg(1, 4096, b"\x00\x10" * 8)[:18]
+    pieces, orig = [], 0
+    for k in range(700):
+        raw = bytearray(rng.integers(0, 256, 65536, dtype=np.uint8).tobytes())
+        for q in range(0, 65536 - 64, 4099):
+            raw[q:q + 18] = fake                       # markers inside payloads
+        if k % 97 == 5:
+            pieces.append(_pkg(77, 9, bytes(raw[:100])))   # unregistered: copied verbatim
+            orig += 100
+        pieces.append(_pkg(255, 65536, bytes(raw)))
+        orig += 65536
+        if k == 350:
+            pieces.append(_pkg(3, 50, orc.huff_encode(b"abcab" * 6)))   # decodes to 30 < 50
+            orig += 50
+    body = b"".join(pieces) + _pkg(0, 0, b"")[:16]
+    assert len(body) > (40 << 20)
+    comp = _compressor()
+    for osz in (orig, orig - 12345, orig // 3):
+        assert comp._adaptive_decompress(body, osz) == orc.decompress_body(body, osz), osz
+    # a corrupted marker: after the stop it is never reached, before it it raises
+    bad = bytearray(body)
+    p = len(pieces[0]) + len(pieces[1])
+    bad[p] = 0
+    assert comp._adaptive_decompress(bytes(bad), len(pieces[0]) - 18) == \
+        orc.decompress_body(bytes(bad), len(pieces[0]) - 18)
+    with pytest.raises(ValueError, match="Marker mismatch"):
+        comp._adaptive_decompress(bytes(bad), orig)
