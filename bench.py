@@ -308,13 +308,19 @@ def main():
         comp = AdaptiveCompressor(chunk_size=args.chunk, mode=args.mode, methods=methods)
         t = time.perf_counter()
         back = comp._adaptive_decompress(body_host, n)
-        dwall = time.perf_counter() - t
+        dcold = time.perf_counter() - t                 # first call: + pinned staging setup
         verified = back == d_in.cpu().numpy().tobytes()
+        del back
+        t = time.perf_counter()
+        back = comp._adaptive_decompress(body_host, n)
+        dwall = time.perf_counter() - t
+        verified = verified and back == d_in.cpu().numpy().tobytes()
         ds = comp._last_device_stats
         decode = {"kernel_ms": round(ds.kernel_ns / 1e6, 3), "header_walk_ms": round(ds.walk_ns / 1e6, 3),
                   "h2d_ms": round(ds.h2d_ns / 1e6, 3), "d2h_ms": round(ds.d2h_ns / 1e6, 3),
                   "kernel_GBps": round(n / max(ds.kernel_ns, 1), 3),
-                  "host_api_GBps": round(n / dwall / 1e9, 3)}
+                  "host_api_GBps": round(n / dwall / 1e9, 3),
+                  "host_api_GBps_first_call": round(n / dcold / 1e9, 3)}
         log(f"round trip bit-exact: {verified}; decode {decode}")
 
     e2e = api = None
