@@ -388,6 +388,8 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
     };
 
     bool huff_su = false;
+    bool huff_defer = false;
+    uint32_t huff_lb = 0;
     if ((eligible(3) || analyze) && (n >= 100 || force)) {
         double part = 0.0;
         uint32_t kc = 0;
@@ -421,10 +423,17 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         }
         huff_su = n >= 100 && H < 7.0;
         if (eligible(3) && (force || huff_su) && kdist >= 2 && kdist <= 255) {
-            // (code lengths stay <= 23 for n <= 65536: a Fibonacci-weighted tree)
-            const uint32_t nb = huff_bits();
-            const uint32_t l = 1 + 5 * kdist + 4 + (nb + 7) / 8;
-            if (l + HDR < best) { best = l + HDR; win = 3; wlen = l; }
+            if (!force && !analyze && !A.bestpre && eligible(9) && n >= 1024) {
+                // LZ4 goes first; Huffman's exact size only if its entropy bound
+                // (average code length >= H) could still beat or tie LZ4's
+                huff_defer = true;
+                huff_lb = 1 + 5 * kdist + 4 + (uint32_t)floor((double)n * H * (1.0 - 1e-9) / 8.0);
+            } else {
+                // (code lengths stay <= 23 for n <= 65536: a Fibonacci-weighted tree)
+                const uint32_t nb = huff_bits();
+                const uint32_t l = 1 + 5 * kdist + 4 + (nb + 7) / 8;
+                if (l + HDR < best) { best = l + HDR; win = 3; wlen = l; }
+            }
         }
     }
 
@@ -449,6 +458,25 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         const bool single = wave_sum_u32(nz) == 1;
         if (lane == 0) A.bestpre[k] = best | (uniform ? 0x80000000u : 0u) | (single ? 0x40000000u : 0u);
     }
+    // the LZ4 walk reuses hist[]/code[] for its tables: count the bytes again
+    auto recount_hist = [&]() {
+        for (uint32_t i = lane; i < 256; i += 64) S.hist()[i] = 0;
+        wave_sync();
+#pragma unroll 1
+        for (int r = 0; r < ROUNDS; r++) {
+            const uint32_t b0 = (uint32_t)(r * 64 + lane) * BS;
+            uint32_t cur = S.chunk[b0], rc = 0;
+            for_block_bytes<BS>(S.chunk, b0, [&](uint32_t p, uint32_t c, uint32_t) {
+                if (p < n) {
+                    if (c == cur) rc++;
+                    else { atomicAdd(&S.hist()[cur], rc); cur = c; rc = 1; }
+                }
+            });
+            if (rc) atomicAdd(&S.hist()[cur], rc);
+        }
+        wave_sync();
+    };
+    const uint32_t best_pre = best;   // before LZ4 (a deferred Huffman compares against it)
     bool lz4_ran = false;   // the LZ4 walk reuses hist[]/code[] for its bucket masks
     // LZ4's frame is at least 23 + 10 + ext(n - 10) bytes: a literal at 0 (no
     // candidate), one match up to n - 5, the last five bytes literal; with the
@@ -701,6 +729,13 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         wave_sync();
     }
 
+    if (huff_defer && huff_lb + HDR < best_pre && (win != 9 || huff_lb <= wlen)) {
+        // Huffman comes before LZ4 in id order: it wins a tie with LZ4
+        if (lz4_ran) recount_hist();
+        const uint32_t nb = huff_bits();
+        const uint32_t l = 1 + 5 * kdist + 4 + (nb + 7) / 8;
+        if (l + HDR < best_pre && (win != 9 || l <= wlen)) { best = l + HDR; win = 3; wlen = l; }
+    }
     STAMP(5);
     // forced Delta (DeltaCompression.compress, compression_methods.py:585-608)
     if (force && ((mm >> 4) & 1u)) { win = 4; wlen = n; }
@@ -781,24 +816,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
             wave_sync();
         }
     } else if (win == 3) {
-        if (lz4_ran) {
-            // the LZ4 walk overwrote hist[]: count again
-            for (uint32_t i = lane; i < 256; i += 64) S.hist()[i] = 0;
-            wave_sync();
-#pragma unroll 1
-            for (int r = 0; r < ROUNDS; r++) {
-                const uint32_t b0 = (uint32_t)(r * 64 + lane) * BS;
-                uint32_t cur = S.chunk[b0], rc = 0;
-                for_block_bytes<BS>(S.chunk, b0, [&](uint32_t p, uint32_t c, uint32_t) {
-                    if (p < n) {
-                        if (c == cur) rc++;
-                        else { atomicAdd(&S.hist()[cur], rc); cur = c; rc = 1; }
-                    }
-                });
-                if (rc) atomicAdd(&S.hist()[cur], rc);
-            }
-            wave_sync();
-        }
+        if (lz4_ran) recount_hist();   // (again: a deferred Huffman may have counted already)
         {
             uint32_t nb2, ml2;
             huff_tree(nb2, ml2);   // codes and lengths of the winner's tree
