@@ -165,10 +165,10 @@ class AdaptiveCompressor:
                 <= self.method_chunk_prefs.get(i, (1, 999999999))[1]]
         if not elig:
             return None
-        if s > _lib.MAX_CHUNK or (5 in elig and s > 16384):
+        if s > _lib.MAX_CHUNK or (5 in elig and s > 16384) or (2 in elig and s > 8192):
             raise NotImplementedError(
                 f"a {s}-byte candidate chunk with methods {elig}: the GPU encoders take chunks "
-                f"up to {_lib.MAX_CHUNK} bytes (DEFLATE up to 16384)")
+                f"up to {_lib.MAX_CHUNK} bytes (DEFLATE up to 16384, Dictionary up to 8192)")
         C_ = (s + 15) & ~15
         p = _lib.Params()
         p.chunk_size = C_

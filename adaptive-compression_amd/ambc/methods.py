@@ -80,11 +80,11 @@ def _gpu_encode(mid, data):
 
 
 def _gpu_should_use(data):
-    """should_use bits from the selector kernel: {1: RLE, 3: Huffman, 4: Delta}."""
+    """should_use bits from the selector kernels: {1: RLE, 2: Dictionary, 3: Huffman, 4: Delta}."""
     data = bytes(data)
     n = len(data)
     if n == 0:
-        return {1: False, 3: False, 4: False}
+        return {1: False, 2: False, 3: False, 4: False}
     if n > _lib.MAX_CHUNK:
         raise ValueError(f"single-chunk analysis is limited to {_lib.MAX_CHUNK} bytes")
     from .compressor import entropy_terms
@@ -102,7 +102,7 @@ def _gpu_should_use(data):
     su = (C.c_uint8 * 1)()
     _lib.check(ctx.lib.ambc_analyze(ctx.h, _lib.addr(data), n, C.byref(p), C.addressof(ids),
                                     C.addressof(pl), C.addressof(su)), ctx.lib)
-    return {1: bool(su[0] & 2), 3: bool(su[0] & 8), 4: bool(su[0] & 16)}
+    return {1: bool(su[0] & 2), 2: bool(su[0] & 4), 3: bool(su[0] & 8), 4: bool(su[0] & 16)}
 
 
 def _gpu_decode(mid, data, original_length):
@@ -140,15 +140,22 @@ class RLECompression(CompressionMethod):
 
 
 class DictionaryCompression(CompressionMethod):
-    """compression_methods.py:183-343 -- GPU decoder; encoder is SURVEY §8(f) next."""
+    """compression_methods.py:183-343 on the GPU (k_dict: the reference's greedy
+    window-4096 / lookahead-32 parse, byte for byte; inputs up to 8192 bytes,
+    the method's preferred maximum chunk)."""
     type_id = 2
 
     def __init__(self, window_size=4096, lookahead_size=32):
+        if (window_size, lookahead_size) != (4096, 32):
+            raise NotImplementedError("the GPU Dictionary encoder implements the reference's "
+                                      "defaults (window_size=4096, lookahead_size=32)")
         self.window_size = window_size
         self.lookahead_size = lookahead_size
 
     def compress(self, data):
-        raise NotImplementedError("Dictionary (id 2) GPU encoder is not built yet (SURVEY §8(f))")
+        if len(data) > 8192:
+            raise NotImplementedError("the GPU Dictionary encoder takes at most 8192 bytes")
+        return _gpu_encode(2, data)
 
     def decompress(self, data, original_length):
         if not data:
@@ -156,7 +163,7 @@ class DictionaryCompression(CompressionMethod):
         return _gpu_decode(2, data, original_length)
 
     def should_use(self, data, threshold=0.9):
-        return False
+        return _gpu_should_use(data)[2]
 
 
 class HuffmanCompression(CompressionMethod):
@@ -279,8 +286,8 @@ class LZMACompression(CompressionMethod):
             return bytes(original_length)
 
 
-GPU_METHODS = {1: RLECompression, 3: HuffmanCompression, 4: DeltaCompression,
-               5: DeflateCompression, 9: LZ4Compression}
+GPU_METHODS = {1: RLECompression, 2: DictionaryCompression, 3: HuffmanCompression,
+               4: DeltaCompression, 5: DeflateCompression, 9: LZ4Compression}
 DECODE_METHODS = {1: RLECompression, 2: DictionaryCompression, 3: HuffmanCompression,
                   4: DeltaCompression, 5: DeflateCompression, 6: Bzip2Compression,
                   7: LZMACompression, 9: LZ4Compression, 255: NoCompression}

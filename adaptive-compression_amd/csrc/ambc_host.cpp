@@ -176,18 +176,25 @@ uint64_t ambc_compress_bound(uint64_t n, uint32_t chunk) {
 // ---------------------------------------------------------------------------
 // compress (device resident)
 // ---------------------------------------------------------------------------
+// the largest chunk id 2 can be eligible for (k_dict's template bucket)
+static uint32_t dict_cmax(const ambc_params* p) { return std::min(p->chunk_size, p->pref_max[AMBC_M_DICT]); }
+
 static int check_params(const ambc_params* p) {
     if (!p) return fail(AMBC_E_INVAL, "params is NULL");
     const uint32_t C = p->chunk_size;
     if (C < 16 || C > AMBC_MAX_CHUNK || (C & 15))
         return fail(AMBC_E_INVAL, "chunk_size must be a multiple of 16 in [16, 65536]");
     if (p->mode > 1) return fail(AMBC_E_INVAL, "mode must be AMBC_MODE_NATIVE or AMBC_MODE_REFERENCE");
-    const uint32_t allowed = (1u << AMBC_M_RLE) | (1u << AMBC_M_HUFFMAN) | (1u << AMBC_M_DELTA) |
-                             (1u << AMBC_M_DEFLATE) | (1u << AMBC_M_LZ4);
+    const uint32_t allowed = (1u << AMBC_M_RLE) | (1u << AMBC_M_DICT) | (1u << AMBC_M_HUFFMAN) |
+                             (1u << AMBC_M_DELTA) | (1u << AMBC_M_DEFLATE) | (1u << AMBC_M_LZ4);
     if (p->method_mask & ~allowed)
-        return fail(AMBC_E_INVAL, "method_mask holds ids without a GPU encoder (allowed: 1, 3, 4, 5, 9)");
+        return fail(AMBC_E_INVAL, "method_mask holds ids without a GPU encoder (allowed: 1, 2, 3, 4, 5, 9)");
     if (((p->method_mask >> AMBC_M_DEFLATE) & 1) && C > 16384)
         return fail(AMBC_E_INVAL, "the GPU DEFLATE encoder supports chunk_size <= 16384");
+    if (((p->method_mask >> AMBC_M_DICT) & 1) && p->pref_min[AMBC_M_DICT] <= dict_cmax(p) &&
+        dict_cmax(p) > 8192)
+        return fail(AMBC_E_INVAL, "the GPU Dictionary encoder takes chunks <= 8192 bytes "
+                                  "(chunk_size or pref_max[2] <= 8192)");
     return AMBC_OK;
 }
 
@@ -261,6 +268,8 @@ static int compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_param
     }
     HIPCHK(hipEventRecord(d.ev[0], s));
     HIPCHK(launch_encode(ea, s));
+    if ((p->method_mask >> AMBC_M_DICT) & 1)
+        HIPCHK(launch_dict(ea, dict_cmax(p), s));   // id 2 against k_encode's winner
     if (deflate) {
         HIPCHK(launch_deflate(ea, s));   // id 5 after 1/3/4, against LZ4 (ties -> 5)
         EncArgs ep = ea;                 // RLE/Huffman payloads id 5 did not replace
@@ -581,6 +590,9 @@ static int run_encode_only(Dev& d, const uint8_t* h_in, uint64_t n, const ambc_p
     ea.flags = flags;
     for (int i = 0; i < 16; i++) { ea.pref_min[i] = p->pref_min[i]; ea.pref_max[i] = p->pref_max[i]; }
     HIPCHK(launch_encode(ea, s));
+    // id 2: selection, and its should_use bit under ENC_ANALYZE
+    if (((p->method_mask >> AMBC_M_DICT) & 1) || (flags & ENC_ANALYZE))
+        HIPCHK(launch_dict(ea, std::min<uint32_t>(dict_cmax(p), 8192), s));
     ids.resize(M);
     plen.resize(M);
     if (M) {
@@ -602,11 +614,13 @@ static int run_encode_only(Dev& d, const uint8_t* h_in, uint64_t n, const ambc_p
 extern "C" int ambc_encode_method(ambc_ctx* ctx, int method_id, const uint8_t* in, uint32_t n,
                                   uint8_t* out, uint32_t out_cap, uint32_t* out_len) {
     if (!ctx || ctx->devs.empty() || !out_len || (!in && n)) return fail(AMBC_E_INVAL, "NULL argument");
-    if (method_id != AMBC_M_RLE && method_id != AMBC_M_HUFFMAN && method_id != AMBC_M_LZ4 &&
-        method_id != AMBC_M_DELTA)
-        return fail(AMBC_E_INVAL, "ambc_encode_method supports ids 1, 3, 4 and 9");
+    if (method_id != AMBC_M_RLE && method_id != AMBC_M_DICT && method_id != AMBC_M_HUFFMAN &&
+        method_id != AMBC_M_LZ4 && method_id != AMBC_M_DELTA)
+        return fail(AMBC_E_INVAL, "ambc_encode_method supports ids 1, 2, 3, 4 and 9");
     if (n == 0) { *out_len = 0; return AMBC_OK; }          // every codec: empty -> b''
     if (n > AMBC_MAX_CHUNK) return fail(AMBC_E_INVAL, "single-chunk encode is limited to 65536 bytes");
+    if (method_id == AMBC_M_DICT && n > 8192)
+        return fail(AMBC_E_INVAL, "the GPU Dictionary encoder takes at most 8192 bytes");
     ambc_params p{};
     p.chunk_size = (n + 15) & ~15u;
     p.method_mask = 1u << method_id;

@@ -26,7 +26,7 @@ struct EncArgs {
     uint64_t* sizes;         // 18 + plen per chunk (scan input)
     const double* ent_full;  // optional exact entropy terms (device)
     const double* ent_tail;
-    uint8_t* su;             // optional: per-chunk should_use bits (1<<1 RLE, 1<<3 Huffman, 1<<4 Delta)
+    uint8_t* su;             // optional: per-chunk should_use bits (1<<1 RLE, 1<<2 Dictionary, 1<<3 Huffman, 1<<4 Delta)
     uint32_t flags;          // ENC_FORCE: encode with the single enabled method, no gates
     unsigned long long* stamps;  // diagnostic build (-DAMBC_STAMPS): per-phase cycle sums
     uint32_t* bestpre;       // optional: best (len + 18) before LZ4 (k_deflate's threshold)
@@ -86,6 +86,7 @@ constexpr uint32_t DEC_SKIP = 257;
 // launchers (ambc_kernels.hip)
 hipError_t launch_encode(const EncArgs& a, hipStream_t s);
 hipError_t launch_deflate(const EncArgs& a, hipStream_t s);   // ambc_deflate.hip
+hipError_t launch_dict(const EncArgs& a, uint32_t cmax, hipStream_t s);   // ambc_dict.hip
 hipError_t launch_compact(const CompactArgs& a, hipStream_t s);
 hipError_t launch_end_chunk(uint8_t* dst, hipStream_t s);
 hipError_t launch_stats(const uint8_t* ids, const uint32_t* plen, uint32_t n_chunks,

@@ -57,7 +57,7 @@ extern "C" {
 
 /* GPU-routable method ids (bit i of method_mask = method id i) */
 #define AMBC_M_RLE 1
-#define AMBC_M_DICT 2  /* decode only (encoder: SURVEY §8(f) next) */
+#define AMBC_M_DICT 2  /* GPU encoder k_dict: the reference's bytes; chunks <= 8192 */
 #define AMBC_M_HUFFMAN 3
 #define AMBC_M_DELTA 4 /* never selected: payload length == n (compression_methods.py:598-608) */
 #define AMBC_M_DEFLATE 5 /* GPU encoder "ambc-deflate v1" (chunk_size <= 16384); decode: host zlib */
@@ -153,10 +153,10 @@ int ambc_compress_device(ambc_ctx* ctx, int dev, const void* d_in, uint64_t n,
                          ambc_stats* st, void* stream);
 
 /* Single-chunk plugin calls (CompressionMethod API, compression_methods.py:7-67).
- * ambc_encode_method = method.compress(chunk) for id 1, 3, 4 or 9 (n <= 65536),
+ * ambc_encode_method = method.compress(chunk) for id 1, 2, 3, 4 or 9 (n <= 65536; id 2: n <= 8192),
  * no gates; AMBC_E_CODEC where the reference raises.  ambc_analyze returns, per
  * C-byte chunk, the winning id, its payload length and the should_use bits
- * (1<<1 RLE, 1<<3 Huffman, 1<<4 Delta) the selector evaluated. */
+ * (1<<1 RLE, 1<<2 Dictionary, 1<<3 Huffman, 1<<4 Delta) the selector evaluated. */
 int ambc_encode_method(ambc_ctx* ctx, int method_id, const uint8_t* in, uint32_t n, uint8_t* out,
                        uint32_t out_cap, uint32_t* out_len);
 int ambc_analyze(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const ambc_params* p, uint8_t* ids,

@@ -183,6 +183,7 @@ def test_decisions_match_oracle(ctx, n, seed, chunk):
         assert bool(su[k] & 2) == orc.should_use(1, ch), k
         assert bool(su[k] & 16) == orc.should_use(4, ch), k
         assert bool(su[k] & 8) == orc.should_use(3, ch), k
+        assert bool(su[k] & 4) == orc.should_use(2, ch), k
 
 
 @pytest.mark.parametrize("n,seed,chunk", CASES)
