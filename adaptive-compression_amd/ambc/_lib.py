@@ -35,6 +35,7 @@ EXPORTS = (
     "ambc_host_free", "ambc_device_alloc", "ambc_device_free", "ambc_memcpy_h2d",
     "ambc_memcpy_d2h", "ambc_synchronize", "ambc_synth_fill", "ambc_synth_device",
     "ambc_last_kernel_times", "ambc_split_body", "ambc_decompress_device",
+    "ambc_last_encode_launches",
 )
 
 
@@ -102,6 +103,7 @@ def _declare(lib):
         "ambc_synth_fill": ([u8p, u64, u64], None),
         "ambc_synth_device": ([vp, i32, vp, u64, u64], i32),
         "ambc_last_kernel_times": ([vp, i32, C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)], i32),
+        "ambc_last_encode_launches": ([vp, i32, C.POINTER(C.c_uint32)], i32),
         "ambc_split_body": ([u8p, u64, u64, C.POINTER(u64), u32, C.POINTER(u64), C.POINTER(u64)], i32),
         "ambc_decompress_device": ([vp, i32, u8p, u64, u64, C.POINTER(u64), vp, C.POINTER(Stats)], i32),
     }

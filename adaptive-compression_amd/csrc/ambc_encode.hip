@@ -912,39 +912,61 @@ __global__ __launch_bounds__(256) void k_compact(CompactArgs A) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t k = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (k >= A.n_chunks) return;
-    const uint64_t o = A.off[k];
+    const uint64_t o = A.off[k] + (A.base ? *A.base : 0ull);
     const uint32_t pl = A.plen[k];
     const uint32_t P = HDR + pl;
     const uint32_t type = A.ids[k];
     const uint64_t p0 = (uint64_t)k * A.chunk_size;
     const uint32_t n = (uint32_t)min((uint64_t)A.chunk_size, A.n_total - p0);
-    const uint8_t* sl = A.slots + (uint64_t)k * A.slot_stride;
+    const uint8_t* __restrict__ sl = A.slots + (uint64_t)k * A.slot_stride;
     const uint64_t d0 = o >> 2, d1 = (o + P - 1) >> 2;
-    uint32_t* out32 = reinterpret_cast<uint32_t*>(A.out);
-    for (uint64_t d = d0 + lane; d <= d1; d += 64) {
-        const int64_t q0 = (int64_t)(d << 2) - (int64_t)o;  // package index of dword's byte 0
-        if (q0 >= (int64_t)HDR && q0 + 4 <= (int64_t)P) {
-            const uint32_t p = (uint32_t)q0 - HDR;
-            const uint32_t* s32 = reinterpret_cast<const uint32_t*>(sl + (p & ~3u));
-            const uint32_t lo = s32[0], hi = s32[1];
-            out32[d] = __builtin_amdgcn_alignbyte(hi, lo, (p & 3u) * 8 / 8);
-        } else if (q0 >= 0 && q0 + 4 <= (int64_t)P) {
-            uint32_t v = 0;
-            for (int b = 0; b < 4; b++) {
-                const uint32_t q = (uint32_t)q0 + b;
-                const uint32_t by = q < HDR ? hdr_byte(q, type, n, pl) : sl[q - HDR];
-                v |= by << (8 * b);
-            }
-            out32[d] = v;
-        } else {
-            for (int b = 0; b < 4; b++) {
-                const int64_t q = q0 + b;
-                if (q < 0 || q >= (int64_t)P) continue;
-                const uint32_t qq = (uint32_t)q;
-                A.out[(d << 2) + b] = (uint8_t)(qq < HDR ? hdr_byte(qq, type, n, pl) : sl[qq - HDR]);
+    uint32_t* __restrict__ out32 = reinterpret_cast<uint32_t*>(A.out);
+    const uint32_t sh = (uint32_t)((0 - o - HDR) & 3u);   // payload byte offset inside a source dword
+    // 256 dwords per step, four per lane at a 64-dword stride (every store
+    // instruction writes 256 contiguous bytes); the interior dwords' loads are
+    // all issued before their stores, the edge dwords go byte by byte
+    for (uint64_t db = d0; db <= d1; db += 256) {
+        uint32_t lo[4], hi[4];
+        bool in[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint64_t d = db + lane + 64 * j;
+            const int64_t q0 = (int64_t)(d << 2) - (int64_t)o;
+            in[j] = d <= d1 && q0 >= (int64_t)HDR && q0 + 4 <= (int64_t)P;
+            const uint32_t* s32 = reinterpret_cast<const uint32_t*>(sl) + (in[j] ? ((uint32_t)q0 - HDR) >> 2 : 0u);
+            lo[j] = in[j] ? s32[0] : 0u;
+            hi[j] = in[j] && sh ? s32[1] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint64_t d = db + lane + 64 * j;
+            if (in[j]) {
+                out32[d] = __builtin_amdgcn_alignbyte(hi[j], lo[j], sh);
+            } else if (d <= d1) {
+                const int64_t qd = (int64_t)(d << 2) - (int64_t)o;
+                if (qd >= 0 && qd + 4 <= (int64_t)P) {
+                    uint32_t v = 0;
+                    for (int b = 0; b < 4; b++) {
+                        const uint32_t q = (uint32_t)qd + b;
+                        const uint32_t by = q < HDR ? hdr_byte(q, type, n, pl) : sl[q - HDR];
+                        v |= by << (8 * b);
+                    }
+                    out32[d] = v;
+                } else {
+                    for (int b = 0; b < 4; b++) {
+                        const int64_t q = qd + b;
+                        if (q < 0 || q >= (int64_t)P) continue;
+                        const uint32_t qq = (uint32_t)q;
+                        A.out[(d << 2) + b] = (uint8_t)(qq < HDR ? hdr_byte(qq, type, n, pl) : sl[qq - HDR]);
+                    }
+                }
             }
         }
     }
+}
+
+__global__ void k_seg_base(uint64_t* base, const uint64_t* off_last, const uint64_t* size_last) {
+    if (threadIdx.x == 0) base[1] = base[0] + off_last[0] + size_last[0];
 }
 
 __global__ void k_end_chunk(uint8_t* dst) {
@@ -1085,6 +1107,11 @@ hipError_t launch_encode(const EncArgs& a, hipStream_t s) {
     if (C <= 16384) return launch_encode_t<16384>(a, s);
     if (C <= 32768) return launch_encode_t<32768>(a, s);
     return launch_encode_t<65536>(a, s);
+}
+
+hipError_t launch_seg_base(uint64_t* base, const uint64_t* off_last, const uint64_t* size_last, hipStream_t s) {
+    hipLaunchKernelGGL(k_seg_base, dim3(1), dim3(64), 0, s, base, off_last, size_last);
+    return hipGetLastError();
 }
 
 hipError_t launch_compact(const CompactArgs& a, hipStream_t s) {

@@ -82,6 +82,10 @@ struct Dev {
     Buf in, out, slots, plen, ids, sizes, off, scan_tmp, acc, ent_full, ent_tail;
     Buf body, jobs, produced, dout, scratch, seg, list, bestpre, gdseq, pending;
     uint64_t t_encode = 0, t_scan = 0, t_compact = 0;
+    uint32_t n_launch = 1;      // k_encode launches of the last compress call (pipelined segments)
+    hipStream_t cs = nullptr;   // scan + compaction of pipelined segments
+    hipEvent_t pev[8] = {};     // segment i encoded
+    Buf segbase;                // body offset of every segment (device)
     // pinned staging for large pageable copies: 2 buffers + 2 events per copy thread
     std::vector<void*> stage;
     std::vector<hipStream_t> stage_st;
@@ -99,6 +103,8 @@ struct ambc_ctx {
 // Huffman bit staging area behind the payload.  A Huffman winner of more than
 // 2812 bytes stages its bits behind the payload too (k_encode's LDS staging
 // holds 2816 B), hence 2C.
+constexpr uint32_t NSEG = 4;   // pipelined compress segments (<= 8 = Dev::pev)
+
 static uint32_t slot_stride_for(uint32_t C, bool forced = false) {
     const uint32_t need = forced ? 3 * C + 1344 : 2 * C + 64;
     return (need + 15) & ~15u;
@@ -140,6 +146,8 @@ int ambc_init(const int* device_ids, int n_devices, ambc_ctx** out) {
         for (auto& ev : d.ev) HIPCHK(hipEventCreate(&ev));
         for (auto& x : d.xs) HIPCHK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
         for (auto& ev : d.xev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        HIPCHK(hipStreamCreateWithFlags(&d.cs, hipStreamNonBlocking));
+        for (auto& ev : d.pev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         ctx->devs.push_back(d);
     }
     *out = ctx.release();
@@ -153,7 +161,7 @@ void ambc_destroy(ambc_ctx* ctx) {
         (void)hipStreamSynchronize(d.stream);
         for (Buf* b : {&d.in, &d.out, &d.slots, &d.plen, &d.ids, &d.sizes, &d.off, &d.scan_tmp,
                        &d.acc, &d.ent_full, &d.ent_tail, &d.body, &d.jobs, &d.produced, &d.dout,
-                       &d.scratch, &d.seg, &d.list, &d.bestpre, &d.gdseq, &d.pending})
+                       &d.scratch, &d.seg, &d.list, &d.bestpre, &d.gdseq, &d.pending, &d.segbase})
             b->release();
         for (void* b : d.stage) (void)hipHostFree(b);
         for (auto& ev : d.stage_ev) (void)hipEventDestroy(ev);
@@ -161,6 +169,9 @@ void ambc_destroy(ambc_ctx* ctx) {
         for (auto& ev : d.ev) (void)hipEventDestroy(ev);
         for (auto& ev : d.xev) (void)hipEventDestroy(ev);
         for (auto& x : d.xs) { (void)hipStreamSynchronize(x); (void)hipStreamDestroy(x); }
+        for (auto& ev : d.pev) (void)hipEventDestroy(ev);
+        (void)hipStreamSynchronize(d.cs);
+        (void)hipStreamDestroy(d.cs);
         (void)hipStreamDestroy(d.stream);
     }
     delete ctx;
@@ -195,6 +206,58 @@ static int check_params(const ambc_params* p) {
         dict_cmax(p) > 8192)
         return fail(AMBC_E_INVAL, "the GPU Dictionary encoder takes chunks <= 8192 bytes "
                                   "(chunk_size or pref_max[2] <= 8192)");
+    return AMBC_OK;
+}
+
+// the raw remainder (reference mode), end chunk, kernel times and stats of one
+// compress call, after the packages are in the body and acc[] is on the host
+static int finish_compress(Dev& d, const ambc_params* p, uint64_t n, uint32_t M, uint32_t R, uint8_t* d_out,
+                           uint64_t body_len, const std::vector<uint64_t>& acc, const uint8_t* d_in,
+                           bool end, uint64_t* out_len, ambc_stats* st, uint64_t t0) {
+    const uint32_t C = p->chunk_size;
+    hipStream_t s = d.stream;
+    uint64_t rem = 0;
+    if (R < M) {
+        rem = n - (uint64_t)R * C;
+        uint8_t h[HDR] = {0xFF, 0xFF, 0, 0, 255, 0};
+        for (int b = 0; b < 4; b++) {
+            h[6 + b] = (uint8_t)(rem >> (8 * b));
+            h[10 + b] = (uint8_t)(rem >> (8 * b));
+            h[14 + b] = (uint8_t)(rem >> (8 * b));
+        }
+        HIPCHK(hipMemcpy(d_out + body_len, h, HDR, hipMemcpyHostToDevice));
+        HIPCHK(launch_copy(d_out + body_len + HDR, d_in + (uint64_t)R * C, rem, s));
+        body_len += HDR + rem;
+    }
+    if (end) {
+        HIPCHK(launch_end_chunk(d_out + body_len, s));
+        body_len += END_CHUNK;
+    }
+    HIPCHK(hipEventRecord(d.ev[4], s));
+    HIPCHK(hipStreamSynchronize(s));
+    TRACE("tail done");
+    float ms_enc = 0, ms_scan = 0, ms_cmp = 0, ms_all = 0;
+    HIPCHK(hipEventElapsedTime(&ms_enc, d.ev[0], d.ev[1]));
+    HIPCHK(hipEventElapsedTime(&ms_scan, d.ev[1], d.ev[2]));
+    HIPCHK(hipEventElapsedTime(&ms_cmp, d.ev[2], d.ev[3]));
+    HIPCHK(hipEventElapsedTime(&ms_all, d.ev[0], d.ev[4]));
+    d.t_encode = (uint64_t)(ms_enc * 1e6);
+    d.t_scan = (uint64_t)(ms_scan * 1e6);
+    d.t_compact = (uint64_t)(ms_cmp * 1e6);
+    *out_len = body_len;
+    if (st) {
+        std::memset(st, 0, sizeof *st);
+        for (int i = 0; i < 256; i++) st->method_usage[i] = acc[i];
+        st->method_usage[255] = 0;   // the reference counts compressed chunks only
+        st->compressed_chunks = acc[256];
+        st->total_chunks = R + (R < M ? 1 : 0);
+        st->raw_chunks = st->total_chunks - st->compressed_chunks;
+        st->payload_bytes = acc[258];
+        st->bytes_saved = acc[259];
+        st->overhead_bytes = (uint64_t)HDR * st->compressed_chunks + (end ? END_CHUNK : 0);
+        st->kernel_ns = (uint64_t)(ms_all * 1e6);
+        st->total_ns = now_ns() - t0;
+    }
     return AMBC_OK;
 }
 
@@ -256,28 +319,97 @@ static int compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_param
         ea.stamps = d.seg.as<unsigned long long>();
     }
     const bool deflate = (p->method_mask >> AMBC_M_DEFLATE) & 1;
+    uint32_t gd_cmax = 1024;                  // launch_deflate's template bucket
+    while (gd_cmax < C) gd_cmax <<= 1;
     if (deflate) {
         HIPCHK(d.bestpre.ensure((size_t)std::max<uint32_t>(M, 1) * 4));
         ea.bestpre = d.bestpre.as<uint32_t>();
-        uint32_t cmax = 1024;                 // launch_deflate's template bucket
-        while (cmax < C) cmax <<= 1;
-        HIPCHK(d.gdseq.ensure((size_t)std::max<uint32_t>(M, 1) * 2 * cmax));
+        HIPCHK(d.gdseq.ensure((size_t)std::max<uint32_t>(M, 1) * 2 * gd_cmax));
         ea.gdseq = d.gdseq.as<uint8_t>();
         HIPCHK(d.pending.ensure((size_t)std::max<uint32_t>(M, 1)));
         ea.pending = d.pending.as<uint8_t>();
     }
+    const bool dict = (p->method_mask >> AMBC_M_DICT) & 1;
+    // the kernels of one chunk range [k0, k1): every per-chunk array offset to k0
+    auto seg_args = [&](uint32_t k0, uint32_t k1) {
+        EncArgs e = ea;
+        e.in += (uint64_t)k0 * C;
+        e.n_total = std::min<uint64_t>(n - (uint64_t)k0 * C, (uint64_t)(k1 - k0) * C);
+        e.n_chunks = k1 - k0;
+        e.slots += (uint64_t)k0 * stride;
+        e.plen += k0;
+        e.ids += k0;
+        e.sizes += k0;
+        if (e.bestpre) e.bestpre += k0;
+        if (e.pending) e.pending += k0;
+        if (e.gdseq) e.gdseq += (uint64_t)k0 * 2 * gd_cmax;
+        return e;
+    };
+    auto encode_range = [&](const EncArgs& e) -> int {
+        HIPCHK(launch_encode(e, s));
+        if (dict) HIPCHK(launch_dict(e, dict_cmax(p), s));   // id 2 against k_encode's winner
+        if (deflate) {
+            HIPCHK(launch_deflate(e, s));   // id 5 after 1/2/3/4, against LZ4 (ties -> 5)
+            EncArgs ep = e;                 // RLE/Huffman payloads id 5 did not replace
+            ep.flags |= ENC_EMIT_PENDING;
+            ep.bestpre = nullptr;
+            ep.stamps = nullptr;
+            HIPCHK(launch_encode(ep, s));
+        }
+        return AMBC_OK;
+    };
+    // Native mode over many chunks runs as NSEG pipelined segments: segment
+    // i+1 encodes on the main stream while segment i is scanned and compacted
+    // on d.cs (memory-bound work under the LDS-bound encoder).  Reference mode
+    // needs every verdict before the scan (remainder-raw rule): one range.
+    const uint32_t S = (p->mode != AMBC_MODE_REFERENCE && M >= 16384 && !ea.stamps) ? NSEG : 1;
+    d.n_launch = S;
     HIPCHK(hipEventRecord(d.ev[0], s));
-    HIPCHK(launch_encode(ea, s));
-    if ((p->method_mask >> AMBC_M_DICT) & 1)
-        HIPCHK(launch_dict(ea, dict_cmax(p), s));   // id 2 against k_encode's winner
-    if (deflate) {
-        HIPCHK(launch_deflate(ea, s));   // id 5 after 1/3/4, against LZ4 (ties -> 5)
-        EncArgs ep = ea;                 // RLE/Huffman payloads id 5 did not replace
-        ep.flags |= ENC_EMIT_PENDING;
-        ep.bestpre = nullptr;
-        ep.stamps = nullptr;
-        HIPCHK(launch_encode(ep, s));
+    if (S > 1) {
+        size_t tmpb = 0;
+        HIPCHK(scan_sizes(nullptr, nullptr, M / S + 1, nullptr, &tmpb, d.cs));
+        HIPCHK(d.scan_tmp.ensure(tmpb));
+        HIPCHK(d.segbase.ensure((S + 1) * 8));
+        HIPCHK(hipMemsetAsync(d.segbase.p, 0, 8, d.cs));
+        uint64_t* sb = d.segbase.as<uint64_t>();
+        for (uint32_t i = 0; i < S; i++) {
+            const uint32_t k0 = (uint32_t)((uint64_t)M * i / S), k1 = (uint32_t)((uint64_t)M * (i + 1) / S);
+            rc = encode_range(seg_args(k0, k1));
+            if (rc) return rc;
+            if (i + 1 == S) HIPCHK(hipEventRecord(d.ev[1], s));
+            HIPCHK(hipEventRecord(d.pev[i], s));
+            HIPCHK(hipStreamWaitEvent(d.cs, d.pev[i], 0));
+            size_t tb = tmpb;
+            HIPCHK(scan_sizes(d.sizes.as<uint64_t>() + k0, d.off.as<uint64_t>() + k0, k1 - k0, d.scan_tmp.p,
+                              &tb, d.cs));
+            HIPCHK(launch_seg_base(sb + i, d.off.as<uint64_t>() + k1 - 1, d.sizes.as<uint64_t>() + k1 - 1, d.cs));
+            if (i + 1 == S) HIPCHK(hipEventRecord(d.ev[2], d.cs));
+            CompactArgs ca{};
+            ca.slots = d.slots.as<uint8_t>() + (uint64_t)k0 * stride;
+            ca.slot_stride = stride;
+            ca.plen = d.plen.as<uint32_t>() + k0;
+            ca.ids = d.ids.as<uint8_t>() + k0;
+            ca.off = d.off.as<uint64_t>() + k0;
+            ca.base = sb + i;
+            ca.n_chunks = k1 - k0;
+            ca.n_total = std::min<uint64_t>(n - (uint64_t)k0 * C, (uint64_t)(k1 - k0) * C);
+            ca.chunk_size = C;
+            ca.out = d_out;
+            HIPCHK(launch_compact(ca, d.cs));
+        }
+        HIPCHK(hipEventRecord(d.ev[3], d.cs));
+        HIPCHK(hipStreamWaitEvent(s, d.ev[3], 0));
+        HIPCHK(hipMemsetAsync(d.acc.p, 0, 260 * 8, s));
+        HIPCHK(launch_stats(d.ids.as<uint8_t>(), d.plen.as<uint32_t>(), M, n, C, d.acc.as<uint64_t>(), s));
+        uint64_t body_len = 0;
+        HIPCHK(hipMemcpyAsync(&body_len, sb + S, 8, hipMemcpyDeviceToHost, s));
+        std::vector<uint64_t> acc(260);
+        HIPCHK(hipMemcpyAsync(acc.data(), d.acc.p, 260 * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        return finish_compress(d, p, n, M, M, d_out, body_len, acc, d_in, end, out_len, st, t0);
     }
+    rc = encode_range(ea);
+    if (rc) return rc;
     HIPCHK(hipEventRecord(d.ev[1], s));
     if (ea.stamps) {
         stamps.resize((size_t)M * 8);
@@ -340,49 +472,7 @@ static int compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_param
     HIPCHK(hipMemcpyAsync(acc.data(), d.acc.p, 260 * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     TRACE("stats done body_len=%llu", (unsigned long long)body_len);
-    uint64_t rem = 0;
-    if (R < M) {
-        rem = n - (uint64_t)R * C;
-        uint8_t h[HDR] = {0xFF, 0xFF, 0, 0, 255, 0};
-        for (int b = 0; b < 4; b++) {
-            h[6 + b] = (uint8_t)(rem >> (8 * b));
-            h[10 + b] = (uint8_t)(rem >> (8 * b));
-            h[14 + b] = (uint8_t)(rem >> (8 * b));
-        }
-        HIPCHK(hipMemcpy(d_out + body_len, h, HDR, hipMemcpyHostToDevice));
-        HIPCHK(launch_copy(d_out + body_len + HDR, d_in + (uint64_t)R * C, rem, s));
-        body_len += HDR + rem;
-    }
-    if (end) {
-        HIPCHK(launch_end_chunk(d_out + body_len, s));
-        body_len += END_CHUNK;
-    }
-    HIPCHK(hipEventRecord(d.ev[4], s));
-    HIPCHK(hipStreamSynchronize(s));
-    TRACE("tail done");
-    float ms_enc = 0, ms_scan = 0, ms_cmp = 0, ms_all = 0;
-    HIPCHK(hipEventElapsedTime(&ms_enc, d.ev[0], d.ev[1]));
-    HIPCHK(hipEventElapsedTime(&ms_scan, d.ev[1], d.ev[2]));
-    HIPCHK(hipEventElapsedTime(&ms_cmp, d.ev[2], d.ev[3]));
-    HIPCHK(hipEventElapsedTime(&ms_all, d.ev[0], d.ev[4]));
-    d.t_encode = (uint64_t)(ms_enc * 1e6);
-    d.t_scan = (uint64_t)(ms_scan * 1e6);
-    d.t_compact = (uint64_t)(ms_cmp * 1e6);
-    *out_len = body_len;
-    if (st) {
-        std::memset(st, 0, sizeof *st);
-        for (int i = 0; i < 256; i++) st->method_usage[i] = acc[i];
-        st->method_usage[255] = 0;   // the reference counts compressed chunks only
-        st->compressed_chunks = acc[256];
-        st->total_chunks = R + (R < M ? 1 : 0);
-        st->raw_chunks = st->total_chunks - st->compressed_chunks;
-        st->payload_bytes = acc[258];
-        st->bytes_saved = acc[259];
-        st->overhead_bytes = (uint64_t)HDR * st->compressed_chunks + (end ? END_CHUNK : 0);
-        st->kernel_ns = (uint64_t)(ms_all * 1e6);
-        st->total_ns = now_ns() - t0;
-    }
-    return AMBC_OK;
+    return finish_compress(d, p, n, M, R, d_out, body_len, acc, d_in, end, out_len, st, t0);
 }
 
 extern "C" int ambc_compress_device(ambc_ctx* ctx, int dev, const void* d_in, uint64_t n,
@@ -1457,6 +1547,12 @@ extern "C" int ambc_synth_device(ambc_ctx* ctx, int dev, void* d_out, uint64_t n
     HIPCHK(hipMemcpyAsync(d.seg.p, seg.data(), seg.size() * 8, hipMemcpyHostToDevice, d.stream));
     HIPCHK(launch_synth((uint8_t*)d_out, n, d.seg.as<uint64_t>(), ns, seed, d.stream));
     HIPCHK(hipStreamSynchronize(d.stream));
+    return AMBC_OK;
+}
+
+extern "C" int ambc_last_encode_launches(ambc_ctx* ctx, int dev, uint32_t* n_launch) {
+    if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || !n_launch) return fail(AMBC_E_INVAL, "bad ctx/dev");
+    *n_launch = ctx->devs[dev].n_launch;
     return AMBC_OK;
 }
 

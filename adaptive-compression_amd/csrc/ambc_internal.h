@@ -43,6 +43,7 @@ struct CompactArgs {
     const uint32_t* plen;
     const uint8_t* ids;
     const uint64_t* off;     // exclusive scan of sizes (n_chunks+1)
+    const uint64_t* base;    // optional: body offset added to off[] (pipelined segments)
     uint32_t n_chunks;       // packages to write
     uint64_t n_total;
     uint32_t chunk_size;
@@ -89,6 +90,8 @@ hipError_t launch_deflate(const EncArgs& a, hipStream_t s);   // ambc_deflate.hi
 hipError_t launch_dict(const EncArgs& a, uint32_t cmax, hipStream_t s);   // ambc_dict.hip
 hipError_t launch_compact(const CompactArgs& a, hipStream_t s);
 hipError_t launch_end_chunk(uint8_t* dst, hipStream_t s);
+// base[1] = base[0] + off_last[0] + size_last[0] (a pipelined segment's end offset)
+hipError_t launch_seg_base(uint64_t* base, const uint64_t* off_last, const uint64_t* size_last, hipStream_t s);
 hipError_t launch_stats(const uint8_t* ids, const uint32_t* plen, uint32_t n_chunks,
                         uint64_t n_total, uint32_t chunk_size, uint64_t* acc, hipStream_t s);
 hipError_t scan_sizes(const uint64_t* sizes, uint64_t* off, uint32_t count, void* tmp,

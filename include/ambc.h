@@ -175,11 +175,15 @@ int ambc_synchronize(ambc_ctx* ctx, int dev);
 void ambc_synth_fill(uint8_t* out, uint64_t n, uint64_t seed);
 int ambc_synth_device(ambc_ctx* ctx, int dev, void* d_out, uint64_t n, uint64_t seed);
 
-/* bench instrumentation: average device time (ns) of the dominant kernel
- * (k_encode) over the last compress call, measured with HIP events on the
- * stream it was launched on. */
+/* bench instrumentation: device time (ns) of the last compress call's encode
+ * launches (k_encode and, when enabled, k_dict / k_deflate), measured with HIP
+ * events on the stream they were launched on, and of the scan / compaction the
+ * encode did not hide.  A native-mode call over >= 16384 chunks runs as
+ * n_launch pipelined segments (segment i+1 encodes while segment i is
+ * compacted on a second stream): encode_ns spans all of them. */
 int ambc_last_kernel_times(ambc_ctx* ctx, int dev, uint64_t* encode_ns, uint64_t* scan_ns,
                            uint64_t* compact_ns);
+int ambc_last_encode_launches(ambc_ctx* ctx, int dev, uint32_t* n_launch);
 
 #ifdef __cplusplus
 }

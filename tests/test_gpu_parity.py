@@ -186,6 +186,28 @@ def test_decisions_match_oracle(ctx, n, seed, chunk):
         assert bool(su[k] & 4) == orc.should_use(2, ch), k
 
 
+@pytest.mark.parametrize("n,chunk,methods", [((16 << 20) + 5, 1024, (1, 3, 4, 9)),
+                                              ((8 << 20) + 777, 512, (1, 2, 3, 4, 5))])
+def test_pipelined_segments_match_oracle(ctx, n, chunk, methods):
+    """>= 16384 chunks in native mode run as pipelined segments (encode of
+    segment i+1 overlapping the scan + compaction of segment i on a second
+    stream, every segment's body offset chained on the device): the body is
+    still byte-identical to the oracle, incl. the ragged tail, Dictionary and
+    DEFLATE's extra launches per segment."""
+    from ambc import _lib
+    data = synth.generate(n, 99)
+    comp = _compressor(chunk_size=chunk, methods=methods)
+    body = comp._adaptive_compress(data)
+    nl = C.c_uint32()
+    _lib.check(ctx.lib.ambc_last_encode_launches(ctx.h, 0, C.byref(nl)), ctx.lib)
+    assert nl.value == 4
+    ref, st = orc.compress_body(data, orc.make_params(chunk, "native", methods, n_total=n,
+                                                      deflate="gd" if 5 in methods else "zlib"))
+    assert body == ref
+    assert comp.chunk_stats["compressed_chunks"] == st.compressed_chunks
+    assert comp._adaptive_decompress(body, n) == data
+
+
 @pytest.mark.parametrize("n,seed,chunk", CASES)
 @pytest.mark.parametrize("mode", ["native", "reference"])
 def test_bodies_match_oracle(ctx, n, seed, chunk, mode):
