@@ -3,8 +3,9 @@
 Native-mode chunks are independent, so a node shards the input into
 contiguous, chunk-aligned ranges: rank r compresses chunks
 [M*r/W, M*(r+1)/W) on its own GPU with no data-path collective, producing its
-packages without the end chunk.  The one real exchange is the reassembly of
-the .ambc body in file order:
+packages without the end chunk.  ``file_offsets`` (an all_gather of the 8-byte
+body sizes) places every rank's packages in the file-order body; the one bulk
+exchange, only when one rank must hold the whole body, is ``reassemble``:
 
   1. all_gather of the per-rank body sizes (8 bytes each) -> file offsets;
   2. point-to-point gather of every rank's body straight into its offset of
@@ -63,6 +64,23 @@ def hip_compress_fn(params, ctx=None, dev=0):
                                                 None), ctx.lib)
         return out[:olen.value], st
     return fn
+
+
+def file_offsets(nbytes, device, group=None):
+    """The body's layout across ranks: all_gather of the per-rank body sizes
+    (8 bytes each) -> (this rank's byte offset in the file-order body, total).
+    With it every rank's packages are addressable in place (a parallel writer
+    puts rank r's bytes at its offset); only ``reassemble`` moves them."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    size = torch.tensor([int(nbytes)], dtype=torch.int64, device=device)
+    sizes = [torch.zeros(1, dtype=torch.int64, device=device) for _ in range(world)]
+    dist.all_gather(sizes, size, group=group)
+    sizes = [int(x.item()) for x in sizes]
+    return sum(sizes[:rank]), sum(sizes)
 
 
 def gather_concat(t, dst=0, group=None, out=None, extra=0):

