@@ -121,7 +121,9 @@ def main():
     print(f"oracle body {len(body)} B in {t_cpu:.1f} s, usage {usage}", file=sys.stderr, flush=True)
     comp = AdaptiveCompressor(chunk_size=args.chunk, methods=(1, 3, 4, 9))
     best = None
+    out = None
     for _ in range(args.reps):
+        out = None                      # free the previous output outside the timed call
         t = time.perf_counter()
         out = comp._adaptive_decompress(body, n)
         dt = time.perf_counter() - t
