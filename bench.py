@@ -205,6 +205,17 @@ def alt_leg(lib, ctx, d_in, n, args, methods, steps):
                        "header_walk_ms": round(ds.walk_ns / 1e6, 3), "host_api_GBps": round(n / dwall / 1e9, 3)}}
 
 
+def percentile(xs, q):
+    """Linear-interpolated percentile of a small sample (rank 0's own step times)."""
+    v = sorted(xs)
+    if not v:
+        return 0.0
+    k = (len(v) - 1) * q / 100.0
+    lo = int(k)
+    hi = min(lo + 1, len(v) - 1)
+    return v[lo] + (v[hi] - v[lo]) * (k - lo)
+
+
 def pmc_traffic(workload):
     """HBM bytes per k_encode launch from a committed rocprofv3 --pmc summary
     (scripts/pmc_summary.py), if one exists for this workload."""
@@ -286,8 +297,11 @@ def main():
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    step_s = []
     for _ in range(args.steps):
-        step()
+        ts = time.perf_counter()
+        step()                      # the library call returns after its stream has drained
+        step_s.append(time.perf_counter() - ts)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -379,6 +393,8 @@ def main():
                        "parallelism": f"chunk-shard dp{world}" if world > 1 else "single GPU",
                        "round_trip_bit_exact": verified, "decode": decode,
                        "reassembly_to_rank0": reasm,
+                       "step_ms_p50": round(percentile(step_s, 50) * 1e3, 3),
+                       "step_ms_p90": round(percentile(step_s, 90) * 1e3, 3),
                        "e2e_pinned_host": e2e, "api_file": api, "alt_method_set": alt},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
