@@ -1218,14 +1218,25 @@ static int decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t or
     hipStream_t s = d.stream;
     HIPCHK(d.body.ensure(blen + 64));
     uint64_t t = now_ns();
+    // a large body goes up on its own thread (pinned staging, 16 copy threads)
+    // while this thread walks the headers: the walk only reads the host body
+    struct Upload {
+        std::thread th;
+        int rc = AMBC_OK;
+        uint64_t ns = 0;
+        void join() { if (th.joinable()) th.join(); }
+        ~Upload() { join(); }
+    } up;
     if (blen >= kStageMin) {
-        int rc = copy_staged(d, d.body.p, body, blen, true);
-        if (rc) return rc;
+        up.th = std::thread([&d, &up, body, blen] {
+            const uint64_t t1 = now_ns();
+            up.rc = copy_staged(d, d.body.p, body, blen, true);
+            up.ns = now_ns() - t1;
+        });
     } else if (blen) {
         HIPCHK(hipMemcpyAsync(d.body.p, body, blen, hipMemcpyHostToDevice, s));
     }
-    HIPCHK(hipStreamSynchronize(s));
-    const uint64_t h2d = now_ns() - t;
+    uint64_t h2d = 0;
     std::map<uint32_t, uint64_t> known;
     Walk w;
     std::vector<ambc_host_chunk> hostinf;   // id-5 packages the GPU handed back
@@ -1235,6 +1246,13 @@ static int decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t or
         t = now_ns();
         walk_body(body, blen, orig_size, reg, known, w);
         walk_ns += now_ns() - t;
+        if (iter == 0) {
+            t = now_ns();
+            up.join();
+            if (up.rc) return fail(AMBC_E_DEVICE, "staged body upload failed");
+            HIPCHK(hipStreamSynchronize(s));
+            h2d = std::max(up.ns, now_ns() - t);   // the upload's own time (overlapped with the walk)
+        }
         if (w.marker_error) return fail(AMBC_E_MARKER, "Marker mismatch in chunk header.");
         const uint32_t nj = (uint32_t)w.jobs.size();
         const uint64_t cap = std::max(w.total, orig_size) + 64;

@@ -80,7 +80,7 @@ def main():
             ms = min(ts)
             r = {"input": name, "methods": list(mset), "encode_ms": round(ms, 3),
                  "GBps": round(n / ms / 1e6, 1), "ratio": round(olen.value / n, 4),
-                 "usage": {k: int(st.method_usage[k]) for k in (1, 3, 5, 9) if st.method_usage[k]}}
+                 "usage": {k: int(st.method_usage[k]) for k in (1, 2, 3, 5, 9) if st.method_usage[k]}}
             res.append(r)
             print(json.dumps(r), flush=True)
     if args.out:
