@@ -20,7 +20,8 @@
 //      a repeat iff an earlier entry of its bucket holds the same 3 bytes;
 //   3. the greedy parse, serial over tokens: for p, the bucket's entries in
 //      the window are a contiguous ascending run (the window start advances
-//      monotonically per bucket, wp[]); 64 candidates per step compare 32
+//      monotonically per bucket, wp[], for chunks beyond the 4096-byte
+//      window); 64 candidates per step compare 32
 //      bytes as dwords (v_alignbyte), and a wave max over (len << 16 | ~i)
 //      keeps the longest, earliest one.  Oldest-first order lets a step stop
 //      as soon as a candidate reaches the lookahead cap (runs, repeats).
@@ -48,11 +49,17 @@ constexpr uint32_t DLOOK = 32;      // :187 lookahead_size
 
 template <int CMAX>
 struct DictSmem {
+    // token staging must hold a winning payload (< n bytes)
+    static constexpr int CUR_BYTES = CMAX > 2 * (int)DNB ? CMAX : 2 * (int)DNB;
     alignas(16) uint8_t ch[CMAX + 64];   // the chunk, zero padded
     alignas(16) uint16_t lst[CMAX];      // 3-gram positions by bucket, ascending inside one
     alignas(16) uint16_t bst[DNB + 8];   // bucket starts (bst[DNB] = entries)
-    alignas(16) uint16_t wp[DNB];        // window start per bucket | sort: 128 lane masks
-    alignas(16) uint32_t cur[DNB];       // counts -> cursors | parse: token staging
+    alignas(16) unsigned long long bk[128];   // sort: lane masks per 7-bit bucket
+    // counts (u16 pairs, 32-bit atomics) -> cursors (u16) | parse: token staging
+    alignas(16) uint32_t cur[CUR_BYTES / 4];
+    // window start per bucket: only chunks longer than the 4096-byte window need it
+    alignas(16) uint16_t wp[CMAX > (int)DWIN ? DNB : 8];
+    __device__ __forceinline__ uint16_t* cur16() { return reinterpret_cast<uint16_t*>(cur); }
 };
 
 __device__ __forceinline__ uint32_t h3(uint32_t v) { return ((v & 0xFFFFFFu) * 2654435761u) >> 21; }
@@ -68,23 +75,34 @@ __device__ __forceinline__ uint32_t gram_at(const DictSmem<CMAX>& S, uint32_t i)
 // stable counting sort of positions [0, m) by h3 into lst[]/bst[]
 template <int CMAX>
 __device__ void build_buckets(DictSmem<CMAX>& S, uint32_t m, uint32_t lane) {
-    for (uint32_t b = lane; b < DNB; b += 64) S.cur[b] = 0;
-    unsigned long long* bk = reinterpret_cast<unsigned long long*>(S.wp);   // 128 x 64-bit
+    for (uint32_t b = lane; b < DNB / 2; b += 64) S.cur[b] = 0;
+    unsigned long long* bk = S.bk;
     for (uint32_t b = lane; b < 128; b += 64) bk[b] = 0;
     wave_sync();
-    for (uint32_t i = lane; i < m; i += 64) atomicAdd(&S.cur[h3(gram_at(S, i))], 1u);
+    // counts < 2^16: two buckets per dword
+    for (uint32_t i = lane; i < m; i += 64) {
+        const uint32_t h = h3(gram_at(S, i));
+        atomicAdd(&S.cur[h >> 1], 1u << (16 * (h & 1)));
+    }
     wave_sync();
     // exclusive scan: 32 buckets per lane
+    uint16_t* cur = S.cur16();
     {
-        uint32_t c[32], t = 0;
+        uint32_t c[16], t = 0;
 #pragma unroll
-        for (int j = 0; j < 32; j++) { c[j] = S.cur[lane * 32 + j]; t += c[j]; }
+        for (int j = 0; j < 16; j++) {
+            c[j] = S.cur[lane * 16 + j];
+            t += (c[j] & 0xFFFFu) + (c[j] >> 16);
+        }
         uint32_t run = wave_incl_sum(t) - t;
+        wave_sync();
 #pragma unroll
-        for (int j = 0; j < 32; j++) {
-            S.bst[lane * 32 + j] = (uint16_t)run;
-            S.cur[lane * 32 + j] = run;
-            run += c[j];
+        for (int j = 0; j < 16; j++) {
+            const uint32_t r0 = run, r1 = run + (c[j] & 0xFFFFu);
+            S.bst[lane * 32 + 2 * j] = (uint16_t)r0;
+            S.bst[lane * 32 + 2 * j + 1] = (uint16_t)r1;
+            S.cur[lane * 16 + j] = r0 | r1 << 16;
+            run = r1 + (c[j] >> 16);
         }
         if (lane == 63) S.bst[DNB] = (uint16_t)run;
     }
@@ -103,12 +121,12 @@ __device__ void build_buckets(DictSmem<CMAX>& S, uint32_t m, uint32_t lane) {
             const uint64_t mb = __ballot(v && ((h >> b) & 1u));
             peers &= ((h >> b) & 1u) ? mb : ~mb;
         }
-        const uint32_t base = v ? S.cur[h] : 0u;
+        const uint32_t base = v ? cur[h] : 0u;
         wave_sync();
         if (v) {
             bk[h & 127u] = 0ull;
             S.lst[base + __popcll(peers & ((1ull << lane) - 1ull))] = (uint16_t)i;
-            if ((peers >> lane) == 1ull) S.cur[h] = base + (uint32_t)__popcll(peers);
+            if ((peers >> lane) == 1ull) cur[h] = (uint16_t)(base + (uint32_t)__popcll(peers));
         }
         wave_sync();
     }
@@ -163,6 +181,21 @@ __global__ __launch_bounds__(64) void k_dict(EncArgs A) {
     if (!force && n >= 100) {
         const uint32_t ss = min(1000u, n);
         const uint32_t lim = min(n - 3, ss);
+        // distinct 13-bit hashes <= distinct 3-grams: when they already reach
+        // 0.8 ss, should_use is False without the exact count (random data)
+        uint32_t* bits = reinterpret_cast<uint32_t*>(S.bk);    // 8192 bits
+        for (uint32_t w = lane; w < 256; w += 64) bits[w] = 0;
+        wave_sync();
+        for (uint32_t i = lane; i < lim; i += 64) {
+            const uint32_t h = (gram_at(S, i) * 2654435761u) >> 19;
+            atomicOr(&bits[h >> 5], 1u << (h & 31));
+        }
+        wave_sync();
+        uint32_t dh = 0;
+        for (uint32_t w = lane; w < 256; w += 64) dh += __popc(bits[w]);
+        dh = wave_sum_u32(dh);
+        wave_sync();
+        if (5 * dh >= 4 * ss) goto su_done;
         build_buckets(S, lim, lane);
         uint32_t rep = 0;
         for (uint32_t i = lane; i < lim; i += 64) {
@@ -178,13 +211,15 @@ __global__ __launch_bounds__(64) void k_dict(EncArgs A) {
         su = 5 * u < 4 * ss;   // u / ss < 0.8 exactly (the quotient is never within an ulp of 0.8)
         wave_sync();
     }
+su_done:
     if (analyze && A.su && lane == 0) A.su[k] |= su ? 4 : 0;
     if (!want || (!force && !su)) return;
 
     // ---- the greedy parse (compression_methods.py:208-233, :279-313) ----
     const uint32_t m = n >= 3 ? n - 2 : 0;
     build_buckets(S, m, lane);
-    for (uint32_t b = lane; b < DNB; b += 64) S.wp[b] = S.bst[b];
+    if (CMAX > (int)DWIN && n > DWIN + 1)
+        for (uint32_t b = lane; b < DNB; b += 64) S.wp[b] = S.bst[b];
     wave_sync();
     uint8_t* slot = A.slots + (uint64_t)k * A.slot_stride;
     uint16_t* stg16 = force ? reinterpret_cast<uint16_t*>(slot) : reinterpret_cast<uint16_t*>(S.cur);
@@ -201,9 +236,9 @@ __global__ __launch_bounds__(64) void k_dict(EncArgs A) {
         uint32_t key = 0;
         if (look >= 3) {
             const uint32_t h = __builtin_amdgcn_readfirstlane(h3(gram_at(S, p)));
-            uint32_t j = __builtin_amdgcn_readfirstlane(S.wp[h]);
+            uint32_t j = __builtin_amdgcn_readfirstlane(CMAX > (int)DWIN && n > DWIN + 1 ? S.wp[h] : S.bst[h]);
             const uint32_t e = __builtin_amdgcn_readfirstlane(S.bst[h + 1]);
-            if (p > DWIN) {
+            if (CMAX > (int)DWIN && p > DWIN) {
                 // window start: skip the bucket's entries below p - 4096 (ascending run)
                 const uint32_t ws = p - DWIN;
                 uint32_t j0 = j;
