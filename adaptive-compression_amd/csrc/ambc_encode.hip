@@ -32,11 +32,12 @@ namespace ambc {
 template <int CMAX>
 struct EncSmem {
     // work = union, by lifetime.  Selection: hist | code | clen | Huffman tree
-    // (parent/pbit) | first occurrences (first/order).  LZ4: last[] hash table +
-    // 128 bucket masks.  Emit: RLE pair starts | Huffman bit staging behind
-    // hist/code/clen.  9.3 KB per workgroup at C = 4096 -> 17 workgroups per CU
-    // (13.4 KB / 12 at 8192, 21.6 KB / 7 at 16384).
-    static constexpr int WORK = 5120;   // every chunk size; larger Huffman payloads stage in the slot
+    // (parent/pbit), whose space the first occurrences (first/order) reuse once
+    // the tree is built.  LZ4: last[] hash table + 64 bucket masks.  Emit: RLE
+    // pair starts | Huffman bit staging behind hist/code/clen.  8.8 KB per
+    // workgroup at C = 4096 -> 18 workgroups per CU (12.9 KB / 12 at 8192,
+    // 21 KB / 7 at 16384).
+    static constexpr int WORK = 4608;   // every chunk size; larger Huffman payloads stage in the slot
     static constexpr int STAGE_OFF = 2304;                  // Huffman bit staging
     static constexpr int STAGE = WORK - STAGE_OFF;
     alignas(16) uint8_t chunk[CMAX + 64];      // zero padded
@@ -47,8 +48,8 @@ struct EncSmem {
     __device__ __forceinline__ uint8_t* clen() { return wb() + 2048; }
     __device__ __forceinline__ uint16_t* parent() { return reinterpret_cast<uint16_t*>(wb() + 2304); }
     __device__ __forceinline__ uint8_t* pbit() { return wb() + 3328; }
-    __device__ __forceinline__ uint32_t* first() { return reinterpret_cast<uint32_t*>(wb() + 3840); }
-    __device__ __forceinline__ uint8_t* order() { return wb() + 4864; }
+    __device__ __forceinline__ uint32_t* first() { return reinterpret_cast<uint32_t*>(wb() + 2304); }
+    __device__ __forceinline__ uint8_t* order() { return wb() + 3328; }
     __device__ __forceinline__ uint16_t* last() { return reinterpret_cast<uint16_t*>(work); }
     __device__ __forceinline__ uint64_t* bk() { return reinterpret_cast<uint64_t*>(wb() + 4096); }
     __device__ __forceinline__ uint32_t* stage() { return reinterpret_cast<uint32_t*>(wb() + STAGE_OFF); }
@@ -486,7 +487,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         uint16_t* last = S.last();
         uint64_t* bk = S.bk();
         for (uint32_t i = lane; i < (1u << LZ4_HASH_BITS); i += 64) last[i] = 0xFFFF;
-        for (uint32_t i = lane; i < 128; i += 64) bk[i] = 0;
+        bk[lane] = 0;
         wave_sync();
         // LZ4 wins iff block < budget; forced (single-method) encodes fall back to a
         // stored block once the compressed block would reach n (LZ4F rule)
@@ -516,17 +517,17 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
             if (__ballot(h != h0) == 0ull) {
                 peers = actm;
             } else {
-                atomicOr(reinterpret_cast<unsigned long long*>(&bk[h & 127u]), act ? 1ull << lane : 0ull);
+                atomicOr(reinterpret_cast<unsigned long long*>(&bk[h & 63u]), act ? 1ull << lane : 0ull);
                 wave_sync();
-                peers = bk[h & 127u] & actm;
+                peers = bk[h & 63u] & actm;
 #pragma unroll
-                for (int b = 7; b < (int)LZ4_HASH_BITS; b++) {
+                for (int b = 6; b < (int)LZ4_HASH_BITS; b++) {
                     const uint64_t m = __ballot((h >> b) & 1u);
                     const uint64_t flip = 0ull - (uint64_t)((h >> b) & 1u);
                     peers &= ~(m ^ flip);
                 }
                 wave_sync();
-                bk[h & 127u] = 0ull;
+                bk[h & 63u] = 0ull;
             }
             const uint64_t lower = peers & ((1ull << lane) - 1ull);
             const int cand = lower ? base + 63 - (int)__clzll((long long)lower)
