@@ -118,8 +118,8 @@ __device__ __forceinline__ void put_bits_plain(uint32_t* words, uint32_t b, uint
 
 template <int CMAX>
 struct GdSmem {
-    // parse: last[] (4 KB) + bucket masks (2 KB); trees: 5 KB; emit: bit staging
-    static constexpr int REGION = (CMAX > 6144 ? CMAX : 6144) + 64;
+    // parse: last[] (4 KB) + 64 bucket masks (512 B); trees: 5 KB; emit: bit staging
+    static constexpr int REGION = (CMAX > 5120 ? CMAX : 5120) + 64;
     static constexpr int ROUNDS = (CMAX + 63) / 64;
     alignas(16) uint8_t chunk[CMAX + 64];  // zero padded
     // parse: last[] (u16 x 2048) | trees: sorted/weights/parents | emit: bit staging
@@ -455,7 +455,7 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     } else {
     uint16_t* last = reinterpret_cast<uint16_t*>(S.region);
     for (uint32_t i = lane; i < 2048; i += 64) last[i] = 0xFFFF;
-    for (uint32_t i = lane; i < 256; i += 64) bk[i] = 0;
+    bk[lane] = 0;
     wave_sync();
     const int hl = (int)n - 4;  // last hashable position
     uint32_t p = 0;
@@ -483,17 +483,17 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
         if (__ballot(h != h0) == 0ull) {
             peers = actm;
         } else {
-            atomicOr(&bk[h & 255], act ? 1ull << lane : 0ull);
+            atomicOr(&bk[h & 63], act ? 1ull << lane : 0ull);
             wave_sync();
-            peers = bk[h & 255] & actm;
+            peers = bk[h & 63] & actm;
 #pragma unroll
-            for (int b = 8; b < 11; b++) {
+            for (int b = 6; b < 11; b++) {
                 const uint64_t m = __ballot((h >> b) & 1u);
                 const uint64_t flip = 0ull - (uint64_t)((h >> b) & 1u);
                 peers &= ~(m ^ flip);
             }
             wave_sync();
-            bk[h & 255] = 0;
+            bk[h & 63] = 0;
         }
         const uint64_t lower = peers & ((1ull << lane) - 1ull);
         const int cand = lower ? base + 63 - (int)__clzll((long long)lower)
