@@ -49,17 +49,16 @@ constexpr uint32_t DLOOK = 32;      // :187 lookahead_size
 
 template <int CMAX>
 struct DictSmem {
-    // token staging must hold a winning payload (< n bytes)
-    static constexpr int CUR_BYTES = CMAX > 2 * (int)DNB ? CMAX : 2 * (int)DNB;
     alignas(16) uint8_t ch[CMAX + 64];   // the chunk, zero padded
     alignas(16) uint16_t lst[CMAX];      // 3-gram positions by bucket, ascending inside one
-    alignas(16) uint16_t bst[DNB + 8];   // bucket starts (bst[DNB] = entries)
+    // counts (u16 pairs, 32-bit atomics) -> bucket starts (the scatter's cursors)
+    // -> bucket ends: after the scatter bucket h is lst[h ? bend[h-1] : 0, bend[h])
+    alignas(16) uint32_t bend32[DNB / 2];
     alignas(16) unsigned long long bk[128];   // sort: lane masks per 7-bit bucket
-    // counts (u16 pairs, 32-bit atomics) -> cursors (u16) | parse: token staging
-    alignas(16) uint32_t cur[CUR_BYTES / 4];
     // window start per bucket: only chunks longer than the 4096-byte window need it
     alignas(16) uint16_t wp[CMAX > (int)DWIN ? DNB : 8];
-    __device__ __forceinline__ uint16_t* cur16() { return reinterpret_cast<uint16_t*>(cur); }
+    __device__ __forceinline__ uint16_t* bend() { return reinterpret_cast<uint16_t*>(bend32); }
+    __device__ __forceinline__ uint32_t bstart(uint32_t h) { return h ? bend()[h - 1] : 0u; }
 };
 
 __device__ __forceinline__ uint32_t h3(uint32_t v) { return ((v & 0xFFFFFFu) * 2654435761u) >> 21; }
@@ -72,26 +71,25 @@ __device__ __forceinline__ uint32_t gram_at(const DictSmem<CMAX>& S, uint32_t i)
     return __builtin_amdgcn_alignbyte(hi, lo, i & 3) & 0xFFFFFFu;
 }
 
-// stable counting sort of positions [0, m) by h3 into lst[]/bst[]
+// stable counting sort of positions [0, m) by h3 into lst[] (bucket ends in bend[])
 template <int CMAX>
 __device__ void build_buckets(DictSmem<CMAX>& S, uint32_t m, uint32_t lane) {
-    for (uint32_t b = lane; b < DNB / 2; b += 64) S.cur[b] = 0;
+    for (uint32_t b = lane; b < DNB / 2; b += 64) S.bend32[b] = 0;
     unsigned long long* bk = S.bk;
     for (uint32_t b = lane; b < 128; b += 64) bk[b] = 0;
     wave_sync();
     // counts < 2^16: two buckets per dword
     for (uint32_t i = lane; i < m; i += 64) {
         const uint32_t h = h3(gram_at(S, i));
-        atomicAdd(&S.cur[h >> 1], 1u << (16 * (h & 1)));
+        atomicAdd(&S.bend32[h >> 1], 1u << (16 * (h & 1)));
     }
     wave_sync();
-    // exclusive scan: 32 buckets per lane
-    uint16_t* cur = S.cur16();
+    // exclusive scan in place (32 buckets per lane): bucket starts = cursors
     {
         uint32_t c[16], t = 0;
 #pragma unroll
         for (int j = 0; j < 16; j++) {
-            c[j] = S.cur[lane * 16 + j];
+            c[j] = S.bend32[lane * 16 + j];
             t += (c[j] & 0xFFFFu) + (c[j] >> 16);
         }
         uint32_t run = wave_incl_sum(t) - t;
@@ -99,15 +97,14 @@ __device__ void build_buckets(DictSmem<CMAX>& S, uint32_t m, uint32_t lane) {
 #pragma unroll
         for (int j = 0; j < 16; j++) {
             const uint32_t r0 = run, r1 = run + (c[j] & 0xFFFFu);
-            S.bst[lane * 32 + 2 * j] = (uint16_t)r0;
-            S.bst[lane * 32 + 2 * j + 1] = (uint16_t)r1;
-            S.cur[lane * 16 + j] = r0 | r1 << 16;
+            S.bend32[lane * 16 + j] = r0 | r1 << 16;
             run = r1 + (c[j] >> 16);
         }
-        if (lane == 63) S.bst[DNB] = (uint16_t)run;
     }
     wave_sync();
-    // scatter, 64 ascending positions per step; equal-hash lanes keep lane order
+    uint16_t* cur = S.bend();
+    // scatter, 64 ascending positions per step; equal-hash lanes keep lane order;
+    // each cursor ends at its bucket's end
 #pragma unroll 1
     for (uint32_t g = 0; g < m; g += 64) {
         const uint32_t i = g + lane;
@@ -201,7 +198,7 @@ __global__ __launch_bounds__(64) void k_dict(EncArgs A) {
         for (uint32_t i = lane; i < lim; i += 64) {
             const uint32_t g = gram_at(S, i);
             const uint32_t h = h3(g);
-            for (uint32_t j = S.bst[h];; j++) {
+            for (uint32_t j = S.bstart(h);; j++) {
                 const uint32_t q = S.lst[j];
                 if (q >= i) break;
                 if (gram_at(S, q) == g) { rep++; break; }
@@ -219,10 +216,14 @@ su_done:
     const uint32_t m = n >= 3 ? n - 2 : 0;
     build_buckets(S, m, lane);
     if (CMAX > (int)DWIN && n > DWIN + 1)
-        for (uint32_t b = lane; b < DNB; b += 64) S.wp[b] = S.bst[b];
+        for (uint32_t b = lane; b < DNB; b += 64) S.wp[b] = (uint16_t)S.bstart(b);
     wave_sync();
     uint8_t* slot = A.slots + (uint64_t)k * A.slot_stride;
-    uint16_t* stg16 = force ? reinterpret_cast<uint16_t*>(slot) : reinterpret_cast<uint16_t*>(S.cur);
+    // tokens: a forced encode writes the slot; otherwise they stage in the
+    // slot's upper half (C bytes >= any winning payload) and move down only if
+    // id 2 wins, so k_encode's payload stays intact
+    uint8_t* stage = force ? slot : slot + A.chunk_size + 64;
+    uint16_t* stg16 = reinterpret_cast<uint16_t*>(stage);
     const uint32_t* c32 = reinterpret_cast<const uint32_t*>(S.ch);
     uint32_t p = 0, o = 0;
     bool lost = false;
@@ -236,8 +237,8 @@ su_done:
         uint32_t key = 0;
         if (look >= 3) {
             const uint32_t h = __builtin_amdgcn_readfirstlane(h3(gram_at(S, p)));
-            uint32_t j = __builtin_amdgcn_readfirstlane(CMAX > (int)DWIN && n > DWIN + 1 ? S.wp[h] : S.bst[h]);
-            const uint32_t e = __builtin_amdgcn_readfirstlane(S.bst[h + 1]);
+            uint32_t j = __builtin_amdgcn_readfirstlane(CMAX > (int)DWIN && n > DWIN + 1 ? S.wp[h] : S.bstart(h));
+            const uint32_t e = __builtin_amdgcn_readfirstlane(S.bend()[h]);
             if (CMAX > (int)DWIN && p > DWIN) {
                 // window start: skip the bucket's entries below p - 4096 (ascending run)
                 const uint32_t ws = p - DWIN;
@@ -312,10 +313,12 @@ su_done:
     if (!force && (lost || (int)o > lim2)) return;
     wave_sync();
     if (!force) {
-        // id 2 wins: its tokens replace k_encode's payload
+        // id 2 wins: its tokens replace k_encode's payload (lane 0's stores made
+        // visible to the whole wave first)
+        __threadfence();
         const uint32_t nw = (o + 3) >> 2;
-        for (uint32_t q = lane; q < nw; q += 64)
-            reinterpret_cast<uint32_t*>(slot)[q] = S.cur[q];
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(stage);
+        for (uint32_t q = lane; q < nw; q += 64) reinterpret_cast<uint32_t*>(slot)[q] = src[q];
     }
     if (lane == 0) {
         A.ids[k] = 2;
