@@ -80,10 +80,19 @@ def cpu_baseline(args, threads):
     t = time.time()
     body, _ = orc.compress_body(data, p, nthreads=threads)
     dt = time.time() - t
+    # the reference is single-threaded by construction: the same port on one core
+    n1 = min(probe, n)
+    p1 = orc.make_params(args.chunk, "native", [int(x) for x in args.methods.split(",")],
+                         n_total=n1)
+    t = time.time()
+    orc.compress_body(data[:n1], p1, nthreads=1)
+    dt1 = time.time() - t
     return {"value": round(n / dt / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
             "sample": f"first {n} bytes (seed {args.seed}) of the same stream, chunk "
                       f"{args.chunk}, oracle/ambc_oracle.c OpenMP restatement, "
-                      f"{dt:.1f} s wall, ratio {len(body) / n:.4f}"}
+                      f"{dt:.1f} s wall, ratio {len(body) / n:.4f}",
+            "single_core": {"value": round(n1 / dt1 / 1e9, 4), "unit": "GB/s", "cores": 1,
+                            "sample": f"first {n1} bytes, same port, one thread, {dt1:.1f} s"}}
 
 
 def e2e_leg(lib, ctx, d_in, d_out, body_len, n, p, reps=3):
