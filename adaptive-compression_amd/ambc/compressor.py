@@ -68,6 +68,8 @@ class AdaptiveCompressor:
     # the reference's default list (adaptive_compressor.py:61-62): set
     # CHUNK_SIZE_CANDIDATES to it for the reference's multi-size walk
     REFERENCE_CHUNK_SIZE_CANDIDATES = list(REFERENCE_CHUNK_SIZE_CANDIDATES)
+    # multi-size walk: encode runs of same-size chunks ahead of the walk in one call
+    MULTISIZE_LOOKAHEAD = True
 
     def __init__(self, marker_max_length=32, sample_size=10000, *, chunk_size=None,
                  mode="native", methods=None, devices=None):
@@ -156,20 +158,23 @@ class AdaptiveCompressor:
     def _ctx(self):
         return _lib.default_context(self.devices)
 
-    def _encode_one(self, ctx, chunk, ids):
-        """One chunk of len(chunk) bytes through ambc_compress_batch: the package
-        of the reference's per-size method loop (adaptive_compressor.py:559-579 +
-        _process_chunk :631-700), or None when no method beats raw."""
-        s = len(chunk)
+    def _encode_run(self, ctx, run, s, ids):
+        """len(run) // s consecutive s-byte chunks through ONE ambc_compress_batch
+        call: for each, the package of the reference's per-size method loop
+        (adaptive_compressor.py:559-579 + _process_chunk :631-700), or None when
+        no method beats raw.  len(run) is s or a multiple of it."""
         elig = [i for i in ids if self.method_chunk_prefs.get(i, (1, 999999999))[0] <= s
                 <= self.method_chunk_prefs.get(i, (1, 999999999))[1]]
+        k = len(run) // s
         if not elig:
-            return None
+            return [None] * k
         if s > _lib.MAX_CHUNK or (5 in elig and s > 16384) or (2 in elig and s > 8192):
             raise NotImplementedError(
                 f"a {s}-byte candidate chunk with methods {elig}: the GPU encoders take chunks "
                 f"up to {_lib.MAX_CHUNK} bytes (DEFLATE up to 16384, Dictionary up to 8192)")
         C_ = (s + 15) & ~15
+        if k > 1 and C_ != s:
+            raise ValueError("runs of several chunks need a 16-byte multiple size")
         p = _lib.Params()
         p.chunk_size = C_
         p.mode = _lib.MODE_NATIVE
@@ -183,14 +188,27 @@ class AdaptiveCompressor:
             p.ent_full = tab.ctypes.data
         else:
             p.ent_tail = tab.ctypes.data
-        cap = ctx.lib.ambc_compress_bound(s, C_)
+        n = len(run)
+        cap = ctx.lib.ambc_compress_bound(n, C_)
         out = bytearray(cap)
         olen = C.c_uint64()
-        src = bytes(chunk)                  # held for the call: addr() does not own it
-        _lib.check(ctx.lib.ambc_compress_batch(ctx.h, _lib.addr(src), s, C.byref(p),
+        src = bytes(run)                    # held for the call: addr() does not own it
+        _lib.check(ctx.lib.ambc_compress_batch(ctx.h, _lib.addr(src), n, C.byref(p),
                                                _lib.addr(out), cap, C.byref(olen), None), ctx.lib)
-        pkg = bytes(memoryview(out)[:olen.value])
-        return None if pkg[4] == 255 else pkg
+        body = memoryview(out)[:olen.value]
+        pkgs, off = [], 0
+        for _ in range(k):                  # 18-B package header: payload length at [14:18]
+            end = off + 18 + struct.unpack_from("<I", body, off + 14)[0]
+            pkg = bytes(body[off:end])
+            pkgs.append(None if pkg[4] == 255 else pkg)
+            off = end
+        if off != len(body):
+            raise RuntimeError("ambc_compress_batch: package walk does not end at the body end")
+        return pkgs
+
+    def _encode_one(self, ctx, chunk, ids):
+        """One chunk of len(chunk) bytes: its package, or None (see _encode_run)."""
+        return self._encode_run(ctx, chunk, len(chunk), ids)[0]
 
     def _adaptive_compress_multisize(self, file_data):
         """_adaptive_compress (adaptive_compressor.py:363-394) with several
@@ -207,6 +225,7 @@ class AdaptiveCompressor:
         usage = {m.type_id: 0 for m in self.compression_methods}
         total = comp = raw = saved = payload = overhead = 0
         out = bytearray()
+        ahead = {}                             # (pos, size) -> package of a look-ahead run
         pos = 0
         while pos < n:
             remain = n - pos
@@ -217,13 +236,27 @@ class AdaptiveCompressor:
                 if s <= 0:
                     break
                 if s not in tried:
-                    tried[s] = self._encode_one(ctx, mv[pos:pos + s], ids)
+                    if self.MULTISIZE_LOOKAHEAD and s == cand and (pos, s) not in ahead and s % 16 == 0:
+                        # look ahead: encode a run of s-byte chunks from pos in one
+                        # call (>= 1 MiB: a launch is latency-bound, so the extra
+                        # chunks cost little); any later position of the walk on
+                        # this run's grid takes its package from the run
+                        k = max(1, min(max(4, (1 << 20) // s), remain // s))
+                        for j, pk in enumerate(self._encode_run(ctx, mv[pos:pos + k * s], s, ids)):
+                            ahead[(pos + j * s, s)] = pk
+                    if s == cand and (pos, s) in ahead:
+                        tried[s] = ahead.pop((pos, s))
+                    else:
+                        tried[s] = self._encode_one(ctx, mv[pos:pos + s], ids)
                 pkg = tried[s]
                 if pkg is not None:
                     ratio = len(pkg) / s          # (len(cdata) + overhead) / len(chunk)
                     if ratio < best_ratio:
                         best_ratio, best_s, best_pkg = ratio, s, pkg
             total += 1
+            if total % 64 == 0 and ahead:         # runs' packages the walk has passed
+                for key in [key for key in ahead if key[0] <= pos]:
+                    del ahead[key]
             if best_pkg is None:                  # (remain, 255): the rest, raw
                 if remain > 0xFFFFFFFF:
                     raise struct.error("argument out of range")
