@@ -26,6 +26,7 @@ chunk and the sizes compare by their fp64 ratio (``_adaptive_compress_multisize`
 """
 import ctypes as C
 import hashlib
+import math
 import os
 import struct
 import threading
@@ -226,6 +227,8 @@ class AdaptiveCompressor:
         total = comp = raw = saved = payload = overhead = 0
         out = bytearray()
         ahead = {}                             # (pos, size) -> package of a look-ahead run
+        g = math.gcd(*cands)
+        arr = np.frombuffer(mv, dtype=np.uint8) if n else None
         pos = 0
         while pos < n:
             remain = n - pos
@@ -237,13 +240,16 @@ class AdaptiveCompressor:
                     break
                 if s not in tried:
                     if self.MULTISIZE_LOOKAHEAD and s == cand and (pos, s) not in ahead and s % 16 == 0:
-                        # look ahead: encode a run of s-byte chunks from pos in one
-                        # call (>= 1 MiB: a launch is latency-bound, so the extra
-                        # chunks cost little); any later position of the walk on
-                        # this run's grid takes its package from the run
-                        k = max(1, min(max(4, (1 << 20) // s), remain // s))
-                        for j, pk in enumerate(self._encode_run(ctx, mv[pos:pos + k * s], s, ids)):
-                            ahead[(pos + j * s, s)] = pk
+                        # look ahead: the s-byte chunks at the next J positions the
+                        # walk can reach (pos + j*g, g = gcd of the sizes), copied
+                        # side by side into one ~4 MiB run and encoded in one call
+                        # (a launch is latency-bound: the extra chunks cost little)
+                        J = max(1, min((4 << 20) // s, (remain - s) // g + 1))
+                        run = np.lib.stride_tricks.as_strided(
+                            arr[pos:], shape=(J, s), strides=(g, 1), writeable=False)
+                        run = np.ascontiguousarray(run).reshape(-1)
+                        for j, pk in enumerate(self._encode_run(ctx, run, s, ids)):
+                            ahead[(pos + j * g, s)] = pk
                     if s == cand and (pos, s) in ahead:
                         tried[s] = ahead.pop((pos, s))
                     else:
