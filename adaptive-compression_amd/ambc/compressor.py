@@ -71,6 +71,7 @@ class AdaptiveCompressor:
     REFERENCE_CHUNK_SIZE_CANDIDATES = list(REFERENCE_CHUNK_SIZE_CANDIDATES)
     # multi-size walk: encode runs of same-size chunks ahead of the walk in one call
     MULTISIZE_LOOKAHEAD = True
+    MULTISIZE_RUN_BYTES = 16 << 20
 
     def __init__(self, marker_max_length=32, sample_size=10000, *, chunk_size=None,
                  mode="native", methods=None, devices=None):
@@ -242,9 +243,9 @@ class AdaptiveCompressor:
                     if self.MULTISIZE_LOOKAHEAD and s == cand and (pos, s) not in ahead and s % 16 == 0:
                         # look ahead: the s-byte chunks at the next J positions the
                         # walk can reach (pos + j*g, g = gcd of the sizes), copied
-                        # side by side into one ~4 MiB run and encoded in one call
+                        # side by side into one MULTISIZE_RUN_BYTES run and encoded in one call
                         # (a launch is latency-bound: the extra chunks cost little)
-                        J = max(1, min((4 << 20) // s, (remain - s) // g + 1))
+                        J = max(1, min(self.MULTISIZE_RUN_BYTES // s, (remain - s) // g + 1))
                         run = np.lib.stride_tricks.as_strided(
                             arr[pos:], shape=(J, s), strides=(g, 1), writeable=False)
                         run = np.ascontiguousarray(run).reshape(-1)

@@ -29,17 +29,19 @@ def mixed(n, seed):
 mib = float(sys.argv[1]) if len(sys.argv) > 1 else 4
 data = mixed(int(mib * (1 << 20)), 7)
 res = {}
-for la in (True, False):
+for la, rb in ((True, 16 << 20), (True, 4 << 20), (True, 64 << 20), (True, 16 << 20), (False, 0)):
     comp = ambc.AdaptiveCompressor(methods=(1, 3, 4, 9))
     comp.CHUNK_SIZE_CANDIDATES = list(comp.REFERENCE_CHUNK_SIZE_CANDIDATES)
     comp.MULTISIZE_LOOKAHEAD = la
-    comp._adaptive_compress(data[:1 << 16])            # warm
+    if rb:
+        comp.MULTISIZE_RUN_BYTES = rb
+    comp._adaptive_compress(data[:4 << 20])            # warm
     t = time.perf_counter()
     body = comp._adaptive_compress(data)
     dt = time.perf_counter() - t
-    res[la] = body
-    print(f"lookahead={la} {len(data)/2**20:.1f} MiB {dt*1e3:.1f} ms "
+    res[(la, rb)] = body
+    print(f"lookahead={la} run={rb >> 20} MiB {len(data)/2**20:.1f} MiB {dt*1e3:.1f} ms "
           f"{len(data)/dt/1e6:.2f} MB/s ratio {len(body)/len(data):.4f} "
           f"chunks {comp.chunk_stats['total_chunks']}", flush=True)
-assert res[True] == res[False], "look-ahead changed the body"
+assert len(set(res.values())) == 1, "look-ahead changed the body"
 print("bodies equal")
