@@ -22,6 +22,10 @@ AMBC_E_MARKER = -5
 AMBC_E_CAPACITY = -6
 AMBC_E_HOSTCODEC = -7
 AMBC_E_CODEC = -8
+AMBC_E_COMM = -9
+
+OP_SUM, OP_MIN, OP_MAX = 0, 1, 2
+COMM_ID_BYTES = 128
 
 MODE_NATIVE = 0
 MODE_REFERENCE = 1
@@ -35,7 +39,11 @@ EXPORTS = (
     "ambc_host_free", "ambc_device_alloc", "ambc_device_free", "ambc_memcpy_h2d",
     "ambc_memcpy_d2h", "ambc_synchronize", "ambc_synth_fill", "ambc_synth_device",
     "ambc_last_kernel_times", "ambc_split_body", "ambc_decompress_device",
-    "ambc_last_encode_launches",
+    "ambc_last_encode_launches", "ambc_memcpy_d2d", "ambc_memset_device",
+    "ambc_comm_unique_id", "ambc_comm_init_rank", "ambc_comm_size", "ambc_comm_barrier",
+    "ambc_comm_allreduce_u64", "ambc_comm_allgather_u64", "ambc_comm_gather", "ambc_shard_range",
+    "ambc_compress_shard", "ambc_decompress_shard", "ambc_decompress_multi",
+    "ambc_synth_device_range", "ambc_device_equal",
 )
 
 
@@ -69,6 +77,11 @@ class Stats(C.Structure):
 class HostChunk(C.Structure):
     _fields_ = [("body_off", C.c_uint64), ("out_off", C.c_uint64), ("clen", C.c_uint32),
                 ("orig", C.c_uint32), ("type", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+class ShardInfo(C.Structure):
+    _fields_ = [("local_len", C.c_uint64), ("offset", C.c_uint64), ("total", C.c_uint64),
+                ("shard_begin", C.c_uint64), ("shard_end", C.c_uint64)]
 
 
 _lib = None
@@ -106,6 +119,23 @@ def _declare(lib):
         "ambc_last_encode_launches": ([vp, i32, C.POINTER(C.c_uint32)], i32),
         "ambc_split_body": ([u8p, u64, u64, C.POINTER(u64), u32, C.POINTER(u64), C.POINTER(u64)], i32),
         "ambc_decompress_device": ([vp, i32, u8p, u64, u64, C.POINTER(u64), vp, C.POINTER(Stats)], i32),
+        "ambc_memcpy_d2d": ([vp, i32, vp, vp, u64], i32),
+        "ambc_memset_device": ([vp, i32, vp, i32, u64], i32),
+        "ambc_comm_unique_id": ([vp], i32),
+        "ambc_comm_init_rank": ([vp, i32, i32, vp], i32),
+        "ambc_comm_size": ([vp, C.POINTER(i32), C.POINTER(i32)], i32),
+        "ambc_comm_barrier": ([vp], i32),
+        "ambc_comm_allreduce_u64": ([vp, C.POINTER(u64), u32, i32], i32),
+        "ambc_comm_allgather_u64": ([vp, C.POINTER(u64), u32, C.POINTER(u64)], i32),
+        "ambc_comm_gather": ([vp, vp, u64, vp, u64, C.POINTER(u64), C.POINTER(u64)], i32),
+        "ambc_shard_range": ([u64, u32, i32, i32, C.POINTER(u64), C.POINTER(u64)], i32),
+        "ambc_compress_shard": ([vp, vp, u64, C.POINTER(Params), vp, u64, i32, C.POINTER(ShardInfo),
+                                 C.POINTER(Stats)], i32),
+        "ambc_decompress_shard": ([vp, u8p, u64, u64, C.POINTER(u64), vp, u64, i32,
+                                   C.POINTER(ShardInfo), C.POINTER(Stats)], i32),
+        "ambc_decompress_multi": ([vp, u8p, u64, u64, C.POINTER(u64), u8p, C.POINTER(Stats)], i32),
+        "ambc_synth_device_range": ([vp, i32, vp, u64, u64, u64, u64], i32),
+        "ambc_device_equal": ([vp, i32, vp, vp, u64, C.POINTER(i32)], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -199,6 +229,51 @@ class Context:
 
     def __exit__(self, *a):
         self.close()
+
+
+class DeviceBuffer:
+    """nbytes of device memory on one device of a Context (ambc_device_alloc):
+    the Python layer's HBM buffers, no PyTorch."""
+
+    def __init__(self, ctx, nbytes, dev=0):
+        self.ctx, self.dev, self.nbytes = ctx, dev, int(nbytes)
+        p = ctx.lib.ambc_device_alloc(ctx.h, dev, max(self.nbytes, 1))
+        if not p:
+            raise MemoryError(f"ambc_device_alloc({self.nbytes}) failed: {last_error(ctx.lib)}")
+        self.ptr = p
+
+    def __int__(self):
+        return self.ptr
+
+    def free(self):
+        if getattr(self, "ptr", None) and self.ctx.h:
+            self.ctx.lib.ambc_device_free(self.ctx.h, self.dev, self.ptr)
+        self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:  # noqa: BLE001 -- interpreter shutdown
+            pass
+
+    def upload(self, data, offset=0):
+        n = len(memoryview(data).cast("B"))
+        if offset + n > self.nbytes:
+            raise ValueError("upload past the end of the device buffer")
+        if n:
+            check(self.ctx.lib.ambc_memcpy_h2d(self.ctx.h, self.dev, self.ptr + offset, addr(data), n),
+                  self.ctx.lib)
+
+    def download(self, n=None, offset=0, out=None):
+        """n bytes from offset into a new bytearray (or the writable buffer out)."""
+        n = self.nbytes - offset if n is None else int(n)
+        if offset + n > self.nbytes:
+            raise ValueError("download past the end of the device buffer")
+        buf = bytearray(n) if out is None else out
+        if n:
+            check(self.ctx.lib.ambc_memcpy_d2h(self.ctx.h, self.dev, addr(buf), self.ptr + offset, n),
+                  self.ctx.lib)
+        return buf
 
 
 _ctx = None

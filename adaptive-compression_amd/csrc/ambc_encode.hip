@@ -1046,27 +1046,31 @@ __constant__ uint8_t c_vlen[16] = {5, 4, 5, 5, 3, 5, 5, 3, 5, 4, 4, 3, 4, 5, 6, 
 
 // seg: [pos, len, idx] triples.  ASCII segments: words are laid out by a
 // block-wide scan over 256-word batches.
-__global__ __launch_bounds__(256) void k_synth(uint8_t* out, const uint64_t* seg, uint64_t seed) {
+// bytes [lo, hi) of the stream land at out[0, hi - lo): a rank generates its
+// own shard of a stream that spans several GPUs
+__global__ __launch_bounds__(256) void k_synth(uint8_t* out, const uint64_t* seg, uint64_t seed, uint64_t lo,
+                                               uint64_t hi) {
     const uint64_t pos = seg[3 * blockIdx.x], L = seg[3 * blockIdx.x + 1], id = seg[3 * blockIdx.x + 2];
     const uint64_t base = mix64(seed ^ (id * 0xD1B54A32D192ED03ULL));
     const uint32_t typ = (uint32_t)(id % 3);
-    uint8_t* o = out + pos;
+    const uint64_t a = lo > pos ? lo - pos : 0;           // segment bytes [a, b) are in range
+    const uint64_t b = hi - pos < L ? hi - pos : L;
+    uint8_t* o = out + pos - lo;                          // o[i] for i in [a, b) only
     const uint32_t t = threadIdx.x;
     if (typ == 0) {
-        for (uint64_t i = t; i < L; i += 256) o[i] = 0;
+        for (uint64_t i = a + t; i < b; i += 256) o[i] = 0;
     } else if (typ == 1) {
-        for (uint64_t j = t; j * 8 < L; j += 256) {
+        for (uint64_t j = a / 8 + t; j * 8 < b; j += 256) {
             const uint64_t w = mix64(base + (j + 1) * 0x9E3779B97F4A7C15ULL);
-            if (j * 8 + 8 <= L) {
-                for (int b = 0; b < 8; b++) o[j * 8 + b] = (uint8_t)(w >> (8 * b));
-            } else {
-                for (int b = 0; j * 8 + b < L; b++) o[j * 8 + b] = (uint8_t)(w >> (8 * b));
+            for (int k = 0; k < 8; k++) {
+                const uint64_t i = j * 8 + k;
+                if (i >= a && i < b) o[i] = (uint8_t)(w >> (8 * k));
             }
         }
     } else {
         __shared__ uint32_t scan[256];
         uint64_t q = 0;  // bytes laid out so far (uniform)
-        for (uint64_t jb = 0; q < L; jb += 256) {
+        for (uint64_t jb = 0; q < b; jb += 256) {
             const uint64_t j = jb + t;
             const uint32_t w = (uint32_t)(mix64(base + (j + 1) * 0x9E3779B97F4A7C15ULL) >> 60);
             const uint32_t wl = c_vlen[w] + 1;
@@ -1079,14 +1083,35 @@ __global__ __launch_bounds__(256) void k_synth(uint8_t* out, const uint64_t* seg
                 __syncthreads();
             }
             const uint64_t st = q + scan[t] - wl;
-            for (uint32_t b = 0; b < wl; b++) {
-                const uint64_t p = st + b;
-                if (p < L) o[p] = b + 1 < wl ? (uint8_t)c_vocab[w][b] : (uint8_t)' ';
+            if (st + wl > a) {
+                for (uint32_t k = 0; k < wl; k++) {
+                    const uint64_t p = st + k;
+                    if (p >= a && p < b) o[p] = k + 1 < wl ? (uint8_t)c_vocab[w][k] : (uint8_t)' ';
+                }
             }
             q += scan[255];
             __syncthreads();
         }
     }
+}
+
+// *neq |= (a[i] != b[i]) over n bytes (vector loads when both are 16-B aligned)
+__global__ __launch_bounds__(256) void k_equal(const uint8_t* a, const uint8_t* b, uint64_t n, uint32_t* neq) {
+    const uint64_t tid = (uint64_t)blockIdx.x * 256 + threadIdx.x, nt = (uint64_t)gridDim.x * 256;
+    uint32_t diff = 0;
+    if ((((uintptr_t)a | (uintptr_t)b) & 15) == 0) {
+        const uint4* a4 = reinterpret_cast<const uint4*>(a);
+        const uint4* b4 = reinterpret_cast<const uint4*>(b);
+        const uint64_t n16 = n / 16;
+        for (uint64_t i = tid; i < n16; i += nt) {
+            const uint4 x = a4[i], y = b4[i];
+            diff |= (x.x ^ y.x) | (x.y ^ y.y) | (x.z ^ y.z) | (x.w ^ y.w);
+        }
+        for (uint64_t i = n16 * 16 + tid; i < n; i += nt) diff |= a[i] ^ b[i];
+    } else {
+        for (uint64_t i = tid; i < n; i += nt) diff |= a[i] ^ b[i];
+    }
+    if (__any(diff != 0) && threadIdx.x % 64 == 0) atomicOr(neq, 1u);
 }
 
 // ---------------------------------------------------------------------------
@@ -1144,11 +1169,19 @@ hipError_t launch_copy(uint8_t* dst, const uint8_t* src, uint64_t len, hipStream
     return hipGetLastError();
 }
 
-hipError_t launch_synth(uint8_t* out, uint64_t n, const uint64_t* seg, uint32_t nseg,
+hipError_t launch_synth(uint8_t* out, uint64_t lo, uint64_t hi, const uint64_t* seg, uint32_t nseg,
                         uint64_t seed, hipStream_t s) {
-    (void)n;
-    if (nseg == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_synth, dim3(nseg), dim3(256), 0, s, out, seg, seed);
+    if (nseg == 0 || hi <= lo) return hipSuccess;
+    hipLaunchKernelGGL(k_synth, dim3(nseg), dim3(256), 0, s, out, seg, seed, lo, hi);
+    return hipGetLastError();
+}
+
+hipError_t launch_equal(const uint8_t* a, const uint8_t* b, uint64_t n, uint32_t* neq, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    uint64_t blocks = (n / 16 + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL(k_equal, dim3((uint32_t)blocks), dim3(256), 0, s, a, b, n, neq);
     return hipGetLastError();
 }
 

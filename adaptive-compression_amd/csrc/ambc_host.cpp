@@ -22,81 +22,15 @@
 #include <zlib.h>
 
 #include "../../include/ambc.h"
+#include "ambc_hostctx.h"
 #include "ambc_internal.h"
 
 using namespace ambc;
 
-namespace {
-
+namespace ambc {
 thread_local std::string g_err;
+}  // namespace ambc
 
-int fail(int code, const std::string& msg) {
-    g_err = msg;
-    return code;
-}
-
-#define HIPCHK(expr)                                                                   \
-    do {                                                                               \
-        hipError_t _e = (expr);                                                        \
-        if (_e != hipSuccess)                                                          \
-            return fail(AMBC_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)); \
-    } while (0)
-
-bool trace_on() {
-    static int on = -1;
-    if (on < 0) on = getenv("AMBC_TRACE") ? 1 : 0;
-    return on == 1;
-}
-#define TRACE(...)                                                   \
-    do {                                                             \
-        if (trace_on()) { fprintf(stderr, "[ambc] " __VA_ARGS__); fputc('\n', stderr); fflush(stderr); } \
-    } while (0)
-
-uint64_t now_ns() {
-    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
-               std::chrono::steady_clock::now().time_since_epoch())
-        .count();
-}
-
-struct Buf {
-    void* p = nullptr;
-    size_t cap = 0;
-    hipError_t ensure(size_t bytes) {
-        if (bytes <= cap && p) return hipSuccess;
-        if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
-        size_t want = std::max<size_t>(bytes, 256);
-        hipError_t e = hipMalloc(&p, want);
-        if (e == hipSuccess) cap = want;
-        return e;
-    }
-    template <typename T> T* as() const { return reinterpret_cast<T*>(p); }
-    void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
-};
-
-struct Dev {
-    int id = 0;
-    hipStream_t stream = nullptr;
-    hipEvent_t ev[6] = {};
-    hipStream_t xs[2] = {};     // copy streams of the slab pipeline: H2D, D2H
-    hipEvent_t xev[6] = {};     // h2d_done[2], comp_done[2], d2h_done[2]
-    Buf in, out, slots, plen, ids, sizes, off, scan_tmp, acc, ent_full, ent_tail;
-    Buf body, jobs, produced, dout, scratch, seg, list, bestpre, gdseq, pending;
-    uint64_t t_encode = 0, t_scan = 0, t_compact = 0;
-    uint32_t n_launch = 1;      // k_encode launches of the last compress call (pipelined segments)
-    hipStream_t cs = nullptr;   // scan + compaction of pipelined segments
-    hipEvent_t pev[8] = {};     // segment i encoded
-    Buf segbase;                // body offset of every segment (device)
-    // pinned staging for large pageable copies: 2 buffers + 2 events per copy thread
-    std::vector<void*> stage;
-    std::vector<hipStream_t> stage_st;
-    std::vector<hipEvent_t> stage_ev;
-};
-
-}  // namespace
-
-struct ambc_ctx {
-    std::vector<Dev> devs;
-};
 
 // a chunk's scratch slot: winners are < n bytes; forced single-method encodes
 // (ambc_encode_method) can reach 2n (RLE) or ~1.13n + 1284 (Huffman), plus the
@@ -105,7 +39,7 @@ struct ambc_ctx {
 // holds 2816 B), hence 2C.
 constexpr uint32_t NSEG = 4;   // pipelined compress segments (<= 8 = Dev::pev)
 
-static uint32_t slot_stride_for(uint32_t C, bool forced = false) {
+uint32_t ambc::slot_stride_for(uint32_t C, bool forced) {
     const uint32_t need = forced ? 3 * C + 1344 : 2 * C + 64;
     return (need + 15) & ~15u;
 }
@@ -156,12 +90,14 @@ int ambc_init(const int* device_ids, int n_devices, ambc_ctx** out) {
 
 void ambc_destroy(ambc_ctx* ctx) {
     if (!ctx) return;
+    if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+    for (ncclComm_t c : ctx->dev_comms) if (c) (void)ncclCommDestroy(c);
     for (auto& d : ctx->devs) {
         (void)hipSetDevice(d.id);
         (void)hipStreamSynchronize(d.stream);
         for (Buf* b : {&d.in, &d.out, &d.slots, &d.plen, &d.ids, &d.sizes, &d.off, &d.scan_tmp,
                        &d.acc, &d.ent_full, &d.ent_tail, &d.body, &d.jobs, &d.produced, &d.dout,
-                       &d.scratch, &d.seg, &d.list, &d.bestpre, &d.gdseq, &d.pending, &d.segbase})
+                       &d.scratch, &d.seg, &d.list, &d.bestpre, &d.gdseq, &d.pending, &d.segbase, &d.coll})
             b->release();
         for (void* b : d.stage) (void)hipHostFree(b);
         for (auto& ev : d.stage_ev) (void)hipEventDestroy(ev);
@@ -190,7 +126,7 @@ uint64_t ambc_compress_bound(uint64_t n, uint32_t chunk) {
 // the largest chunk id 2 can be eligible for (k_dict's template bucket)
 static uint32_t dict_cmax(const ambc_params* p) { return std::min(p->chunk_size, p->pref_max[AMBC_M_DICT]); }
 
-static int check_params(const ambc_params* p) {
+int ambc::check_params(const ambc_params* p) {
     if (!p) return fail(AMBC_E_INVAL, "params is NULL");
     const uint32_t C = p->chunk_size;
     if (C < 16 || C > AMBC_MAX_CHUNK || (C & 15))
@@ -209,16 +145,26 @@ static int check_params(const ambc_params* p) {
     return AMBC_OK;
 }
 
-// the raw remainder (reference mode), end chunk, kernel times and stats of one
-// compress call, after the packages are in the body and acc[] is on the host
-static int finish_compress(Dev& d, const ambc_params* p, uint64_t n, uint32_t M, uint32_t R, uint8_t* d_out,
+// The raw remainder of reference mode (adaptive_compressor.py:586-588: the
+// first position with no winner stores the rest of the file as ONE raw chunk).
+// In a sharded call the remainder can span ranks: the rank holding its first
+// chunk writes the 18-B header with the WHOLE remainder's length and its own
+// bytes of it; every later rank contributes its shard's bytes verbatim.
+struct Remainder {
+    bool hdr = false;        // this rank writes the remainder's chunk header
+    uint64_t rem_total = 0;  // used / orig / comp_len of that header
+    uint64_t copy_off = 0;   // local input bytes [copy_off, copy_off + copy_len) follow
+    uint64_t copy_len = 0;
+};
+
+// the raw remainder, end chunk, kernel times and stats of one compress call,
+// after the R packages are in the body and acc[] is on the host
+static int finish_compress(Dev& d, const ambc_params* p, uint32_t R, const Remainder& rm, uint8_t* d_out,
                            uint64_t body_len, const std::vector<uint64_t>& acc, const uint8_t* d_in,
                            bool end, uint64_t* out_len, ambc_stats* st, uint64_t t0) {
-    const uint32_t C = p->chunk_size;
     hipStream_t s = d.stream;
-    uint64_t rem = 0;
-    if (R < M) {
-        rem = n - (uint64_t)R * C;
+    if (rm.hdr) {
+        const uint64_t rem = rm.rem_total;
         uint8_t h[HDR] = {0xFF, 0xFF, 0, 0, 255, 0};
         for (int b = 0; b < 4; b++) {
             h[6 + b] = (uint8_t)(rem >> (8 * b));
@@ -226,8 +172,11 @@ static int finish_compress(Dev& d, const ambc_params* p, uint64_t n, uint32_t M,
             h[14 + b] = (uint8_t)(rem >> (8 * b));
         }
         HIPCHK(hipMemcpy(d_out + body_len, h, HDR, hipMemcpyHostToDevice));
-        HIPCHK(launch_copy(d_out + body_len + HDR, d_in + (uint64_t)R * C, rem, s));
-        body_len += HDR + rem;
+        body_len += HDR;
+    }
+    if (rm.copy_len) {
+        HIPCHK(launch_copy(d_out + body_len, d_in + rm.copy_off, rm.copy_len, s));
+        body_len += rm.copy_len;
     }
     if (end) {
         HIPCHK(launch_end_chunk(d_out + body_len, s));
@@ -250,7 +199,7 @@ static int finish_compress(Dev& d, const ambc_params* p, uint64_t n, uint32_t M,
         for (int i = 0; i < 256; i++) st->method_usage[i] = acc[i];
         st->method_usage[255] = 0;   // the reference counts compressed chunks only
         st->compressed_chunks = acc[256];
-        st->total_chunks = R + (R < M ? 1 : 0);
+        st->total_chunks = R + (rm.hdr ? 1 : 0);
         st->raw_chunks = st->total_chunks - st->compressed_chunks;
         st->payload_bytes = acc[258];
         st->bytes_saved = acc[259];
@@ -258,11 +207,12 @@ static int finish_compress(Dev& d, const ambc_params* p, uint64_t n, uint32_t M,
         st->kernel_ns = (uint64_t)(ms_all * 1e6);
         st->total_ns = now_ns() - t0;
     }
+    (void)p;
     return AMBC_OK;
 }
 
-static int compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params* p, uint8_t* d_out,
-                       uint64_t out_cap, uint64_t* out_len, ambc_stats* st) {
+int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params* p, uint8_t* d_out,
+                      uint64_t out_cap, uint64_t* out_len, ambc_stats* st, const ShardInfo* si) {
     int rc = check_params(p);
     if (rc) return rc;
     const uint32_t C = p->chunk_size;
@@ -406,7 +356,7 @@ static int compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_param
         std::vector<uint64_t> acc(260);
         HIPCHK(hipMemcpyAsync(acc.data(), d.acc.p, 260 * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
-        return finish_compress(d, p, n, M, M, d_out, body_len, acc, d_in, end, out_len, st, t0);
+        return finish_compress(d, p, M, Remainder(), d_out, body_len, acc, d_in, end, out_len, st, t0);
     }
     rc = encode_range(ea);
     if (rc) return rc;
@@ -435,13 +385,38 @@ static int compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_param
 
     // reference mode: the first chunk with no winner swallows the remainder
     uint32_t R = M;
-    if (p->mode == AMBC_MODE_REFERENCE && M) {
+    Remainder rm;
+    if (p->mode == AMBC_MODE_REFERENCE && (M || si)) {
         std::vector<uint8_t> ids(M);
-        HIPCHK(hipMemcpyAsync(ids.data(), d.ids.p, M, hipMemcpyDeviceToHost, s));
+        if (M) HIPCHK(hipMemcpyAsync(ids.data(), d.ids.p, M, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         for (uint32_t k = 0; k < M; k++) if (ids[k] == 255) { R = k; break; }
-        if (R < M && n - (uint64_t)R * C > 0xFFFFFFFFull)
-            return fail(AMBC_E_RANGE, "raw remainder does not fit the u32 chunk fields (struct.error)");
+        uint64_t g = R < M ? R : UINT64_MAX;          // first no-winner chunk (global index)
+        uint64_t n_total = n, k0 = 0;
+        if (si) {
+            k0 = si->k0;
+            n_total = si->n_total;
+            if (g != UINT64_MAX) g += k0;
+            int rc2 = shard_allreduce_min(si->t, &g);  // AllReduce(MIN) across the ranks
+            if (rc2) return rc2;
+        }
+        if (g != UINT64_MAX) {
+            const uint64_t rem_total = n_total - g * C;
+            if (rem_total > 0xFFFFFFFFull)
+                return fail(AMBC_E_RANGE, "raw remainder does not fit the u32 chunk fields (struct.error)");
+            if (g >= k0 + M) {
+                R = M;                                  // a later rank holds the remainder's start
+            } else if (g >= k0) {
+                R = (uint32_t)(g - k0);                 // it starts in this shard
+                rm.hdr = true;
+                rm.rem_total = rem_total;
+                rm.copy_off = (uint64_t)R * C;
+                rm.copy_len = n - rm.copy_off;
+            } else {
+                R = 0;                                  // an earlier rank started it: all raw bytes
+                rm.copy_len = n;
+            }
+        }
     }
     HIPCHK(hipMemsetAsync(d.sizes.as<uint64_t>() + R, 0, 8, s));
     size_t tmpb = 0;
@@ -472,7 +447,7 @@ static int compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_param
     HIPCHK(hipMemcpyAsync(acc.data(), d.acc.p, 260 * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     TRACE("stats done body_len=%llu", (unsigned long long)body_len);
-    return finish_compress(d, p, n, M, R, d_out, body_len, acc, d_in, end, out_len, st, t0);
+    return finish_compress(d, p, R, rm, d_out, body_len, acc, d_in, end, out_len, st, t0);
 }
 
 extern "C" int ambc_compress_device(ambc_ctx* ctx, int dev, const void* d_in, uint64_t n,
@@ -566,67 +541,32 @@ extern "C" int ambc_compress_batch(ambc_ctx* ctx, const uint8_t* in, uint64_t n,
     const uint64_t t0 = now_ns();
     const uint32_t C = p->chunk_size;
     const uint64_t M = (n + C - 1) / C;
-    int G = (int)ctx->devs.size();
-    if (p->mode == AMBC_MODE_REFERENCE || M < (uint64_t)G * 4) G = 1;  // remainder rule is global
-    if (G == 1 && p->mode == AMBC_MODE_NATIVE && n > kSlabBytes)
-        return compress_slabs(ctx->devs[0], in, n, p, out, out_cap, out_len, st);
-    ambc_stats total{};
-    std::vector<uint64_t> lens(G, 0);
-    std::vector<int> rcs(G, 0);
-    std::vector<std::string> errs(G);
-    std::vector<uint64_t> h2d(G, 0), d2h(G, 0);
-    // (multi-device: run the shards concurrently, then gather in file order)
-    std::vector<ambc_stats> sst(G);
-    std::vector<std::thread> th;
-    for (int g = 0; g < G; g++) {
-        auto fn = [&, g]() {
-            Dev& d = ctx->devs[g];
-            const uint64_t k0 = M * g / G, k1 = M * (g + 1) / G;
-            const uint64_t b0 = k0 * C, b1 = std::min<uint64_t>(k1 * C, n);
-            const uint64_t sn = b1 - b0;
-            ambc_params q = *p;
-            if (g != G - 1) { q.flags |= AMBC_FLAG_NO_END_CHUNK; q.ent_tail = nullptr; }
-            const uint64_t bound = ambc_compress_bound(sn, C);
-            auto body = [&]() -> int {
-                TRACE("shard %d sn=%llu", g, (unsigned long long)sn);
-                HIPCHK(hipSetDevice(d.id));
-                HIPCHK(d.in.ensure(sn + 64));
-                HIPCHK(d.out.ensure(bound + 64));
-                uint64_t t = now_ns();
-                if (sn) HIPCHK(hipMemcpyAsync(d.in.p, in + b0, sn, hipMemcpyHostToDevice, d.stream));
-                HIPCHK(hipStreamSynchronize(d.stream));
-                h2d[g] = now_ns() - t;
-                TRACE("h2d done");
-                return compress_on(d, d.in.as<uint8_t>(), sn, &q, d.out.as<uint8_t>(), d.out.cap,
-                                   &lens[g], &sst[g]);
-            };
-            rcs[g] = body();
-            if (rcs[g]) errs[g] = g_err;
-        };
-        if (G == 1) fn();
-        else th.emplace_back(fn);
-    }
-    for (auto& t : th) t.join();
-    for (int g = 0; g < G; g++)
-        if (rcs[g]) return fail(rcs[g], errs[g]);
-    uint64_t tot = 0;
-    for (int g = 0; g < G; g++) tot += lens[g];
-    if (tot > out_cap) return fail(AMBC_E_CAPACITY, "output buffer too small for the body");
-    uint64_t o = 0;
-    for (int g = 0; g < G; g++) {
-        Dev& d = ctx->devs[g];
-        HIPCHK(hipSetDevice(d.id));
-        uint64_t t = now_ns();
-        HIPCHK(hipMemcpyAsync(out + o, d.out.p, lens[g], hipMemcpyDeviceToHost, d.stream));
-        HIPCHK(hipStreamSynchronize(d.stream));
-        d2h[g] = now_ns() - t;
-        o += lens[g];
-        add_stats(&total, sst[g]);
-    }
-    *out_len = tot;
+    // several devices in the ctx: contiguous chunk shards, one host thread per
+    // device, sizes / stats / the reference-mode remainder over RCCL (ambc_shard.cpp)
+    if (ctx->devs.size() > 1 && M >= ctx->devs.size())
+        return compress_batch_multi(ctx, in, n, p, out, out_cap, out_len, st);
+    Dev& d = ctx->devs[0];
+    if (p->mode == AMBC_MODE_NATIVE && n > kSlabBytes)
+        return compress_slabs(d, in, n, p, out, out_cap, out_len, st);
+    const uint64_t bound = ambc_compress_bound(n, C);
+    HIPCHK(hipSetDevice(d.id));
+    HIPCHK(d.in.ensure(n + 64));
+    HIPCHK(d.out.ensure(bound + 64));
+    uint64_t t = now_ns();
+    if (n) HIPCHK(hipMemcpyAsync(d.in.p, in, n, hipMemcpyHostToDevice, d.stream));
+    HIPCHK(hipStreamSynchronize(d.stream));
+    const uint64_t h2d = now_ns() - t;
+    uint64_t len = 0;
+    rc = compress_on(d, d.in.as<uint8_t>(), n, p, d.out.as<uint8_t>(), d.out.cap, &len, st);
+    if (rc) return rc;
+    if (len > out_cap) return fail(AMBC_E_CAPACITY, "output buffer too small for the body");
+    t = now_ns();
+    HIPCHK(hipMemcpyAsync(out, d.out.p, len, hipMemcpyDeviceToHost, d.stream));
+    HIPCHK(hipStreamSynchronize(d.stream));
+    *out_len = len;
     if (st) {
-        *st = total;
-        for (int g = 0; g < G; g++) { st->h2d_ns += h2d[g]; st->d2h_ns += d2h[g]; }
+        st->h2d_ns = h2d;
+        st->d2h_ns = now_ns() - t;
         st->total_ns = now_ns() - t0;
     }
     return AMBC_OK;
@@ -1210,9 +1150,9 @@ static int copy_staged(Dev& d, void* dst, const void* src, uint64_t n, bool to_d
     return AMBC_OK;
 }
 
-static int decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t orig_size,
-                         const uint64_t reg[4], uint8_t* out, std::vector<ambc_host_chunk>& host,
-                         ambc_stats* st, uint8_t* d_out_ext = nullptr) {
+int ambc::decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t orig_size,
+                        const uint64_t reg[4], uint8_t* out, std::vector<ambc_host_chunk>& host,
+                        ambc_stats* st, uint8_t* d_out_ext) {
     const uint64_t t0 = now_ns();
     HIPCHK(hipSetDevice(d.id));
     hipStream_t s = d.stream;
@@ -1374,6 +1314,12 @@ static int decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t or
     return AMBC_OK;
 }
 
+void ambc::default_registered(const uint64_t* registered, uint64_t reg[4]) {
+    reg[0] = reg[1] = reg[2] = reg[3] = 0;
+    if (registered) std::memcpy(reg, registered, 4 * sizeof(uint64_t));
+    else for (uint32_t t : {1u, 2u, 3u, 4u, 5u, 6u, 7u, 9u, 255u}) reg[t >> 6] |= 1ull << (t & 63);
+}
+
 extern "C" int ambc_decompress_ex(ambc_ctx* ctx, const uint8_t* body, uint64_t body_len,
                                   uint64_t orig_size, const uint64_t registered[4], uint8_t* out,
                                   ambc_host_chunk* host_chunks, uint32_t host_cap, uint32_t* n_host,
@@ -1496,6 +1442,19 @@ extern "C" int ambc_memcpy_d2h(ambc_ctx* ctx, int dev, void* dst, const void* sr
     HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
     return AMBC_OK;
 }
+extern "C" int ambc_memcpy_d2d(ambc_ctx* ctx, int dev, void* dst, const void* src, uint64_t bytes) {
+    if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) return fail(AMBC_E_INVAL, "bad ctx/dev");
+    HIPCHK(hipSetDevice(ctx->devs[dev].id));
+    HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToDevice));
+    return AMBC_OK;
+}
+extern "C" int ambc_memset_device(ambc_ctx* ctx, int dev, void* dst, int value, uint64_t bytes) {
+    if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) return fail(AMBC_E_INVAL, "bad ctx/dev");
+    HIPCHK(hipSetDevice(ctx->devs[dev].id));
+    HIPCHK(hipMemset(dst, value, bytes));
+    HIPCHK(hipDeviceSynchronize());
+    return AMBC_OK;
+}
 extern "C" int ambc_synchronize(ambc_ctx* ctx, int dev) {
     if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) return fail(AMBC_E_INVAL, "bad ctx/dev");
     HIPCHK(hipSetDevice(ctx->devs[dev].id));
@@ -1554,17 +1513,39 @@ extern "C" void ambc_synth_fill(uint8_t* out, uint64_t n, uint64_t seed) {
     for (auto& t : th) t.join();
 }
 
-extern "C" int ambc_synth_device(ambc_ctx* ctx, int dev, void* d_out, uint64_t n, uint64_t seed) {
+extern "C" int ambc_synth_device_range(ambc_ctx* ctx, int dev, void* d_out, uint64_t n_total, uint64_t begin,
+                                       uint64_t end, uint64_t seed) {
     if (!ctx || dev < 0 || dev >= (int)ctx->devs.size()) return fail(AMBC_E_INVAL, "bad ctx/dev");
+    if (begin > end || end > n_total) return fail(AMBC_E_INVAL, "need begin <= end <= n_total");
     Dev& d = ctx->devs[dev];
     HIPCHK(hipSetDevice(d.id));
-    std::vector<uint64_t> seg;
-    synth_segments(n, seed, seg);
-    const uint32_t ns = (uint32_t)(seg.size() / 3);
-    HIPCHK(d.seg.ensure(seg.size() * 8 + 8));
-    HIPCHK(hipMemcpyAsync(d.seg.p, seg.data(), seg.size() * 8, hipMemcpyHostToDevice, d.stream));
-    HIPCHK(launch_synth((uint8_t*)d_out, n, d.seg.as<uint64_t>(), ns, seed, d.stream));
+    std::vector<uint64_t> seg, mine;
+    synth_segments(n_total, seed, seg);
+    for (size_t g = 0; g < seg.size(); g += 3)       // the segments that meet [begin, end)
+        if (seg[g] < end && seg[g] + seg[g + 1] > begin) mine.insert(mine.end(), &seg[g], &seg[g] + 3);
+    const uint32_t ns = (uint32_t)(mine.size() / 3);
+    HIPCHK(d.seg.ensure(mine.size() * 8 + 8));
+    if (ns) HIPCHK(hipMemcpyAsync(d.seg.p, mine.data(), mine.size() * 8, hipMemcpyHostToDevice, d.stream));
+    HIPCHK(launch_synth((uint8_t*)d_out, begin, end, d.seg.as<uint64_t>(), ns, seed, d.stream));
     HIPCHK(hipStreamSynchronize(d.stream));
+    return AMBC_OK;
+}
+
+extern "C" int ambc_synth_device(ambc_ctx* ctx, int dev, void* d_out, uint64_t n, uint64_t seed) {
+    return ambc_synth_device_range(ctx, dev, d_out, n, 0, n, seed);
+}
+
+extern "C" int ambc_device_equal(ambc_ctx* ctx, int dev, const void* a, const void* b, uint64_t n, int* equal) {
+    if (!ctx || dev < 0 || dev >= (int)ctx->devs.size() || !equal) return fail(AMBC_E_INVAL, "bad argument");
+    Dev& d = ctx->devs[dev];
+    HIPCHK(hipSetDevice(d.id));
+    HIPCHK(d.coll.ensure(64));
+    HIPCHK(hipMemsetAsync(d.coll.p, 0, 4, d.stream));
+    HIPCHK(launch_equal((const uint8_t*)a, (const uint8_t*)b, n, d.coll.as<uint32_t>(), d.stream));
+    uint32_t neq = 1;
+    HIPCHK(hipMemcpyAsync(&neq, d.coll.p, 4, hipMemcpyDeviceToHost, d.stream));
+    HIPCHK(hipStreamSynchronize(d.stream));
+    *equal = neq == 0;
     return AMBC_OK;
 }
 

@@ -1,0 +1,130 @@
+// ambc_hostctx.h -- host-side state shared by ambc_host.cpp (single-device
+// compress / decompress) and ambc_shard.cpp (sharded calls over RCCL).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "../../include/ambc.h"
+#include "ambc_internal.h"
+
+namespace ambc {
+
+extern thread_local std::string g_err;
+
+inline int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                   \
+    do {                                                                               \
+        hipError_t _e = (expr);                                                        \
+        if (_e != hipSuccess)                                                          \
+            return ::ambc::fail(AMBC_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+#define NCCLCHK(expr)                                                                  \
+    do {                                                                               \
+        ncclResult_t _r = (expr);                                                      \
+        if (_r != ncclSuccess)                                                         \
+            return ::ambc::fail(AMBC_E_COMM, std::string(#expr) + ": " + ncclGetErrorString(_r)); \
+    } while (0)
+
+inline bool trace_on() {
+    static int on = -1;
+    if (on < 0) on = getenv("AMBC_TRACE") ? 1 : 0;
+    return on == 1;
+}
+#define TRACE(...)                                                   \
+    do {                                                             \
+        if (::ambc::trace_on()) { fprintf(stderr, "[ambc] " __VA_ARGS__); fputc('\n', stderr); fflush(stderr); } \
+    } while (0)
+
+inline uint64_t now_ns() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+struct Buf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap && p) return hipSuccess;
+        if (p) { (void)hipFree(p); p = nullptr; cap = 0; }
+        size_t want = std::max<size_t>(bytes, 256);
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    template <typename T> T* as() const { return reinterpret_cast<T*>(p); }
+    void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
+};
+
+struct Dev {
+    int id = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[6] = {};
+    hipStream_t xs[2] = {};     // copy streams of the slab pipeline: H2D, D2H
+    hipEvent_t xev[6] = {};     // h2d_done[2], comp_done[2], d2h_done[2]
+    Buf in, out, slots, plen, ids, sizes, off, scan_tmp, acc, ent_full, ent_tail;
+    Buf body, jobs, produced, dout, scratch, seg, list, bestpre, gdseq, pending;
+    Buf coll;                   // small device buffers of the collectives (sizes, stats, flags)
+    uint64_t t_encode = 0, t_scan = 0, t_compact = 0;
+    uint32_t n_launch = 1;      // k_encode launches of the last compress call (pipelined segments)
+    hipStream_t cs = nullptr;   // scan + compaction of pipelined segments
+    hipEvent_t pev[8] = {};     // segment i encoded
+    Buf segbase;                // body offset of every segment (device)
+    // pinned staging for large pageable copies: 2 buffers + 2 events per copy thread
+    std::vector<void*> stage;
+    std::vector<hipStream_t> stage_st;
+    std::vector<hipEvent_t> stage_ev;
+};
+
+// One shard of a sharded compress (ambc_shard.cpp): in reference mode the
+// remainder-raw rule is global, so compress_on asks the transport for the first
+// chunk without a winner on ANY rank (AllReduce MIN) before it compacts.
+struct Transport;
+struct ShardInfo {
+    Transport* t;
+    uint64_t k0;        // global index of this shard's first chunk
+    uint64_t n_total;   // bytes of the whole logical input
+};
+
+}  // namespace ambc
+
+struct ambc_ctx {
+    std::vector<ambc::Dev> devs;
+    // process-per-GPU communicator (ambc_comm_init_rank): this process is rank
+    // `rank` of `nranks`, on devs[0]
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+    // in-process multi-device communicators (ncclCommInitAll over distinct devices),
+    // created on the first sharded call
+    std::vector<ncclComm_t> dev_comms;
+};
+
+namespace ambc {
+
+uint32_t slot_stride_for(uint32_t C, bool forced = false);
+int check_params(const ambc_params* p);
+int compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params* p, uint8_t* d_out,
+                uint64_t out_cap, uint64_t* out_len, ambc_stats* st, const ShardInfo* si = nullptr);
+int decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t orig_size, const uint64_t reg[4],
+                  uint8_t* out, std::vector<ambc_host_chunk>& host, ambc_stats* st,
+                  uint8_t* d_out_ext = nullptr);
+void default_registered(const uint64_t* registered, uint64_t reg[4]);
+
+// collective of the sharded calls (ambc_shard.cpp)
+int shard_allreduce_min(Transport* t, uint64_t* v);
+int compress_batch_multi(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const ambc_params* p, uint8_t* out,
+                         uint64_t out_cap, uint64_t* out_len, ambc_stats* st);
+
+}  // namespace ambc

@@ -99,7 +99,9 @@ hipError_t scan_sizes(const uint64_t* sizes, uint64_t* off, uint32_t count, void
 hipError_t launch_copy(uint8_t* dst, const uint8_t* src, uint64_t len, hipStream_t s);
 hipError_t launch_decode(int kind, const DecArgs& a, hipStream_t s);
 hipError_t launch_inflate(int kind, const DecArgs& a, hipStream_t s);   // ambc_inflate.hip
-hipError_t launch_synth(uint8_t* out, uint64_t n, const uint64_t* seg, uint32_t nseg,
+// bytes [lo, hi) of the synthetic stream (segment table seg) into out[0, hi - lo)
+hipError_t launch_synth(uint8_t* out, uint64_t lo, uint64_t hi, const uint64_t* seg, uint32_t nseg,
                         uint64_t seed, hipStream_t s);
+hipError_t launch_equal(const uint8_t* a, const uint8_t* b, uint64_t n, uint32_t* neq, hipStream_t s);
 
 }  // namespace ambc

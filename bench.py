@@ -1,26 +1,33 @@
 #!/usr/bin/env python3
-"""Benchmark of the MI355X compress path (BASELINE.json metric).
+"""Benchmark of the MI355X compress path (BASELINE.json metric).  No PyTorch:
+device memory, synthetic input, RCCL and timing all go through libambc_hip.
 
 A step = one device-resident compress of the whole per-GPU input (configs[1]:
 4 GiB "ambc-mixed v1" synthetic mixed-entropy bytes, chunk 4096, native mode,
-GPU methods {RLE, Huffman, Delta, LZ4}) into a device-resident .ambc body;
-with N > 1 ranks every rank compresses its own 4 GiB shard (weak scaling; the
-chunks are independent, so there is no data-path collective) and the step ends
-with the all_gather of the 8-byte body sizes that gives every rank its offset in
-the file-order body (ambc.distributed.file_offsets).  Gathering the whole body
-onto rank 0 over RCCL/xGMI (ambc.distributed.reassemble) is timed separately,
-after the timed steps ("reassembly_to_rank0").  value = input bytes of all
-ranks / time (GB/s, 1e9).
+GPU methods {RLE, Huffman, Delta, LZ4}) into a device-resident .ambc body.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+With N > 1 ranks (one process per GPU) the input is ONE stream of N x 4 GiB and
+rank r compresses its contiguous chunk shard (ambc_compress_shard; weak
+scaling: the chunks are independent, so the data path has no collective); a
+step ends with the RCCL AllGather of the body sizes (every rank's file offset)
+and AllReduce(SUM) of the statistics.  Gathering the whole body onto rank 0
+over xGMI (grouped ncclSend/ncclRecv) is timed separately, after the timed
+steps ("reassembly_to_rank0").  value = input bytes of all ranks / time (GB/s).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3-1024|c3-16384|c4]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \\
         --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
+
+``--gpus N`` without a launcher starts the N rank processes itself (before any
+GPU call) and exits with the worst exit code.
 """
 import argparse
 import ctypes as C
 import glob
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -30,6 +37,12 @@ sys.path[:0] = [REPO, os.path.join(REPO, "adaptive-compression_amd")]
 METRIC = ("compress GB/s + ratio, 4 GiB synthetic mixed-entropy @ chunk=4096; "
           "decompress round-trip bit-exact")
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md)
+GiB = 1 << 30
+# BASELINE.json configs (per-GPU input, chunk): c4 = 32 GiB over 8 GPUs at chunk 8192
+CONFIGS = {"c2": (4 * GiB, 4096), "c3-1024": (4 * GiB, 1024), "c3-16384": (4 * GiB, 16384),
+           "c4": (4 * GiB, 8192)}
+LZ4_NOTE = ("id 9 bytes are this project's 'ambc-lz4 greedy v1' LZ4 frames (valid LZ4, decodable by any "
+            "LZ4 frame decoder), not python-lz4's HC-9 output, which is absent here and unpinned")
 
 
 def log(*a):
@@ -41,7 +54,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--size", type=int, default=4 << 30, help="input bytes per GPU")
+    ap.add_argument("--config", choices=sorted(CONFIGS), default=None,
+                    help="BASELINE.json config preset (sets --size and --chunk)")
+    ap.add_argument("--size", type=int, default=4 * GiB, help="input bytes per GPU")
     ap.add_argument("--chunk", type=int, default=4096)
     ap.add_argument("--mode", default="native", choices=["native", "reference"])
     ap.add_argument("--methods", default="1,3,4,9")
@@ -49,58 +64,117 @@ def parse():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--py-seconds", type=float, default=12.0,
+                    help="budget of the single-core pure-Python restatement leg")
     ap.add_argument("--no-e2e", action="store_true", help="skip the pinned host-to-host leg")
-    ap.add_argument("--alt-methods", default="1,3,4,5",
-                    help="second method set reported beside the headline ('' to skip): "
-                         "1,3,4,5 = RLE/Huffman/Delta/DEFLATE (every package decodable by the "
-                         "stdlib-only reference)")
+    ap.add_argument("--alt-methods", default="1,3,4,5;1,2,3,4",
+                    help="';'-separated method sets reported beside the headline ('' to skip): "
+                         "1,3,4,5 = every package decodable by the stdlib-only reference; "
+                         "1,2,3,4 = the reference's own bytes (byte-pinned set)")
     ap.add_argument("--api-bytes", type=int, default=256 << 20,
                     help="input size of the AdaptiveCompressor.compress(path, path) leg (0: skip)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.config:
+        a.size, a.chunk = CONFIGS[a.config]
+    return a
 
 
-def cpu_baseline(args, threads):
-    """The CPU restatement (oracle, "port") on a bounded prefix of the same
-    workload, on the host cores; the reference itself is pure Python and is
-    not present on the GPU box (BASELINE.md §2-3 has its numbers)."""
+def spawn_ranks(n):
+    """bench.py --gpus N without a launcher: N child processes, one per GPU,
+    each with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set.  This process
+    never touches the GPU."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc]
+    return bad[0] if bad else 0
+
+
+def make_params(args, methods, n):
+    from ambc import _lib
+    from ambc.compressor import entropy_terms
+    from ambc.registry import METHOD_CHUNK_PREFS, method_mask
+    p = _lib.Params()
+    p.chunk_size = args.chunk
+    p.mode = _lib.MODE_REFERENCE if args.mode == "reference" else _lib.MODE_NATIVE
+    p.method_mask = method_mask(methods)
+    for i in range(16):
+        lo, hi = METHOD_CHUNK_PREFS.get(i, (1, 0))
+        p.pref_min[i], p.pref_max[i] = lo, min(hi, 0xFFFFFFFF)
+    keep = [entropy_terms(args.chunk)]
+    p.ent_full = keep[0].ctypes.data
+    if n % args.chunk:
+        keep.append(entropy_terms(n % args.chunk))
+        p.ent_tail = keep[1].ctypes.data
+    p._keep = keep
+    return p
+
+
+def cpu_baseline(args, threads, methods):
+    """The CPU restatements of the oracle on bounded prefixes of the same
+    stream, on the host: the C/OpenMP port on the box's CPU share, and the
+    pure-Python restatement on one core.  The reference
+    itself is pure Python and cannot be on the GPU box (BASELINE.md §2 has its
+    numbers: 1.00 MB/s for {1,3,4} at chunk 4096 in the survey container)."""
     os.environ.setdefault("OMP_NUM_THREADS", str(threads))
     from oracle import oracle as orc
+    from oracle import pyref
     probe = 16 << 20
     data = orc.synth(probe, args.seed)
-    p = orc.make_params(args.chunk, "native", [int(x) for x in args.methods.split(",")],
-                        n_total=probe)
+    p = orc.make_params(args.chunk, "native", methods, n_total=probe)
     t = time.time()
     orc.compress_body(data, p, nthreads=threads)
     rate = probe / max(time.time() - t, 1e-6)
     n = int(min(args.size, max(probe, rate * args.cpu_seconds)))
     n -= n % args.chunk
     data = orc.synth(n, args.seed)
-    p = orc.make_params(args.chunk, "native", [int(x) for x in args.methods.split(",")],
-                        n_total=n)
+    p = orc.make_params(args.chunk, "native", methods, n_total=n)
     t = time.time()
     body, _ = orc.compress_body(data, p, nthreads=threads)
     dt = time.time() - t
-    # the reference is single-threaded by construction: the same port on one core
-    n1 = min(probe, n)
-    p1 = orc.make_params(args.chunk, "native", [int(x) for x in args.methods.split(",")],
-                         n_total=n1)
+    del data
+    # the reference's algorithm in CPython on one core: {1,3,4} (BASELINE.md §2's row)
+    py_set = [m for m in (1, 3, 4)]
+    pn = 1 << 20
+    pdata = orc.synth(pn, args.seed)
     t = time.time()
-    orc.compress_body(data[:n1], p1, nthreads=1)
-    dt1 = time.time() - t
+    pbody = pyref.compress_body_native(pdata, args.chunk, py_set)
+    prate = pn / max(time.time() - t, 1e-6)
+    pn2 = int(min(64 << 20, max(pn, prate * args.py_seconds)))
+    pn2 -= pn2 % args.chunk
+    if pn2 > pn:
+        pdata = orc.synth(pn2, args.seed)
+        t = time.time()
+        pbody = pyref.compress_body_native(pdata, args.chunk, py_set)
+        prate = pn2 / max(time.time() - t, 1e-6)
+    else:
+        pn2 = pn
+    same = pbody == orc.compress_body(pdata, orc.make_params(args.chunk, "native", py_set + [255],
+                                                             n_total=pn2))[0]
     return {"value": round(n / dt / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
-            "sample": f"first {n} bytes (seed {args.seed}) of the same stream, chunk "
-                      f"{args.chunk}, oracle/ambc_oracle.c OpenMP restatement, "
-                      f"{dt:.1f} s wall, ratio {len(body) / n:.4f}",
-            "single_core": {"value": round(n1 / dt1 / 1e9, 4), "unit": "GB/s", "cores": 1,
-                            "sample": f"first {n1} bytes, same port, one thread, {dt1:.1f} s"}}
+            "os_cpu_count": os.cpu_count(),
+            "cores_note": "the box's CPU share for one GPU (OMP_NUM_THREADS); os_cpu_count is the whole host",
+            "sample": f"first {n} bytes (seed {args.seed}) of the same stream, chunk {args.chunk}, methods "
+                      f"{methods}, oracle/ambc_oracle.c OpenMP restatement, {dt:.1f} s wall, "
+                      f"ratio {len(body) / n:.4f}",
+            "python_single_core": {
+                "value": round(prate / 1e9, 7), "unit": "GB/s", "cores": 1, "kind": "port",
+                "sample": f"first {pn2} bytes of the same stream, chunk {args.chunk}, methods {py_set} "
+                          f"(the reference's {{1,3,4,255}} set), oracle/pyref.py pure-Python restatement of "
+                          f"adaptive_compressor.py:537-700, body identical to the C port: {same}",
+                "extrapolated_4GiB_s": round((4 * GiB) / prate, 1)}}
 
 
-def e2e_leg(lib, ctx, d_in, d_out, body_len, n, p, reps=3):
+def e2e_leg(lib, ctx, d_in, body_len, n, p, d_out, reps=3):
     """T_e2e: page-locked host input -> page-locked host body through
     ambc_compress_batch (slab pipeline: H2D, compress and D2H overlapped).  The
     body must equal the device-resident one byte for byte."""
-    import numpy as np
-    import torch
     from ambc import _lib
     cap = lib.ambc_compress_bound(n, p.chunk_size)
     h_in = lib.ambc_host_alloc(n)
@@ -108,7 +182,7 @@ def e2e_leg(lib, ctx, d_in, d_out, body_len, n, p, reps=3):
     if not h_in or not h_out:
         return None
     try:
-        _lib.check(lib.ambc_memcpy_d2h(ctx.h, 0, h_in, d_in.data_ptr(), n), lib)
+        _lib.check(lib.ambc_memcpy_d2h(ctx.h, 0, h_in, int(d_in), n), lib)
         olen = C.c_uint64()
         st = _lib.Stats()
         u8p = C.POINTER(C.c_uint8)
@@ -120,9 +194,7 @@ def e2e_leg(lib, ctx, d_in, d_out, body_len, n, p, reps=3):
                                                C.byref(st)), lib)
             if i:
                 ts.append(time.perf_counter() - t)
-        got = np.ctypeslib.as_array((C.c_uint8 * olen.value).from_address(h_out))
-        same = olen.value == body_len and bool(
-            torch.equal(torch.from_numpy(got).to(d_out.device), d_out[:body_len]))
+        same = olen.value == body_len and device_equals_host(ctx, h_out, body_len, d_out)
         ts.sort()
         return {"GBps": round(n / ts[len(ts) // 2] / 1e9, 3), "ms": round(ts[len(ts) // 2] * 1e3, 3),
                 "reps": reps, "host_buffers": "pinned (ambc_host_alloc)", "body_equal_device": same,
@@ -132,14 +204,29 @@ def e2e_leg(lib, ctx, d_in, d_out, body_len, n, p, reps=3):
         lib.ambc_host_free(h_out)
 
 
+def device_equals_host(ctx, host, n, d_ref):
+    """host bytes (object or address) == n bytes at device pointer d_ref (uploaded, compared on the device)."""
+    from ambc import _lib
+    tmp = _lib.DeviceBuffer(ctx, n + 64)
+    try:
+        src = host if isinstance(host, int) else _lib.addr(host)
+        _lib.check(ctx.lib.ambc_memcpy_h2d(ctx.h, 0, tmp.ptr, src, n), ctx.lib)
+        eq = C.c_int(0)
+        _lib.check(ctx.lib.ambc_device_equal(ctx.h, 0, tmp.ptr, int(d_ref), n, C.byref(eq)), ctx.lib)
+        return bool(eq.value)
+    finally:
+        tmp.free()
+
+
 def api_leg(nbytes, chunk, mode, methods, seed):
     """T_api: AdaptiveCompressor.compress(path, path) wall time on a
     file of the same stream (file read, MD5, compress, file write included),
     then decompress(path, path) with its MD5 check."""
     import tempfile
     from ambc import AdaptiveCompressor
-    from oracle import synth
-    data = synth.generate(nbytes, seed)
+    from ambc import _lib
+    data = bytearray(nbytes)
+    _lib.load().ambc_synth_fill(_lib.addr(data), nbytes, seed)
     with tempfile.TemporaryDirectory(dir=os.environ.get("TMPDIR", "/tmp")) as td:
         src, dst, back = (os.path.join(td, x) for x in ("in.bin", "out.ambc", "back.bin"))
         with open(src, "wb") as f:
@@ -162,70 +249,45 @@ def api_leg(nbytes, chunk, mode, methods, seed):
 def alt_leg(lib, ctx, d_in, n, args, methods, steps):
     """The same input under another method set (device-resident, same clock
     discipline as the headline), its ratio and a bit-exact decode."""
-    import torch
     from ambc import _lib, AdaptiveCompressor
-    from ambc.compressor import entropy_terms
-    from ambc.registry import METHOD_CHUNK_PREFS, method_mask
-    p = _lib.Params()
-    p.chunk_size = args.chunk
-    p.mode = _lib.MODE_REFERENCE if args.mode == "reference" else _lib.MODE_NATIVE
-    p.method_mask = method_mask(methods)
-    for i in range(16):
-        lo, hi = METHOD_CHUNK_PREFS.get(i, (1, 0))
-        p.pref_min[i], p.pref_max[i] = lo, min(hi, 0xFFFFFFFF)
-    tabs = [entropy_terms(args.chunk)]
-    p.ent_full = tabs[0].ctypes.data
-    if n % args.chunk:
-        tabs.append(entropy_terms(n % args.chunk))
-        p.ent_tail = tabs[1].ctypes.data
+    p = make_params(args, methods, n)
     cap = lib.ambc_compress_bound(n, args.chunk)
-    d_out = torch.empty(cap + 64, dtype=torch.uint8, device=d_in.device)
+    d_out = _lib.DeviceBuffer(ctx, cap + 64)
     olen = C.c_uint64()
     st = _lib.Stats()
     enc = []
 
     def once():
-        _lib.check(lib.ambc_compress_device(ctx.h, 0, d_in.data_ptr(), n, C.byref(p), d_out.data_ptr(),
+        _lib.check(lib.ambc_compress_device(ctx.h, 0, d_in.ptr, n, C.byref(p), d_out.ptr,
                                             cap, C.byref(olen), C.byref(st), None), lib)
         e = C.c_uint64()
         lib.ambc_last_kernel_times(ctx.h, 0, C.byref(e), None, None)
         enc.append(e.value)
 
-    once()
-    enc.clear()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
+    try:
         once()
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / steps
-    body = d_out[:olen.value].cpu().numpy().tobytes()
+        enc.clear()
+        lib.ambc_synchronize(ctx.h, 0)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            once()
+        lib.ambc_synchronize(ctx.h, 0)
+        dt = (time.perf_counter() - t0) / steps
+        body = d_out.download(olen.value)
+        usage = {i: int(st.method_usage[i]) for i in range(256) if st.method_usage[i]}
+    finally:
+        d_out.free()
     comp = AdaptiveCompressor(chunk_size=args.chunk, mode=args.mode, methods=methods)
     t = time.perf_counter()
     back = comp._adaptive_decompress(body, n)
     dwall = time.perf_counter() - t
-    ok = equals_device(back, d_in)
+    ok = device_equals_host(ctx, back, n, d_in)
     ds = comp._last_device_stats
-    usage = {i: int(st.method_usage[i]) for i in range(256) if st.method_usage[i]}
     return {"methods": methods, "GBps": round(n / dt / 1e9, 3), "ms_per_step": round(dt * 1e3, 3),
             "steps": steps, "ratio": round(olen.value / n, 5), "method_usage": usage,
             "kernels_ms": round(sum(enc) / len(enc) / 1e6, 3), "round_trip_bit_exact": ok,
             "decode": {"kernel_ms": round(ds.kernel_ns / 1e6, 3), "host_zlib_ms": round(ds.host_codec_ns / 1e6, 3),
                        "header_walk_ms": round(ds.walk_ns / 1e6, 3), "host_api_GBps": round(n / dwall / 1e9, 3)}}
-
-
-def equals_device(host_bytes, d_ref):
-    """host_bytes == the device tensor d_ref, compared on the device (no 4 GiB
-    host temporaries that would fragment the memory the next decode faults in)."""
-    import warnings
-
-    import torch
-    if len(host_bytes) != d_ref.numel():
-        return False
-    with warnings.catch_warnings():
-        warnings.simplefilter("ignore")               # read-only buffer: we only read it
-        h = torch.frombuffer(host_bytes, dtype=torch.uint8)
-    return bool(torch.equal(h.to(d_ref.device), d_ref))
 
 
 def percentile(xs, q):
@@ -241,7 +303,7 @@ def percentile(xs, q):
 
 def pmc_traffic(workload):
     """HBM bytes per k_encode launch from a committed rocprofv3 --pmc summary
-    (scripts/pmc_summary.py), if one exists for this workload."""
+    (scripts/pmc_summary.py), if one exists for this workload (newest round wins)."""
     best = None
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*.json"))):
         try:
@@ -250,158 +312,154 @@ def pmc_traffic(workload):
         except (OSError, ValueError):
             continue
         if d.get("workload") == workload and d.get("hbm_bytes_per_launch"):
+            d["_file"] = f
             best = d
     return best
 
 
 def main():
     args = parse()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    import torch
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     from ambc import _lib
-    from ambc.compressor import entropy_terms
-    from ambc.registry import METHOD_CHUNK_PREFS, method_mask
-
-    ctx = _lib.Context([local])
-    lib = ctx.lib
+    from ambc.comm import GpuGroup, env_ranks
+    from ambc.distributed import gather, shard_range
+    rank, world, local = env_ranks()
+    if world != args.gpus:
+        log(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch one process per GPU "
+            f"(torch.distributed.run --nproc-per-node {args.gpus}) or run bench.py --gpus N alone")
+        sys.exit(2)
+    lib = _lib.load()
+    ndev = C.c_int(0)
+    if lib.ambc_device_count(C.byref(ndev)) != 0 or ndev.value <= local:
+        log(f"bench.py: rank {rank} needs GPU {local}, {ndev.value} visible")
+        sys.exit(3)
+    group = GpuGroup(rank, world, local)
+    ctx = group.ctx
     n = args.size
+    n_total = n * world
     methods = [int(x) for x in args.methods.split(",")]
-    p = _lib.Params()
-    p.chunk_size = args.chunk
-    p.mode = _lib.MODE_REFERENCE if args.mode == "reference" else _lib.MODE_NATIVE
-    p.method_mask = method_mask(methods)
-    for i in range(16):
-        lo, hi = METHOD_CHUNK_PREFS.get(i, (1, 0))
-        p.pref_min[i], p.pref_max[i] = lo, min(hi, 0xFFFFFFFF)
-    tabs = [entropy_terms(args.chunk)]
-    p.ent_full = tabs[0].ctypes.data
-    if n % args.chunk:
-        tabs.append(entropy_terms(n % args.chunk))
-        p.ent_tail = tabs[1].ctypes.data
-    if world > 1:
-        p.flags |= _lib.FLAG_NO_END_CHUNK
-
-    d_in = torch.empty(n, dtype=torch.uint8, device=dev)
-    _lib.check(lib.ambc_synth_device(ctx.h, 0, d_in.data_ptr(), n, args.seed + rank), lib)
-    cap = lib.ambc_compress_bound(n, args.chunk)
-    # rank 0 compresses straight into the front of the reassembly buffer
-    out_cap = cap * (world if rank == 0 and world > 1 else 1) + 64
-    d_out = torch.empty(out_cap, dtype=torch.uint8, device=dev)
+    p = make_params(args, methods, n_total if world > 1 else n)
+    b0, b1 = (0, n) if world == 1 else shard_range(n_total, args.chunk, world, rank)
+    sn = b1 - b0
+    # this rank's bytes [b0, b1) of ONE n_total-byte stream
+    d_in = _lib.DeviceBuffer(ctx, sn + 64)
+    _lib.check(lib.ambc_synth_device_range(ctx.h, 0, d_in.ptr, n_total, b0, b1, args.seed), lib)
+    cap = lib.ambc_compress_bound(sn, args.chunk)
+    d_out = _lib.DeviceBuffer(ctx, cap + 64)
     olen = C.c_uint64()
     st = _lib.Stats()
+    info = _lib.ShardInfo()
     enc_ns = []
     launches = [1]      # k_encode launches per call (pipelined segments)
 
     def step():
-        _lib.check(lib.ambc_compress_device(ctx.h, 0, d_in.data_ptr(), n, C.byref(p),
-                                            d_out.data_ptr(), cap, C.byref(olen), C.byref(st),
-                                            None), lib)
+        if world == 1:
+            _lib.check(lib.ambc_compress_device(ctx.h, 0, d_in.ptr, n, C.byref(p), d_out.ptr, cap,
+                                                C.byref(olen), C.byref(st), None), lib)
+        else:
+            _lib.check(lib.ambc_compress_shard(ctx.h, d_in.ptr, n_total, C.byref(p), d_out.ptr, cap, -1,
+                                               C.byref(info), C.byref(st)), lib)
+            olen.value = info.local_len
         e = C.c_uint64()
         lib.ambc_last_kernel_times(ctx.h, 0, C.byref(e), None, None)
         nl = C.c_uint32()
         lib.ambc_last_encode_launches(ctx.h, 0, C.byref(nl))
         enc_ns.append(e.value / max(1, nl.value))     # per k_encode launch
         launches[0] = max(1, nl.value)
-        if world > 1:
-            from ambc.distributed import file_offsets
-            file_offsets(olen.value, dev)
 
     for _ in range(args.warmup):
         step()
     enc_ns.clear()
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
+    group.barrier()
     t0 = time.perf_counter()
     step_s = []
     for _ in range(args.steps):
         ts = time.perf_counter()
         step()                      # the library call returns after its stream has drained
         step_s.append(time.perf_counter() - ts)
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
+    group.barrier()
     dt = time.perf_counter() - t0
     body_len = olen.value
+    body_total = body_len if world == 1 else info.total
     if world > 1:
-        import torch.distributed as dist
-        t = torch.tensor([dt, float(body_len)], dtype=torch.float64, device=dev)
-        tmax = t.clone()
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        tsum = t.clone()
-        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
-        dt = float(tmax[0].item())
-        body_total = float(tsum[1].item()) + 16
-    else:
-        body_total = float(body_len)
+        dt = max(x[0] for x in group.host.allgather_obj([dt]))
 
-    reasm = None
+    reasm = shard_check = None
     if world > 1:
-        # the whole body onto rank 0 in file order (P2P over xGMI), outside the timed steps
-        from ambc.distributed import reassemble
-        torch.distributed.barrier()
-        torch.cuda.synchronize()
+        # the whole body onto rank 0 in file order (grouped send/recv over xGMI), outside the timed steps
+        d_all = _lib.DeviceBuffer(ctx, (body_total if rank == 0 else 0) + 64)
+        group.barrier()
         tr = time.perf_counter()
-        reassemble(d_out[:body_len], dst=0, out=d_out if rank == 0 else None)
-        torch.cuda.synchronize()
-        tr = time.perf_counter() - tr
-        tt = torch.tensor([tr], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
-        reasm = {"ms": round(tt.item() * 1e3, 3), "body_bytes": int(body_total),
-                 "GBps_into_rank0": round(body_total / tt.item() / 1e9, 3)}
+        _, tot = gather(group, d_out.ptr, body_len, d_all.ptr if rank == 0 else None,
+                        body_total + 64 if rank == 0 else 0)
+        group.barrier()
+        tr = max(x[0] for x in group.host.allgather_obj([time.perf_counter() - tr]))
+        same = True
+        if rank == 0:       # rank 0's own packages lead the gathered body
+            eq = C.c_int(0)
+            _lib.check(lib.ambc_device_equal(ctx.h, 0, d_all.ptr, d_out.ptr, body_len, C.byref(eq)), lib)
+            same = bool(eq.value) and tot == body_total
+        d_all.free()
+        reasm = {"ms": round(tr * 1e3, 3), "body_bytes": int(body_total),
+                 "GBps_into_rank0": round(body_total / tr / 1e9, 3), "rank0_prefix_equal": same}
+        if not args.no_verify:
+            # every rank decodes its own packages (the file-order body is their concatenation)
+            from ambc import AdaptiveCompressor
+            comp = AdaptiveCompressor(chunk_size=args.chunk, mode=args.mode, methods=methods)
+            back = comp._adaptive_decompress(bytes(d_out.download(body_len)), sn)
+            ok = device_equals_host(ctx, back, sn, d_in)
+            oks = group.host.allgather_obj([1.0 if ok else 0.0])
+            shard_check = all(x[0] == 1.0 for x in oks)
 
-    verified = None
-    decode = None
-    if not args.no_verify and rank == 0:
+    verified = decode = None
+    if not args.no_verify and world == 1:
         # bit-exact round trip of the last step's body (outside the timed region)
-        body_host = d_out[:body_len if world == 1 else body_len].cpu().numpy().tobytes()
-        if world > 1:
-            body_host += b"\xff\xff" + b"\x00" * 14
+        body_host = bytes(d_out.download(body_len))
         from ambc import AdaptiveCompressor
         comp = AdaptiveCompressor(chunk_size=args.chunk, mode=args.mode, methods=methods)
         t = time.perf_counter()
         back = comp._adaptive_decompress(body_host, n)
         dcold = time.perf_counter() - t                 # first call: + pinned staging setup
-        verified = equals_device(back, d_in)
+        verified = device_equals_host(ctx, back, n, d_in)
         del back
         t = time.perf_counter()
         back = comp._adaptive_decompress(body_host, n)
         dwall = time.perf_counter() - t
-        verified = verified and equals_device(back, d_in)
+        verified = verified and device_equals_host(ctx, back, n, d_in)
+        del back
         ds = comp._last_device_stats
         decode = {"kernel_ms": round(ds.kernel_ns / 1e6, 3), "header_walk_ms": round(ds.walk_ns / 1e6, 3),
                   "h2d_ms": round(ds.h2d_ns / 1e6, 3), "d2h_ms": round(ds.d2h_ns / 1e6, 3),
                   "kernel_GBps": round(n / max(ds.kernel_ns, 1), 3),
                   "host_api_GBps": round(n / dwall / 1e9, 3),
-                  "host_api_GBps_first_call": round(n / dcold / 1e9, 3)}
+                  "host_api_GBps_first_call": round(n / dcold / 1e9, 3),
+                  "process": "torch-free (bench.py imports no torch)"}
         log(f"round trip bit-exact: {verified}; decode {decode}")
+    elif shard_check is not None:
+        verified = shard_check
 
     e2e = api = None
+    alts = []
     if rank == 0 and world == 1 and not args.no_e2e:
-        e2e = e2e_leg(lib, ctx, d_in, d_out, body_len, n, p)
+        e2e = e2e_leg(lib, ctx, d_in.ptr, body_len, n, p, d_out.ptr)
         log(f"e2e: {e2e}")
-    alt = None
     if rank == 0 and world == 1 and args.alt_methods:
-        alt = alt_leg(lib, ctx, d_in, n, args, [int(x) for x in args.alt_methods.split(",")], args.steps)
-        log(f"alt: {alt}")
+        for ms in args.alt_methods.split(";"):
+            if ms.strip():
+                alt = alt_leg(lib, ctx, d_in, n, args, [int(x) for x in ms.split(",")], max(2, args.steps // 2))
+                log(f"alt: {alt}")
+                alts.append(alt)
     if rank == 0 and world == 1 and args.api_bytes:
         api = api_leg(args.api_bytes, args.chunk, args.mode, methods, args.seed)
         log(f"api: {api}")
 
-    result = None
     if rank == 0:
-        total_in = n * world * args.steps
+        total_in = n_total * args.steps
         value = total_in / dt / 1e9
         enc_avg = sum(enc_ns) / max(1, len(enc_ns))
         # read input once + write body once, per launch (a call = launches[0] equal segments)
-        algo_bytes = (n + body_len) / launches[0]
+        algo_bytes = (sn + body_len) / launches[0]
         achieved = algo_bytes / (enc_avg * 1e-9) / 1e9 if enc_avg else 0.0
         workload = f"ambc-mixed-v1 {n >> 30} GiB/GPU chunk={args.chunk} {args.mode}"
         pmc = pmc_traffic(workload)
@@ -410,32 +468,35 @@ def main():
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-            "config": {"workload": workload, "input_bytes_per_gpu": n, "chunk_size": args.chunk,
-                       "mode": args.mode, "methods": methods, "seed": args.seed,
-                       "ratio": round(body_total / (n * world), 5),
-                       "parallelism": f"chunk-shard dp{world}" if world > 1 else "single GPU",
+            "config": {"workload": workload, "config": args.config or "c2",
+                       "input_bytes_per_gpu": n, "input_bytes_total": n_total,
+                       "chunk_size": args.chunk, "mode": args.mode, "methods": methods, "seed": args.seed,
+                       "ratio": round(body_total / n_total, 5),
+                       "parallelism": f"chunk-shard dp{world} (RCCL)" if world > 1 else "single GPU",
                        "round_trip_bit_exact": verified, "decode": decode,
+                       "lz4_bytes": LZ4_NOTE if 9 in methods else None,
                        "reassembly_to_rank0": reasm,
                        "step_ms_p50": round(percentile(step_s, 50) * 1e3, 3),
                        "step_ms_p90": round(percentile(step_s, 90) * 1e3, 3),
-                       "e2e_pinned_host": e2e, "api_file": api, "alt_method_set": alt},
+                       "e2e_pinned_host": e2e, "api_file": api, "alt_method_sets": alts},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
+                         "traffic_source": os.path.relpath(pmc["_file"], REPO) if pmc and "_file" in pmc else None,
                          "kernel": "k_encode", "kernel_ms": round(enc_avg * 1e-6, 3),
                          "algorithmic_bytes_per_launch": round(algo_bytes),
                          "launches_per_step": launches[0]},
         }
         if world == 1 and not args.no_cpu_baseline:
-            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-            result["cpu_baseline"] = cpu_baseline(args, threads)
+            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+            result["cpu_baseline"] = cpu_baseline(args, threads, methods)
         else:
             result["cpu_baseline"] = None
         print(json.dumps(result), flush=True)
-    if world > 1:
-        torch.distributed.barrier()
-        torch.distributed.destroy_process_group()
-    ctx.close()
+    d_in.free()
+    d_out.free()
+    group.barrier()
+    group.close()
 
 
 if __name__ == "__main__":

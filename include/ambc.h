@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define AMBC_ABI_VERSION 2
+#define AMBC_ABI_VERSION 3
 
 #define AMBC_OK 0
 #define AMBC_E_INVAL (-1)     /* bad argument */
@@ -49,6 +49,7 @@ extern "C" {
 #define AMBC_E_CAPACITY (-6)  /* output buffer too small */
 #define AMBC_E_HOSTCODEC (-7) /* body holds ids 6/7 chunks: use ambc_decompress_ex */
 #define AMBC_E_CODEC (-8)     /* the codec raises in the reference (e.g. Huffman on 1 or 256 symbols) */
+#define AMBC_E_COMM (-9)      /* RCCL error, or another rank / shard of the call failed */
 
 #define AMBC_MODE_NATIVE 0    /* every C-byte chunk decided independently */
 #define AMBC_MODE_REFERENCE 1 /* CHUNK_SIZE_CANDIDATES=[C] loop incl. the remainder-raw rule */
@@ -162,6 +163,76 @@ int ambc_encode_method(ambc_ctx* ctx, int method_id, const uint8_t* in, uint32_t
 int ambc_analyze(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const ambc_params* p, uint8_t* ids,
                  uint32_t* payload_len, uint8_t* should_use);
 
+/* ---------------------------------------------------------------------------
+ * Multi-GPU.  The reference is single-threaded
+ * (adaptive_compressor.py:363-394); native-mode chunks are independent, so the
+ * input shards into contiguous chunk ranges: rank r of W owns chunks
+ * [M*r/W, M*(r+1)/W) of the M = ceil(n_total/C) chunks (ambc_shard_range).
+ * Exchanges, all RCCL over xGMI: AllGather of the per-rank body sizes (file
+ * offsets), AllReduce(SUM) of the statistics, reference mode's AllReduce(MIN) of
+ * the first chunk with no winner (the remainder-raw rule is global,
+ * adaptive_compressor.py:586-588), and optionally a grouped Send/Recv gather of
+ * the bodies into file order on rank 0.
+ *
+ * Process per GPU: rank 0 calls ambc_comm_unique_id, the caller hands the 128
+ * bytes to every rank (ambc.comm does it over TCP), each rank calls
+ * ambc_comm_init_rank on a one-device ctx.  Without ambc_comm_init_rank a ctx
+ * is one rank of one.  In one process, ambc_compress_batch /
+ * ambc_decompress_multi on a ctx with several devices run one host thread per
+ * device (ncclCommInitAll over distinct devices; a ctx listing a device twice
+ * holds several shards on that GPU and exchanges through host memory).
+ * ------------------------------------------------------------------------- */
+#define AMBC_COMM_ID_BYTES 128
+#define AMBC_OP_SUM 0
+#define AMBC_OP_MIN 1
+#define AMBC_OP_MAX 2
+
+typedef struct {
+    uint64_t local_len;   /* bytes this rank produced (its packages / decoded range) */
+    uint64_t offset;      /* where they sit in the file-order body / output */
+    uint64_t total;       /* bytes of the whole body (end chunk included) / output */
+    uint64_t shard_begin; /* compress: input bytes [begin, end) of this rank */
+    uint64_t shard_end;   /* decompress: body bytes [begin, end) it decoded */
+} ambc_shard_info;
+
+int ambc_comm_unique_id(uint8_t* id);  /* AMBC_COMM_ID_BYTES bytes; host only */
+int ambc_comm_init_rank(ambc_ctx* ctx, int nranks, int rank, const uint8_t* id);
+int ambc_comm_size(ambc_ctx* ctx, int* nranks, int* rank);
+int ambc_comm_barrier(ambc_ctx* ctx);  /* AllReduce of one word + device synchronize */
+int ambc_comm_allreduce_u64(ambc_ctx* ctx, uint64_t* v, uint32_t k, int op);
+int ambc_comm_allgather_u64(ambc_ctx* ctx, const uint64_t* mine, uint32_t k, uint64_t* all);
+/* every rank's d_src (len bytes) into file order in rank 0's d_dst (grouped
+ * ncclSend/ncclRecv); *offset = this rank's offset, *total = all bytes */
+int ambc_comm_gather(ambc_ctx* ctx, const void* d_src, uint64_t len, void* d_dst, uint64_t dst_cap,
+                     uint64_t* offset, uint64_t* total);
+
+/* [*begin, *end) = input bytes of rank `rank` (host only) */
+int ambc_shard_range(uint64_t n_total, uint32_t chunk, int nranks, int rank, uint64_t* begin, uint64_t* end);
+
+/* This rank's shard (d_shard = input bytes [begin, end) of ambc_shard_range on
+ * the device) of an n_total-byte input.  root 0: rank 0's d_out receives the
+ * whole body in file order (its own packages first; out_cap >= the body);
+ * root -1: every rank keeps its packages, info->offset places them.  The last
+ * rank's packages end with the 16-B end chunk (unless AMBC_FLAG_NO_END_CHUNK).
+ * st = statistics of the whole body (AllReduce SUM).  The result equals
+ * ambc_compress_batch of the whole input on one GPU, byte for byte, in both modes. */
+int ambc_compress_shard(ambc_ctx* ctx, const void* d_shard, uint64_t n_total, const ambc_params* p, void* d_out,
+                        uint64_t out_cap, int root, ambc_shard_info* info, ambc_stats* st);
+
+/* Decode across the ranks; every rank passes the whole host body.  root 0:
+ * rank 0's d_out (out_cap >= orig_size) receives the whole output; root -1:
+ * every rank keeps its decoded range (info->offset / local_len).  A body whose
+ * packages decode to other lengths than their headers announce is decoded by
+ * rank 0 alone (root 0; root -1 fails with AMBC_E_INVAL). */
+int ambc_decompress_shard(ambc_ctx* ctx, const uint8_t* body, uint64_t body_len, uint64_t orig_size,
+                          const uint64_t registered[4], void* d_out, uint64_t out_cap, int root,
+                          ambc_shard_info* info, ambc_stats* st);
+
+/* In-process decode over all devices of the ctx into the host buffer out
+ * (each device decodes a range and copies it back at its offset). */
+int ambc_decompress_multi(ambc_ctx* ctx, const uint8_t* body, uint64_t body_len, uint64_t orig_size,
+                          const uint64_t registered[4], uint8_t* out, ambc_stats* st);
+
 /* memory / device helpers (so the Python layer needs no PyTorch) */
 void* ambc_host_alloc(uint64_t bytes);        /* pinned */
 void ambc_host_free(void* p);
@@ -169,11 +240,18 @@ void* ambc_device_alloc(ambc_ctx* ctx, int dev, uint64_t bytes);
 void ambc_device_free(ambc_ctx* ctx, int dev, void* p);
 int ambc_memcpy_h2d(ambc_ctx* ctx, int dev, void* d_dst, const void* h_src, uint64_t bytes);
 int ambc_memcpy_d2h(ambc_ctx* ctx, int dev, void* h_dst, const void* d_src, uint64_t bytes);
+int ambc_memcpy_d2d(ambc_ctx* ctx, int dev, void* d_dst, const void* d_src, uint64_t bytes);
+int ambc_memset_device(ambc_ctx* ctx, int dev, void* d_dst, int value, uint64_t bytes);
 int ambc_synchronize(ambc_ctx* ctx, int dev);
 
 /* "ambc-mixed v1" synthetic input: host fill and device fill */
 void ambc_synth_fill(uint8_t* out, uint64_t n, uint64_t seed);
 int ambc_synth_device(ambc_ctx* ctx, int dev, void* d_out, uint64_t n, uint64_t seed);
+/* bytes [begin, end) of the n_total-byte stream into d_out[0, end - begin) (a rank's shard) */
+int ambc_synth_device_range(ambc_ctx* ctx, int dev, void* d_out, uint64_t n_total, uint64_t begin,
+                            uint64_t end, uint64_t seed);
+/* *equal = (the n bytes at a and b on device dev are identical) */
+int ambc_device_equal(ambc_ctx* ctx, int dev, const void* a, const void* b, uint64_t n, int* equal);
 
 /* bench instrumentation: device time (ns) of the last compress call's encode
  * launches (k_encode and, when enabled, k_dict / k_deflate), measured with HIP

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
 def test_abi_version_and_bound():
     from ambc import _lib
     lib = _lib.load()
-    assert lib.ambc_abi_version() == 2
+    assert lib.ambc_abi_version() == 3
     assert lib.ambc_compress_bound(0, 4096) == 16
     assert lib.ambc_compress_bound(4096, 4096) == 4096 + 18 + 16
     assert lib.ambc_compress_bound(4097, 4096) == 4097 + 36 + 16
@@ -57,3 +57,20 @@ def test_missing_library_raises(tmp_path):
     from ambc import _lib
     with pytest.raises(_lib.AmbcUnavailable):
         _lib.load(str(tmp_path / "nope.so"))
+
+
+def test_library_links_rccl():
+    """The multi-GPU exchanges are RCCL inside the library (no PyTorch)."""
+    import subprocess
+    path = os.path.join(REPO, "adaptive-compression_amd", "ambc", "libambc_hip.so")
+    out = subprocess.run(["ldd", path], capture_output=True, text=True).stdout
+    assert "librccl" in out
+
+
+def test_shard_range_host_only():
+    from ambc import _lib
+    lib = _lib.load()
+    b, e = C.c_uint64(), C.c_uint64()
+    assert lib.ambc_shard_range(32 << 30, 8192, 8, 7, C.byref(b), C.byref(e)) == 0
+    assert (b.value, e.value) == (28 << 30, 32 << 30)
+    assert lib.ambc_shard_range(100, 16, 0, 0, C.byref(b), C.byref(e)) == _lib.AMBC_E_INVAL

@@ -1,16 +1,23 @@
-"""World-size-2 (gloo, CPU) coverage of the multi-GPU path: contiguous
-chunk-aligned shards compressed independently, reassembled in file order on
-rank 0 via all_gather(sizes) + send/recv; must equal the single-process body.
-The per-shard compressor here is the CPU oracle (test infrastructure); on the
-GPU box the same reassembly runs over RCCL with the HIP compressor."""
+"""World-size 2-4 CPU coverage of the multi-GPU path's host side, torch-free:
+
+* ``ambc.comm.HostGroup`` -- the TCP rendezvous that carries the RCCL unique id
+  and the bench's control messages -- in real separate processes;
+* the shard layout of ``ambc_shard_range`` (library host code): every rank
+  compresses its contiguous chunk-aligned shard independently (the CPU oracle
+  stands in for the GPU here), the sizes are all-gathered into file offsets,
+  and the concatenation in rank order equals the single-process body;
+* ``ambc_split_body`` (library host code): each rank decodes its package range
+  and the ranges concatenate to the input.
+
+On the GPU box the same layout runs inside libambc_hip over RCCL
+(tests/test_gpu_distributed.py).
+"""
+import multiprocessing as mp
 import os
 import socket
+import struct
 
 import pytest
-
-torch = pytest.importorskip("torch")
-import torch.distributed as dist  # noqa: E402
-import torch.multiprocessing as mp  # noqa: E402
 
 
 def _free_port():
@@ -21,103 +28,17 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n, chunk, seed, q):
+def _paths():
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path[:0] = [os.path.dirname(here), os.path.join(os.path.dirname(here), "adaptive-compression_amd")]
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    from ambc.distributed import compress_sharded, shard_range
-    from oracle import oracle as orc
-
-    data = torch.frombuffer(bytearray(orc.synth(n, seed)), dtype=torch.uint8)
-
-    def fn(shard):
-        body, st = orc.compress_body(bytes(shard.numpy()),
-                                     orc.make_params(chunk, "native", (1, 3, 4, 9),
-                                                     n_total=shard.numel()))
-        return torch.frombuffer(bytearray(body[:-16]), dtype=torch.uint8), st
-
-    s, e = shard_range(n, chunk, world, rank)
-    assert s % chunk == 0
-    out = compress_sharded(data, chunk, fn)
-    if rank == 0:
-        q.put(bytes(out.numpy()))
-    # in place: every rank's packages are the file-order body's bytes at its offset
-    from ambc.distributed import file_offsets
-    mine, _ = fn(data[s:e])
-    off, total = file_offsets(mine.numel(), torch.device("cpu"))
-    ref, _ = orc.compress_body(bytes(data.numpy()), orc.make_params(chunk, "native", (1, 3, 4, 9),
-                                                                    n_total=n))
-    assert total + 16 == len(ref)
-    assert ref[off:off + mine.numel()] == bytes(mine.numpy())
-    dist.barrier()
-    dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n,chunk", [(2, 1 << 20, 4096), (2, 300001, 1024), (3, 77777, 4096),
-                                           (4, 4096 * 5 + 7, 4096)])
-def test_sharded_reassembly_equals_single_process(world, n, chunk):
-    from oracle import oracle as orc
+def _run(target, world, *args):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, chunk, 42, q))
-             for r in range(world)]
-    for p in procs:
-        p.start()
-    got = q.get(timeout=240)
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    data = orc.synth(n, 42)
-    ref, _ = orc.compress_body(data, orc.make_params(chunk, "native", (1, 3, 4, 9), n_total=n))
-    assert got == ref
-
-
-def test_shard_ranges_cover_input():
-    from ambc.distributed import shard_range
-    for n, chunk, world in ((10 ** 6, 4096, 8), (4096, 4096, 8), (1, 16, 3), (4 << 30, 8192, 8)):
-        prev = 0
-        for r in range(world):
-            s, e = shard_range(n, chunk, world, r)
-            assert s == prev and (s % chunk == 0 or s == n)
-            prev = e
-        assert prev == n
-
-
-# ---------------------------------------------------------------------------
-# sharded decode: split at package boundaries, per-rank decode, file-order gather
-# ---------------------------------------------------------------------------
-def _dec_worker(rank, world, port, body, orig, q):
-    import sys
-    here = os.path.dirname(os.path.abspath(__file__))
-    sys.path[:0] = [os.path.dirname(here), os.path.join(os.path.dirname(here), "adaptive-compression_amd")]
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    from ambc.distributed import decompress_sharded
-    from oracle import oracle as orc
-
-    def fn(sub, n):
-        out, produced = orc.decompress_body(bytes(sub), n, return_produced=True)
-        return torch.frombuffer(bytearray(out), dtype=torch.uint8) if out else \
-            torch.empty(0, dtype=torch.uint8), produced
-
-    out = decompress_sharded(body, orig, fn)
-    if rank == 0:
-        q.put(bytes(out.numpy()))
-    dist.barrier()
-    dist.destroy_process_group()
-
-
-def _run_dec(world, body, orig):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_dec_worker, args=(r, world, port, body, orig, q))
-             for r in range(world)]
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=240)
@@ -127,32 +48,95 @@ def _run_dec(world, body, orig):
     return got
 
 
+def _group_worker(rank, world, port, q):
+    _paths()
+    from ambc.comm import HostGroup
+    g = HostGroup(rank, world, "127.0.0.1", port, timeout=60)
+    parts = g.allgather(bytes([rank]) * (rank + 1))
+    assert parts == [bytes([r]) * (r + 1) for r in range(world)]
+    uid = g.broadcast(os.urandom(128) if rank == 0 else b"")
+    assert len(uid) == 128
+    ids = g.allgather(uid)
+    assert all(x == uid for x in ids)
+    t = g.allgather_obj([rank * 1.5, 7])
+    assert [x[0] for x in t] == [r * 1.5 for r in range(world)]
+    g.barrier()
+    if rank == 0:
+        q.put("ok")
+    g.close()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_host_group_rendezvous(world):
+    assert _run(_group_worker, world) == "ok"
+
+
+def _compress_worker(rank, world, port, q, n, chunk, seed):
+    _paths()
+    from ambc.comm import HostGroup
+    from ambc.distributed import shard_range
+    from oracle import oracle as orc
+    g = HostGroup(rank, world, "127.0.0.1", port, timeout=60)
+    data = orc.synth(n, seed)
+    s, e = shard_range(n, chunk, world, rank)
+    assert s % chunk == 0
+    body, _ = orc.compress_body(data[s:e], orc.make_params(chunk, "native", (1, 3, 4, 9), n_total=e - s))
+    mine = body if rank == world - 1 else body[:-16]     # only the last rank ends the body
+    sizes = [struct.unpack("<Q", x)[0] for x in g.allgather(struct.pack("<Q", len(mine)))]
+    off = sum(sizes[:rank])
+    ref, _ = orc.compress_body(data, orc.make_params(chunk, "native", (1, 3, 4, 9), n_total=n))
+    assert sum(sizes) == len(ref)
+    assert ref[off:off + len(mine)] == mine          # in place at its file offset
+    parts = g.allgather(mine)
+    if rank == 0:
+        q.put(b"".join(parts))
+    g.close()
+
+
+@pytest.mark.parametrize("world,n,chunk", [(2, 1 << 20, 4096), (2, 300001, 1024), (3, 77777, 4096),
+                                           (4, 4096 * 5 + 7, 4096)])
+def test_sharded_layout_equals_single_process(world, n, chunk):
+    from oracle import oracle as orc
+    got = _run(_compress_worker, world, n, chunk, 42)
+    data = orc.synth(n, 42)
+    ref, _ = orc.compress_body(data, orc.make_params(chunk, "native", (1, 3, 4, 9), n_total=n))
+    assert got == ref
+
+
+def test_shard_ranges_cover_input():
+    from ambc.distributed import shard_range
+    for n, chunk, world in ((10 ** 6, 4096, 8), (4096, 4096, 8), (1, 16, 3), (4 << 30, 8192, 8),
+                            (32 << 30, 8192, 8)):
+        prev = 0
+        M = (n + chunk - 1) // chunk
+        for r in range(world):
+            s, e = shard_range(n, chunk, world, r)
+            assert s == prev and (s % chunk == 0 or s == n)
+            assert s == min(M * r // world * chunk, n)
+            prev = e
+        assert prev == n
+
+
+def _dec_worker(rank, world, port, q, body, orig):
+    _paths()
+    from ambc.comm import HostGroup
+    from ambc.distributed import split_body
+    from oracle import oracle as orc
+    g = HostGroup(rank, world, "127.0.0.1", port, timeout=60)
+    b0, b1, o0, o1 = split_body(body, orig, world)[rank]
+    out = orc.decompress_body(body[b0:b1], o1 - o0) if b1 > b0 else b""
+    parts = g.allgather(out)
+    if rank == 0:
+        q.put(b"".join(parts))
+    g.close()
+
+
 @pytest.mark.parametrize("world,n,chunk", [(2, 1 << 20, 4096), (3, 300001, 1024), (4, 9000, 4096)])
 def test_sharded_decode_equals_single_process(world, n, chunk):
     from oracle import oracle as orc
     data = orc.synth(n, 7)
     body, _ = orc.compress_body(data, orc.make_params(chunk, "native", (1, 3, 4, 9), n_total=n))
-    assert _run_dec(world, body, n) == data
-
-
-def test_sharded_decode_lenient_bodies_fall_back():
-    """Packages that decode to other lengths than announced (unregistered id,
-    short Delta) and a truncated final package: the split cannot be trusted, the
-    destination decodes alone -- the result still equals the sequential decode."""
-    import struct
-    from oracle import oracle as orc
-    pk = []
-    huff = orc.huff_encode(b"aaab" * 8)   # 32 symbols; announced orig 60 -> decodes short
-    for t, payload, orig in ((3, huff, 60), (255, b"a" * 100, 100), (4, b"\x05" * 30, 60),
-                             (77, b"xyz" * 10, 50), (255, b"b" * 200, 200), (1, b"\x07\x05", 5),
-                             (255, b"c" * 90, 90)):
-        pk.append(b"\xff\xff\x00\x00" + bytes([t, 0]) + struct.pack("<III", len(payload), orig,
-                                                                     len(payload)) + payload)
-    body = b"".join(pk) + b"\xff\xff\x00\x00" + bytes(12)
-    orig = 505
-    ref = orc.decompress_body(body, orig)
-    assert orc.decompress_body(pk[0], 60, return_produced=True)[1] == 32   # the short package
-    assert _run_dec(2, body, orig) == ref
+    assert _run(_dec_worker, world, body, n) == data
 
 
 def test_split_body_ranges():
@@ -172,3 +156,16 @@ def test_split_body_ranges():
                 assert orc.decompress_body(body[b0:b1], o1 - o0) == data[o0:o1]
     with pytest.raises(ValueError):
         split_body(b"\x00" * 40, 10, 2)
+
+
+def test_bench_rejects_mismatched_world(tmp_path):
+    """bench.py --gpus 2 under a launcher that started one rank must fail fast,
+    before any GPU call (a silent 1-GPU measurement is the bug this guards)."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2
+    assert "WORLD_SIZE=1" in r.stderr
