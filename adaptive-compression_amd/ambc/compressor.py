@@ -29,6 +29,7 @@ import hashlib
 import math
 import os
 import struct
+import sys
 import threading
 import time
 
@@ -160,13 +161,17 @@ class AdaptiveCompressor:
     def _ctx(self):
         return _lib.default_context(self.devices)
 
+    def _eligible(self, s, ids):
+        """ids whose method_chunk_prefs admit an s-byte chunk (adaptive_compressor.py:565-567)."""
+        return [i for i in ids if self.method_chunk_prefs.get(i, (1, 999999999))[0] <= s
+                <= self.method_chunk_prefs.get(i, (1, 999999999))[1]]
+
     def _encode_run(self, ctx, run, s, ids):
         """len(run) // s consecutive s-byte chunks through ONE ambc_compress_batch
         call: for each, the package of the reference's per-size method loop
         (adaptive_compressor.py:559-579 + _process_chunk :631-700), or None when
         no method beats raw.  len(run) is s or a multiple of it."""
-        elig = [i for i in ids if self.method_chunk_prefs.get(i, (1, 999999999))[0] <= s
-                <= self.method_chunk_prefs.get(i, (1, 999999999))[1]]
+        elig = self._eligible(s, ids)
         k = len(run) // s
         if not elig:
             return [None] * k
@@ -239,6 +244,8 @@ class AdaptiveCompressor:
                 s = min(cand, remain)
                 if s <= 0:
                     break
+                if s not in tried and not self._eligible(s, ids):
+                    tried[s] = None                   # no method takes this size: nothing to encode
                 if s not in tried:
                     if self.MULTISIZE_LOOKAHEAD and s == cand and (pos, s) not in ahead and s % 16 == 0:
                         # look ahead: the s-byte chunks at the next J positions the
@@ -330,10 +337,16 @@ class AdaptiveCompressor:
             raise NotImplementedError("only the reference's constant 32-bit marker is supported")
         ctx = self._ctx()
         data = bytes(data)
-        # large outputs: decode straight into a fresh (calloc'd, lazily zeroed)
-        # bytes object that nothing else references yet -- saves a full copy
+        # Large outputs: decode straight into a fresh (calloc'd, lazily zeroed)
+        # bytes object -- this saves a full copy of the output (a second of CPU
+        # per 4 GiB).  Writing into a bytes object is sound only while it is
+        # private: created here, referenced by `out` alone, never hashed or
+        # shared before the library has filled it.  The refcount check below
+        # guards that invariant (2 = `out` + getrefcount's own argument).
         direct = orig_size >= (1 << 16)
         out = bytes(orig_size) if direct else bytearray(max(orig_size, 1))
+        if direct and sys.getrefcount(out) != 2:
+            raise RuntimeError("decode buffer is shared: refusing to write into it")
         reg = (C.c_uint64 * 4)()
         for t in self.method_lookup:
             reg[t >> 6] |= 1 << (t & 63)

@@ -5,9 +5,9 @@ Same contract as compression_methods.py:7-67: ``type_id``,
 ``should_use(data, threshold=0.9) -> bool``, ``calculate_overhead() -> int``,
 exceptions raised like the reference's.
 
-* ids 1, 3, 4, 9 (RLE, Huffman, Delta, LZ4) and 255 run on the GPU through
-  libambc_hip (single-chunk calls of the same kernels the batched path uses);
-* id 2 (Dictionary) decodes on the GPU; its encoder is SURVEY §8(f) "next";
+* ids 1, 2, 3, 4, 9 (RLE, Dictionary, Huffman, Delta, LZ4) and 255 run on the
+  GPU through libambc_hip (single-chunk calls of the same kernels the batched
+  path uses; Dictionary emits the reference's own bytes for chunks <= 8192);
 * ids 5, 6, 7 are the reference's own stdlib library wrappers
   (advanced_compression.py:71-213), registered so that reference-produced files
   holding such chunks decode.  When id 5 is among ``methods`` the batched engine
