@@ -11,10 +11,12 @@
 //   Huffman should_use entropy (fp64; numpy-exact terms for near-ties,
 //           :562-574), tree by repeated wave-min merges of (weight, first
 //           symbol) keys (:482-494), exact payload size 1+5k+4+ceil(bits/8)
-//   LZ4     "ambc-lz4 greedy v1": per 64-position round, hash-bucket
-//           predecessors by ballot peers + an LDS last[] table, then a
-//           wave-cooperative greedy walk that emits straight into the chunk's
-//           scratch slot and gives up as soon as it cannot beat the best so far
+//   LZ4     "ambc-lz4 greedy v2": per 64-position window, candidates from an
+//           LDS hash table of the earlier windows (ds_max keeps each hash's
+//           last position; the first window resolves its own repeats by
+//           ballots), then a wave-cooperative greedy walk that emits straight
+//           into the chunk's scratch slot and gives up as soon as it cannot
+//           beat the best so far
 //   emit    the winner's payload into the slot (raw / RLE / Huffman bits)
 //
 // Work is integer/byte work bound by LDS and issue, not by HBM: every input
@@ -33,14 +35,16 @@ template <int CMAX>
 struct EncSmem {
     // work = union, by lifetime.  Selection: hist | code | clen | Huffman tree
     // (parent/pbit), whose space the first occurrences (first/order) reuse once
-    // the tree is built.  LZ4: last[] hash table + 64 bucket masks.  Emit: RLE
-    // pair starts | Huffman bit staging behind hist/code/clen.  8.8 KB per
-    // workgroup at C = 4096 -> 18 workgroups per CU (12.9 KB / 12 at 8192,
-    // 21 KB / 7 at 16384).
-    static constexpr int WORK = 4608;   // every chunk size; larger Huffman payloads stage in the slot
+    // the tree is built.  LZ4: the hash table (u32 per bucket).  Emit: RLE pair
+    // starts | Huffman bit staging behind hist/code/clen.  8 KB per workgroup at
+    // C = 4096 -> 20 workgroups per CU (12 KB / 13 at 8192, 20 KB / 8 at 16384).
+    static constexpr int WORK = 4096;   // every chunk size; larger Huffman payloads stage in the slot
     static constexpr int STAGE_OFF = 2304;                  // Huffman bit staging
     static constexpr int STAGE = WORK - STAGE_OFF;
-    alignas(16) uint8_t chunk[CMAX + 64];      // zero padded
+    // zero padded up to CMAX; reads past CMAX (the LZ4 loads of lanes beyond n,
+    // match lengths capped below n) land in work[], which follows: in bounds,
+    // and never part of a result
+    alignas(16) uint8_t chunk[CMAX];
     alignas(16) uint32_t work[WORK / 4];
     __device__ __forceinline__ uint8_t* wb() { return reinterpret_cast<uint8_t*>(work); }
     __device__ __forceinline__ uint32_t* hist() { return work; }
@@ -50,11 +54,10 @@ struct EncSmem {
     __device__ __forceinline__ uint8_t* pbit() { return wb() + 3328; }
     __device__ __forceinline__ uint32_t* first() { return reinterpret_cast<uint32_t*>(wb() + 2304); }
     __device__ __forceinline__ uint8_t* order() { return wb() + 3328; }
-    __device__ __forceinline__ uint16_t* last() { return reinterpret_cast<uint16_t*>(work); }
-    __device__ __forceinline__ uint64_t* bk() { return reinterpret_cast<uint64_t*>(wb() + 4096); }
+    __device__ __forceinline__ uint32_t* last() { return work; }
     __device__ __forceinline__ uint32_t* stage() { return reinterpret_cast<uint32_t*>(wb() + STAGE_OFF); }
 };
-static_assert((1u << LZ4_HASH_BITS) * 2 <= 4096, "LZ4 table must fit the work area");
+static_assert((1u << LZ4_HASH_BITS) * 4 <= 4096, "LZ4 table must fit the work area");
 
 // Visit the bytes of a lane's block [b0, b0+BS) 16 at a time (one ds_read_b128
 // per step; the 16-byte body is unrolled, the sub-block loop is not, which
@@ -162,7 +165,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         } else {
             for (uint32_t i = lane; i < n; i += 64) S.chunk[i] = src[i];
         }
-        for (uint32_t i = n + lane; i < (uint32_t)CMAX + 64; i += 64) S.chunk[i] = 0;
+        for (uint32_t i = n + lane; i < (uint32_t)CMAX; i += 64) S.chunk[i] = 0;
         for (uint32_t i = lane; i < 256; i += 64) S.hist()[i] = 0;
     }
     wave_sync();
@@ -440,9 +443,10 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
 
     STAMP(1);
     // ---- LZ4 (id 9): frame = 15 B header + 4 B block size + block + 4 B end mark ----
-    // "ambc-lz4 greedy v1": cand(i) = last j < i with the same 12-bit hash, valid
-    // iff the 4 bytes match; greedy from the first valid position; matches start
-    // at i <= n-12 and end by n-5 (LZ4 block end rules).
+    // "ambc-lz4 greedy v2": cand(i) = last j with the same 10-bit hash among the
+    // earlier 64-position windows (j < 64*floor(i/64); in the first window any
+    // j < i), valid iff the 4 bytes match; greedy from the first valid
+    // position; matches start at i <= n-12 and end by n-5 (LZ4 block end rules).
     if (A.bestpre) {
         // for k_deflate: the best (len + 18) before LZ4, and bit 31 = DEFLATE's
         // should_use is False (calculate_entropy == 8.0: an exactly uniform histogram)
@@ -484,10 +488,8 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
     // 18-B header it cannot win unless best > 51 + ext(n - 10) (zero runs: RLE 52)
     if (eligible(9) && (force || (n >= 1024 && best > 51 + ext_len(n - 10)))) {
         lz4_ran = true;
-        uint16_t* last = S.last();
-        uint64_t* bk = S.bk();
-        for (uint32_t i = lane; i < (1u << LZ4_HASH_BITS); i += 64) last[i] = 0xFFFF;
-        bk[lane] = 0;
+        uint32_t* last = S.last();          // 1 + last position per hash, 0 = none
+        for (uint32_t i = lane; i < (1u << LZ4_HASH_BITS); i += 64) last[i] = 0;
         wave_sync();
         // LZ4 wins iff block < budget; forced (single-method) encodes fall back to a
         // stored block once the compressed block would reach n (LZ4F rule)
@@ -505,38 +507,28 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
             emitted = __builtin_amdgcn_readfirstlane(emitted);
             const int i = base + (int)lane;
             const bool act = i <= mlim;
-            // loads run for every lane (the chunk is zero padded past n + 63)
+            // loads run for every lane (past n: padding / work[] bytes of inactive lanes)
             const uint32_t v = lds_rd32(S.chunk, (uint32_t)i);
             const uint32_t h = (v * 2654435761u) >> (32 - LZ4_HASH_BITS);
-            const uint32_t c16 = last[h];
-            // lanes with my hash: one shared hash (runs) is the active mask; else an
-            // order-free LDS OR per 7-bit bucket, then 4 ballots for the top bits
-            const uint64_t actm = base + 63 <= mlim ? ~0ull : __ballot(act);
-            const uint32_t h0 = __builtin_amdgcn_readfirstlane(h);
-            uint64_t peers;
-            if (__ballot(h != h0) == 0ull) {
-                peers = actm;
-            } else {
-                atomicOr(reinterpret_cast<unsigned long long*>(&bk[h & 63u]), act ? 1ull << lane : 0ull);
-                wave_sync();
-                peers = bk[h & 63u] & actm;
+            // candidate: the last earlier 64-position window's position with my hash
+            int cand = (int)last[h] - 1;
+            if (base == 0) {
+                // first window: the highest lower lane with my hash (peers by one ballot per bit)
+                uint64_t peers = ~0ull;
 #pragma unroll
-                for (int b = 6; b < (int)LZ4_HASH_BITS; b++) {
+                for (int b = 0; b < (int)LZ4_HASH_BITS; b++) {
                     const uint64_t m = __ballot((h >> b) & 1u);
-                    const uint64_t flip = 0ull - (uint64_t)((h >> b) & 1u);
-                    peers &= ~(m ^ flip);
+                    peers &= ((h >> b) & 1u) ? m : ~m;
                 }
-                wave_sync();
-                bk[h & 63u] = 0ull;
+                const uint64_t lower = peers & ((1ull << lane) - 1ull);
+                cand = lower ? 63 - (int)__clzll((long long)lower) : -1;
             }
-            const uint64_t lower = peers & ((1ull << lane) - 1ull);
-            const int cand = lower ? base + 63 - (int)__clzll((long long)lower)
-                                   : (c16 == 0xFFFFu ? -1 : (int)c16);
+            // the window's highest position per hash (the reads above see earlier windows only)
+            atomicMax(&last[h], (uint32_t)i + 1u);
             const uint32_t cv = lds_rd32(S.chunk, (uint32_t)max(cand, 0));
             const bool valid = act && cand >= 0 && cv == v;
             const uint64_t vm = __ballot(valid);
             wave_sync();
-            if (act && (peers >> lane) == 1ull) last[h] = (uint16_t)i;
             STAMP(2);
             if (base + 63 < (int)nextp) continue;   // round lies inside the previous match
             uint32_t p = __builtin_amdgcn_readfirstlane((int)nextp > base ? nextp - (uint32_t)base : 0u);
@@ -661,7 +653,11 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                 // 32-bit offsets from the (uniform) block pointer: saddr stores
                 const uint32_t q0 = emitted + incl - sz;     // token
                 const uint32_t ql = q0 + 1 + xl;             // first literal
+#ifdef AMBC_EXP_NOSTORE
+                if (0) {
+#else
                 if (me) {
+#endif
                     blk[q0] = (uint8_t)((lit >= 15 ? 15 : lit) << 4 | (ml >= 15 ? 15 : ml));
                     const uint32_t offv = (uint32_t)(i - cand);
                     blk[ql + lit] = (uint8_t)offv;
@@ -673,7 +669,11 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                 }
                 // literals: short runs per lane (8 bytes per step from two unaligned
                 // LDS dwords), long runs by the whole wave (one byte per lane)
+#ifdef AMBC_EXP_NOSTORE
+                if (0) {
+#else
                 if (me && lit && lit < 32) {
+#endif
 #pragma unroll 1
                     for (uint32_t t = 0; t < lit; t += 8) {
                         const uint32_t w0 = lds_rd32(S.chunk, (uint32_t)pe + t);

@@ -7,7 +7,7 @@ namespace ambc {
 
 constexpr uint32_t HDR = 18;       // chunk header: marker4 type k used4 orig4 clen4
 constexpr uint32_t END_CHUNK = 16; // _create_end_chunk (u16 used field)
-constexpr uint32_t LZ4_HASH_BITS = 11;   // "ambc-lz4 greedy v1" hash width
+constexpr uint32_t LZ4_HASH_BITS = 10;   // "ambc-lz4 greedy v2" hash width
 constexpr uint32_t ENC_FORCE = 1;    // CompressionMethod.compress(chunk) semantics
 constexpr uint32_t ENC_ANALYZE = 2;  // also evaluate every should_use
 constexpr uint32_t ENC_EMIT_PENDING = 4;  // emit only the chunks the first pass deferred and id 5 did not take

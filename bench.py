@@ -41,7 +41,7 @@ GiB = 1 << 30
 # BASELINE.json configs (per-GPU input, chunk): c4 = 32 GiB over 8 GPUs at chunk 8192
 CONFIGS = {"c2": (4 * GiB, 4096), "c3-1024": (4 * GiB, 1024), "c3-16384": (4 * GiB, 16384),
            "c4": (4 * GiB, 8192)}
-LZ4_NOTE = ("id 9 bytes are this project's 'ambc-lz4 greedy v1' LZ4 frames (valid LZ4, decodable by any "
+LZ4_NOTE = ("id 9 bytes are this project's 'ambc-lz4 greedy v2' LZ4 frames (valid LZ4, decodable by any "
             "LZ4 frame decoder), not python-lz4's HC-9 output, which is absent here and unpinned")
 
 

@@ -10,7 +10,7 @@
  * Pinned against the reference's own outputs: tests/golden/ JSON files and
  * tests/golden/files/ containers were produced by importing the reference
  * (tests/golden/make_golden.py); tests/test_oracle.py checks every vector.
- * The LZ4 block parse ("ambc-lz4 greedy v1") is this project's own algorithm
+ * The LZ4 block parse ("ambc-lz4 greedy v2") is this project's own algorithm
  * (python-lz4 is absent): its validity is pinned by the
  * system liblz4 decoding its frames, its bytes are parity-unpinned vs python-lz4.
  *
@@ -415,15 +415,17 @@ EXPORT uint32_t orc_xxh32(const uint8_t* p, uint64_t len, uint32_t seed) {
 }
 
 /* ------------------------------------------------------------------------ */
-/* LZ4 ("ambc-lz4 greedy v1", this project's parse; frame = what            */
+/* LZ4 ("ambc-lz4 greedy v2", this project's parse; frame = what            */
 /* LZ4F_compressFrame emits for one <=64 KiB block, advanced_compression.py */
 /* :272-281 calls lz4.frame.compress)                                        */
-/*   hash h(i) = (u32le(d+i) * 2654435761) >> (32-11)                        */
-/*   cand(i)   = max{ j < i : h(j) == h(i) };  valid iff the 4 bytes match   */
+/*   hash h(i) = (u32le(d+i) * 2654435761) >> (32-10)                        */
+/*   cand(i)   = max{ j < w(i) : h(j) == h(i) },  w(i) = i for i < 64, else   */
+/*               64*floor(i/64) (earlier 64-position windows only);          */
+/*               valid iff the 4 bytes match                                 */
 /*   matchable i <= n-12; match end <= n-5 (LZ4 end-of-block rules)          */
 /*   greedy: take the match at the first valid position, jump past it       */
 /* ------------------------------------------------------------------------ */
-#define LZ4_HB 11
+#define LZ4_HB 10
 static inline uint32_t lz4_hash(uint32_t v) { return (v * 2654435761U) >> (32 - LZ4_HB); }
 
 static int64_t put_len(uint8_t* out, int64_t o, uint32_t v) {   /* ext bytes for v >= 15 */
@@ -441,7 +443,8 @@ EXPORT int64_t orc_lz4_block_encode(const uint8_t* d, uint32_t n, uint8_t* out) 
     if (n >= 13) {
         uint32_t mlim = n - 12;
         while (i <= mlim) {
-            for (; ins < i; ins++) last[lz4_hash(rd32(d + ins))] = (int32_t)ins;
+            const uint32_t w = i < 64 ? i : (i & ~63u);   /* earlier windows only */
+            for (; ins < w; ins++) last[lz4_hash(rd32(d + ins))] = (int32_t)ins;
             uint32_t v = rd32(d + i);
             int32_t c = last[lz4_hash(v)];
             if (c >= 0 && rd32(d + c) == v) {
