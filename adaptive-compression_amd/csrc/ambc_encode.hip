@@ -566,38 +566,40 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
             // (1) greedy walk over this round's positions.  Every lane first links
             // itself to the next match start the greedy parse would take after it
             // (first valid position >= its match end; 64 = leaves the round, 65 =
-            // its match needs extending beyond LCAP), and two bpermutes extend the
-            // link to the next four starts, packed 7 bits each.  The scalar walk
-            // then consumes four matches per v_readlane.
+            // its match needs extending beyond LCAP).  Three doubling steps (three
+            // bpermutes each) turn the links into chains of up to eight starts per
+            // lane: the mask of the chain's starts and the link after its last one.
+            // The scalar walk then takes eight matches per step (one OR and three
+            // v_readlane), which keeps the scalar unit -- the ASCII chunks' busiest
+            // port -- out of the per-match work.
             const bool longl = run_l && L >= LCAP && L < lim;
             const uint32_t E = lane + L;    // match end relative to base (lanes with L)
-            uint32_t nx1;
+            uint32_t hop;
             {
                 const uint64_t mm = E < 64 ? (vm & (~0ull << E)) : 0ull;
-                nx1 = longl ? 65u : (mm ? (uint32_t)__builtin_ctzll(mm) : 64u);
+                hop = longl ? 65u : (mm ? (uint32_t)__builtin_ctzll(mm) : 64u);
             }
-            uint32_t nx2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(min(nx1, 63u) << 2), (int)nx1);
-            if (nx1 >= 64) nx2 = nx1;
-            const uint32_t pr = nx1 | nx2 << 7;
-            uint32_t pr2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(min(nx2, 63u) << 2), (int)pr);
-            if (nx2 >= 64) pr2 = nx2 | nx2 << 7;
-            const uint32_t pack = pr | pr2 << 14;
+            uint32_t chlo = lane < 32 ? 1u << lane : 0u, chhi = lane < 32 ? 0u : 1u << (lane - 32);
+#pragma unroll
+            for (int lv = 0; lv < 3; lv++) {
+                const int idx = (int)(min(hop, 63u) << 2);
+                const uint32_t tlo = (uint32_t)__builtin_amdgcn_ds_bpermute(idx, (int)chlo);
+                const uint32_t thi = (uint32_t)__builtin_amdgcn_ds_bpermute(idx, (int)chhi);
+                const uint32_t th = (uint32_t)__builtin_amdgcn_ds_bpermute(idx, (int)hop);
+                const bool in = hop < 64;
+                chlo |= in ? tlo : 0u;
+                chhi |= in ? thi : 0u;
+                hop = in ? th : hop;
+            }
             uint64_t sel = 0;
             {
                 const uint64_t m0 = vm & (~0ull << p);
                 uint32_t cur = m0 ? (uint32_t)__builtin_ctzll(m0) : 64u;
                 while (cur < 64) {
-                    sel |= 1ull << cur;
-                    const uint32_t pk = readlane(pack, cur);
-                    uint32_t x = pk & 127u, f = 1;
-                    while (x < 64) {
-                        sel |= 1ull << x;
-                        cur = x;
-                        if (f == 4) break;
-                        x = (pk >> (7 * f)) & 127u;
-                        f++;
-                    }
-                    if (x < 64) continue;          // four more starts taken; go on from cur
+                    sel |= (uint64_t)readlane(chlo, cur) | (uint64_t)readlane(chhi, cur) << 32;
+                    const uint32_t x = readlane(hop, cur);
+                    if (x < 64) { cur = x; continue; }   // eight more starts taken
+                    cur = 63u - (uint32_t)__builtin_clzll(sel);   // the chain's last start
                     if (x == 64) {                 // cur's match is the round's last
                         p = readlane(E, cur);
                         break;
