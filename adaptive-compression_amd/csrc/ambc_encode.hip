@@ -498,7 +498,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         uint8_t* blk = slot + 19;
         uint32_t emitted = 0, anchor = 0, nextp = 0;
         bool alive = true;
-        constexpr uint32_t LCAP = 32;       // per-lane precomputed match length cap
+        constexpr uint32_t LCAP = 16;       // per-lane precomputed match length cap
 #pragma unroll 1
         for (int base = 0; base <= mlim && alive; base += 64) {
             // control state is wave-uniform: keep it in SGPRs
@@ -533,33 +533,28 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
             if (base + 63 < (int)nextp) continue;   // round lies inside the previous match
             uint32_t p = __builtin_amdgcn_readfirstlane((int)nextp > base ? nextp - (uint32_t)base : 0u);
             if ((vm & (~0ull << p)) == 0ull) continue;   // no match starts here: all literals
-            // per-lane match length: 16 bytes per step (five aligned dwords per side
-            // issued together), capped at LCAP; the walk extends longer ones
-            uint32_t L = 0;
+            // per-lane match length in one step: bytes 4..15 behind the known four
+            // (four aligned dwords per side, issued together), so L <= LCAP = 16;
+            // the walk extends the selected longer ones with the whole wave
             const bool run_l = valid && (uint32_t)i >= nextp;
-            bool run = run_l;
-            const uint32_t lim = run ? n - 5 - (uint32_t)i : 0u;
-            const uint32_t cap = min(lim, LCAP);
-            if (run) L = 4;
-            const uint32_t* c32 = reinterpret_cast<const uint32_t*>(S.chunk);
-            const uint32_t si = (uint32_t)i & 3u, sc = (uint32_t)cand & 3u;
-#pragma unroll 1
-            while (__ballot(run && L < cap)) {
-                if (run && L < cap) {
-                    const uint32_t ai = ((uint32_t)i + L) >> 2, ac = ((uint32_t)cand + L) >> 2;
-                    uint32_t wi[5], wc[5];
+            const uint32_t lim = run_l ? n - 5 - (uint32_t)i : 0u;
+            uint32_t L;
+            {
+                const uint32_t* c32 = reinterpret_cast<const uint32_t*>(S.chunk);
+                const uint32_t cs = (uint32_t)max(cand, 0);
+                const uint32_t si = (uint32_t)i & 3u, sc = cs & 3u;
+                const uint32_t ai = ((uint32_t)i + 4) >> 2, ac = (cs + 4) >> 2;
+                uint32_t wi[4], wc[4];
 #pragma unroll
-                    for (int t = 0; t < 5; t++) { wi[t] = c32[ai + t]; wc[t] = c32[ac + t]; }
-                    uint32_t add = 16;
+                for (int t = 0; t < 4; t++) { wi[t] = c32[ai + t]; wc[t] = c32[ac + t]; }
+                uint32_t add = 12;
 #pragma unroll
-                    for (int t = 3; t >= 0; t--) {
-                        const uint32_t x = __builtin_amdgcn_alignbyte(wi[t + 1], wi[t], si) ^
-                                           __builtin_amdgcn_alignbyte(wc[t + 1], wc[t], sc);
-                        if (x) add = 4 * t + ((uint32_t)__builtin_ctz(x) >> 3);
-                    }
-                    L += add;
-                    if (add < 16) run = false;
+                for (int t = 2; t >= 0; t--) {
+                    const uint32_t x = __builtin_amdgcn_alignbyte(wi[t + 1], wi[t], si) ^
+                                       __builtin_amdgcn_alignbyte(wc[t + 1], wc[t], sc);
+                    if (x) add = 4 * t + ((uint32_t)__builtin_ctz(x) >> 3);
                 }
+                L = run_l ? 4 + add : 0u;
             }
             L = min(L, lim);
             STAMP(3);
@@ -669,29 +664,23 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                     for (uint32_t t = 0; t < xl; t++) blk[q0 + 1 + t] = (uint8_t)ext_byte(lit, xl, t);
                     for (uint32_t t = 0; t < xm; t++) blk[ql + lit + 2 + t] = (uint8_t)ext_byte(ml, xm, t);
                 }
-                // literals: short runs per lane (8 bytes per step from two unaligned
-                // LDS dwords), long runs by the whole wave (one byte per lane)
-#ifdef AMBC_EXP_NOSTORE
-                if (0) {
-#else
-                if (me && lit && lit < 32) {
+                // literals, one byte per lane: a lane inside this round that no
+                // selected match covers and that some selected match follows is a
+                // literal of the next selected lane's sequence, at offset i - pe
+                // of its literals (its pe is that sequence's literal start); the
+                // first sequence's literals from before this round by the whole wave
+                {
+                    const uint64_t rest = sel >> lane;
+                    const uint32_t nx = rest ? lane + (uint32_t)__builtin_ctzll(rest) : lane;
+                    const uint32_t qn = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(nx << 2), (int)ql);
+#ifndef AMBC_EXP_NOSTORE
+                    if (!me && rest && i >= pe) blk[qn + (uint32_t)(i - pe)] = (uint8_t)v;
 #endif
-#pragma unroll 1
-                    for (uint32_t t = 0; t < lit; t += 8) {
-                        const uint32_t w0 = lds_rd32(S.chunk, (uint32_t)pe + t);
-                        const uint32_t w1 = lds_rd32(S.chunk, (uint32_t)pe + t + 4);
-#pragma unroll
-                        for (uint32_t b = 0; b < 8; b++)
-                            if (t + b < lit) blk[ql + t + b] = (uint8_t)((b < 4 ? w0 : w1) >> (8 * (b & 3)));
+                    if (anchor < (uint32_t)base) {
+                        const uint32_t dst = readlane(ql, (uint32_t)__builtin_ctzll(sel));
+                        const uint32_t len = (uint32_t)base - anchor;
+                        for (uint32_t t = lane; t < len; t += 64) blk[dst + t] = S.chunk[anchor + t];
                     }
-                }
-                uint64_t lmask = __ballot(lit >= 32);
-                while (lmask) {
-                    const uint32_t j = (uint32_t)__builtin_ctzll(lmask);
-                    lmask &= lmask - 1;
-                    const uint32_t src = readlane((uint32_t)pe, j), dst = readlane(ql, j),
-                                   len = readlane(lit, j);
-                    for (uint32_t t = lane; t < len; t += 64) blk[dst + t] = S.chunk[src + t];
                 }
                 emitted = __builtin_amdgcn_readfirstlane(emitted + tot);
                 anchor = __builtin_amdgcn_readfirstlane(np);
