@@ -214,17 +214,15 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                 if (chg == 0) {
                     rc += nv;                         // the current run goes on
                 } else {
+                    // a run ends in this dword: flush the run carried in and count
+                    // the dword's bytes one by one (branch-free); the last byte's
+                    // run carries on with nothing counted yet
+                    atomicAdd(&S.hist()[cur], rc);
 #pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        if ((uint32_t)j < nv) {
-                            if ((chg >> (8 * j + 7)) & 1u) {
-                                if (rc) atomicAdd(&S.hist()[cur], rc);
-                                cur = (w >> (8 * j)) & 0xFFu;
-                                rc = 0;
-                            }
-                            rc++;
-                        }
-                    }
+                    for (int j = 0; j < 4; j++)
+                        atomicAdd(&S.hist()[(w >> (8 * j)) & 0xFFu], (uint32_t)j < nv ? 1u : 0u);
+                    cur = w >> 24;
+                    rc = 0;
                 }
                 pw = w;
             }
@@ -463,31 +461,16 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         const bool single = wave_sum_u32(nz) == 1;
         if (lane == 0) A.bestpre[k] = best | (uniform ? 0x80000000u : 0u) | (single ? 0x40000000u : 0u);
     }
-    // the LZ4 walk reuses hist[]/code[] for its tables: count the bytes again
-    auto recount_hist = [&]() {
-        for (uint32_t i = lane; i < 256; i += 64) S.hist()[i] = 0;
-        wave_sync();
-#pragma unroll 1
-        for (int r = 0; r < ROUNDS; r++) {
-            const uint32_t b0 = (uint32_t)(r * 64 + lane) * BS;
-            uint32_t cur = S.chunk[b0], rc = 0;
-            for_block_bytes<BS>(S.chunk, b0, [&](uint32_t p, uint32_t c, uint32_t) {
-                if (p < n) {
-                    if (c == cur) rc++;
-                    else { atomicAdd(&S.hist()[cur], rc); cur = c; rc = 1; }
-                }
-            });
-            if (rc) atomicAdd(&S.hist()[cur], rc);
-        }
-        wave_sync();
-    };
     const uint32_t best_pre = best;   // before LZ4 (a deferred Huffman compares against it)
-    bool lz4_ran = false;   // the LZ4 walk reuses hist[]/code[] for its bucket masks
     // LZ4's frame is at least 23 + 10 + ext(n - 10) bytes: a literal at 0 (no
     // candidate), one match up to n - 5, the last five bytes literal; with the
     // 18-B header it cannot win unless best > 51 + ext(n - 10) (zero runs: RLE 52)
     if (eligible(9) && (force || (n >= 1024 && best > 51 + ext_len(n - 10)))) {
-        lz4_ran = true;
+        // the walk's hash table overlays hist[]: keep the counts in registers
+        uint32_t hsave[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) hsave[j] = S.hist()[lane + 64 * j];
+        wave_sync();
         uint32_t* last = S.last();          // 1 + last position per hash, 0 = none
         for (uint32_t i = lane; i < (1u << LZ4_HASH_BITS); i += 64) last[i] = 0;
         wave_sync();
@@ -719,11 +702,13 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
             wlen = n + 23;
         }
         wave_sync();
+#pragma unroll
+        for (int j = 0; j < 4; j++) S.hist()[lane + 64 * j] = hsave[j];
+        wave_sync();
     }
 
     if (huff_defer && huff_lb + HDR < best_pre && (win != 9 || huff_lb <= wlen)) {
         // Huffman comes before LZ4 in id order: it wins a tie with LZ4
-        if (lz4_ran) recount_hist();
         const uint32_t nb = huff_bits();
         const uint32_t l = 1 + 5 * kdist + 4 + (nb + 7) / 8;
         if (l + HDR < best_pre && (win != 9 || l <= wlen)) { best = l + HDR; win = 3; wlen = l; }
@@ -746,7 +731,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         const uint32_t nv = (n + 15) >> 4;
         for (uint32_t v = lane; v < nv; v += 64)
             reinterpret_cast<uint4*>(slot)[v] = reinterpret_cast<const uint4*>(S.chunk)[v];
-    } else if (win == 1 && S.hist()[S.chunk[0]] == n && !lz4_ran) {
+    } else if (win == 1 && S.hist()[S.chunk[0]] == n) {
         // one byte value: (c, 255) pairs and the remainder (compression_methods.py:95-109)
         const uint32_t c = S.chunk[0];
         for (uint32_t j = lane; j < pairs; j += 64) {
@@ -808,7 +793,6 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
             wave_sync();
         }
     } else if (win == 3) {
-        if (lz4_ran) recount_hist();   // (again: a deferred Huffman may have counted already)
         {
             uint32_t nb2, ml2;
             huff_tree(nb2, ml2);   // codes and lengths of the winner's tree
