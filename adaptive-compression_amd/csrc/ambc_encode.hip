@@ -884,10 +884,7 @@ __device__ __forceinline__ uint32_t hdr_byte(uint32_t q, uint32_t type, uint32_t
     return (clen >> (8 * (q - 14))) & 0xFF;              // compressed_length
 }
 
-__global__ __launch_bounds__(256) void k_compact(CompactArgs A) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t k = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (k >= A.n_chunks) return;
+__device__ __forceinline__ void compact_package(const CompactArgs& A, uint32_t k, uint32_t lane) {
     const uint64_t o = A.off[k] + (A.base ? *A.base : 0ull);
     const uint32_t pl = A.plen[k];
     const uint32_t P = HDR + pl;
@@ -939,6 +936,14 @@ __global__ __launch_bounds__(256) void k_compact(CompactArgs A) {
             }
         }
     }
+}
+
+// a fixed grid of resident workgroups that stride over the packages: launched
+// beside the encoder, it gets its slots once instead of once per package group
+__global__ __launch_bounds__(256) void k_compact(CompactArgs A) {
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t k = blockIdx.x * 4 + (threadIdx.x >> 6); k < A.n_chunks; k += gridDim.x * 4)
+        compact_package(A, k, lane);
 }
 
 __global__ void k_seg_base(uint64_t* base, const uint64_t* off_last, const uint64_t* size_last) {
@@ -1117,7 +1122,10 @@ hipError_t launch_seg_base(uint64_t* base, const uint64_t* off_last, const uint6
 
 hipError_t launch_compact(const CompactArgs& a, hipStream_t s) {
     if (a.n_chunks == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_compact, dim3((a.n_chunks + 3) / 4), dim3(256), 0, s, a);
+    // beside the encoder: a resident grid; alone (the last segment): every package group
+    const uint32_t blocks = a.resident ? std::min<uint32_t>((a.n_chunks + 3) / 4, a.resident)
+                                       : (a.n_chunks + 3) / 4;
+    hipLaunchKernelGGL(k_compact, dim3(blocks), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -45,6 +45,7 @@ struct CompactArgs {
     const uint64_t* off;     // exclusive scan of sizes (n_chunks+1)
     const uint64_t* base;    // optional: body offset added to off[] (pipelined segments)
     uint32_t n_chunks;       // packages to write
+    uint32_t resident;       // > 0: a grid of this many workgroups striding over the packages
     uint64_t n_total;
     uint32_t chunk_size;
     uint8_t* out;
