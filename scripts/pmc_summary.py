@@ -31,6 +31,18 @@ def counter(d, name, kernel="k_encode"):
     return vals
 
 
+def kernel_totals(d, name):
+    """sum of a counter per kernel name over every dispatch of the run"""
+    tot = {}
+    for f in os.listdir(d):
+        if f.endswith("counter_collection.csv"):
+            with open(os.path.join(d, f)) as fh:
+                for r in csv.DictReader(fh):
+                    if r["Counter_Name"] == name:
+                        tot[r["Kernel_Name"]] = tot.get(r["Kernel_Name"], 0.0) + float(r["Counter_Value"])
+    return tot
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--round", required=True)
@@ -54,6 +66,19 @@ def main():
                "hbm_bytes_per_launch": int(f_kib * 1024 * 2 + w_kib * 1024),
                "note": "FETCH_SIZE x2 (gfx950: 16-B-per-lane streaming reads count half), "
                        "separate --pmc passes, median over launches"}
+        # whole compress call: every kernel of the call (encode, scan, segment
+        # bases, compaction, stats, end chunk, fills/copies), per call
+        fk, wk = kernel_totals(args.fetch, "FETCH_SIZE"), kernel_totals(args.write, "WRITE_SIZE")
+        calls = max(1, len(fetch) // 4)
+        skip = ("k_synth", "k_equal")
+        step_f = sum(v for k, v in fk.items() if not any(x in k for x in skip)) * 1024 * 2 / calls
+        step_w = sum(v for k, v in wk.items() if not any(x in k for x in skip)) * 1024 / calls
+        rec["whole_call"] = {"calls": calls, "fetch_bytes_corrected": int(step_f), "write_bytes": int(step_w),
+                             "hbm_bytes": int(step_f + step_w),
+                             "per_kernel_kib": {k.split("(")[0][-40:]: [round(fk.get(k, 0) / calls),
+                                                                         round(wk.get(k, 0) / calls)]
+                                                for k in sorted(set(fk) | set(wk))
+                                                if not any(x in k for x in skip)}}
         if args.bench:
             with open(args.bench) as fh:
                 b = json.loads(fh.read().strip().splitlines()[-1])

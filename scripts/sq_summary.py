@@ -39,7 +39,7 @@ def main():
     labels = a.labels.split(",") if a.labels else []
     res = {}
     for name in d1:
-        short = name.split("(")[0].replace("void ", "").replace("ambc::", "")
+        short = name.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("ambc::", "")
         if not any(k in short for k in a.kernels.split(",")):
             continue
         recs = [dict(x, **y) for x, y in zip(d1[name], d2.get(name, []))]
