@@ -812,6 +812,177 @@ __device__ int64_t dec_dict(const uint8_t* p, uint32_t plen, uint32_t orig, uint
     return __shfl(ret, 0);
 }
 
+// ---------------------------------------------------------------------------
+// Dictionary (id 2), parallel form: the token stream is self-delimiting
+// (flag 0: [0, b], else [1, dist_lo, dist_hi, len]; a token cut by the payload
+// end is one byte), so the decode runs like lz4_block_par: 256 payload
+// positions per step, every lane computes where the token at each of its
+// positions would end, the scalar unit follows the real chain (one v_readlane
+// per token), the marked tokens are laid out by wave prefix sums of their
+// output lengths and write source-map entries, and pointer jumping resolves
+// the map.  Semantics of DictionaryCompression.decompress
+// (compression_methods.py:236-281): tokens run while the output is shorter
+// than orig; a match copies output[len - dist + i] with Python indexing
+// (negative indices count from the current end; dist == 0 repeats the last
+// byte); an index error is the codec exception (orig zero bytes).
+// Returns min(output, orig), -1 for an index error.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t dict_next(uint32_t pos, uint32_t flag, uint32_t plen) {
+    return flag == 0 ? (pos + 1 < plen ? pos + 2 : pos + 1) : (pos + 3 < plen ? pos + 4 : pos + 1);
+}
+
+// source of output byte O + i of a match (O: output length before it); false: index error
+__device__ __forceinline__ bool dict_src(uint32_t O, uint32_t dist, uint32_t i, uint32_t& s) {
+    if (dist == 0) { s = O - 1; return O > 0; }              // decompressed[-1]
+    if (O >= dist) { s = O - dist + i % dist; return true; }  // the period before the match
+    const int32_t ix = (int32_t)O - (int32_t)dist + (int32_t)i;
+    if (ix >= 0) { s = (uint32_t)ix; return true; }
+    const int32_t py = (int32_t)(O + i) + ix;               // Python negative index
+    s = (uint32_t)py;
+    return py >= 0;
+}
+
+template <typename T>
+__device__ int64_t dec_dict_par(const uint8_t* g, uint32_t plen, uint32_t orig, T* src, uint32_t cap,
+                                uint32_t lane) {
+    constexpr uint32_t SRC_LIT = SrcLit<T>::v;
+    uint32_t op = 0, x0 = 0;
+    bool bad = false;
+    while (x0 < plen && op < orig) {
+        const uint32_t wlo = x0;
+        uint32_t fb[4], nx[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t pos = wlo + lane + 64 * q;
+            fb[q] = pos < plen ? g[pos] : 0u;
+            nx[q] = pos < plen ? dict_next(pos, fb[q], plen) : TOK_END;
+        }
+        // the token chain through this window (scalar)
+        uint64_t mk[4] = {0, 0, 0, 0};
+        uint32_t s = x0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t hi = wlo + 64u * (q + 1);
+            uint64_t m = 0;
+            while (s < hi && s < plen) {
+                const uint32_t r = s - wlo - 64u * q;
+                m |= 1ull << r;
+                s = readlane(nx[q], r);
+            }
+            mk[q] = m;
+        }
+        // output length of every marked token, laid out in position order; a
+        // token starting at or after orig is not run (the loop test), nor any after it
+        uint32_t kO[4], kol[4], kd[4], ky[4];
+        uint32_t base = op;
+        bool lng = false;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t pos = wlo + lane + 64 * q;
+            kol[q] = kd[q] = 0;
+            ky[q] = pos + 1;
+            if ((mk[q] >> lane) & 1) {
+                if (fb[q] == 0) {
+                    kol[q] = pos + 1 < plen ? 1u : 0u;
+                } else if (pos + 3 < plen) {
+                    kd[q] = (uint32_t)g[pos + 1] | (uint32_t)g[pos + 2] << 8;
+                    kol[q] = g[pos + 3];
+                }
+            }
+            const uint32_t incl = wave_incl_sum(kol[q]);
+            kO[q] = base + incl - kol[q];
+            base += readlane(incl, 63);
+        }
+        uint32_t run_end = base;            // output length after the last token run
+        bool stop = false;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const bool run = ((mk[q] >> lane) & 1) && kO[q] < orig;
+            const uint64_t cut = __ballot(((mk[q] >> lane) & 1) && kO[q] >= orig);
+            if (cut && !stop) {             // the first token not run: its start ends the output
+                run_end = readlane(kO[q], (uint32_t)__builtin_ctzll(cut));
+                stop = true;
+            }
+            if (!run) kol[q] = 0;
+            else lng |= kol[q] > 32;
+        }
+        if (run_end > cap) return -1;       // (cap >= orig + 255 by the host: never)
+        // source-map entries: literals and short matches per lane, long matches by the wave
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            if (kol[q] == 0 || kol[q] > 32) continue;
+            if (fb[q] == 0) {
+                src[kO[q]] = (T)(SRC_LIT | ky[q]);
+            } else if (kd[q] && kO[q] >= kd[q]) {   // the common case: the period before the match
+                const uint32_t m0 = kO[q] - kd[q];
+                uint32_t c = 0;
+                for (uint32_t i = 0; i < kol[q]; i++) {
+                    src[kO[q] + i] = (T)(m0 + c);
+                    if (++c == kd[q]) c = 0;
+                }
+            } else {
+                for (uint32_t i = 0; i < kol[q]; i++) {
+                    uint32_t sidx;
+                    bad |= !dict_src(kO[q], kd[q], i, sidx);
+                    src[kO[q] + i] = (T)sidx;
+                }
+            }
+        }
+        uint64_t lm = __ballot(lng);
+        while (lm) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(lm);
+            lm &= lm - 1;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t ol = readlane(kol[q], l);
+                if (ol <= 32) continue;
+                const uint32_t O = readlane(kO[q], l), dd = readlane(kd[q], l);
+                if (dd && O >= dd) {
+                    const uint32_t lmod = lane % dd;
+                    uint32_t bmod = 0;
+                    for (uint32_t b = 0; b < ol; b += 64) {
+                        uint32_t c = bmod + lmod;
+                        if (c >= dd) c -= dd;
+                        if (b + lane < ol) src[O + b + lane] = (T)(O - dd + c);
+                        bmod = (bmod + 64) % dd;
+                    }
+                } else {
+                    for (uint32_t b = 0; b < ol; b += 64)
+                        if (b + lane < ol) {
+                            uint32_t sidx;
+                            bad |= !dict_src(O, dd, b + lane, sidx);
+                            src[O + b + lane] = (T)sidx;
+                        }
+                }
+            }
+        }
+        op = run_end;
+        if (stop) break;
+        x0 = s;
+    }
+    if (__any(bad)) return -1;
+    wave_sync();
+    // pointer jumping: every entry names an earlier output byte or a payload byte
+    for (;;) {
+        bool more = false;
+        for (uint32_t q0 = lane * 4; q0 < op; q0 += 256) {
+            uint32_t v[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) v[k] = q0 + k < op ? src[q0 + k] : SRC_LIT;
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (!(v[k] & SRC_LIT)) {
+                    v[k] = src[v[k]];
+                    src[q0 + k] = (T)v[k];
+                    more |= !(v[k] & SRC_LIT);
+                }
+        }
+        wave_sync();
+        if (!__any(more)) break;
+    }
+    return (int64_t)min(op, orig);
+}
+
 // raw / verbatim / skip / RLE / Delta: no LDS beyond a 64-entry scan
 __device__ __forceinline__ bool decode_light(const DecJob& J, const uint8_t* p, uint8_t* out,
                                              uint32_t lane, uint32_t* scan, int64_t& produced) {
@@ -904,6 +1075,29 @@ __global__ __launch_bounds__(64) void k_decode_lz4_g(DecArgs A) {
             threadIdx.x);
 }
 
+// Dictionary packages whose output (+ one match of overshoot) fits the LDS map
+template <uint32_t OUTMAX>
+__global__ __launch_bounds__(64) void k_decode_dict(DecArgs A) {
+    __shared__ uint16_t src[OUTMAX];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t j = job_index(A);
+    const DecJob J = A.jobs[j];
+    const uint8_t* g = uniform_ptr(A.body + J.body_off);
+    uint8_t* out = uniform_ptr(A.out + J.out_off);
+    const uint32_t orig = uniform_u32(J.orig);
+    const int64_t r = dec_dict_par(g, uniform_u32(J.clen), orig, src, OUTMAX, lane);
+    wave_sync();
+    int64_t produced;
+    if (r < 0) {
+        wave_zero(out, orig, lane);
+        produced = orig;
+    } else {
+        lz4_gather(out, g, src, (uint32_t)r, lane);
+        produced = r;
+    }
+    put_produced(A, j, produced, lane);
+}
+
 // everything else: Huffman, Dictionary, LZ4 frames that need the serial decoder
 __global__ __launch_bounds__(64) void k_decode(DecArgs A) {
     __shared__ DecSmem S;
@@ -987,6 +1181,9 @@ hipError_t launch_decode(int kind, const DecArgs& a, hipStream_t s) {
     case DEC_KIND_LZ4_8K: hipLaunchKernelGGL(k_decode_lz4<8192>, dim3(a.n_list), dim3(64), 0, s, a); break;
     case DEC_KIND_LZ4_16K: hipLaunchKernelGGL(k_decode_lz4<16384>, dim3(a.n_list), dim3(64), 0, s, a); break;
     case DEC_KIND_LZ4_G: hipLaunchKernelGGL(k_decode_lz4_g, dim3(a.n_list), dim3(64), 0, s, a); break;
+    case DEC_KIND_DICT_4K: hipLaunchKernelGGL(k_decode_dict<4352>, dim3(a.n_list), dim3(64), 0, s, a); break;
+    case DEC_KIND_DICT_8K: hipLaunchKernelGGL(k_decode_dict<8448>, dim3(a.n_list), dim3(64), 0, s, a); break;
+    case DEC_KIND_DICT_16K: hipLaunchKernelGGL(k_decode_dict<16640>, dim3(a.n_list), dim3(64), 0, s, a); break;
     case DEC_KIND_INFLATE_4K:
     case DEC_KIND_INFLATE_8K:
     case DEC_KIND_INFLATE_16K: return launch_inflate(kind, a, s);

@@ -802,7 +802,10 @@ bool make_job(const uint8_t* body, uint64_t blen, uint64_t hp, uint32_t ord, con
                 sneed = (cb + 15) & ~15ull;
             }
         }
-        if (t == 2 && clen && (uint64_t)orig + 256 > STAGE_DEC) {
+        if (t == 2 && clen && clen <= 0x7FFF && (uint64_t)orig + 256 <= 16640) {
+            // dec_dict_par: an LDS source map of u16 entries (payload index < 0x8000)
+            kind = orig + 256 <= 4352 ? DEC_KIND_DICT_4K : orig + 256 <= 8448 ? DEC_KIND_DICT_8K : DEC_KIND_DICT_16K;
+        } else if (t == 2 && clen && (uint64_t)orig + 256 > STAGE_DEC) {
             j.scratch_cap = (uint64_t)orig + 256;
             sneed = (j.scratch_cap + 15) & ~15ull;
         }

@@ -135,3 +135,42 @@ def test_dict_wins_and_ties(ctx):
     ref, st = orc.compress_body(data, orc.make_params(4096, "native", (1, 2, 3, 4), n_total=len(data)))
     assert body == ref
     assert st.method_usage[2] > 0
+
+
+def _dict_tokens(rnd, n_tok, max_dist):
+    """a random Dictionary token stream: literals, matches with any distance
+    (0, beyond the output: Python negative indices, index errors) and length"""
+    out = bytearray()
+    for _ in range(n_tok):
+        if rnd.random() < 0.5:
+            out += bytes((0, rnd.randrange(256)))
+        else:
+            d = rnd.choice((0, 1, 2, 3, rnd.randrange(1, 64), rnd.randrange(1, max_dist)))
+            out += bytes((rnd.randrange(1, 256), d & 255, d >> 8, rnd.choice((0, 1, 3, 40, 255, rnd.randrange(256)))))
+    return bytes(out)
+
+
+def test_dict_parallel_decode_lenient_streams(ctx):
+    """dec_dict_par (k_decode_dict) against the oracle's restatement of
+    DictionaryCompression.decompress (compression_methods.py:236-281) on crafted
+    token streams: distances past the output start (negative indices, index
+    errors -> zeros), distance 0 (repeat the last byte), tokens cut by the
+    payload end, output reaching orig mid-window and mid-match, payloads that
+    run out before orig (short packages: the host re-walk)."""
+    import struct
+    from ambc import AdaptiveCompressor
+    rnd = random.Random(77)
+    pk, orig_total = [], 0
+    for k in range(400):
+        toks = _dict_tokens(rnd, rnd.randrange(1, 700), rnd.choice((8, 300, 5000, 65535)))
+        if k % 3 == 0:
+            toks = toks[:rnd.randrange(1, len(toks) + 1)]          # cut anywhere
+        if k % 5 == 0:                                             # valid prefix: literals first
+            toks = bytes((0, 65)) * rnd.randrange(1, 40) + toks
+        orig = rnd.choice((1, 7, 100, 1000, 4096, 4096, 8000, rnd.randrange(1, 8193)))
+        pk.append(b"\xff\xff\x00\x00" + bytes((2, 0)) + struct.pack("<III", len(toks), orig, len(toks)) + toks)
+        orig_total += orig
+    body = b"".join(pk) + b"\xff\xff\x00\x00" + bytes(12)
+    want = orc.decompress_body(body, orig_total)
+    comp = AdaptiveCompressor(chunk_size=4096, methods=(1, 2, 3, 4))
+    assert comp._adaptive_decompress(body, orig_total) == want
