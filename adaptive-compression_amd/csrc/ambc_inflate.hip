@@ -241,6 +241,248 @@ __device__ __forceinline__ int inf_sym(InfSmem<OUTMAX>& S, int t, InBits& I) {
     return -1;
 }
 
+// reposition the reader at absolute payload bit `bit`
+__device__ __forceinline__ void in_seek(InBits& I, uint32_t bit) {
+    I.pos = bit >> 3;
+    I.buf = 0;
+    I.cnt = 0;
+    in_window(I, I.pos & ~3u);
+    uint32_t v;
+    if (bit & 7) (void)in_take(I, bit & 7, v);
+}
+
+// one item (literal, length/distance pair or end of block) decoded serially
+// through the reader: 1 = end of block, 0 = item done, -1 invalid, -2 too large
+template <uint32_t OUTMAX>
+__device__ int inf_item_serial(InfSmem<OUTMAX>& S, InBits& I, uint32_t& op, uint32_t lane) {
+    const int sy = inf_sym(S, 0, I);
+    if (sy < 0) return -1;
+    if (sy < 256) {
+        if (op >= OUTMAX) return -2;
+        if (lane == 0) S.src[op] = (uint16_t)(IN_LIT | (uint32_t)sy);
+        op++;
+        return 0;
+    }
+    if (sy == 256) return 1;
+    const uint32_t k = (uint32_t)sy - 257;
+    if (k >= 29) return -1;  // 286, 287
+    uint32_t L;
+    if (k < 8) {
+        L = 3 + k;
+    } else if (k == 28) {
+        L = 258;
+    } else {
+        const uint32_t eb = (k >> 2) - 1, base = ((4u | (k & 3)) << eb) + 3;
+        uint32_t x;
+        if (!in_take(I, eb, x)) return -1;
+        L = base + x;
+    }
+    const int ds = inf_sym(S, 1, I);
+    if (ds < 0 || ds >= 30) return -1;
+    uint32_t D;
+    if (ds < 4) {
+        D = (uint32_t)ds + 1;
+    } else {
+        const uint32_t eb = ((uint32_t)ds >> 1) - 1, base = ((2u | ((uint32_t)ds & 1)) << eb) + 1;
+        uint32_t x;
+        if (!in_take(I, eb, x)) return -1;
+        D = base + x;
+    }
+    if (D > op) return -1;  // invalid distance too far back
+    if (op + L > OUTMAX) return -2;
+    // entries point into the period before the match (chains stay short)
+    const uint32_t m0 = op - D;
+    if (D >= L) {
+        for (uint32_t b = 0; b < L; b += 64)
+            if (b + lane < L) S.src[op + b + lane] = (uint16_t)(m0 + b + lane);
+    } else {
+        const uint32_t lmod = lane % D;
+        uint32_t bmod = 0;
+        for (uint32_t b = 0; b < L; b += 64) {
+            uint32_t c = bmod + lmod;
+            if (c >= D) c -= D;
+            if (b + lane < L) S.src[op + b + lane] = (uint16_t)(m0 + c);
+            bmod = (bmod + 64) % D;
+        }
+    }
+    op += L;
+    return 0;
+}
+
+// ---- speculative parallel symbol decode of one Huffman-coded block ----
+// Every lane decodes a whole item (literal, length + distance with their extra
+// bits, or end of block) at each of 4 bit positions of a 256-bit window
+// (lane l: window start + l + 64q) through the LDS tables; the scalar unit
+// then follows the real item chain with one v_readlane per item; the chain's
+// items are laid out by wave prefix sums of their output lengths, validated
+// (distance too far back, map overflow) and their source-map entries written
+// in parallel.  Codes longer than the table (canonical search) are decoded by
+// inf_item_serial in order.  Same results as the serial loop: any error in a
+// window is reported (an error and an overflow both end in orig zero bytes,
+// the overflow through the host zlib path).
+constexpr uint32_t IT_EOB = 0xFFFFFFF0u, IT_SLOW = 0xFFFFFFF1u, IT_ERR = 0xFFFFFFF2u;
+enum : uint32_t { IK_LIT = 0, IK_MATCH = 1, IK_EOB = 2, IK_OTHER = 3 };
+
+template <uint32_t OUTMAX>
+__device__ __forceinline__ uint32_t spec_item(const InfSmem<OUTMAX>& S, const uint8_t* g, uint32_t p,
+                                              uint32_t nbits, uint32_t& kind, uint32_t& val,
+                                              uint32_t& L, uint32_t& D) {
+    // 64 payload bits from bit p, zero past the payload (the body buffer has
+    // slack beyond every payload, so the three dword loads stay in bounds)
+    const uintptr_t a = reinterpret_cast<uintptr_t>(g) + (p >> 3);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3) * 8 + (p & 7);
+    const uint64_t lo = (uint64_t)w[0] | (uint64_t)w[1] << 32;
+    uint64_t b = sh ? (lo >> sh) | ((uint64_t)w[2] << (64 - sh)) : lo;
+    const uint32_t avail = nbits > p ? nbits - p : 0u;
+    if (avail < 64) b &= (1ull << avail) - 1;
+    kind = IK_OTHER;
+    val = L = D = 0;
+    const uint32_t e = S.lut[0][b & ((1u << LUTB) - 1)];
+    if (!(e & 1)) return e == LUT_LONG ? IT_SLOW : IT_ERR;
+    const uint32_t c1 = (e >> 1) & 15, sym = e >> 5;
+    uint32_t need = c1;
+    if (sym < 256) {
+        kind = IK_LIT;
+        val = sym;
+    } else if (sym == 256) {
+        kind = IK_EOB;
+        L = c1;                     // the code's length: where the block ends
+    } else {
+        const uint32_t k = sym - 257;
+        if (k >= 29) return IT_ERR;
+        uint32_t eb = 0, base;
+        if (k < 8) base = 3 + k;
+        else if (k == 28) base = 258;
+        else { eb = (k >> 2) - 1; base = ((4u | (k & 3)) << eb) + 3; }
+        L = base + (uint32_t)((b >> c1) & ((1u << eb) - 1));
+        const uint32_t o2 = c1 + eb;
+        const uint32_t e2 = S.lut[1][(b >> o2) & ((1u << LUTB) - 1)];
+        if (!(e2 & 1)) { kind = IK_OTHER; return e2 == LUT_LONG ? IT_SLOW : IT_ERR; }
+        const uint32_t c2 = (e2 >> 1) & 15, ds = e2 >> 5;
+        if (ds >= 30) return IT_ERR;
+        uint32_t deb = 0, dbase;
+        if (ds < 4) dbase = ds + 1;
+        else { deb = (ds >> 1) - 1; dbase = ((2u | (ds & 1)) << deb) + 1; }
+        D = dbase + (uint32_t)((b >> (o2 + c2)) & ((1u << deb) - 1));
+        need = o2 + c2 + deb;
+        kind = IK_MATCH;
+    }
+    if (need > avail) { kind = IK_OTHER; return IT_ERR; }   // the stream ends inside the item
+    return kind == IK_EOB ? IT_EOB : p + need;
+}
+
+// symbols of one Huffman block from the reader's position to its end-of-block
+// code; the reader is left after it.  0 done, -1 invalid, -2 too large.
+template <uint32_t OUTMAX>
+__device__ int inflate_block_par(InfSmem<OUTMAX>& S, InBits& I, const uint8_t* g, uint32_t plen,
+                                 uint32_t& op, uint32_t lane) {
+    const uint32_t nbits = plen * 8;
+    uint32_t p0 = __builtin_amdgcn_readfirstlane(I.pos * 8 - I.cnt);
+    for (;;) {
+        const uint32_t w0 = p0;
+        uint32_t nx[4], kd[4], vl[4], ln[4], dd[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) nx[q] = spec_item(S, g, w0 + lane + 64 * q, nbits, kd[q], vl[q], ln[q], dd[q]);
+        // the item chain through this window (scalar)
+        uint64_t mk[4] = {0, 0, 0, 0};
+        uint32_t s = p0, stop = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t hi = w0 + 64u * (q + 1);
+            uint64_t m = 0;
+            while (stop == 0 && s < hi) {
+                const uint32_t r = s - w0 - 64u * q;
+                const uint32_t t = readlane(nx[q], r);
+                if (t >= IT_EOB) {
+                    stop = t;
+                    if (t == IT_EOB) m |= 1ull << r;     // (no output; its end is read below)
+                } else {
+                    m |= 1ull << r;
+                    s = t;
+                }
+            }
+            mk[q] = m;
+        }
+        if (stop == IT_ERR) return -1;
+        // the chain's items in bit order: output offsets, checks, entries
+        uint32_t ko[4];
+        uint32_t base = op;
+        bool bad = false, big = false, lng = false;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const bool me = (mk[q] >> lane) & 1;
+            const uint32_t ol = me ? (kd[q] == IK_LIT ? 1u : kd[q] == IK_MATCH ? ln[q] : 0u) : 0u;
+            const uint32_t incl = wave_incl_sum(ol);
+            ko[q] = base + incl - ol;
+            base += readlane(incl, 63);
+            if (me && kd[q] == IK_MATCH) {
+                bad |= dd[q] > ko[q];
+                lng |= ln[q] > 32;
+            }
+            if (me && ol) big |= ko[q] + ol > OUTMAX;
+        }
+        if (__any(bad)) return -1;
+        if (__any(big)) return -2;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            if (!((mk[q] >> lane) & 1)) continue;
+            if (kd[q] == IK_LIT) {
+                S.src[ko[q]] = (uint16_t)(IN_LIT | vl[q]);
+            } else if (kd[q] == IK_MATCH && ln[q] <= 32) {
+                const uint32_t m0 = ko[q] - dd[q];
+                uint32_t c = 0;
+                for (uint32_t t = 0; t < ln[q]; t++) {
+                    S.src[ko[q] + t] = (uint16_t)(m0 + c);
+                    if (++c == dd[q]) c = 0;
+                }
+            }
+        }
+        uint64_t lm = __ballot(lng);
+        while (lm) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(lm);
+            lm &= lm - 1;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                if (!((mk[q] >> l) & 1) || readlane(kd[q], l) != IK_MATCH) continue;
+                const uint32_t Lm = readlane(ln[q], l);
+                if (Lm <= 32) continue;
+                const uint32_t O = readlane(ko[q], l), Dm = readlane(dd[q], l), m0 = O - Dm;
+                const uint32_t lmod = lane % Dm;
+                uint32_t bmod = 0;
+                for (uint32_t b = 0; b < Lm; b += 64) {
+                    uint32_t c = bmod + lmod;
+                    if (c >= Dm) c -= Dm;
+                    if (b + lane < Lm) S.src[O + b + lane] = (uint16_t)(m0 + c);
+                    bmod = (bmod + 64) % Dm;
+                }
+            }
+        }
+        op = base;
+        if (stop == IT_EOB) {                    // the block ends after the end-of-block code
+            const uint32_t r = s - w0;
+            uint32_t c1;
+            switch (r >> 6) {   // (constant register indices)
+            case 0: c1 = readlane(ln[0], r & 63); break;
+            case 1: c1 = readlane(ln[1], r & 63); break;
+            case 2: c1 = readlane(ln[2], r & 63); break;
+            default: c1 = readlane(ln[3], r & 63); break;
+            }
+            in_seek(I, s + c1);
+            return 0;
+        }
+        if (stop == IT_SLOW) {                   // a code beyond the table: the serial decoder
+            in_seek(I, s);
+            const int rc = inf_item_serial(S, I, op, lane);
+            if (rc < 0) return rc;
+            if (rc == 1) return 0;
+            p0 = __builtin_amdgcn_readfirstlane(I.pos * 8 - I.cnt);
+            continue;
+        }
+        p0 = s;
+    }
+}
+
 // the whole zlib stream; returns the decoded length, -1 invalid, -2 output
 // larger than OUTMAX (host path)
 #ifdef AMBC_STAMPS
@@ -358,60 +600,9 @@ __device__ int64_t inflate_stream(InfSmem<OUTMAX>& S, const uint8_t* g, uint32_t
                 if (!uniform_u32(inf_build(S, 1, S.lens + 288, 32, 1, lane))) return -1;
             }
             ISTAMP(0);
-            // symbols
-            for (;;) {
-                const int sy = inf_sym(S, 0, I);
-                if (sy < 0) return -1;
-                if (sy < 256) {
-                    if (op >= OUTMAX) return -2;
-                    if (lane == 0) S.src[op] = (uint16_t)(IN_LIT | (uint32_t)sy);
-                    op++;
-                    continue;
-                }
-                if (sy == 256) break;
-                const uint32_t k = (uint32_t)sy - 257;
-                if (k >= 29) return -1;  // 286, 287
-                uint32_t L;
-                if (k < 8) {
-                    L = 3 + k;
-                } else if (k == 28) {
-                    L = 258;
-                } else {
-                    const uint32_t eb = (k >> 2) - 1, base = ((4u | (k & 3)) << eb) + 3;
-                    uint32_t x;
-                    if (!in_take(I, eb, x)) return -1;
-                    L = base + x;
-                }
-                const int ds = inf_sym(S, 1, I);
-                if (ds < 0 || ds >= 30) return -1;
-                uint32_t D;
-                if (ds < 4) {
-                    D = (uint32_t)ds + 1;
-                } else {
-                    const uint32_t eb = ((uint32_t)ds >> 1) - 1, base = ((2u | ((uint32_t)ds & 1)) << eb) + 1;
-                    uint32_t x;
-                    if (!in_take(I, eb, x)) return -1;
-                    D = base + x;
-                }
-                if (D > op) return -1;  // invalid distance too far back
-                if (op + L > OUTMAX) return -2;
-                // entries point into the period before the match (chains stay short)
-                const uint32_t m0 = op - D;
-                if (D >= L) {
-                    if (lane < L) S.src[op + lane] = (uint16_t)(m0 + lane);
-                    for (uint32_t b = 64; b < L; b += 64)
-                        if (b + lane < L) S.src[op + b + lane] = (uint16_t)(m0 + b + lane);
-                } else {
-                    const uint32_t lmod = lane % D;
-                    uint32_t bmod = 0;
-                    for (uint32_t b = 0; b < L; b += 64) {
-                        uint32_t c = bmod + lmod;
-                        if (c >= D) c -= D;
-                        if (b + lane < L) S.src[op + b + lane] = (uint16_t)(m0 + c);
-                        bmod = (bmod + 64) % D;
-                    }
-                }
-                op += L;
+            {
+                const int rc = inflate_block_par(S, I, g, plen, op, lane);
+                if (rc < 0) return rc;
             }
             ISTAMP(1);
         } else {
