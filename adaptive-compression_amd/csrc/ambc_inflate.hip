@@ -323,17 +323,34 @@ __device__ int inf_item_serial(InfSmem<OUTMAX>& S, InBits& I, uint32_t& op, uint
 constexpr uint32_t IT_EOB = 0xFFFFFFF0u, IT_SLOW = 0xFFFFFFF1u, IT_ERR = 0xFFFFFFF2u;
 enum : uint32_t { IK_LIT = 0, IK_MATCH = 1, IK_EOB = 2, IK_OTHER = 3 };
 
+// the payload as dwords of the 4-aligned stream around it: 64 of them in a
+// register (dword wbase + lane), the bits of any position fetched by ds_bpermute
+struct SpecWin {
+    const uint32_t* a0;   // payload start rounded down to 4 bytes
+    uint32_t boff;        // bit offset of payload byte 0 in that stream
+    uint32_t ndw;         // dwords that may be read (payload + the body's slack)
+    uint32_t wbase;       // stream dword held by lane 0
+    uint32_t v;
+};
+
+__device__ __forceinline__ void spec_win_at(SpecWin& W, uint32_t dw, uint32_t lane) {
+    W.wbase = __builtin_amdgcn_readfirstlane(dw);
+    W.v = W.wbase + lane < W.ndw ? W.a0[W.wbase + lane] : 0u;
+}
+
 template <uint32_t OUTMAX>
-__device__ __forceinline__ uint32_t spec_item(const InfSmem<OUTMAX>& S, const uint8_t* g, uint32_t p,
+__device__ __forceinline__ uint32_t spec_item(const InfSmem<OUTMAX>& S, const SpecWin& W, uint32_t p,
                                               uint32_t nbits, uint32_t& kind, uint32_t& val,
                                               uint32_t& L, uint32_t& D) {
-    // 64 payload bits from bit p, zero past the payload (the body buffer has
-    // slack beyond every payload, so the three dword loads stay in bounds)
-    const uintptr_t a = reinterpret_cast<uintptr_t>(g) + (p >> 3);
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
-    const uint32_t sh = (uint32_t)(a & 3) * 8 + (p & 7);
-    const uint64_t lo = (uint64_t)w[0] | (uint64_t)w[1] << 32;
-    uint64_t b = sh ? (lo >> sh) | ((uint64_t)w[2] << (64 - sh)) : lo;
+    // 64 payload bits from bit p (zero past the payload): three window dwords
+    const uint32_t P = p + W.boff;
+    const int di = (int)((P >> 5) - W.wbase) << 2;
+    const uint32_t sh = P & 31;
+    const uint32_t d0 = (uint32_t)__builtin_amdgcn_ds_bpermute(di, (int)W.v);
+    const uint32_t d1 = (uint32_t)__builtin_amdgcn_ds_bpermute(di + 4, (int)W.v);
+    const uint32_t d2 = (uint32_t)__builtin_amdgcn_ds_bpermute(di + 8, (int)W.v);
+    const uint64_t lo = (uint64_t)d0 | (uint64_t)d1 << 32;
+    uint64_t b = sh ? (lo >> sh) | ((uint64_t)d2 << (64 - sh)) : lo;
     const uint32_t avail = nbits > p ? nbits - p : 0u;
     if (avail < 64) b &= (1ull << avail) - 1;
     kind = IK_OTHER;
@@ -379,11 +396,19 @@ __device__ int inflate_block_par(InfSmem<OUTMAX>& S, InBits& I, const uint8_t* g
                                  uint32_t& op, uint32_t lane) {
     const uint32_t nbits = plen * 8;
     uint32_t p0 = __builtin_amdgcn_readfirstlane(I.pos * 8 - I.cnt);
+    SpecWin W;
+    W.a0 = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(g) & ~(uintptr_t)3);
+    W.boff = (uint32_t)(reinterpret_cast<uintptr_t>(g) & 3) * 8;
+    W.ndw = (W.boff / 8 + plen + 64) / 4;
+    spec_win_at(W, (p0 + W.boff) >> 5, lane);
     for (;;) {
         const uint32_t w0 = p0;
+        // positions w0 .. w0 + 255 read up to 64 bits each: stream dwords
+        // (w0 + boff) / 32 .. + 10 must be in the register window
+        if (((w0 + W.boff) >> 5) + 11 > W.wbase + 64) spec_win_at(W, (w0 + W.boff) >> 5, lane);
         uint32_t nx[4], kd[4], vl[4], ln[4], dd[4];
 #pragma unroll
-        for (int q = 0; q < 4; q++) nx[q] = spec_item(S, g, w0 + lane + 64 * q, nbits, kd[q], vl[q], ln[q], dd[q]);
+        for (int q = 0; q < 4; q++) nx[q] = spec_item(S, W, w0 + lane + 64 * q, nbits, kd[q], vl[q], ln[q], dd[q]);
         // the item chain through this window (scalar)
         uint64_t mk[4] = {0, 0, 0, 0};
         uint32_t s = p0, stop = 0;
@@ -557,12 +582,20 @@ __device__ int64_t inflate_stream(InfSmem<OUTMAX>& S, const uint8_t* g, uint32_t
                 }
                 wave_sync();
                 if (!uniform_u32(inf_build(S, 0, S.lens, 19, 0, lane))) return -1;
+                // code-length codes are at most 7 bits: their 128 table entries
+                // in one register (lane l: entries 2l, 2l + 1), one v_readlane each
+                const uint32_t clut = reinterpret_cast<const uint32_t*>(S.lut[0])[lane];
                 uint32_t have = 0;
                 const uint32_t tot = nlen + ndist;
                 uint32_t lastlen = 0;
                 while (have < tot) {
-                    const int sy = inf_sym(S, 0, I);
-                    if (sy < 0) return -1;
+                    if (I.cnt < 15) in_fill(I);
+                    const uint32_t x = __builtin_amdgcn_readfirstlane((uint32_t)I.buf & 127u);
+                    const uint32_t e = (readlane(clut, x >> 1) >> ((x & 1) * 16)) & 0xFFFFu;
+                    if (!(e & 1) || ((e >> 1) & 15) > I.cnt) return -1;
+                    I.buf >>= (e >> 1) & 15;
+                    I.cnt -= (e >> 1) & 15;
+                    const int sy = (int)(e >> 5);
                     uint32_t ln = 0, copy = 1;
                     if (sy < 16) {
                         ln = (uint32_t)sy;
