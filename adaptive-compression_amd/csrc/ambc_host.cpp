@@ -97,7 +97,8 @@ void ambc_destroy(ambc_ctx* ctx) {
         (void)hipStreamSynchronize(d.stream);
         for (Buf* b : {&d.in, &d.out, &d.slots, &d.plen, &d.ids, &d.sizes, &d.off, &d.scan_tmp,
                        &d.acc, &d.ent_full, &d.ent_tail, &d.body, &d.jobs, &d.produced, &d.dout,
-                       &d.scratch, &d.seg, &d.list, &d.bestpre, &d.gdseq, &d.pending, &d.segbase, &d.coll})
+                       &d.scratch, &d.seg, &d.list, &d.bestpre, &d.gdseq, &d.pending, &d.segbase, &d.coll,
+                       &d.inffix})
             b->release();
         for (void* b : d.stage) (void)hipHostFree(b);
         for (auto& ev : d.stage_ev) (void)hipEventDestroy(ev);
@@ -1231,6 +1232,12 @@ int ambc::decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t ori
         a.n_jobs = nj;
         a.scratch = d.scratch.as<uint8_t>();
         a.produced = d.produced.as<uint32_t>();
+        if (!d.inffix_ok) {
+            HIPCHK(d.inffix.ensure(INF_FIXED_U16 * 2));
+            HIPCHK(launch_inflate_fixed_tables(d.inffix.as<uint16_t>(), s));
+            d.inffix_ok = true;
+        }
+        a.inf_fixed = d.inffix.as<uint16_t>();
         if (getenv("AMBC_STAMPS") && nj) {
             HIPCHK(d.seg.ensure((size_t)nj * 64));
             HIPCHK(hipMemsetAsync(d.seg.p, 0, (size_t)nj * 64, s));

@@ -77,6 +77,8 @@ struct Dev {
     Buf in, out, slots, plen, ids, sizes, off, scan_tmp, acc, ent_full, ent_tail;
     Buf body, jobs, produced, dout, scratch, seg, list, bestpre, gdseq, pending;
     Buf coll;                   // small device buffers of the collectives (sizes, stats, flags)
+    Buf inffix;                 // fixed-Huffman inflate tables (built on the first decode)
+    bool inffix_ok = false;
     uint64_t t_encode = 0, t_scan = 0, t_compact = 0;
     uint32_t n_launch = 1;      // k_encode launches of the last compress call (pipelined segments)
     hipStream_t cs = nullptr;   // scan + compaction of pipelined segments

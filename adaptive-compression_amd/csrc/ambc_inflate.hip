@@ -143,9 +143,8 @@ __device__ bool inf_build(InfSmem<OUTMAX>& S, int t, const uint8_t* len, int nsy
         count[b] = c;
         if (c) maxl = b;
     }
-    // table fill: every entry "no code" first
-    for (uint32_t i = lane; i < (1u << LUTB); i += 64) S.lut[t][i] = LUT_BAD;
     if (maxl == 0) {  // no symbols: decoding any code is an error (zlib: valid table)
+        for (uint32_t i = lane; i < (1u << LUTB); i += 64) S.lut[t][i] = LUT_BAD;
         if (lane < 16) { S.cnt[t][lane] = 0; S.first[t][lane] = 0; S.offs[t][lane] = 0; }
         wave_sync();
         return true;
@@ -161,10 +160,16 @@ __device__ bool inf_build(InfSmem<OUTMAX>& S, int t, const uint8_t* len, int nsy
     // canonical codes; sorted order (length, symbol)
     uint32_t first = 0, prev = 0, off = 0;
     uint32_t code[J];
+    uint32_t fL[LUTB + 1], oL[LUTB + 1], lim[LUTB + 1];   // per length <= LUTB (wave-uniform)
     const uint64_t lt = (1ull << lane) - 1;
 #pragma unroll
     for (int b = 1; b < 16; b++) {
         first = (first + prev) << 1;
+        if (b <= LUTB) {
+            fL[b] = first;
+            oL[b] = off;
+            lim[b] = (first + count[b]) << (LUTB - b);
+        }
         if (lane == (uint32_t)b) {
             S.first[t][b] = (uint16_t)first;
             S.cnt[t][b] = (uint16_t)count[b];
@@ -185,24 +190,24 @@ __device__ bool inf_build(InfSmem<OUTMAX>& S, int t, const uint8_t* len, int nsy
         off += count[b];
     }
     wave_sync();
-    // lookup entries: entry x holds the code whose bits (read LSB first) prefix x
-    const uint32_t first10 = (uint32_t)S.first[t][LUTB], cnt10 = count[LUTB];
-    (void)first10;
+    // lookup entries: entry x holds the code whose bits (read LSB first) prefix
+    // x.  Left-justified, a canonical code's codes of length L fill the 10-bit
+    // MSB-first range [fL[L] << (10 - L), lim[L]) and the ranges follow each
+    // other by length: the first L with v < lim[L] is the code's length
     for (uint32_t x = lane; x < (1u << LUTB); x += 64) {
         const uint32_t v = __builtin_bitreverse32(x) >> (32 - LUTB);  // MSB-first 10-bit window
-        uint16_t e = LUT_BAD;
-        uint32_t f = 0, pv = 0, of = 0;
+        uint32_t L = 0, f = 0, o = 0;
 #pragma unroll
-        for (int L = 1; L <= LUTB; L++) {
-            f = (f + pv) << 1;                 // first code of length L (same recurrence)
-            const uint32_t c = v >> (LUTB - L);
-            if (e == LUT_BAD && count[L] && c >= f && c - f < count[L])
-                e = (uint16_t)(S.sorted[t][of + (c - f)] << 5 | (uint32_t)L << 1 | 1);
-            pv = count[L];
-            of += count[L];
+        for (int b = LUTB; b >= 1; b--) {
+            const bool in = v < lim[b];
+            L = in ? (uint32_t)b : L;
+            f = in ? fL[b] : f;
+            o = in ? oL[b] : o;
         }
-        if (e == LUT_BAD && maxl > (uint32_t)LUTB && v >= f + cnt10) e = LUT_LONG;
-        S.lut[t][x] = e;
+        uint32_t e;
+        if (L) e = (uint32_t)S.sorted[t][o + (v >> (LUTB - L)) - f] << 5 | L << 1 | 1;
+        else e = maxl > (uint32_t)LUTB ? LUT_LONG : LUT_BAD;   // a longer code, or none (incomplete set)
+        S.lut[t][x] = (uint16_t)e;
     }
     (void)code;
     wave_sync();
@@ -239,6 +244,43 @@ __device__ __forceinline__ int inf_sym(InfSmem<OUTMAX>& S, int t, InBits& I) {
         }
     }
     return -1;
+}
+
+// the fixed-Huffman block's tables (RFC 1951 3.2.6): literal/length 0..287,
+// distance 0..29 (+30, 31: codes that decode as invalid)
+template <uint32_t OUTMAX>
+__device__ void fixed_tables_build(InfSmem<OUTMAX>& S, uint32_t lane) {
+    for (uint32_t s = lane; s < 320; s += 64)
+        S.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : 5;
+    wave_sync();
+    (void)inf_build(S, 0, S.lens, 288, 1, lane);
+    (void)inf_build(S, 1, S.lens + 288, 32, 1, lane);
+}
+
+// table parts of InfSmem in the global layout of launch_inflate_fixed_tables:
+// lut[2][1024] | sorted[2][288] | first[2][16] | cnt[2][16] | offs[2][16]
+template <uint32_t OUTMAX>
+__device__ __forceinline__ uint16_t* fixed_part(InfSmem<OUTMAX>& S, uint32_t i) {
+    if (i < 2048) return &S.lut[0][0] + i;
+    i -= 2048;
+    if (i < 576) return &S.sorted[0][0] + i;
+    i -= 576;
+    if (i < 32) return &S.first[0][0] + i;
+    i -= 32;
+    if (i < 32) return &S.cnt[0][0] + i;
+    return &S.offs[0][0] + (i - 32);
+}
+
+template <uint32_t OUTMAX>
+__device__ __forceinline__ void fixed_tables_in(InfSmem<OUTMAX>& S, const uint16_t* fixed, uint32_t lane) {
+    for (uint32_t i = lane; i < INF_FIXED_U16; i += 64) *fixed_part(S, i) = fixed[i];
+    wave_sync();
+}
+
+__global__ __launch_bounds__(64) void k_inflate_fixed(uint16_t* out) {
+    __shared__ InfSmem<64> S;
+    fixed_tables_build(S, threadIdx.x);
+    for (uint32_t i = threadIdx.x; i < INF_FIXED_U16; i += 64) out[i] = *fixed_part(S, i);
 }
 
 // reposition the reader at absolute payload bit `bit`
@@ -518,7 +560,8 @@ __device__ int inflate_block_par(InfSmem<OUTMAX>& S, InBits& I, const uint8_t* g
 #define ISTAMP_ARGS
 #endif
 template <uint32_t OUTMAX>
-__device__ int64_t inflate_stream(InfSmem<OUTMAX>& S, const uint8_t* g, uint32_t plen, uint32_t lane ISTAMP_PARAMS) {
+__device__ int64_t inflate_stream(InfSmem<OUTMAX>& S, const uint8_t* g, uint32_t plen, const uint16_t* fixed,
+                                  uint32_t lane ISTAMP_PARAMS) {
     InBits I;
     I.g = g;
     I.plen = plen;
@@ -561,13 +604,10 @@ __device__ int64_t inflate_stream(InfSmem<OUTMAX>& S, const uint8_t* g, uint32_t
             I.pos += ln - k;
             op += ln;
         } else if (btype == 1 || btype == 2) {
-            if (btype == 1) {
-                for (uint32_t s = lane; s < 320; s += 64)
-                    S.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : (s < 320 ? 5 : 0);
-                wave_sync();
-                // literal/length 0..287, distance 0..29 (+30, 31: codes that decode as invalid)
-                if (!uniform_u32(inf_build(S, 0, S.lens, 288, 1, lane))) return -1;
-                if (!uniform_u32(inf_build(S, 1, S.lens + 288, 32, 1, lane))) return -1;
+            if (btype == 1 && fixed) {
+                fixed_tables_in(S, fixed, lane);     // built once per device
+            } else if (btype == 1) {
+                fixed_tables_build(S, lane);
             } else {
                 uint32_t h;
                 if (!in_take(I, 14, h)) return -1;
@@ -694,7 +734,8 @@ __global__ __launch_bounds__(64) void k_decode_inflate(DecArgs A) {
     uint64_t _st_t = __builtin_amdgcn_s_memtime();
     uint64_t _acc[4] = {0, 0, 0, 0};
 #endif
-    const int64_t r = inflate_stream(S, uniform_ptr(A.body + J.body_off), uniform_u32(J.clen), lane ISTAMP_ARGS);
+    const int64_t r = inflate_stream(S, uniform_ptr(A.body + J.body_off), uniform_u32(J.clen), A.inf_fixed,
+                                     lane ISTAMP_ARGS);
     wave_sync();
     if (r == -2) {  // larger than the map: the host inflates it
         if (lane == 0) A.produced[j] = 0xFFFFFFFEu;
@@ -727,6 +768,11 @@ __global__ __launch_bounds__(64) void k_decode_inflate(DecArgs A) {
 }
 
 }  // namespace
+
+hipError_t launch_inflate_fixed_tables(uint16_t* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_inflate_fixed, dim3(1), dim3(64), 0, s, out);
+    return hipGetLastError();
+}
 
 hipError_t launch_inflate(int kind, const DecArgs& a, hipStream_t s) {
     if (a.n_list == 0) return hipSuccess;

@@ -74,6 +74,7 @@ struct DecArgs {
     unsigned long long* stamps;  // diagnostic build (-DAMBC_STAMPS): per-job phase cycles
     const uint32_t* list;   // job indices this launch decodes (nullptr = 0..n_jobs-1)
     uint32_t n_list;
+    const uint16_t* inf_fixed;  // optional: the fixed-Huffman decode tables (launch_inflate_fixed_tables)
 };
 
 // decode kernels by LDS footprint (host routes each job to one of them)
@@ -101,6 +102,9 @@ hipError_t scan_sizes(const uint64_t* sizes, uint64_t* off, uint32_t count, void
 hipError_t launch_copy(uint8_t* dst, const uint8_t* src, uint64_t len, hipStream_t s);
 hipError_t launch_decode(int kind, const DecArgs& a, hipStream_t s);
 hipError_t launch_inflate(int kind, const DecArgs& a, hipStream_t s);   // ambc_inflate.hip
+// the fixed-Huffman (btype 1) decode tables, built once per device into out
+constexpr size_t INF_FIXED_U16 = 2 * 1024 + 2 * 288 + 3 * 2 * 16;
+hipError_t launch_inflate_fixed_tables(uint16_t* out, hipStream_t s);
 // bytes [lo, hi) of the synthetic stream (segment table seg) into out[0, hi - lo)
 hipError_t launch_synth(uint8_t* out, uint64_t lo, uint64_t hi, const uint64_t* seg, uint32_t nseg,
                         uint64_t seed, hipStream_t s);

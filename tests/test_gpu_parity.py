@@ -534,6 +534,8 @@ def _zero_then_random():
 
 
 @pytest.mark.parametrize("methods,cands", [((1, 3, 4), REF_CANDS), ((1, 3, 4, 9), REF_CANDS),
+                                           ((1, 2, 3, 4), REF_CANDS),           # Dictionary: <= 8192 by prefs
+                                           ((1, 2, 3, 4, 9), REF_CANDS),
                                            ((1, 3, 4, 5), [16384, 8192, 4096, 2048, 1024])])
 def test_multisize_walk_matches_oracle(ctx, methods, cands):
     inputs = [synth.generate(12288, 3), synth.generate(65536, 21), synth.generate(200000, 22),
@@ -550,6 +552,41 @@ def test_multisize_walk_matches_oracle(ctx, methods, cands):
         assert comp._adaptive_decompress(body, len(data)) == data
         blob, stats = comp.compress_bytes(data)           # header, MD5, raw fallback
         assert comp.decompress_bytes(blob) == data if blob[:4] == b"AMBC" else blob == data
+
+
+def test_multisize_lookahead_runs_match_serial_walk(ctx):
+    """The look-ahead runs (many same-size chunks per call, past 16384 chunks
+    per run so a run takes the segmented pipeline) give the body and stats of
+    the plain serial walk (one call per candidate and position)."""
+    import numpy as np
+    rng = np.random.default_rng(11)
+    parts = []
+    while sum(len(x) for x in parts) < (18 << 20):
+        k = int(rng.integers(3))
+        m = int(rng.integers(8, 65)) << 10
+        if k == 0:
+            parts.append(np.repeat(rng.integers(0, 256, m // 256 + 1, dtype=np.uint8), 256)[:m].tobytes())
+        elif k == 1:
+            parts.append(rng.choice(np.frombuffer(b"etaoin shrdlu,.ETAOIN", np.uint8), m).tobytes())
+        else:
+            parts.append(np.minimum(rng.geometric(0.08, m), 255).astype(np.uint8).tobytes())
+    data = b"".join(parts)[:18 << 20]
+    bodies, stats = [], []
+    for la, run in ((True, 17 << 20), (True, 1 << 20), (False, 0)):
+        comp = _compressor(methods=(1, 3, 4, 9))
+        comp.CHUNK_SIZE_CANDIDATES = [2048, 1024]          # a 1024-byte run of 17 MiB: 17408 chunks
+        comp.MULTISIZE_LOOKAHEAD = la
+        if run:
+            comp.MULTISIZE_RUN_BYTES = run
+        src = data if la else data[:1 << 20]
+        bodies.append(comp._adaptive_compress(src))
+        stats.append(dict(comp.chunk_stats))
+    assert bodies[0] == bodies[1] and stats[0] == stats[1]
+    ref1, _ = orc.compress_body_multisize(data[:1 << 20], [2048, 1024], (1, 3, 4, 9, 255))
+    assert bodies[2] == ref1
+    comp = _compressor(methods=(1, 3, 4, 9))
+    comp.CHUNK_SIZE_CANDIDATES = [2048, 1024]
+    assert comp._adaptive_compress(data[:1 << 20]) == ref1
 
 
 def test_multisize_rejects_oversize_gpu_chunks(ctx):
