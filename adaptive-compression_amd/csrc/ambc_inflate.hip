@@ -39,7 +39,7 @@ namespace {
 #endif
 
 constexpr uint32_t IN_LIT = 0x8000u;
-constexpr int LUTB = 10;            // primary lookup bits
+constexpr int LUTB = INF_LUTB;       // primary lookup bits (9: 2 KB of tables, 13 workgroups/CU at 4 KiB)
 // lookup entries: symbol << 5 | length << 1 | 1; 0 = no code, 2 = a code
 // longer than LUTB bits (canonical search)
 constexpr uint16_t LUT_BAD = 0;
@@ -195,7 +195,7 @@ __device__ bool inf_build(InfSmem<OUTMAX>& S, int t, const uint8_t* len, int nsy
     // MSB-first range [fL[L] << (10 - L), lim[L]) and the ranges follow each
     // other by length: the first L with v < lim[L] is the code's length
     for (uint32_t x = lane; x < (1u << LUTB); x += 64) {
-        const uint32_t v = __builtin_bitreverse32(x) >> (32 - LUTB);  // MSB-first 10-bit window
+        const uint32_t v = __builtin_bitreverse32(x) >> (32 - LUTB);  // MSB-first LUTB-bit window
         uint32_t L = 0, f = 0, o = 0;
 #pragma unroll
         for (int b = LUTB; b >= 1; b--) {
@@ -258,11 +258,11 @@ __device__ void fixed_tables_build(InfSmem<OUTMAX>& S, uint32_t lane) {
 }
 
 // table parts of InfSmem in the global layout of launch_inflate_fixed_tables:
-// lut[2][1024] | sorted[2][288] | first[2][16] | cnt[2][16] | offs[2][16]
+// lut[2][1 << LUTB] | sorted[2][288] | first[2][16] | cnt[2][16] | offs[2][16]
 template <uint32_t OUTMAX>
 __device__ __forceinline__ uint16_t* fixed_part(InfSmem<OUTMAX>& S, uint32_t i) {
-    if (i < 2048) return &S.lut[0][0] + i;
-    i -= 2048;
+    if (i < (2u << LUTB)) return &S.lut[0][0] + i;
+    i -= 2u << LUTB;
     if (i < 576) return &S.sorted[0][0] + i;
     i -= 576;
     if (i < 32) return &S.first[0][0] + i;

@@ -103,7 +103,8 @@ hipError_t launch_copy(uint8_t* dst, const uint8_t* src, uint64_t len, hipStream
 hipError_t launch_decode(int kind, const DecArgs& a, hipStream_t s);
 hipError_t launch_inflate(int kind, const DecArgs& a, hipStream_t s);   // ambc_inflate.hip
 // the fixed-Huffman (btype 1) decode tables, built once per device into out
-constexpr size_t INF_FIXED_U16 = 2 * 1024 + 2 * 288 + 3 * 2 * 16;
+constexpr int INF_LUTB = 9;   // primary lookup bits of the inflate tables (longer codes: canonical search)
+constexpr size_t INF_FIXED_U16 = 2 * (1 << INF_LUTB) + 2 * 288 + 3 * 2 * 16;
 hipError_t launch_inflate_fixed_tables(uint16_t* out, hipStream_t s);
 // bytes [lo, hi) of the synthetic stream (segment table seg) into out[0, hi - lo)
 hipError_t launch_synth(uint8_t* out, uint64_t lo, uint64_t hi, const uint64_t* seg, uint32_t nseg,
