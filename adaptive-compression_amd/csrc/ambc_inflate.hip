@@ -395,40 +395,30 @@ __device__ __forceinline__ uint32_t spec_item(const InfSmem<OUTMAX>& S, const Sp
     uint64_t b = sh ? (lo >> sh) | ((uint64_t)d2 << (64 - sh)) : lo;
     const uint32_t avail = nbits > p ? nbits - p : 0u;
     if (avail < 64) b &= (1ull << avail) - 1;
-    kind = IK_OTHER;
-    val = L = D = 0;
+    // branch-free: both the literal and the length/distance reading are
+    // computed for every lane (the distance table is read unconditionally)
     const uint32_t e = S.lut[0][b & ((1u << LUTB) - 1)];
-    if (!(e & 1)) return e == LUT_LONG ? IT_SLOW : IT_ERR;
     const uint32_t c1 = (e >> 1) & 15, sym = e >> 5;
-    uint32_t need = c1;
-    if (sym < 256) {
-        kind = IK_LIT;
-        val = sym;
-    } else if (sym == 256) {
-        kind = IK_EOB;
-        L = c1;                     // the code's length: where the block ends
-    } else {
-        const uint32_t k = sym - 257;
-        if (k >= 29) return IT_ERR;
-        uint32_t eb = 0, base;
-        if (k < 8) base = 3 + k;
-        else if (k == 28) base = 258;
-        else { eb = (k >> 2) - 1; base = ((4u | (k & 3)) << eb) + 3; }
-        L = base + (uint32_t)((b >> c1) & ((1u << eb) - 1));
-        const uint32_t o2 = c1 + eb;
-        const uint32_t e2 = S.lut[1][(b >> o2) & ((1u << LUTB) - 1)];
-        if (!(e2 & 1)) { kind = IK_OTHER; return e2 == LUT_LONG ? IT_SLOW : IT_ERR; }
-        const uint32_t c2 = (e2 >> 1) & 15, ds = e2 >> 5;
-        if (ds >= 30) return IT_ERR;
-        uint32_t deb = 0, dbase;
-        if (ds < 4) dbase = ds + 1;
-        else { deb = (ds >> 1) - 1; dbase = ((2u | (ds & 1)) << deb) + 1; }
-        D = dbase + (uint32_t)((b >> (o2 + c2)) & ((1u << deb) - 1));
-        need = o2 + c2 + deb;
-        kind = IK_MATCH;
-    }
-    if (need > avail) { kind = IK_OTHER; return IT_ERR; }   // the stream ends inside the item
-    return kind == IK_EOB ? IT_EOB : p + need;
+    const bool lit = sym < 256, eob = sym == 256;
+    const uint32_t k = min(sym - 257u, 28u);                  // (literals: clamped, unused)
+    const uint32_t eb = (k < 8 || k == 28) ? 0u : (k >> 2) - 1;
+    const uint32_t lbase = k < 8 ? 3 + k : k == 28 ? 258u : ((4u | (k & 3)) << eb) + 3;
+    const uint32_t o2 = c1 + eb;
+    const uint32_t e2 = S.lut[1][(b >> o2) & ((1u << LUTB) - 1)];
+    const uint32_t c2 = (e2 >> 1) & 15, ds = min(e2 >> 5, 29u);
+    const uint32_t deb = ds < 4 ? 0u : (ds >> 1) - 1;
+    const uint32_t dbase = ds < 4 ? ds + 1 : ((2u | (ds & 1)) << deb) + 1;
+    const bool match = !lit && !eob;
+    const uint32_t need = match ? o2 + c2 + deb : c1;
+    kind = lit ? IK_LIT : eob ? IK_EOB : IK_MATCH;
+    val = sym;
+    L = eob ? c1 : lbase + (uint32_t)((b >> c1) & ((1u << eb) - 1));
+    D = dbase + (uint32_t)((b >> (o2 + c2)) & ((1u << deb) - 1));
+    // a code beyond the tables goes to the serial decoder (which also sees any
+    // error of that item); otherwise every zlib error of the item
+    const bool slow = e == LUT_LONG || (match && (e & 1) && sym - 257u < 29u && e2 == LUT_LONG);
+    const bool bad = !(e & 1) || (match && (sym - 257u >= 29u || !(e2 & 1) || (e2 >> 5) >= 30)) || need > avail;
+    return slow ? IT_SLOW : bad ? IT_ERR : eob ? IT_EOB : p + need;
 }
 
 // symbols of one Huffman block from the reader's position to its end-of-block
