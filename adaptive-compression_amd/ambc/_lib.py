@@ -43,7 +43,8 @@ EXPORTS = (
     "ambc_comm_unique_id", "ambc_comm_init_rank", "ambc_comm_size", "ambc_comm_barrier",
     "ambc_comm_allreduce_u64", "ambc_comm_allgather_u64", "ambc_comm_gather", "ambc_shard_range",
     "ambc_compress_shard", "ambc_decompress_shard", "ambc_decompress_multi",
-    "ambc_synth_device_range", "ambc_device_equal",
+    "ambc_synth_device_range", "ambc_device_equal", "ambc_compress_multisize",
+    "ambc_last_multisize_info",
 )
 
 
@@ -136,6 +137,10 @@ def _declare(lib):
         "ambc_decompress_multi": ([vp, u8p, u64, u64, C.POINTER(u64), u8p, C.POINTER(Stats)], i32),
         "ambc_synth_device_range": ([vp, i32, vp, u64, u64, u64, u64], i32),
         "ambc_device_equal": ([vp, i32, vp, vp, u64, C.POINTER(i32)], i32),
+        "ambc_compress_multisize": ([vp, u8p, u64, C.POINTER(Params), C.POINTER(u32), u32, C.POINTER(u32),
+                                     C.POINTER(C.c_void_p), u32, u8p, u64, C.POINTER(u64),
+                                     C.POINTER(Stats)], i32),
+        "ambc_last_multisize_info": ([vp, C.POINTER(u32), C.POINTER(u64)], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

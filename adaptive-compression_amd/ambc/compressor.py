@@ -20,9 +20,9 @@ engine runs a single chunk size C (``chunk_size=``, default 4096), i.e.
   chunk nothing compresses swallows the rest of the file as one raw chunk).
 
 With several ``CHUNK_SIZE_CANDIDATES`` (e.g. the reference's default
-``REFERENCE_CHUNK_SIZE_CANDIDATES``) the reference's serial multi-size walk runs
-instead: at every position each candidate size is encoded on the GPU as one
-chunk and the sizes compare by their fp64 ratio (``_adaptive_compress_multisize``).
+``REFERENCE_CHUNK_SIZE_CANDIDATES``) the reference's multi-size walk runs
+instead, on the device (``_adaptive_compress_multisize`` ->
+ambc_compress_multisize).
 """
 import ctypes as C
 import hashlib
@@ -70,9 +70,6 @@ class AdaptiveCompressor:
     # the reference's default list (adaptive_compressor.py:61-62): set
     # CHUNK_SIZE_CANDIDATES to it for the reference's multi-size walk
     REFERENCE_CHUNK_SIZE_CANDIDATES = list(REFERENCE_CHUNK_SIZE_CANDIDATES)
-    # multi-size walk: encode runs of same-size chunks ahead of the walk in one call
-    MULTISIZE_LOOKAHEAD = True
-    MULTISIZE_RUN_BYTES = 16 << 20
 
     def __init__(self, marker_max_length=32, sample_size=10000, *, chunk_size=None,
                  mode="native", methods=None, devices=None):
@@ -161,140 +158,59 @@ class AdaptiveCompressor:
     def _ctx(self):
         return _lib.default_context(self.devices)
 
-    def _eligible(self, s, ids):
-        """ids whose method_chunk_prefs admit an s-byte chunk (adaptive_compressor.py:565-567)."""
-        return [i for i in ids if self.method_chunk_prefs.get(i, (1, 999999999))[0] <= s
-                <= self.method_chunk_prefs.get(i, (1, 999999999))[1]]
-
-    def _encode_run(self, ctx, run, s, ids):
-        """len(run) // s consecutive s-byte chunks through ONE ambc_compress_batch
-        call: for each, the package of the reference's per-size method loop
-        (adaptive_compressor.py:559-579 + _process_chunk :631-700), or None when
-        no method beats raw.  len(run) is s or a multiple of it."""
-        elig = self._eligible(s, ids)
-        k = len(run) // s
-        if not elig:
-            return [None] * k
-        if s > _lib.MAX_CHUNK or (5 in elig and s > 16384) or (2 in elig and s > 8192):
-            raise NotImplementedError(
-                f"a {s}-byte candidate chunk with methods {elig}: the GPU encoders take chunks "
-                f"up to {_lib.MAX_CHUNK} bytes (DEFLATE up to 16384, Dictionary up to 8192)")
-        C_ = (s + 15) & ~15
-        if k > 1 and C_ != s:
-            raise ValueError("runs of several chunks need a 16-byte multiple size")
+    def _adaptive_compress_multisize(self, file_data):
+        """_adaptive_compress (adaptive_compressor.py:363-394) with several
+        CHUNK_SIZE_CANDIDATES: one C-ABI call, ambc_compress_multisize, runs the
+        reference's walk (_pick_best_chunk_and_method :537-590: every candidate
+        size clamped to the remainder, encoded as one chunk by the per-size method
+        loop; sizes compared by their fp64 ratio, strictly, in list order; no
+        winner -> the remainder raw) as many lock-step walks over the device-
+        resident input, one batched encode per size and step."""
+        n = len(file_data)
+        ctx = self._ctx()
+        cands = [int(c) for c in self.CHUNK_SIZE_CANDIDATES]
         p = _lib.Params()
-        p.chunk_size = C_
-        p.mode = _lib.MODE_NATIVE
-        p.flags = _lib.FLAG_NO_END_CHUNK
-        p.method_mask = method_mask(elig)
+        p.method_mask = method_mask([m.type_id for m in self.compression_methods])
         for i in range(16):
             lo, hi = self.method_chunk_prefs.get(i, (1, 0))
             p.pref_min[i], p.pref_max[i] = max(0, lo), min(hi, 0xFFFFFFFF)
-        tab = entropy_terms(s)
-        if s == C_:
-            p.ent_full = tab.ctypes.data
-        else:
-            p.ent_tail = tab.ctypes.data
-        n = len(run)
-        cap = ctx.lib.ambc_compress_bound(n, C_)
+        # numpy-exact entropy terms for every size Huffman may take on the walk:
+        # the candidates and the remainders n - k*g (g = gcd: every position)
+        lo3, hi3 = self.method_chunk_prefs.get(3, (1, 0))
+        sizes = set()
+        if 3 in [m.type_id for m in self.compression_methods]:
+            g = math.gcd(*cands)
+            sizes = {c for c in cands if lo3 <= c <= hi3}
+            k0, k1 = max(0, -(-(n - hi3) // g)), (n - lo3) // g if n >= lo3 else -1
+            sizes |= {n - k * g for k in range(k0, k1 + 1)}
+        tabs = [entropy_terms(sz) for sz in sorted(sizes)]
+        ent_sizes = (C.c_uint32 * max(1, len(tabs)))(*sorted(sizes))
+        ent_ptrs = (C.c_void_p * max(1, len(tabs)))(*[t.ctypes.data for t in tabs])
+        carr = (C.c_uint32 * len(cands))(*cands)
+        cap = n + 64            # compressed packages are shorter than their chunks; one raw remainder
         out = bytearray(cap)
         olen = C.c_uint64()
-        src = bytes(run)                    # held for the call: addr() does not own it
-        _lib.check(ctx.lib.ambc_compress_batch(ctx.h, _lib.addr(src), n, C.byref(p),
-                                               _lib.addr(out), cap, C.byref(olen), None), ctx.lib)
-        body = memoryview(out)[:olen.value]
-        pkgs, off = [], 0
-        for _ in range(k):                  # 18-B package header: payload length at [14:18]
-            end = off + 18 + struct.unpack_from("<I", body, off + 14)[0]
-            pkg = bytes(body[off:end])
-            pkgs.append(None if pkg[4] == 255 else pkg)
-            off = end
-        if off != len(body):
-            raise RuntimeError("ambc_compress_batch: package walk does not end at the body end")
-        return pkgs
-
-    def _encode_one(self, ctx, chunk, ids):
-        """One chunk of len(chunk) bytes: its package, or None (see _encode_run)."""
-        return self._encode_run(ctx, chunk, len(chunk), ids)[0]
-
-    def _adaptive_compress_multisize(self, file_data):
-        """_adaptive_compress (adaptive_compressor.py:363-394) with several
-        CHUNK_SIZE_CANDIDATES: at every position each candidate size, clamped to
-        the remainder, is encoded as one chunk on the GPU (its in-size winner in id
-        order); sizes compare by (len + 18) / size in fp64, strictly, in list
-        order (:548-584); a position where no size beats raw stores the whole
-        remainder raw (:586-588)."""
-        n = len(file_data)
-        ctx = self._ctx()
-        ids = [m.type_id for m in self.compression_methods if m.type_id != 255]
-        cands = [int(c) for c in self.CHUNK_SIZE_CANDIDATES]
-        mv = memoryview(file_data)
-        usage = {m.type_id: 0 for m in self.compression_methods}
-        total = comp = raw = saved = payload = overhead = 0
-        out = bytearray()
-        ahead = {}                             # (pos, size) -> package of a look-ahead run
-        g = math.gcd(*cands)
-        arr = np.frombuffer(mv, dtype=np.uint8) if n else None
-        pos = 0
-        while pos < n:
-            remain = n - pos
-            best_ratio, best_s, best_pkg = 1.0, remain, None
-            tried = {}
-            for cand in cands:
-                s = min(cand, remain)
-                if s <= 0:
-                    break
-                if s not in tried and not self._eligible(s, ids):
-                    tried[s] = None                   # no method takes this size: nothing to encode
-                if s not in tried:
-                    if self.MULTISIZE_LOOKAHEAD and s == cand and (pos, s) not in ahead and s % 16 == 0:
-                        # look ahead: the s-byte chunks at the next J positions the
-                        # walk can reach (pos + j*g, g = gcd of the sizes), copied
-                        # side by side into one MULTISIZE_RUN_BYTES run and encoded in one call
-                        # (a launch is latency-bound: the extra chunks cost little)
-                        J = max(1, min(self.MULTISIZE_RUN_BYTES // s, (remain - s) // g + 1))
-                        run = np.lib.stride_tricks.as_strided(
-                            arr[pos:], shape=(J, s), strides=(g, 1), writeable=False)
-                        run = np.ascontiguousarray(run).reshape(-1)
-                        for j, pk in enumerate(self._encode_run(ctx, run, s, ids)):
-                            ahead[(pos + j * g, s)] = pk
-                    if s == cand and (pos, s) in ahead:
-                        tried[s] = ahead.pop((pos, s))
-                    else:
-                        tried[s] = self._encode_one(ctx, mv[pos:pos + s], ids)
-                pkg = tried[s]
-                if pkg is not None:
-                    ratio = len(pkg) / s          # (len(cdata) + overhead) / len(chunk)
-                    if ratio < best_ratio:
-                        best_ratio, best_s, best_pkg = ratio, s, pkg
-            total += 1
-            if total % 64 == 0 and ahead:         # runs' packages the walk has passed
-                for key in [key for key in ahead if key[0] <= pos]:
-                    del ahead[key]
-            if best_pkg is None:                  # (remain, 255): the rest, raw
-                if remain > 0xFFFFFFFF:
-                    raise struct.error("argument out of range")
-                out += MARKER_BYTES + bytes((255, 0)) + struct.pack("<III", remain, remain, remain)
-                out += mv[pos:]
-                raw += 1
-                break
-            mid, pl = best_pkg[4], len(best_pkg) - 18
-            out += best_pkg
-            comp += 1
-            usage[mid] = usage.get(mid, 0) + 1
-            payload += pl
-            overhead += 18
-            saved += best_s - (pl + 18)
-            pos += best_s
-        out += MARKER_BYTES + bytes(12)           # _create_end_chunk (:595-607)
-        overhead += 16
-        self._last_device_stats = None
-        self.chunk_stats = {"total_chunks": total, "compressed_chunks": comp, "raw_chunks": raw,
-                            "method_usage": usage, "bytes_saved": saved, "original_size": n,
-                            "compressed_size_without_overhead": payload,
-                            "overhead_bytes": overhead}
+        st = _lib.Stats()
+        src = bytes(file_data)
+        rc = ctx.lib.ambc_compress_multisize(ctx.h, _lib.addr(src), n, C.byref(p), carr, len(cands), ent_sizes,
+                                             ent_ptrs, len(tabs), _lib.addr(out), cap, C.byref(olen),
+                                             C.byref(st))
+        if rc == _lib.AMBC_E_RANGE:
+            raise struct.error("argument out of range")
+        if rc == _lib.AMBC_E_INVAL:
+            raise NotImplementedError(_lib.last_error(ctx.lib))
+        _lib.check(rc, ctx.lib)
+        del tabs
+        self._last_device_stats = st
+        self.chunk_stats = {
+            "total_chunks": int(st.total_chunks), "compressed_chunks": int(st.compressed_chunks),
+            "raw_chunks": int(st.raw_chunks),
+            "method_usage": {m.type_id: int(st.method_usage[m.type_id]) for m in self.compression_methods},
+            "bytes_saved": int(st.bytes_saved), "original_size": n,
+            "compressed_size_without_overhead": int(st.payload_bytes),
+            "overhead_bytes": int(st.overhead_bytes)}
         self.method_usage_ids = [m.type_id for m in self.compression_methods]
-        return bytes(out)
+        return bytes(memoryview(out)[:olen.value])
 
     def _adaptive_compress(self, file_data):
         """One C-ABI call: input bytes -> .ambc body (packages + end chunk)."""

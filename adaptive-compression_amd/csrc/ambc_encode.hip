@@ -147,8 +147,8 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
 
     const uint32_t lane = threadIdx.x;
     const uint32_t k = blockIdx.x;
-    const uint64_t pos0 = (uint64_t)k * A.chunk_size;
-    const uint32_t n = (uint32_t)min((uint64_t)A.chunk_size, A.n_total - pos0);
+    const uint64_t pos0 = A.coff ? A.coff[k] : (uint64_t)k * A.chunk_size;
+    const uint32_t n = A.coff ? A.clen[k] : (uint32_t)min((uint64_t)A.chunk_size, A.n_total - pos0);
     const uint8_t* src = A.in + pos0;
     uint8_t* slot = A.slots + (uint64_t)k * A.slot_stride;
     // second pass after k_deflate: only the deferred chunks id 5 did not take
@@ -890,7 +890,7 @@ __device__ __forceinline__ void compact_package(const CompactArgs& A, uint32_t k
     const uint32_t P = HDR + pl;
     const uint32_t type = A.ids[k];
     const uint64_t p0 = (uint64_t)k * A.chunk_size;
-    const uint32_t n = (uint32_t)min((uint64_t)A.chunk_size, A.n_total - p0);
+    const uint32_t n = A.clen ? A.clen[k] : (uint32_t)min((uint64_t)A.chunk_size, A.n_total - p0);
     const uint8_t* __restrict__ sl = A.slots + (uint64_t)k * A.slot_stride;
     const uint64_t d0 = o >> 2, d1 = (o + P - 1) >> 2;
     uint32_t* __restrict__ out32 = reinterpret_cast<uint32_t*>(A.out);

@@ -68,6 +68,15 @@ struct Buf {
     void release() { if (p) (void)hipFree(p); p = nullptr; cap = 0; }
 };
 
+// device buffers of one multi-size walk batch (ambc_multisize.cpp)
+struct Batch {
+    Buf coff, clen, slots, plen, ids, sizes, bestpre, gdseq, pending, ent, off;
+    void release() {
+        for (Buf* b : {&coff, &clen, &slots, &plen, &ids, &sizes, &bestpre, &gdseq, &pending, &ent, &off})
+            b->release();
+    }
+};
+
 struct Dev {
     int id = 0;
     hipStream_t stream = nullptr;
@@ -79,6 +88,9 @@ struct Dev {
     Buf coll;                   // small device buffers of the collectives (sizes, stats, flags)
     Buf inffix;                 // fixed-Huffman inflate tables (built on the first decode)
     bool inffix_ok = false;
+    Batch msb;                  // multi-size walk batches
+    uint32_t ms_steps = 0;      // last multi-size walk: batched evaluation rounds,
+    uint64_t ms_evaluated = 0;  //   chunk encodes they ran
     uint64_t t_encode = 0, t_scan = 0, t_compact = 0;
     uint32_t n_launch = 1;      // k_encode launches of the last compress call (pipelined segments)
     hipStream_t cs = nullptr;   // scan + compaction of pipelined segments

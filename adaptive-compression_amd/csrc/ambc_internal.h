@@ -34,6 +34,8 @@ struct EncArgs {
     uint8_t* pending;        // with k_deflate: 1 = the RLE/Huffman payload was not emitted (id 5 may win)
     uint32_t pref_min[16];
     uint32_t pref_max[16];
+    const uint64_t* coff;    // optional chunk table (multi-size walk): chunk k = in[coff[k], coff[k] + clen[k])
+    const uint32_t* clen;    //   (else chunk k = in[k * chunk_size, ...) clamped to n_total)
 };
 
 // gather the packages into the body at their scanned offsets
@@ -45,6 +47,7 @@ struct CompactArgs {
     const uint64_t* off;     // exclusive scan of sizes (n_chunks+1)
     const uint64_t* base;    // optional: body offset added to off[] (pipelined segments)
     uint32_t n_chunks;       // packages to write
+    const uint32_t* clen;    // optional: original length of package k (else chunk_size clamped to n_total)
     uint32_t resident;       // > 0: a grid of this many workgroups striding over the packages
     uint64_t n_total;
     uint32_t chunk_size;

@@ -117,6 +117,23 @@ uint64_t ambc_compress_bound(uint64_t n, uint32_t chunk);
 int ambc_compress_batch(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const ambc_params* p,
                         uint8_t* out, uint64_t out_cap, uint64_t* out_len, ambc_stats* st);
 
+/* The reference's multi-size walk (several CHUNK_SIZE_CANDIDATES): replaces
+ * _adaptive_compress (adaptive_compressor.py:363-394) with
+ * _pick_best_chunk_and_method (:537-590) when CHUNK_SIZE_CANDIDATES holds more
+ * than one size.  cands[0..n_cands) in the reference's list order (each in
+ * [1, 131072]); p supplies method_mask and the prefs (chunk_size and mode are
+ * ignored).  ent_sizes/ent_tabs: optional numpy-exact p*log2(p) tables for the
+ * chunk sizes Huffman may take (see ambc_params.ent_full).  Writes the .ambc
+ * body (packages + end chunk); AMBC_E_INVAL when a size the walk needs has an
+ * eligible method the GPU encoders do not take at that size (DEFLATE > 16384,
+ * Dictionary > 8192, any > 65536), AMBC_E_RANGE for a raw remainder > 4 GiB. */
+int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const ambc_params* p,
+                            const uint32_t* cands, uint32_t n_cands, const uint32_t* ent_sizes,
+                            const double* const* ent_tabs, uint32_t n_ent, uint8_t* out,
+                            uint64_t out_cap, uint64_t* out_len, ambc_stats* st);
+/* of the last ambc_compress_multisize: batched evaluation rounds and chunk encodes */
+int ambc_last_multisize_info(ambc_ctx* ctx, uint32_t* steps, uint64_t* evaluated);
+
 int ambc_decompress_batch(ambc_ctx* ctx, const uint8_t* body, uint64_t body_len,
                           uint64_t orig_size, uint8_t* out, ambc_stats* st);
 

@@ -1,7 +1,16 @@
 """Time the reference's multi-size walk (REFERENCE_CHUNK_SIZE_CANDIDATES) on the
-GPU with and without the look-ahead runs, and check both bodies are equal.
-Usage: python scripts/multisize_bench.py [MiB]"""
-import os, sys, time
+GPU (ambc_compress_multisize) and check the body against the oracle's walk.
+
+    python scripts/multisize_bench.py [MiB ...]      (default: 32 256)
+
+Input: runs, text-like bytes and skewed random bytes in 8-64 KiB segments, so
+every position compresses and the walk never ends in the remainder-raw rule."""
+import ctypes as C
+import json
+import os
+import sys
+import time
+
 ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "adaptive-compression_amd"))
@@ -10,8 +19,6 @@ import ambc  # noqa: E402
 
 
 def mixed(n, seed):
-    """runs, text-like bytes and skewed random bytes in 8-64 KiB segments: every
-    position compresses, so the walk never ends in the remainder-raw rule"""
     rng = np.random.default_rng(seed)
     out, have = [], 0
     while have < n:
@@ -26,22 +33,35 @@ def mixed(n, seed):
         out.append(seg.tobytes())
         have += m
     return b"".join(out)[:n]
-mib = float(sys.argv[1]) if len(sys.argv) > 1 else 4
-data = mixed(int(mib * (1 << 20)), 7)
-res = {}
-for la, rb in ((True, 16 << 20), (True, 4 << 20), (True, 64 << 20), (True, 16 << 20), (False, 0)):
-    comp = ambc.AdaptiveCompressor(methods=(1, 3, 4, 9))
-    comp.CHUNK_SIZE_CANDIDATES = list(comp.REFERENCE_CHUNK_SIZE_CANDIDATES)
-    comp.MULTISIZE_LOOKAHEAD = la
-    if rb:
-        comp.MULTISIZE_RUN_BYTES = rb
-    comp._adaptive_compress(data[:4 << 20])            # warm
-    t = time.perf_counter()
-    body = comp._adaptive_compress(data)
-    dt = time.perf_counter() - t
-    res[(la, rb)] = body
-    print(f"lookahead={la} run={rb >> 20} MiB {len(data)/2**20:.1f} MiB {dt*1e3:.1f} ms "
-          f"{len(data)/dt/1e6:.2f} MB/s ratio {len(body)/len(data):.4f} "
-          f"chunks {comp.chunk_stats['total_chunks']}", flush=True)
-assert len(set(res.values())) == 1, "look-ahead changed the body"
-print("bodies equal")
+
+
+def main():
+    sizes = [float(x) for x in sys.argv[1:]] or [32, 256]
+    for methods in ((1, 3, 4, 9), (1, 2, 3, 4)):
+        for mib in sizes:
+            data = mixed(int(mib * (1 << 20)), 7)
+            comp = ambc.AdaptiveCompressor(methods=methods)
+            comp.CHUNK_SIZE_CANDIDATES = list(comp.REFERENCE_CHUNK_SIZE_CANDIDATES)
+            comp._adaptive_compress(data[:1 << 20])            # warm
+            t = time.perf_counter()
+            body = comp._adaptive_compress(data)
+            dt = time.perf_counter() - t
+            steps, ev = C.c_uint32(), C.c_uint64()
+            lib = ambc._lib.load()
+            lib.ambc_last_multisize_info(ambc._lib.default_context().h, C.byref(steps), C.byref(ev))
+            rec = {"MiB": mib, "methods": list(methods), "seconds": round(dt, 4),
+                   "GBps": round(len(data) / dt / 1e9, 3), "ratio": round(len(body) / len(data), 5),
+                   "chunks": comp.chunk_stats["total_chunks"], "walk_steps": steps.value,
+                   "chunk_encodes": ev.value}
+            if mib <= 32:
+                from oracle import oracle as orc
+                t = time.perf_counter()
+                ref, _ = orc.compress_body_multisize(data, comp.CHUNK_SIZE_CANDIDATES, tuple(methods) + (255,))
+                rec["oracle_seconds"] = round(time.perf_counter() - t, 2)
+                rec["body_equals_oracle"] = ref == body
+            rec["round_trip"] = comp._adaptive_decompress(body, len(data)) == data
+            print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()

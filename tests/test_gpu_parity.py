@@ -554,14 +554,14 @@ def test_multisize_walk_matches_oracle(ctx, methods, cands):
         assert comp.decompress_bytes(blob) == data if blob[:4] == b"AMBC" else blob == data
 
 
-def test_multisize_lookahead_runs_match_serial_walk(ctx):
-    """The look-ahead runs (many same-size chunks per call, past 16384 chunks
-    per run so a run takes the segmented pipeline) give the body and stats of
-    the plain serial walk (one call per candidate and position)."""
+def test_multisize_many_walks_match_oracle(ctx):
+    """Inputs long enough for many lock-step walks (one per 128 KiB) that merge
+    into one another: the body and stats of the reference's single walk (the
+    oracle), with the reference's eight candidates and with two."""
     import numpy as np
     rng = np.random.default_rng(11)
     parts = []
-    while sum(len(x) for x in parts) < (18 << 20):
+    while sum(len(x) for x in parts) < (4 << 20):
         k = int(rng.integers(3))
         m = int(rng.integers(8, 65)) << 10
         if k == 0:
@@ -570,23 +570,17 @@ def test_multisize_lookahead_runs_match_serial_walk(ctx):
             parts.append(rng.choice(np.frombuffer(b"etaoin shrdlu,.ETAOIN", np.uint8), m).tobytes())
         else:
             parts.append(np.minimum(rng.geometric(0.08, m), 255).astype(np.uint8).tobytes())
-    data = b"".join(parts)[:18 << 20]
-    bodies, stats = [], []
-    for la, run in ((True, 17 << 20), (True, 1 << 20), (False, 0)):
-        comp = _compressor(methods=(1, 3, 4, 9))
-        comp.CHUNK_SIZE_CANDIDATES = [2048, 1024]          # a 1024-byte run of 17 MiB: 17408 chunks
-        comp.MULTISIZE_LOOKAHEAD = la
-        if run:
-            comp.MULTISIZE_RUN_BYTES = run
-        src = data if la else data[:1 << 20]
-        bodies.append(comp._adaptive_compress(src))
-        stats.append(dict(comp.chunk_stats))
-    assert bodies[0] == bodies[1] and stats[0] == stats[1]
-    ref1, _ = orc.compress_body_multisize(data[:1 << 20], [2048, 1024], (1, 3, 4, 9, 255))
-    assert bodies[2] == ref1
-    comp = _compressor(methods=(1, 3, 4, 9))
-    comp.CHUNK_SIZE_CANDIDATES = [2048, 1024]
-    assert comp._adaptive_compress(data[:1 << 20]) == ref1
+    data = b"".join(parts)[:(4 << 20) - 777]
+    for cands, methods in ((REF_CANDS, (1, 3, 4, 9)), ([2048, 1024], (1, 2, 3, 4))):
+        comp = _compressor(methods=methods)
+        comp.CHUNK_SIZE_CANDIDATES = list(cands)
+        body = comp._adaptive_compress(data)
+        ref, st = orc.compress_body_multisize(data, cands, tuple(methods) + (255,))
+        assert body == ref, cands
+        for k in ("total_chunks", "compressed_chunks", "raw_chunks", "bytes_saved",
+                  "compressed_size_without_overhead", "overhead_bytes"):
+            assert comp.chunk_stats[k] == st[k], k
+        assert comp._adaptive_decompress(body, len(data)) == data
 
 
 def test_multisize_rejects_oversize_gpu_chunks(ctx):
