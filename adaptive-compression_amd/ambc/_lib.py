@@ -140,7 +140,7 @@ def _declare(lib):
         "ambc_compress_multisize": ([vp, u8p, u64, C.POINTER(Params), C.POINTER(u32), u32, C.POINTER(u32),
                                      C.POINTER(C.c_void_p), u32, u8p, u64, C.POINTER(u64),
                                      C.POINTER(Stats)], i32),
-        "ambc_last_multisize_info": ([vp, C.POINTER(u32), C.POINTER(u64)], i32),
+        "ambc_last_multisize_info": ([vp, C.POINTER(u32), C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

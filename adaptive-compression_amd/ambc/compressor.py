@@ -188,12 +188,12 @@ class AdaptiveCompressor:
         ent_ptrs = (C.c_void_p * max(1, len(tabs)))(*[t.ctypes.data for t in tabs])
         carr = (C.c_uint32 * len(cands))(*cands)
         cap = n + 64            # compressed packages are shorter than their chunks; one raw remainder
-        out = bytearray(cap)
+        out = np.empty(cap, dtype=np.uint8)     # (no zero fill: the call writes what it returns)
         olen = C.c_uint64()
         st = _lib.Stats()
-        src = bytes(file_data)
+        src = file_data if isinstance(file_data, (bytes, bytearray)) else bytes(file_data)
         rc = ctx.lib.ambc_compress_multisize(ctx.h, _lib.addr(src), n, C.byref(p), carr, len(cands), ent_sizes,
-                                             ent_ptrs, len(tabs), _lib.addr(out), cap, C.byref(olen),
+                                             ent_ptrs, len(tabs), out.ctypes.data, cap, C.byref(olen),
                                              C.byref(st))
         if rc == _lib.AMBC_E_RANGE:
             raise struct.error("argument out of range")
@@ -210,7 +210,7 @@ class AdaptiveCompressor:
             "compressed_size_without_overhead": int(st.payload_bytes),
             "overhead_bytes": int(st.overhead_bytes)}
         self.method_usage_ids = [m.type_id for m in self.compression_methods]
-        return bytes(memoryview(out)[:olen.value])
+        return out[:olen.value].tobytes()
 
     def _adaptive_compress(self, file_data):
         """One C-ABI call: input bytes -> .ambc body (packages + end chunk)."""

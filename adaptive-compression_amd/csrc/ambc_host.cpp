@@ -100,7 +100,8 @@ void ambc_destroy(ambc_ctx* ctx) {
                        &d.scratch, &d.seg, &d.list, &d.bestpre, &d.gdseq, &d.pending, &d.segbase, &d.coll,
                        &d.inffix})
             b->release();
-        d.msb.release();
+        for (auto& b : d.msb) b.release();
+        for (auto& x : d.mss) if (x) { (void)hipStreamSynchronize(x); (void)hipStreamDestroy(x); }
         for (void* b : d.stage) (void)hipHostFree(b);
         for (auto& ev : d.stage_ev) (void)hipEventDestroy(ev);
         for (auto& x : d.stage_st) (void)hipStreamDestroy(x);

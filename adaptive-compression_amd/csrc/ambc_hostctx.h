@@ -71,9 +71,25 @@ struct Buf {
 // device buffers of one multi-size walk batch (ambc_multisize.cpp)
 struct Batch {
     Buf coff, clen, slots, plen, ids, sizes, bestpre, gdseq, pending, ent, off;
+    uint32_t* hplen = nullptr;  // pinned copies of plen / ids for the host walk
+    uint8_t* hids = nullptr;
+    size_t hcap = 0;
+    hipError_t host_ensure(size_t n) {
+        if (n <= hcap) return hipSuccess;
+        if (hplen) (void)hipHostFree(hplen);
+        if (hids) (void)hipHostFree(hids);
+        hplen = nullptr; hids = nullptr; hcap = 0;
+        hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&hplen), n * 4);
+        if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&hids), n);
+        if (e == hipSuccess) hcap = n;
+        return e;
+    }
     void release() {
         for (Buf* b : {&coff, &clen, &slots, &plen, &ids, &sizes, &bestpre, &gdseq, &pending, &ent, &off})
             b->release();
+        if (hplen) (void)hipHostFree(hplen);
+        if (hids) (void)hipHostFree(hids);
+        hplen = nullptr; hids = nullptr; hcap = 0;
     }
 };
 
@@ -88,9 +104,11 @@ struct Dev {
     Buf coll;                   // small device buffers of the collectives (sizes, stats, flags)
     Buf inffix;                 // fixed-Huffman inflate tables (built on the first decode)
     bool inffix_ok = false;
-    Batch msb;                  // multi-size walk batches
+    Batch msb[8];               // multi-size walk batches, one per concurrent size class
+    hipStream_t mss[8] = {};    //   and their streams (created on the first walk)
     uint32_t ms_steps = 0;      // last multi-size walk: batched evaluation rounds,
-    uint64_t ms_evaluated = 0;  //   chunk encodes they ran
+    uint64_t ms_evaluated = 0;  //   chunk encodes they ran,
+    uint64_t ms_walk_ns = 0, ms_emit_ns = 0;  // and the time of the walk / of the final encode
     uint64_t t_encode = 0, t_scan = 0, t_compact = 0;
     uint32_t n_launch = 1;      // k_encode launches of the last compress call (pipelined segments)
     hipStream_t cs = nullptr;   // scan + compaction of pipelined segments

@@ -61,15 +61,16 @@ int check_size(const ambc_params* p, uint32_t s) {
     return AMBC_OK;
 }
 
-// The encoders over the s-byte chunks at pos[] (one workgroup each): per chunk
-// the winner of the reference's method loop for that size, its payload left in
-// the batch's slot k.  The launch sequence is compress_on's (k_encode, k_dict
-// against its winner, k_deflate against both, then the deferred emits).
-int run_batch(Dev& d, Batch& b, const uint8_t* d_in, uint64_t n, const ambc_params* p, uint32_t s,
-              const std::vector<uint64_t>& pos, const double* ent, std::vector<uint32_t>& plen,
-              std::vector<uint8_t>& ids) {
-    hipStream_t st = d.stream;
+// The encoders over the s-byte chunks at pos[] (one workgroup each) on stream
+// st: per chunk the winner of the reference's method loop for that size, its
+// payload left in the batch's slot k, plen / ids copied back into hp / hi (valid
+// after the stream synchronizes).  The launch sequence is compress_on's
+// (k_encode, k_dict against its winner, k_deflate against both, then the
+// deferred emits).
+int launch_batch(Batch& b, hipStream_t st, const uint8_t* d_in, uint64_t n, const ambc_params* p, uint32_t s,
+                 const std::vector<uint64_t>& pos, const double* ent) {
     const uint32_t cnt = (uint32_t)pos.size();
+    HIPCHK(b.host_ensure(cnt));
     const uint32_t C = (s + 15) & ~15u;
     const uint32_t stride = slot_stride_for(C);
     HIPCHK(b.coff.ensure((size_t)cnt * 8));
@@ -78,9 +79,8 @@ int run_batch(Dev& d, Batch& b, const uint8_t* d_in, uint64_t n, const ambc_para
     HIPCHK(b.plen.ensure((size_t)cnt * 4 + 4));
     HIPCHK(b.ids.ensure((size_t)cnt + 16));
     HIPCHK(b.sizes.ensure((size_t)cnt * 8 + 8));
-    std::vector<uint32_t> cl(cnt, s);
     HIPCHK(hipMemcpyAsync(b.coff.p, pos.data(), (size_t)cnt * 8, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(b.clen.p, cl.data(), (size_t)cnt * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(b.clen.p), (int)s, cnt, st));
     EncArgs ea{};
     ea.in = d_in;
     ea.n_total = n;
@@ -122,11 +122,8 @@ int run_batch(Dev& d, Batch& b, const uint8_t* d_in, uint64_t n, const ambc_para
         ep.bestpre = nullptr;
         HIPCHK(launch_encode(ep, st));
     }
-    plen.resize(cnt);
-    ids.resize(cnt);
-    HIPCHK(hipMemcpyAsync(plen.data(), b.plen.p, (size_t)cnt * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(ids.data(), b.ids.p, cnt, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipMemcpyAsync(b.hplen, b.plen.p, (size_t)cnt * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(b.hids, b.ids.p, cnt, hipMemcpyDeviceToHost, st));
     return AMBC_OK;
 }
 
@@ -177,88 +174,153 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
     for (uint32_t i = 0; i < n_cands; i++) g = std::gcd(g, (uint64_t)cands[i]);
     std::unordered_map<uint64_t, Eval> cache;          // (pos, s) -> the size's winner
     std::unordered_map<uint64_t, Decision> dec;        // pos -> the reference's decision there
-    std::vector<uint64_t> active;
+    struct Walk { uint64_t pos; uint32_t last; };      // last: the size it took the step before
+    std::vector<Walk> active;
+    // walks: one per 512 KiB, at most 512; speculation: 2 positions ahead (256
+    // MiB of mixed data, reference candidates: best of 1-8 ahead x 256-2048
+    // walks; AMBC_MS_WALKS / AMBC_MS_SPEC override them for such sweeps)
+    static const uint64_t KMAX_ = getenv("AMBC_MS_WALKS") ? strtoull(getenv("AMBC_MS_WALKS"), nullptr, 10) : 512;
+    uint32_t max_cand = 0;
+    for (uint32_t i = 0; i < n_cands; i++)
+        if (any_eligible(p, cands[i])) max_cand = std::max(max_cand, cands[i]);
     {
-        const uint64_t K = std::max<uint64_t>(1, std::min<uint64_t>(2048, n / (128 << 10)));
+        // walk starts on the lattice of the largest eligible size: where that size
+        // wins everywhere (homogeneous data) every walk runs on the same lattice
+        // and joins the next one at once; elsewhere the mixed choices shift their
+        // phases until they meet
+        const uint64_t K = std::max<uint64_t>(1, std::min<uint64_t>(KMAX_, n / (512 << 10)));
+        const uint64_t lat = max_cand ? max_cand : g;
         std::set<uint64_t> starts;
-        for (uint64_t k = 0; k < K; k++) starts.insert((k * n / K) / g * g);
-        active.assign(starts.begin(), starts.end());
-        if (n == 0) active.clear();
+        for (uint64_t k = 0; k < K; k++) starts.insert((k * n / K) / lat * lat);
+        if (n)
+            for (uint64_t b0 : starts) active.push_back(Walk{b0, max_cand ? max_cand : cands[0]});
     }
-    Batch& B = d.msb;
+    for (auto& x : d.mss)
+        if (!x) HIPCHK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+    HIPCHK(hipStreamSynchronize(s));                   // (the input upload)
     uint32_t steps = 0;
     uint64_t evaluated = 0;
     uint64_t kernel_ns = 0;
+    // the (position, size) pairs a decision at pos needs; false when all are known
+    auto needs = [&](uint64_t pos, std::map<uint32_t, std::vector<uint64_t>>* req) -> bool {
+        bool any = false;
+        const uint64_t remain = n - pos;
+        for (uint32_t i = 0; i < n_cands; i++) {
+            const uint32_t sz = (uint32_t)std::min<uint64_t>(cands[i], remain);
+            if (!any_eligible(p, sz)) continue;
+            const uint64_t kk = key(pos, sz);
+            if (cache.count(kk)) continue;
+            any = true;
+            if (req) {
+                cache[kk] = Eval{0, 0xFE};     // requested (filled by the batch)
+                (*req)[sz].push_back(pos);
+            }
+        }
+        return any;
+    };
+    // the reference's decision at pos (adaptive_compressor.py:546-590), all sizes known
+    auto decide = [&](uint64_t pos) -> Decision {
+        const uint64_t remain = n - pos;
+        double best_ratio = 1.0;
+        uint32_t best_s = 0, best_plen = 0;
+        uint8_t best_id = 255;
+        std::vector<uint32_t> seen;
+        for (uint32_t i = 0; i < n_cands; i++) {
+            const uint32_t sz = (uint32_t)std::min<uint64_t>(cands[i], remain);
+            // the same clamped size again: same package, same ratio (never strictly better)
+            if (std::find(seen.begin(), seen.end(), sz) != seen.end()) continue;
+            seen.push_back(sz);
+            if (!any_eligible(p, sz)) continue;
+            const Eval& e = cache[key(pos, sz)];
+            if (e.id == 255) continue;
+            const double ratio = (double)(e.plen + HDR) / (double)sz;
+            if (ratio < best_ratio) {
+                best_ratio = ratio;
+                best_s = sz;
+                best_plen = e.plen;
+                best_id = e.id;
+            }
+        }
+        if (best_id == 255) return Decision{(uint32_t)std::min<uint64_t>(remain, 0xFFFFFFFFull), (uint32_t)remain, 255};
+        return Decision{best_s, best_plen, best_id};
+    };
+    // Rounds: every walk decides as far as the known sizes reach; then ONE batch
+    // per size evaluates each walk's next position and SPEC positions further
+    // along the path it would take if it kept its last step size (a guess: a
+    // right one saves a round, whose latency -- the slowest 64 KiB encode -- is
+    // the walk's cost; a wrong one costs idle device time only)
+    static const int SPEC = getenv("AMBC_MS_SPEC") ? atoi(getenv("AMBC_MS_SPEC")) : 2;
     while (!active.empty()) {
-        steps++;
-        // (a position another walk decided meanwhile needs nothing more)
-        active.erase(std::remove_if(active.begin(), active.end(), [&](uint64_t q) { return dec.count(q) > 0; }),
-                     active.end());
+        std::vector<Walk> still;
+        for (Walk w : active) {
+            for (;;) {
+                if (dec.count(w.pos)) break;               // joined a decided path
+                if (needs(w.pos, nullptr)) { still.push_back(w); break; }
+                const Decision dd = decide(w.pos);
+                if (dd.id == 255 && n - w.pos > 0xFFFFFFFFull)
+                    return fail(AMBC_E_RANGE, "raw remainder exceeds a u32 chunk field");
+                dec[w.pos] = dd;
+                if (dd.id == 255) break;                   // the rest is raw: done
+                w.last = dd.s;
+                w.pos += dd.s;
+                if (w.pos >= n) break;
+            }
+        }
+        // (two walks at one position: keep one)
+        std::sort(still.begin(), still.end(), [](const Walk& x, const Walk& y) { return x.pos < y.pos; });
+        still.erase(std::unique(still.begin(), still.end(), [](const Walk& x, const Walk& y) { return x.pos == y.pos; }),
+                    still.end());
+        active.swap(still);
         if (active.empty()) break;
-        // every (position, size) an active walk needs that is not known yet, per size
+        steps++;
         std::map<uint32_t, std::vector<uint64_t>> req;
-        for (uint64_t pos : active) {
-            const uint64_t remain = n - pos;
-            for (uint32_t i = 0; i < n_cands; i++) {
-                const uint32_t sz = (uint32_t)std::min<uint64_t>(cands[i], remain);
-                if (!any_eligible(p, sz)) continue;
-                const uint64_t kk = key(pos, sz);
-                if (cache.count(kk)) continue;
-                int rc = check_size(p, sz);
-                if (rc) return rc;
-                cache[kk] = Eval{0, 0xFE};     // requested (filled below)
-                req[sz].push_back(pos);
+        for (const Walk& w : active) {
+            uint64_t q = w.pos;
+            for (int k = 0; k <= SPEC && q < n; k++, q += w.last) {
+                if (k && dec.count(q)) break;
+                (void)needs(q, &req);
+            }
+        }
+        for (auto& r : req) {
+            int rc = check_size(p, r.first);
+            if (rc) {
+                // only an error if a walk itself needs this size (not a speculative position)
+                for (uint64_t q : r.second)
+                    if (std::binary_search(active.begin(), active.end(), Walk{q, 0},
+                                           [](const Walk& x, const Walk& y) { return x.pos < y.pos; }))
+                        return rc;
             }
         }
         const uint64_t tk = now_ns();
+        std::vector<std::pair<uint32_t, std::vector<uint64_t>>> jobs;
         for (auto& r : req) {
-            std::vector<uint32_t> pl;
-            std::vector<uint8_t> id;
-            int rc = run_batch(d, B, d_in, n, p, r.first, r.second, ent_of(r.first), pl, id);
-            if (rc) return rc;
-            for (size_t j = 0; j < r.second.size(); j++) cache[key(r.second[j], r.first)] = Eval{pl[j], id[j]};
-            evaluated += r.second.size();
-        }
-        kernel_ns += now_ns() - tk;
-        // the decisions (adaptive_compressor.py:546-590) and the next positions
-        std::set<uint64_t> next;
-        for (uint64_t pos : active) {
-            const uint64_t remain = n - pos;
-            double best_ratio = 1.0;
-            uint32_t best_s = 0, best_plen = 0;
-            uint8_t best_id = 255;
-            uint32_t seen[64];
-            uint32_t nseen = 0;
-            for (uint32_t i = 0; i < n_cands; i++) {
-                const uint32_t sz = (uint32_t)std::min<uint64_t>(cands[i], remain);
-                if (std::find(seen, seen + nseen, sz) != seen + nseen) {
-                    // the same clamped size again: same package, same ratio (never strictly better)
-                    continue;
-                }
-                if (nseen < 64) seen[nseen++] = sz;
-                if (!any_eligible(p, sz)) continue;
-                const Eval& e = cache[key(pos, sz)];
-                if (e.id == 255) continue;
-                const double ratio = (double)(e.plen + HDR) / (double)sz;
-                if (ratio < best_ratio) {
-                    best_ratio = ratio;
-                    best_s = sz;
-                    best_plen = e.plen;
-                    best_id = e.id;
-                }
-            }
-            if (best_id == 255) {            // (remain, 255): the rest, raw
-                if (remain > 0xFFFFFFFFull) return fail(AMBC_E_RANGE, "raw remainder exceeds a u32 chunk field");
-                dec[pos] = Decision{(uint32_t)remain, (uint32_t)remain, 255};
+            if (check_size(p, r.first)) {       // speculative only: never decided from
+                for (uint64_t q : r.second) cache.erase(key(q, r.first));
                 continue;
             }
-            dec[pos] = Decision{best_s, best_plen, best_id};
-            const uint64_t nx = pos + best_s;
-            if (nx < n && !dec.count(nx)) next.insert(nx);
+            jobs.emplace_back(r.first, std::move(r.second));
         }
-        active.assign(next.begin(), next.end());
+        // up to 8 size classes at once, each on its own stream and batch buffers
+        // (the 64 KiB class runs at 2 workgroups per CU: the small ones fill in)
+        for (size_t j0 = 0; j0 < jobs.size(); j0 += 8) {
+            const size_t j1 = std::min(jobs.size(), j0 + 8);
+            for (size_t j = j0; j < j1; j++) {
+                int rc = launch_batch(d.msb[j - j0], d.mss[j - j0], d_in, n, p, jobs[j].first, jobs[j].second,
+                                      ent_of(jobs[j].first));
+                if (rc) return rc;
+            }
+            for (size_t j = j0; j < j1; j++) {
+                HIPCHK(hipStreamSynchronize(d.mss[j - j0]));
+                const Batch& bb = d.msb[j - j0];
+                for (size_t q = 0; q < jobs[j].second.size(); q++)
+                    cache[key(jobs[j].second[q], jobs[j].first)] = Eval{bb.hplen[q], bb.hids[q]};
+                evaluated += jobs[j].second.size();
+            }
+        }
+        kernel_ns += now_ns() - tk;
     }
 
+    const uint64_t t_walk = now_ns() - t0;
     // ---- the reference's walk from 0, read off the decisions ----
     struct Pkg { uint64_t pos; uint32_t s, plen; uint8_t id; uint64_t off; };
     std::vector<Pkg> path;
@@ -282,35 +344,45 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
     std::map<uint32_t, std::vector<size_t>> groups;
     for (size_t i = 0; i < path.size(); i++)
         if (path[i].id != 255) groups[path[i].s].push_back(i);
-    for (auto& gr : groups) {
-        const uint32_t sz = gr.first;
-        std::vector<uint64_t> pos;
-        for (size_t i : gr.second) pos.push_back(path[i].pos);
-        std::vector<uint32_t> pl;
-        std::vector<uint8_t> id;
-        int rc = run_batch(d, B, d_in, n, p, sz, pos, ent_of(sz), pl, id);
-        if (rc) return rc;
-        std::vector<uint64_t> offs;
-        for (size_t j = 0; j < gr.second.size(); j++) {
-            const Pkg& pk = path[gr.second[j]];
-            if (pl[j] != pk.plen || id[j] != pk.id) return fail(AMBC_E_DEVICE, "multi-size walk: re-encode differs");
-            offs.push_back(pk.off);
+    std::vector<std::pair<uint32_t, std::vector<size_t>>> gl(groups.begin(), groups.end());
+    for (size_t j0 = 0; j0 < gl.size(); j0 += 8) {
+        const size_t j1 = std::min(gl.size(), j0 + 8);
+        std::vector<std::vector<uint64_t>> offs(j1 - j0);
+        for (size_t j = j0; j < j1; j++) {
+            const uint32_t sz = gl[j].first;
+            Batch& bb = d.msb[j - j0];
+            hipStream_t xs = d.mss[j - j0];
+            std::vector<uint64_t> pos;
+            for (size_t i : gl[j].second) {
+                pos.push_back(path[i].pos);
+                offs[j - j0].push_back(path[i].off);
+            }
+            int rc = launch_batch(bb, xs, d_in, n, p, sz, pos, ent_of(sz));
+            if (rc) return rc;
+            HIPCHK(bb.off.ensure(pos.size() * 8));
+            HIPCHK(hipMemcpyAsync(bb.off.p, offs[j - j0].data(), pos.size() * 8, hipMemcpyHostToDevice, xs));
+            CompactArgs ca{};
+            ca.slots = bb.slots.as<uint8_t>();
+            ca.slot_stride = slot_stride_for((sz + 15) & ~15u);
+            ca.plen = bb.plen.as<uint32_t>();
+            ca.ids = bb.ids.as<uint8_t>();
+            ca.off = bb.off.as<uint64_t>();
+            ca.n_chunks = (uint32_t)pos.size();
+            ca.clen = bb.clen.as<uint32_t>();
+            ca.n_total = n;
+            ca.chunk_size = (sz + 15) & ~15u;
+            ca.out = d_body;
+            HIPCHK(launch_compact(ca, xs));
         }
-        HIPCHK(B.off.ensure(offs.size() * 8));
-        HIPCHK(hipMemcpyAsync(B.off.p, offs.data(), offs.size() * 8, hipMemcpyHostToDevice, s));
-        CompactArgs ca{};
-        ca.slots = B.slots.as<uint8_t>();
-        ca.slot_stride = slot_stride_for((sz + 15) & ~15u);
-        ca.plen = B.plen.as<uint32_t>();
-        ca.ids = B.ids.as<uint8_t>();
-        ca.off = B.off.as<uint64_t>();
-        ca.n_chunks = (uint32_t)offs.size();
-        ca.clen = B.clen.as<uint32_t>();
-        ca.n_total = n;
-        ca.chunk_size = (sz + 15) & ~15u;
-        ca.out = d_body;
-        HIPCHK(launch_compact(ca, s));
-        HIPCHK(hipStreamSynchronize(s));   // the next group reuses the batch buffers
+        for (size_t j = j0; j < j1; j++) {
+            HIPCHK(hipStreamSynchronize(d.mss[j - j0]));
+            const Batch& bb = d.msb[j - j0];
+            for (size_t q = 0; q < gl[j].second.size(); q++) {
+                const Pkg& pk = path[gl[j].second[q]];
+                if (bb.hplen[q] != pk.plen || bb.hids[q] != pk.id)
+                    return fail(AMBC_E_DEVICE, "multi-size walk: re-encode differs");
+            }
+        }
     }
     if (!path.empty() && path.back().id == 255) {   // the raw remainder package
         const Pkg& pk = path.back();
@@ -330,6 +402,8 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
     *out_len = body;
     d.ms_steps = steps;
     d.ms_evaluated = evaluated;
+    d.ms_walk_ns = t_walk;
+    d.ms_emit_ns = now_ns() - te;
     TRACE("multisize n=%llu steps=%u evaluated=%llu path=%zu", (unsigned long long)n, steps,
           (unsigned long long)evaluated, path.size());
     if (st) {
@@ -349,9 +423,12 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
     return AMBC_OK;
 }
 
-extern "C" int ambc_last_multisize_info(ambc_ctx* ctx, uint32_t* steps, uint64_t* evaluated) {
+extern "C" int ambc_last_multisize_info(ambc_ctx* ctx, uint32_t* steps, uint64_t* evaluated,
+                                        uint64_t* walk_ns, uint64_t* emit_ns) {
     if (!ctx || ctx->devs.empty()) return fail(AMBC_E_INVAL, "bad context");
     if (steps) *steps = ctx->devs[0].ms_steps;
     if (evaluated) *evaluated = ctx->devs[0].ms_evaluated;
+    if (walk_ns) *walk_ns = ctx->devs[0].ms_walk_ns;
+    if (emit_ns) *emit_ns = ctx->devs[0].ms_emit_ns;
     return AMBC_OK;
 }

@@ -131,8 +131,10 @@ int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const 
                             const uint32_t* cands, uint32_t n_cands, const uint32_t* ent_sizes,
                             const double* const* ent_tabs, uint32_t n_ent, uint8_t* out,
                             uint64_t out_cap, uint64_t* out_len, ambc_stats* st);
-/* of the last ambc_compress_multisize: batched evaluation rounds and chunk encodes */
-int ambc_last_multisize_info(ambc_ctx* ctx, uint32_t* steps, uint64_t* evaluated);
+/* of the last ambc_compress_multisize: batched evaluation rounds, chunk encodes,
+ * wall time of the walks and of the final encode + body assembly */
+int ambc_last_multisize_info(ambc_ctx* ctx, uint32_t* steps, uint64_t* evaluated, uint64_t* walk_ns,
+                             uint64_t* emit_ns);
 
 int ambc_decompress_batch(ambc_ctx* ctx, const uint8_t* body, uint64_t body_len,
                           uint64_t orig_size, uint8_t* out, ambc_stats* st);

@@ -35,24 +35,32 @@ def mixed(n, seed):
     return b"".join(out)[:n]
 
 
+def text(n, seed):
+    """homogeneous text: the largest size wins almost everywhere"""
+    rng = np.random.default_rng(seed)
+    return rng.choice(np.frombuffer(b"etaoin shrdlu,.ETAOIN", np.uint8), n).tobytes()
+
+
 def main():
     sizes = [float(x) for x in sys.argv[1:]] or [32, 256]
-    for methods in ((1, 3, 4, 9), (1, 2, 3, 4)):
+    for kind, methods in (("mixed", (1, 3, 4, 9)), ("mixed", (1, 2, 3, 4)), ("text", (1, 3, 4, 9))):
         for mib in sizes:
-            data = mixed(int(mib * (1 << 20)), 7)
+            data = (mixed if kind == "mixed" else text)(int(mib * (1 << 20)), 7)
             comp = ambc.AdaptiveCompressor(methods=methods)
             comp.CHUNK_SIZE_CANDIDATES = list(comp.REFERENCE_CHUNK_SIZE_CANDIDATES)
             comp._adaptive_compress(data[:1 << 20])            # warm
             t = time.perf_counter()
             body = comp._adaptive_compress(data)
             dt = time.perf_counter() - t
-            steps, ev = C.c_uint32(), C.c_uint64()
+            steps, ev, wns, ens = C.c_uint32(), C.c_uint64(), C.c_uint64(), C.c_uint64()
             lib = ambc._lib.load()
-            lib.ambc_last_multisize_info(ambc._lib.default_context().h, C.byref(steps), C.byref(ev))
-            rec = {"MiB": mib, "methods": list(methods), "seconds": round(dt, 4),
+            lib.ambc_last_multisize_info(ambc._lib.default_context().h, C.byref(steps), C.byref(ev), C.byref(wns),
+                                         C.byref(ens))
+            rec = {"input": kind, "MiB": mib, "methods": list(methods), "seconds": round(dt, 4),
                    "GBps": round(len(data) / dt / 1e9, 3), "ratio": round(len(body) / len(data), 5),
                    "chunks": comp.chunk_stats["total_chunks"], "walk_steps": steps.value,
-                   "chunk_encodes": ev.value}
+                   "chunk_encodes": ev.value, "walk_ms": round(wns.value / 1e6, 2),
+                   "final_encode_ms": round(ens.value / 1e6, 2)}
             if mib <= 32:
                 from oracle import oracle as orc
                 t = time.perf_counter()

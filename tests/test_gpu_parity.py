@@ -555,13 +555,13 @@ def test_multisize_walk_matches_oracle(ctx, methods, cands):
 
 
 def test_multisize_many_walks_match_oracle(ctx):
-    """Inputs long enough for many lock-step walks (one per 128 KiB) that merge
+    """Inputs long enough for many lock-step walks (one per 512 KiB) that merge
     into one another: the body and stats of the reference's single walk (the
     oracle), with the reference's eight candidates and with two."""
     import numpy as np
     rng = np.random.default_rng(11)
     parts = []
-    while sum(len(x) for x in parts) < (4 << 20):
+    while sum(len(x) for x in parts) < (6 << 20):
         k = int(rng.integers(3))
         m = int(rng.integers(8, 65)) << 10
         if k == 0:
@@ -570,7 +570,7 @@ def test_multisize_many_walks_match_oracle(ctx):
             parts.append(rng.choice(np.frombuffer(b"etaoin shrdlu,.ETAOIN", np.uint8), m).tobytes())
         else:
             parts.append(np.minimum(rng.geometric(0.08, m), 255).astype(np.uint8).tobytes())
-    data = b"".join(parts)[:(4 << 20) - 777]
+    data = b"".join(parts)[:(6 << 20) - 777]
     for cands, methods in ((REF_CANDS, (1, 3, 4, 9)), ([2048, 1024], (1, 2, 3, 4))):
         comp = _compressor(methods=methods)
         comp.CHUNK_SIZE_CANDIDATES = list(cands)
