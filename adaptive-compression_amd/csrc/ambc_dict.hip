@@ -47,20 +47,46 @@ constexpr uint32_t DNB = 2048;      // 3-gram hash buckets (11 bits)
 constexpr uint32_t DWIN = 4096;     // compression_methods.py:187 window_size
 constexpr uint32_t DLOOK = 32;      // :187 lookahead_size
 
+#ifndef AMBC_DICT_DG
+#define AMBC_DICT_DG 16
+#endif
+constexpr uint32_t DG = AMBC_DICT_DG;   // lanes per walker (8 or 16)
+#ifndef AMBC_DICT_NW4K
+#define AMBC_DICT_NW4K 8
+#endif
+// NW waves per chunk, 64 / DG walkers of DG lanes each
+template <int CMAX> struct DictCfg {
+    static constexpr int NW = CMAX <= 1024 ? 2 : (CMAX <= 2048 ? 4 : (CMAX <= 4096 ? AMBC_DICT_NW4K : 8));
+};
+
+// one 64-position step of the path walk: first position, token bytes before
+// it, the path's positions among the 64
+struct DictWin {
+    uint32_t p, o;
+    unsigned long long on;
+};
+
 template <int CMAX>
 struct DictSmem {
+    static constexpr int NW = DictCfg<CMAX>::NW;
     alignas(16) uint8_t ch[CMAX + 64];   // the chunk, zero padded
-    alignas(16) uint16_t lst[CMAX];      // 3-gram positions by bucket, ascending inside one
+    union {
+        // 3-gram positions by bucket, ascending inside one
+        alignas(16) uint16_t lst[CMAX];
+        uint32_t bits[256];                 // before the sort: should_use's hash bitmap
+        unsigned long long bk[NW][128];     // the sort: per-wave lane masks per 7-bit bucket
+        DictWin win[CMAX / 64 + 1];         // after the parse: the path's steps
+    };
     // counts (u16 pairs, 32-bit atomics) -> bucket starts (the scatter's cursors)
     // -> bucket ends: after the scatter bucket h is lst[h ? bend[h-1] : 0, bend[h])
     alignas(16) uint32_t bend32[DNB / 2];
-    union {
-        unsigned long long bk[128];      // sort: lane masks per 7-bit bucket
-        // the parse: tok[p] = 0 (not visited) or 1 << 31 | len << 16 | dist
-        // (a literal: len 1) for every position a walker has visited
-        uint32_t tok[CMAX];
-    };
-    uint32_t flag;                       // should_use / abort broadcast
+    // the sort: per position h | group rank << 11 | group count << 18 | last << 25;
+    // the parse: tok[p] = 0 (not visited) or 1 << 31 | len << 16 | dist (a
+    // literal: len 1) for every position a walker has visited
+    alignas(16) uint32_t tok[CMAX];
+    uint32_t flag;    // abort broadcast
+    uint32_t cnt;     // should_use's repeats, then the path's step count
+    uint32_t olen;    // the path's token bytes
     __device__ __forceinline__ uint16_t* bend() { return reinterpret_cast<uint16_t*>(bend32); }
     __device__ __forceinline__ uint32_t bstart(uint32_t h) { return h ? bend()[h - 1] : 0u; }
 };
@@ -82,43 +108,24 @@ __device__ __forceinline__ uint32_t gram_at(const DictSmem<CMAX>& S, uint32_t i)
     return __builtin_amdgcn_alignbyte(hi, lo, i & 3) & 0xFFFFFFu;
 }
 
-// stable counting sort of positions [0, m) by h3 into lst[] (bucket ends in bend[])
+// Stable counting sort of positions [0, m) by h3 into lst[] (bucket ends in
+// bend[]), all waves: every 64-position group ranks its lanes among the
+// group's equal-hash lanes (LDS bucket masks + four ballots) and counts
+// buckets -- groups spread over the waves --, one wave scans the counts, and
+// the scatter is the only serial part: one cursor read per group, in order.
 template <int CMAX>
-__device__ void build_buckets(DictSmem<CMAX>& S, uint32_t m, uint32_t lane) {
-    for (uint32_t b = lane; b < DNB / 2; b += 64) S.bend32[b] = 0;
-    unsigned long long* bk = S.bk;
+__device__ void build_buckets(DictSmem<CMAX>& S, uint32_t m, uint32_t wave, uint32_t lane) {
+    constexpr uint32_t NW = DictSmem<CMAX>::NW, T = 64u * NW;
+    const uint32_t tid = wave * 64u + lane;
+    for (uint32_t b = tid; b < DNB / 2; b += T) S.bend32[b] = 0;
+    unsigned long long* bk = S.bk[wave];
     for (uint32_t b = lane; b < 128; b += 64) bk[b] = 0;
-    wave_sync();
-    // counts < 2^16: two buckets per dword
-    for (uint32_t i = lane; i < m; i += 64) {
-        const uint32_t h = h3(gram_at(S, i));
-        atomicAdd(&S.bend32[h >> 1], 1u << (16 * (h & 1)));
-    }
-    wave_sync();
-    // exclusive scan in place (32 buckets per lane): bucket starts = cursors
-    {
-        uint32_t c[16], t = 0;
-#pragma unroll
-        for (int j = 0; j < 16; j++) {
-            c[j] = S.bend32[lane * 16 + j];
-            t += (c[j] & 0xFFFFu) + (c[j] >> 16);
-        }
-        uint32_t run = wave_incl_sum(t) - t;
-        wave_sync();
-#pragma unroll
-        for (int j = 0; j < 16; j++) {
-            const uint32_t r0 = run, r1 = run + (c[j] & 0xFFFFu);
-            S.bend32[lane * 16 + j] = r0 | r1 << 16;
-            run = r1 + (c[j] >> 16);
-        }
-    }
-    wave_sync();
-    uint16_t* cur = S.bend();
-    // scatter, 64 ascending positions per step; equal-hash lanes keep lane order;
-    // each cursor ends at its bucket's end
+    __syncthreads();
+    const uint64_t below = (1ull << lane) - 1ull;
+    const uint32_t ng = (m + 63) / 64;
 #pragma unroll 1
-    for (uint32_t g = 0; g < m; g += 64) {
-        const uint32_t i = g + lane;
+    for (uint32_t g = wave; g < ng; g += NW) {
+        const uint32_t i = g * 64 + lane;
         const bool v = i < m;
         const uint32_t h = v ? h3(gram_at(S, i)) : 0u;
         if (v) atomicOr(&bk[h & 127u], 1ull << lane);
@@ -129,15 +136,52 @@ __device__ void build_buckets(DictSmem<CMAX>& S, uint32_t m, uint32_t lane) {
             const uint64_t mb = __ballot(v && ((h >> b) & 1u));
             peers &= ((h >> b) & 1u) ? mb : ~mb;
         }
-        const uint32_t base = v ? cur[h] : 0u;
         wave_sync();
         if (v) {
             bk[h & 127u] = 0ull;
-            S.lst[base + __popcll(peers & ((1ull << lane) - 1ull))] = (uint16_t)i;
-            if ((peers >> lane) == 1ull) cur[h] = (uint16_t)(base + (uint32_t)__popcll(peers));
+            const uint32_t cnt = (uint32_t)__popcll(peers);
+            const bool last = (peers >> lane) == 1ull;
+            S.tok[i] = h | (uint32_t)__popcll(peers & below) << 11 | cnt << 18 | (last ? 1u << 25 : 0u);
+            // counts < 2^16: two buckets per dword
+            if (last) atomicAdd(&S.bend32[h >> 1], cnt << (16 * (h & 1)));
         }
         wave_sync();
     }
+    __syncthreads();
+    if (wave == 0) {
+        // exclusive scan in place (32 buckets per lane): bucket starts = cursors
+        uint32_t c[16], t = 0;
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            c[j] = S.bend32[lane * 16 + j];
+            t += (c[j] & 0xFFFFu) + (c[j] >> 16);
+        }
+        uint32_t run = wave_incl_sum(t) - t;
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const uint32_t r0 = run, r1 = run + (c[j] & 0xFFFFu);
+            S.bend32[lane * 16 + j] = r0 | r1 << 16;
+            run = r1 + (c[j] >> 16);
+        }
+        wave_sync();
+        // scatter in position order: equal-hash lanes keep lane order and each
+        // cursor ends at its bucket's end (LDS accesses of one wave stay ordered)
+        uint16_t* cur = S.bend();
+        uint32_t x = lane < m ? S.tok[lane] : 0u;
+#pragma unroll 1
+        for (uint32_t g = 0; g < ng; g++) {
+            const uint32_t i = g * 64 + lane;
+            const uint32_t xn = i + 64 < m ? S.tok[i + 64] : 0u;   // next group's record, early
+            if (i < m) {
+                const uint32_t h = x & 0x7FFu;
+                const uint32_t base = cur[h];
+                S.lst[base + ((x >> 11) & 127u)] = (uint16_t)i;
+                if ((x >> 25) & 1u) cur[h] = (uint16_t)(base + ((x >> 18) & 127u));
+            }
+            x = xn;
+        }
+    }
+    __syncthreads();
 }
 
 // minimum token bytes to cover r more bytes: 4 per 32, the rest one match or literals
@@ -146,59 +190,87 @@ __device__ __forceinline__ uint32_t lb_cost(uint32_t r) {
     return 4u * (r >> 5) + (q ? min(4u, 2u * q) : 0u);
 }
 
-// should_use (compression_methods.py:315-343) by one wave
-template <int CMAX>
-__device__ bool dict_should_use(DictSmem<CMAX>& S, uint32_t n, uint32_t lane) {
-    const uint32_t ss = min(1000u, n);
-    const uint32_t lim = min(n - 3, ss);
-    // distinct 13-bit hashes <= distinct 3-grams: when they already reach
-    // 0.8 ss, should_use is False without the exact count (random data)
-    uint32_t* bits = reinterpret_cast<uint32_t*>(S.bk);    // 8192 bits
-    for (uint32_t w = lane; w < 256; w += 64) bits[w] = 0;
-    wave_sync();
-    for (uint32_t i = lane; i < lim; i += 64) {
-        const uint32_t h = (gram_at(S, i) * 2654435761u) >> 19;
-        atomicOr(&bits[h >> 5], 1u << (h & 31));
+#ifdef AMBC_STAMPS
+// diagnostic build only: wave 0's phase cycles per parsed chunk (s_memtime) in
+// A.stamps[(2 M + k) * 8 + phase]; phase 7 = 1 marks a chunk that was parsed
+#define DSTAMP_DECL uint64_t _st_t = __builtin_amdgcn_s_memtime(); uint64_t _acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define DSTAMP(ph)                                                 \
+    do {                                                           \
+        __builtin_amdgcn_s_waitcnt(0xC07F);                        \
+        const uint64_t _t = __builtin_amdgcn_s_memtime();          \
+        _acc[ph] += _t - _st_t;                                    \
+        _st_t = _t;                                                \
+    } while (0)
+#define DSTAMP_FLUSH                                                                  \
+    if (threadIdx.x == 0 && A.stamps) {                                               \
+        _acc[7] = 1;                                                                  \
+        for (int _p = 0; _p < 8; _p++) A.stamps[(2ull * A.n_chunks + k) * 8 + _p] = _acc[_p]; \
     }
-    wave_sync();
+#else
+#define DSTAMP_DECL
+#define DSTAMP(ph) do {} while (0)
+#define DSTAMP_FLUSH
+#endif
+
+// should_use (compression_methods.py:315-343), all waves.  First the distinct
+// 13-bit hashes of the first lim 3-grams (<= the distinct 3-grams): when they
+// already reach 0.8 ss it is False without the exact count (random data).
+template <int CMAX>
+__device__ bool dict_su_maybe(DictSmem<CMAX>& S, uint32_t n, uint32_t wave, uint32_t lane) {
+    constexpr uint32_t T = 64u * DictSmem<CMAX>::NW;
+    const uint32_t tid = wave * 64u + lane;
+    const uint32_t ss = min(1000u, n), lim = min(n - 3, ss);
+    for (uint32_t w = tid; w < 256; w += T) S.bits[w] = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < lim; i += T) {
+        const uint32_t h = (gram_at(S, i) * 2654435761u) >> 19;
+        atomicOr(&S.bits[h >> 5], 1u << (h & 31));
+    }
+    __syncthreads();
     uint32_t dh = 0;
-    for (uint32_t w = lane; w < 256; w += 64) dh += __popc(bits[w]);
+    for (uint32_t w = lane; w < 256; w += 64) dh += __popc(S.bits[w]);
     dh = wave_sum_u32(dh);
-    wave_sync();
-    if (5 * dh >= 4 * ss) return false;
-    build_buckets(S, lim, lane);
+    __syncthreads();   // the bitmap's words are the sort's next
+    return 5 * dh < 4 * ss;
+}
+
+// the exact count over the buckets (ascending positions: a position repeats iff
+// an earlier entry of its bucket holds the same 3 bytes); S.cnt = 0 beforehand
+template <int CMAX>
+__device__ bool dict_su_exact(DictSmem<CMAX>& S, uint32_t n, uint32_t wave, uint32_t lane) {
+    constexpr uint32_t T = 64u * DictSmem<CMAX>::NW;
+    const uint32_t tid = wave * 64u + lane;
+    const uint32_t ss = min(1000u, n), lim = min(n - 3, ss);
     uint32_t rep = 0;
-    for (uint32_t i = lane; i < lim; i += 64) {
+    for (uint32_t i = tid; i < lim; i += T) {
         const uint32_t g = gram_at(S, i);
-        const uint32_t h = h3(g);
-        for (uint32_t j = S.bstart(h);; j++) {
+        for (uint32_t j = S.bstart(h3(g));; j++) {
             const uint32_t q = S.lst[j];
             if (q >= i) break;
             if (gram_at(S, q) == g) { rep++; break; }
         }
     }
-    const uint32_t u = lim - wave_sum_u32(rep);
-    wave_sync();
-    return 5 * u < 4 * ss;   // u / ss < 0.8 exactly (the quotient is never within an ulp of 0.8)
+    rep = wave_sum_u32(rep);
+    if (lane == 0 && rep) atomicAdd(&S.cnt, rep);
+    __syncthreads();
+    return 5 * (lim - S.cnt) < 4 * ss;   // u / ss < 0.8 exactly (the quotient is never within an ulp of 0.8)
 }
 
-// max over the 16 lanes of a DPP row (every lane gets it): quad butterflies,
-// then rotations by 4 and 8 inside the row
-__device__ __forceinline__ uint32_t row16_max(uint32_t x) {
+// max over the DG lanes of a group (every lane gets it): quad butterflies,
+// then the half-row mirror (8 lanes) and the row mirror (16 lanes)
+__device__ __forceinline__ uint32_t grp_max(uint32_t x) {
     x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, true));   // quad_perm [1,0,3,2]
     x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, true));   // quad_perm [2,3,0,1]
-    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x124, 0xF, 0xF, true));  // row_ror:4
-    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x128, 0xF, 0xF, true));  // row_ror:8
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, true));  // row_half_mirror
+    if (DG == 16) x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x140, 0xF, 0xF, true));  // row_mirror
     return x;
 }
 
-// lanes of my 16-lane group set in a ballot
-__device__ __forceinline__ uint32_t grp16(uint64_t m, uint32_t g) { return (uint32_t)(m >> (16 * g)) & 0xFFFFu; }
+// lanes of my group set in a ballot
+__device__ __forceinline__ uint32_t grp_bits(uint64_t m, uint32_t g) {
+    return (uint32_t)(m >> (DG * g)) & ((1u << DG) - 1u);
+}
 
-constexpr uint32_t DG = 16;   // lanes per walker: 4 walkers per wave
-
-// NW waves per chunk, 4 walkers of 16 lanes each
-template <int CMAX> struct DictCfg { static constexpr int NW = CMAX <= 1024 ? 2 : (CMAX <= 2048 ? 4 : 8); };
 
 // The greedy parse's walkers (compression_methods.py:208-233).  The longest
 // match at p (:279-313) -- the earliest i among the longest, found over the
@@ -225,9 +297,18 @@ __device__ __forceinline__ void dict_walkers(DictSmem<CMAX>& S, uint32_t n, uint
     bool done = false;
 #pragma unroll 1
     for (;;) {
+        // the lookahead bytes p .. p+31 as dwords (the group's lanes read the
+        // same words), issued together with the visited check
+        uint32_t tg[8];
         {
+            const uint32_t a = p < n ? p >> 2 : 0u, sh = p & 3;
+            uint32_t w[9];
+#pragma unroll
+            for (int q = 0; q < 9; q++) w[q] = c32[a + q];
             const uint32_t seen = p < n ? vt[p] : 1u;
             done = done || seen != 0 || *vflag != 0;
+#pragma unroll
+            for (int q = 0; q < 8; q++) tg[q] = __builtin_amdgcn_alignbyte(w[q + 1], w[q], sh);
         }
         if (w0 && !done && !force && (int)(o + lb_cost(n - p)) > lim2) {
             if (r == 0) *vflag = 1u;   // id 2 cannot win: every walker stops
@@ -235,16 +316,6 @@ __device__ __forceinline__ void dict_walkers(DictSmem<CMAX>& S, uint32_t n, uint
         }
         if (__all(done)) break;
         const uint32_t look = done ? 0u : min(DLOOK, n - p);
-        // the lookahead bytes p .. p+31 as dwords (the group's lanes read the same words)
-        uint32_t tg[8];
-        {
-            const uint32_t a = done ? 0u : p >> 2, sh = p & 3;
-            uint32_t w[9];
-#pragma unroll
-            for (int q = 0; q < 9; q++) w[q] = c32[a + q];
-#pragma unroll
-            for (int q = 0; q < 8; q++) tg[q] = __builtin_amdgcn_alignbyte(w[q + 1], w[q], sh);
-        }
         const uint32_t h = h3(tg[0]);
         uint32_t j = S.bstart(h);
         const uint32_t e = look >= 3 ? (uint32_t)S.bend()[h] : j;
@@ -258,7 +329,7 @@ __device__ __forceinline__ void dict_walkers(DictSmem<CMAX>& S, uint32_t n, uint
                 const uint32_t len = hi - lo;
                 const uint32_t st = (len + DG - 1) / DG;
                 const uint32_t idx = lo + r * st;
-                const uint32_t c = __popc(grp16(__ballot(hi > lo && idx < hi && S.lst[idx] < ws), g));
+                const uint32_t c = __popc(grp_bits(__ballot(hi > lo && idx < hi && S.lst[idx] < ws), g));
                 if (hi > lo) {
                     if (c == 0) hi = lo;
                     else {
@@ -289,11 +360,11 @@ __device__ __forceinline__ void dict_walkers(DictSmem<CMAX>& S, uint32_t n, uint
                 f[q] = ffbl_raw((uint32_t)__builtin_amdgcn_alignbyte(w[q + 1], w[q], sh) ^ tg[q]) | (uint32_t)q << 5;
             const uint32_t fm = min(min(min(f[0], f[1]), min(f[2], f[3])), min(min(f[4], f[5]), min(f[6], f[7])));
             const uint32_t L = v ? min(fm >> 3, look) : 0u;
-            key = max(key, row16_max(v ? (L << 16 | (0xFFFFu - i)) : 0u));
+            key = max(key, grp_max(v ? (L << 16 | (0xFFFFu - i)) : 0u));
             // ascending candidates: stop at the cap (the earliest reaching it
             // wins) or once the run reached p or the bucket's end
-            const uint32_t vg = grp16(__ballot(v), g);
-            gd = gd || vg != 0xFFFFu || (key >> 16) >= look;
+            const uint32_t vg = grp_bits(__ballot(v), g);
+            gd = gd || vg != (1u << DG) - 1u || (key >> 16) >= look;
             j += DG;
         }
         if (!done) {
@@ -331,6 +402,7 @@ __global__ __launch_bounds__(64 * DictCfg<CMAX>::NW) void k_dict(EncArgs A) {
     }
     const bool want = elig && (force || lim2 >= (int)(2 + lb_cost(n - 1)));
     if (!want && !analyze) return;
+    DSTAMP_DECL
     const uint8_t* src = A.in + pos0;
     const uint32_t ns = min(n, (uint32_t)CMAX);
     {
@@ -345,78 +417,102 @@ __global__ __launch_bounds__(64 * DictCfg<CMAX>::NW) void k_dict(EncArgs A) {
         }
         for (uint32_t i = ns + threadIdx.x; i < (uint32_t)CMAX + 64; i += T) S.ch[i] = 0;
     }
-    __syncthreads();
-
-    const uint32_t m = n >= 3 ? n - 2 : 0;
-    if (wave == 0) {
-        const bool su = !force && n >= 100 && dict_should_use(S, n, lane);
-        if (analyze && A.su && lane == 0) A.su[k] |= su ? 4 : 0;
-        const bool go = want && (force || su);
-        if (go) build_buckets(S, m, lane);
-        if (lane == 0) S.flag = go ? 0u : 1u;
+    if (threadIdx.x == 0) {
+        S.flag = 0;
+        S.cnt = 0;
     }
     __syncthreads();
-    if (S.flag) return;
+    DSTAMP(0);
+
+    // ---- should_use (compression_methods.py:315-343) and the buckets ----
+    const uint32_t m = n >= 3 ? n - 2 : 0;
+    const bool need_su = !force && n >= 100;
+    const bool maybe = need_su && dict_su_maybe(S, n, wave, lane);
+    DSTAMP(1);
+    if (!(force || maybe)) return;   // su False: nothing to record, no parse
+    // (analyze mode also sees chunks beyond CMAX: should_use reads only the
+    // first 1003 bytes, and the sort stays inside the loaded ns)
+    build_buckets(S, min(m, ns - 2), wave, lane);
+    DSTAMP(2);
+    const bool su = need_su && dict_su_exact(S, n, wave, lane);
+    if (analyze && A.su && threadIdx.x == 0) A.su[k] |= su ? 4 : 0;
+    DSTAMP(1);
+    if (!want || (!force && !su)) return;
     for (uint32_t i = threadIdx.x; i < (uint32_t)CMAX; i += 64u * NW) S.tok[i] = 0;
     __syncthreads();
+    DSTAMP(3);
 
     // ---- the greedy parse (compression_methods.py:208-233) ----
     dict_walkers(S, n, wave, lane, force, lim2);
+    DSTAMP(4);
     __syncthreads();
-    if (wave != 0 || S.flag) return;
+    DSTAMP(5);
+    if (S.flag) return;
 
-    // ---- walker 0's path, 64 positions per step: chain walk over tok[] in
-    // registers, then every token of the step written at its prefix offset ----
-    uint8_t* slot = A.slots + (uint64_t)k * A.slot_stride;
-    // tokens: a forced encode writes the slot; otherwise they stage in the
-    // slot's upper half (C bytes >= any winning payload) and move down only if
-    // id 2 wins, so k_encode's payload stays intact
-    uint8_t* stage = force ? slot : slot + A.chunk_size + 64;
-    uint16_t* stg16 = reinterpret_cast<uint16_t*>(stage);
-    uint32_t p = 0, o = 0;
+    // ---- walker 0's path from 0 in 64-position steps: a chain walk over tok[]
+    // in registers (wave 0) records each step, and the token bytes decide the
+    // selection before anything is written ----
     const uint64_t below = (1ull << lane) - 1ull;
+    if (wave == 0) {
+        uint32_t p = 0, o = 0, nw = 0;
+        bool lost = false;
 #pragma unroll 1
-    while (p < n) {
-        const uint32_t t = p + lane < n ? S.tok[p + lane] : 0u;
-        uint64_t on = 0;
-        uint32_t q = p;
-        while (q < n && q < p + 64) {
-            const uint32_t tq = __builtin_amdgcn_readlane(t, q - p);
-            on |= 1ull << (q - p);
-            q += max(1u, (tq >> 16) & 0xFFu);
+        while (p < n) {
+            const uint32_t t = p + lane < n ? S.tok[p + lane] : 0u;
+            uint64_t on = 0;
+            uint32_t q = p;
+            while (q < n && q < p + 64) {
+                const uint32_t tq = __builtin_amdgcn_readlane(t, q - p);
+                on |= 1ull << (q - p);
+                q += max(1u, (tq >> 16) & 0xFFu);
+            }
+            const uint64_t mm = __ballot(((on >> lane) & 1u) && ((t >> 16) & 0xFFu) > 2);
+            const uint32_t tot = 2u * (uint32_t)(__popcll(on) + __popcll(mm));
+            if (!force && (int)(o + tot) > lim2) { lost = true; break; }   // id 2 loses
+            if (lane == 0) S.win[nw] = DictWin{p, o, on};
+            o += tot;
+            nw++;
+            p = q;
         }
-        const bool me = (on >> lane) & 1u;
+        if (lane == 0) {
+            S.flag = lost ? 1u : 0u;
+            S.cnt = nw;
+            S.olen = o;
+        }
+    }
+    __syncthreads();
+    if (S.flag) return;
+    // ---- id 2 wins (or is forced): every wave writes its steps' tokens into
+    // the slot at their prefix offsets ----
+    uint8_t* slot = A.slots + (uint64_t)k * A.slot_stride;
+    uint16_t* s16 = reinterpret_cast<uint16_t*>(slot);
+    const uint32_t nw = S.cnt, o = S.olen;
+#pragma unroll 1
+    for (uint32_t wi = wave; wi < nw; wi += NW) {
+        const DictWin w = S.win[wi];
+        const uint32_t t = w.p + lane < n ? S.tok[w.p + lane] : 0u;
+        const bool me = (w.on >> lane) & 1u;
         const uint32_t L = (t >> 16) & 0xFFu;
         const bool mt = me && L > 2;
         const uint64_t mm = __ballot(mt);
-        const uint32_t tot = 2u * (uint32_t)(__popcll(on) + __popcll(mm));
-        if (!force && (int)(o + tot) > lim2) return;   // id 2 loses
-        const uint32_t off = o + 2u * (uint32_t)(__popcll(on & below) + __popcll(mm & below));
+        const uint32_t off = w.o + 2u * (uint32_t)(__popcll(w.on & below) + __popcll(mm & below));
         if (mt) {
             const uint32_t d = t & 0xFFFFu;
-            stg16[off >> 1] = (uint16_t)(1u | (d & 0xFFu) << 8);
-            stg16[(off >> 1) + 1] = (uint16_t)((d >> 8) | L << 8);
+            s16[off >> 1] = (uint16_t)(1u | (d & 0xFFu) << 8);
+            s16[(off >> 1) + 1] = (uint16_t)((d >> 8) | L << 8);
         } else if (me) {
-            stg16[off >> 1] = (uint16_t)(S.ch[p + lane] << 8);
+            s16[off >> 1] = (uint16_t)(S.ch[w.p + lane] << 8);
         }
-        o += tot;
-        p = q;
     }
-    if (!force) {
-        // id 2 wins: its tokens replace k_encode's payload
-        __threadfence();
-        wave_sync();
-        const uint32_t nw = (o + 3) >> 2;
-        const uint32_t* src32 = reinterpret_cast<const uint32_t*>(stage);
-        for (uint32_t q = lane; q < nw; q += 64) reinterpret_cast<uint32_t*>(slot)[q] = src32[q];
-    }
-    if (lane == 0) {
+    if (threadIdx.x == 0) {
         A.ids[k] = 2;
         A.plen[k] = o;
         A.sizes[k] = (uint64_t)HDR + o;
         if (A.pending) A.pending[k] = 0;
         if (A.bestpre) A.bestpre[k] = (A.bestpre[k] & 0xC0000000u) | (o + HDR);
     }
+    DSTAMP(6);
+    DSTAMP_FLUSH
 }
 
 template <int CMAX>

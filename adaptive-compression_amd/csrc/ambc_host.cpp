@@ -267,8 +267,8 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
     TRACE("compress_on n=%llu M=%u C=%u", (unsigned long long)n, M, C);
     std::vector<unsigned long long> stamps;
     if (getenv("AMBC_STAMPS")) {   // k_encode: M x 8 records, k_deflate: the next M x 8
-        HIPCHK(d.seg.ensure((size_t)std::max<uint32_t>(M, 1) * 128));
-        HIPCHK(hipMemsetAsync(d.seg.p, 0, (size_t)M * 128, s));
+        HIPCHK(d.seg.ensure((size_t)std::max<uint32_t>(M, 1) * 192));   // + k_dict: the third M x 8
+        HIPCHK(hipMemsetAsync(d.seg.p, 0, (size_t)M * 192, s));
         ea.stamps = d.seg.as<unsigned long long>();
     }
     const bool deflate = (p->method_mask >> AMBC_M_DEFLATE) & 1;
@@ -379,6 +379,18 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
         fprintf(stderr, "[ambc stamps] M=%u cycles/chunk: passA %.0f huff %.0f lz4hash %.0f lz4len %.0f "
                 "lz4walk %.0f lz4tail+emit %.0f final %.0f lz4emit %.0f\n", M, sum[0] / M, sum[1] / M,
                 sum[2] / M, sum[3] / M, sum[4] / M, sum[5] / M, sum[6] / M, sum[7] / M);
+        if ((p->method_mask >> AMBC_M_DICT) & 1) {
+            std::vector<unsigned long long> g((size_t)M * 8);
+            HIPCHK(hipMemcpyAsync(g.data(), d.seg.as<unsigned long long>() + (size_t)M * 16, (size_t)M * 64,
+                                  hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            double gs[8] = {0};
+            for (size_t q = 0; q < g.size(); q++) gs[q & 7] += (double)g[q];
+            const double c = std::max(gs[7], 1.0);
+            fprintf(stderr, "[ambc stamps] dict parsed=%.0f wave-0 cycles/chunk: load %.0f should_use %.0f "
+                    "buckets %.0f clear %.0f walk %.0f wait %.0f path+out %.0f\n", gs[7], gs[0] / c, gs[1] / c,
+                    gs[2] / c, gs[3] / c, gs[4] / c, gs[5] / c, gs[6] / c);
+        }
         if (deflate) {
             std::vector<unsigned long long> g((size_t)M * 8);
             HIPCHK(hipMemcpyAsync(g.data(), d.seg.as<unsigned long long>() + (size_t)M * 8, (size_t)M * 64,
