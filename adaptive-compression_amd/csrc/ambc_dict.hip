@@ -59,12 +59,6 @@ template <int CMAX> struct DictCfg {
     static constexpr int NW = CMAX <= 1024 ? 2 : (CMAX <= 2048 ? 4 : (CMAX <= 4096 ? AMBC_DICT_NW4K : 8));
 };
 
-// one 64-position step of the path walk: first position, token bytes before
-// it, the path's positions among the 64
-struct DictWin {
-    uint32_t p, o;
-    unsigned long long on;
-};
 
 template <int CMAX>
 struct DictSmem {
@@ -75,7 +69,12 @@ struct DictSmem {
         alignas(16) uint16_t lst[CMAX];
         uint32_t bits[256];                 // before the sort: should_use's hash bitmap
         unsigned long long bk[NW][128];     // the sort: per-wave lane masks per 7-bit bucket
-        DictWin win[CMAX / 64 + 1];         // after the parse: the path's steps
+        struct {
+            // after the parse, per wave's block of 64-position windows and entry
+            // offset e < 32 into its first window: the next block's entry | bytes << 8
+            uint32_t etab[NW][32];
+            uint32_t be[NW], bo[NW];        // each block's entry and token bytes before it
+        } path;
     };
     // counts (u16 pairs, 32-bit atomics) -> bucket starts (the scatter's cursors)
     // -> bucket ends: after the scatter bucket h is lst[h ? bend[h-1] : 0, bend[h])
@@ -449,59 +448,96 @@ __global__ __launch_bounds__(64 * DictCfg<CMAX>::NW) void k_dict(EncArgs A) {
     DSTAMP(5);
     if (S.flag) return;
 
-    // ---- walker 0's path from 0 in 64-position steps: a chain walk over tok[]
-    // in registers (wave 0) records each step, and the token bytes decide the
+    // ---- walker 0's path from 0.  Each wave takes a block of consecutive
+    // 64-position windows; per window, pointer doubling over lanes gives every
+    // position's chain to the first position past the window (entries are the
+    // window's first 32 positions) and its token bytes; composed over the block
+    // they form a 32-entry table, and one short serial pass over the blocks
+    // yields every block's entry and output offset -- the token bytes decide the
     // selection before anything is written ----
+    constexpr uint32_t WPB = ((uint32_t)CMAX / 64 + NW - 1) / NW;   // windows per block, at most
+    const uint32_t nwin = (n + 63) / 64;
+    const uint32_t wpb = (nwin + NW - 1) / NW;
+    const uint32_t wb0 = wave * wpb;
     const uint64_t below = (1ull << lane) - 1ull;
-    if (wave == 0) {
-        uint32_t p = 0, o = 0, nw = 0;
-        bool lost = false;
-#pragma unroll 1
-        while (p < n) {
-            const uint32_t t = p + lane < n ? S.tok[p + lane] : 0u;
-            uint64_t on = 0;
-            uint32_t q = p;
-            while (q < n && q < p + 64) {
-                const uint32_t tq = __builtin_amdgcn_readlane(t, q - p);
-                on |= 1ull << (q - p);
-                q += max(1u, (tq >> 16) & 0xFFu);
+    {
+        uint32_t E = lane & 31u, BB = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < WPB; i++) {
+            const uint32_t wi = wb0 + i;
+            if (i >= wpb || wi >= nwin) break;
+            const uint32_t pos = wi * 64 + lane;
+            const uint32_t t = pos < n ? S.tok[pos] : 0u;
+            const uint32_t L = (t >> 16) & 0xFFu;
+            uint32_t J = pos < n ? lane + max(L, 1u) : 64u;
+            uint32_t B = pos < n && t ? (L > 2 ? 4u : 2u) : 0u;
+#pragma unroll
+            for (int r = 0; r < 6; r++) {
+                const int src = (int)(min(J, 63u) << 2);
+                const uint32_t Bj = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)B);
+                const uint32_t Jj = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)J);
+                B = J < 64 ? B + Bj : B;
+                J = J < 64 ? Jj : J;
             }
-            const uint64_t mm = __ballot(((on >> lane) & 1u) && ((t >> 16) & 0xFFu) > 2);
-            const uint32_t tot = 2u * (uint32_t)(__popcll(on) + __popcll(mm));
-            if (!force && (int)(o + tot) > lim2) { lost = true; break; }   // id 2 loses
-            if (lane == 0) S.win[nw] = DictWin{p, o, on};
-            o += tot;
-            nw++;
-            p = q;
+            // J - 64 < 32: the entry into the next window
+            const uint32_t x = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(E << 2), (int)((J - 64) | B << 8));
+            BB += x >> 8;
+            E = x & 31u;
         }
-        if (lane == 0) {
-            S.flag = lost ? 1u : 0u;
-            S.cnt = nw;
-            S.olen = o;
+        if (lane < 32) S.path.etab[wave][lane] = E | BB << 8;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t e = 0, o = 0;
+        for (uint32_t w = 0; w < (uint32_t)NW; w++) {
+            S.path.be[w] = e;
+            S.path.bo[w] = o;
+            if (w * wpb < nwin) {
+                const uint32_t x = S.path.etab[w][e];
+                e = x & 31u;
+                o += x >> 8;
+            }
         }
+        S.olen = o;
+        if (!force && (int)o > lim2) S.flag = 1u;   // id 2 loses
     }
     __syncthreads();
     if (S.flag) return;
-    // ---- id 2 wins (or is forced): every wave writes its steps' tokens into
-    // the slot at their prefix offsets ----
+    // ---- id 2 wins (or is forced): every wave walks its block's path from its
+    // entry (chain walk in registers) and writes the tokens into the slot at
+    // their prefix offsets ----
     uint8_t* slot = A.slots + (uint64_t)k * A.slot_stride;
     uint16_t* s16 = reinterpret_cast<uint16_t*>(slot);
-    const uint32_t nw = S.cnt, o = S.olen;
+    const uint32_t o = S.olen;
+    {
+        uint32_t e = S.path.be[wave], ob = S.path.bo[wave];
 #pragma unroll 1
-    for (uint32_t wi = wave; wi < nw; wi += NW) {
-        const DictWin w = S.win[wi];
-        const uint32_t t = w.p + lane < n ? S.tok[w.p + lane] : 0u;
-        const bool me = (w.on >> lane) & 1u;
-        const uint32_t L = (t >> 16) & 0xFFu;
-        const bool mt = me && L > 2;
-        const uint64_t mm = __ballot(mt);
-        const uint32_t off = w.o + 2u * (uint32_t)(__popcll(w.on & below) + __popcll(mm & below));
-        if (mt) {
-            const uint32_t d = t & 0xFFFFu;
-            s16[off >> 1] = (uint16_t)(1u | (d & 0xFFu) << 8);
-            s16[(off >> 1) + 1] = (uint16_t)((d >> 8) | L << 8);
-        } else if (me) {
-            s16[off >> 1] = (uint16_t)(S.ch[w.p + lane] << 8);
+        for (uint32_t i = 0; i < wpb; i++) {
+            const uint32_t wi = wb0 + i;
+            if (wi >= nwin) break;
+            const uint32_t p0 = wi * 64;
+            const uint32_t t = p0 + lane < n ? S.tok[p0 + lane] : 0u;
+            uint64_t on = 0;
+            uint32_t q = e;
+            while (q < 64 && p0 + q < n) {
+                const uint32_t tq = __builtin_amdgcn_readlane(t, q);
+                on |= 1ull << q;
+                q += max(1u, (tq >> 16) & 0xFFu);
+            }
+            const bool me = (on >> lane) & 1u;
+            const uint32_t L = (t >> 16) & 0xFFu;
+            const bool mt = me && L > 2;
+            const uint64_t mm = __ballot(mt);
+            const uint32_t off = ob + 2u * (uint32_t)(__popcll(on & below) + __popcll(mm & below));
+            if (mt) {
+                const uint32_t d = t & 0xFFFFu;
+                s16[off >> 1] = (uint16_t)(1u | (d & 0xFFu) << 8);
+                s16[(off >> 1) + 1] = (uint16_t)((d >> 8) | L << 8);
+            } else if (me) {
+                s16[off >> 1] = (uint16_t)(S.ch[p0 + lane] << 8);
+            }
+            ob += 2u * (uint32_t)(__popcll(on) + __popcll(mm));
+            e = q - 64;
         }
     }
     if (threadIdx.x == 0) {
