@@ -10,29 +10,32 @@
 // reproduced byte for byte (oracle/ambc_oracle.c orc_dict_*).
 //
 // A match of length > 2 starts with the same 3 bytes, so the candidates of p
-// are exactly the earlier positions of its 3-gram.  One 64-lane wavefront per
-// chunk:
-//   1. the chunk in LDS; the 3-gram positions counting-sorted by an 11-bit
-//      hash into lst[] -- STABLY (positions ascending inside a bucket: ranks
-//      among equal-hash lanes of a 64-position group from LDS bucket masks +
-//      four ballots), bst[] = bucket starts;
-//   2. should_use: the same sort over the first lim positions; a position is
-//      a repeat iff an earlier entry of its bucket holds the same 3 bytes;
-//   3. the greedy parse, serial over tokens: for p, the bucket's entries in
-//      the window are a contiguous ascending run (the window start advances
-//      monotonically per bucket, wp[], for chunks beyond the 4096-byte
-//      window); 64 candidates per step compare 32
-//      bytes as dwords (v_alignbyte), and a wave max over (len << 16 | ~i)
-//      keeps the longest, earliest one.  Oldest-first order lets a step stop
-//      as soon as a candidate reaches the lookahead cap (runs, repeats).
+// are exactly the earlier positions of its 3-gram -- and the match at p does
+// not depend on how the parse reached p.  One workgroup of NW waves per chunk:
+//   1. the chunk in LDS; should_use's quick reject (distinct 13-bit hashes);
+//   2. the 3-gram positions counting-sorted by an 11-bit hash into lst[],
+//      STABLY (ascending inside a bucket): per 1024-position range and wave,
+//      ballot ranks + range cursors, then per-bucket range offsets;
+//      should_use exactly over the buckets (a repeat = an earlier entry of
+//      the bucket with the same 3 bytes);
+//   3. the parse by 64 / DG walkers per wave (DG-lane groups) from NW * 64 / DG
+//      starts: a walker's match search takes the bucket's ascending run DG
+//      candidates at a time (12 bytes compared first, 32 only when a
+//      candidate matched 12), a group max over (len << 16 | ~i) keeps the
+//      longest, earliest one; it records tok[p] and stops on a position another
+//      walker visited (parses meet within a few tokens);
+//   4. the path from 0 through tok[]: pointer doubling per 64-position window,
+//      window tables composed per wave block, one serial pass over the blocks,
+//      then every wave writes its block's tokens at their prefix offsets.
 //
 // Selection keeps the reference's order (ids ascending, strict '<'): k_encode
 // has already picked the best of ids 1/3/4/9 (exact length of the winner;
 // everything it skipped is provably no shorter), so id 2 wins iff
 // len + 18 < T, or len + 18 == T against ids 3/4/9; T = winner len + 18 (raw:
-// n).  The parse stops as soon as its length plus a lower bound of the rest
-// (4 bytes per 32 still to cover) can no longer win, and stages its tokens in
-// LDS, so the slot keeps k_encode's payload unless id 2 wins.  Runs between
+// n).  Walker 0 stops the parse as soon as its length plus a lower bound of the
+// rest (4 bytes per 32 still to cover) can no longer win, and the path's token
+// bytes are known before any is written, so the slot keeps k_encode's payload
+// unless id 2 wins.  Runs between
 // k_encode and k_deflate, which then sees id 2's length as the bar to beat.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -48,9 +51,12 @@ constexpr uint32_t DWIN = 4096;     // compression_methods.py:187 window_size
 constexpr uint32_t DLOOK = 32;      // :187 lookahead_size
 
 #ifndef AMBC_DICT_DG
-#define AMBC_DICT_DG 16
+#define AMBC_DICT_DG 8
 #endif
 constexpr uint32_t DG = AMBC_DICT_DG;   // lanes per walker (8 or 16)
+#ifndef AMBC_DICT_2STAGE
+#define AMBC_DICT_2STAGE 1
+#endif
 #ifndef AMBC_DICT_NW4K
 #define AMBC_DICT_NW4K 8
 #endif
@@ -68,7 +74,6 @@ struct DictSmem {
         // 3-gram positions by bucket, ascending inside one
         alignas(16) uint16_t lst[CMAX];
         uint32_t bits[256];                 // before the sort: should_use's hash bitmap
-        unsigned long long bk[NW][128];     // the sort: per-wave lane masks per 7-bit bucket
         struct {
             // after the parse, per wave's block of 64-position windows and entry
             // offset e < 32 into its first window: the next block's entry | bytes << 8
@@ -79,7 +84,7 @@ struct DictSmem {
     // counts (u16 pairs, 32-bit atomics) -> bucket starts (the scatter's cursors)
     // -> bucket ends: after the scatter bucket h is lst[h ? bend[h-1] : 0, bend[h])
     alignas(16) uint32_t bend32[DNB / 2];
-    // the sort: per position h | group rank << 11 | group count << 18 | last << 25;
+    // the sort: per range and bucket a cursor (u16);
     // the parse: tok[p] = 0 (not visited) or 1 << 31 | len << 16 | dist (a
     // literal: len 1) for every position a walker has visited
     alignas(16) uint32_t tok[CMAX];
@@ -108,47 +113,56 @@ __device__ __forceinline__ uint32_t gram_at(const DictSmem<CMAX>& S, uint32_t i)
 }
 
 // Stable counting sort of positions [0, m) by h3 into lst[] (bucket ends in
-// bend[]), all waves: every 64-position group ranks its lanes among the
-// group's equal-hash lanes (LDS bucket masks + four ballots) and counts
-// buckets -- groups spread over the waves --, one wave scans the counts, and
-// the scatter is the only serial part: one cursor read per group, in order.
+// bend[]).  The chunk splits into CMAX / 1024 ranges of 16 64-position groups,
+// one wave each, with its own cursor per bucket (in tok[], free until the
+// parse): a group ranks its lanes among its equal-hash lanes (eleven ballots)
+// and advances the range's cursors -- 16 dependent steps per range, ranges in
+// parallel.  Per bucket the ranges' counts turn into offsets, one wave scans
+// the totals into bucket ends, and the ranges scatter without further order.
 template <int CMAX>
 __device__ void build_buckets(DictSmem<CMAX>& S, uint32_t m, uint32_t wave, uint32_t lane) {
     constexpr uint32_t NW = DictSmem<CMAX>::NW, T = 64u * NW;
+    constexpr uint32_t NR = (uint32_t)CMAX / 1024, GR = 16;
+    static_assert(NR >= 1 && NR <= NW && NR * DNB * 2 <= (uint32_t)CMAX * 4, "cursor arrays live in tok[]");
+    uint16_t* cnt = reinterpret_cast<uint16_t*>(S.tok);   // [NR][DNB]
     const uint32_t tid = wave * 64u + lane;
-    for (uint32_t b = tid; b < DNB / 2; b += T) S.bend32[b] = 0;
-    unsigned long long* bk = S.bk[wave];
-    for (uint32_t b = lane; b < 128; b += 64) bk[b] = 0;
+    for (uint32_t b = tid; b < NR * DNB / 2; b += T) S.tok[b] = 0;
     __syncthreads();
     const uint64_t below = (1ull << lane) - 1ull;
-    const uint32_t ng = (m + 63) / 64;
-#pragma unroll 1
-    for (uint32_t g = wave; g < ng; g += NW) {
-        const uint32_t i = g * 64 + lane;
-        const bool v = i < m;
-        const uint32_t h = v ? h3(gram_at(S, i)) : 0u;
-        if (v) atomicOr(&bk[h & 127u], 1ull << lane);
-        wave_sync();
-        uint64_t peers = v ? bk[h & 127u] : 0ull;
+    uint32_t loc[GR];   // my index inside my bucket's part of the range | h << 16, ~0: none
+    if (wave < NR) {
+        uint16_t* c = cnt + wave * DNB;
 #pragma unroll
-        for (int b = 7; b < 11; b++) {
-            const uint64_t mb = __ballot(v && ((h >> b) & 1u));
-            peers &= ((h >> b) & 1u) ? mb : ~mb;
+        for (uint32_t g = 0; g < GR; g++) {
+            const uint32_t i = (wave * GR + g) * 64 + lane;
+            const bool v = i < m;
+            const uint32_t h = v ? h3(gram_at(S, i)) : 0u;
+            uint64_t peers = __ballot(v);
+#pragma unroll
+            for (int b = 0; b < 11; b++) {
+                const uint64_t mb = __ballot(v && ((h >> b) & 1u));
+                peers &= ((h >> b) & 1u) ? mb : ~mb;
+            }
+            const uint32_t base = v ? (uint32_t)c[h] : 0u;
+            loc[g] = v ? (base + (uint32_t)__popcll(peers & below)) | h << 16 : ~0u;
+            if (v && (peers >> lane) == 1ull) c[h] = (uint16_t)(base + (uint32_t)__popcll(peers));
         }
-        wave_sync();
-        if (v) {
-            bk[h & 127u] = 0ull;
-            const uint32_t cnt = (uint32_t)__popcll(peers);
-            const bool last = (peers >> lane) == 1ull;
-            S.tok[i] = h | (uint32_t)__popcll(peers & below) << 11 | cnt << 18 | (last ? 1u << 25 : 0u);
-            // counts < 2^16: two buckets per dword
-            if (last) atomicAdd(&S.bend32[h >> 1], cnt << (16 * (h & 1)));
+    }
+    __syncthreads();
+    // per bucket: the ranges' counts -> their offsets inside the bucket; the total
+    for (uint32_t h = tid; h < DNB; h += T) {
+        uint32_t run = 0;
+#pragma unroll
+        for (uint32_t r = 0; r < NR; r++) {
+            const uint32_t x = cnt[r * DNB + h];
+            cnt[r * DNB + h] = (uint16_t)run;
+            run += x;
         }
-        wave_sync();
+        S.bend()[h] = (uint16_t)run;
     }
     __syncthreads();
     if (wave == 0) {
-        // exclusive scan in place (32 buckets per lane): bucket starts = cursors
+        // inclusive scan in place (32 buckets per lane): bucket ends
         uint32_t c[16], t = 0;
 #pragma unroll
         for (int j = 0; j < 16; j++) {
@@ -158,26 +172,19 @@ __device__ void build_buckets(DictSmem<CMAX>& S, uint32_t m, uint32_t wave, uint
         uint32_t run = wave_incl_sum(t) - t;
 #pragma unroll
         for (int j = 0; j < 16; j++) {
-            const uint32_t r0 = run, r1 = run + (c[j] & 0xFFFFu);
+            const uint32_t r0 = run + (c[j] & 0xFFFFu), r1 = r0 + (c[j] >> 16);
             S.bend32[lane * 16 + j] = r0 | r1 << 16;
-            run = r1 + (c[j] >> 16);
+            run = r1;
         }
-        wave_sync();
-        // scatter in position order: equal-hash lanes keep lane order and each
-        // cursor ends at its bucket's end (LDS accesses of one wave stay ordered)
-        uint16_t* cur = S.bend();
-        uint32_t x = lane < m ? S.tok[lane] : 0u;
-#pragma unroll 1
-        for (uint32_t g = 0; g < ng; g++) {
-            const uint32_t i = g * 64 + lane;
-            const uint32_t xn = i + 64 < m ? S.tok[i + 64] : 0u;   // next group's record, early
-            if (i < m) {
-                const uint32_t h = x & 0x7FFu;
-                const uint32_t base = cur[h];
-                S.lst[base + ((x >> 11) & 127u)] = (uint16_t)i;
-                if ((x >> 25) & 1u) cur[h] = (uint16_t)(base + ((x >> 18) & 127u));
+    }
+    __syncthreads();
+    if (wave < NR) {
+#pragma unroll
+        for (uint32_t g = 0; g < GR; g++) {
+            if (loc[g] != ~0u) {
+                const uint32_t h = loc[g] >> 16;
+                S.lst[S.bstart(h) + cnt[wave * DNB + h] + (loc[g] & 0xFFFFu)] = (uint16_t)((wave * GR + g) * 64 + lane);
             }
-            x = xn;
         }
     }
     __syncthreads();
@@ -350,6 +357,24 @@ __device__ __forceinline__ void dict_walkers(DictSmem<CMAX>& S, uint32_t n, uint
             // the candidate's 32 bytes (nine dwords issued together), compared
             // as dwords: 32 q + the first differing bit of dword q, ffbl(0) = ~0
             const uint32_t a = v ? i >> 2 : 0u, sh = i & 3;
+#if AMBC_DICT_2STAGE
+            // the first 12 bytes; the other 20 only when a candidate matches all 12
+            uint32_t w[9], f[8];
+#pragma unroll
+            for (int q = 0; q < 4; q++) w[q] = c32[a + q];
+#pragma unroll
+            for (int q = 0; q < 3; q++)
+                f[q] = ffbl_raw((uint32_t)__builtin_amdgcn_alignbyte(w[q + 1], w[q], sh) ^ tg[q]) | (uint32_t)q << 5;
+            uint32_t fm = min(min(f[0], f[1]), f[2]);
+            if (__any(v && fm == ~0u)) {
+#pragma unroll
+                for (int q = 4; q < 9; q++) w[q] = c32[a + q];
+#pragma unroll
+                for (int q = 3; q < 8; q++)
+                    f[q] = ffbl_raw((uint32_t)__builtin_amdgcn_alignbyte(w[q + 1], w[q], sh) ^ tg[q]) | (uint32_t)q << 5;
+                fm = min(fm, min(min(min(f[3], f[4]), min(f[5], f[6])), f[7]));
+            }
+#else
             uint32_t w[9];
 #pragma unroll
             for (int q = 0; q < 9; q++) w[q] = c32[a + q];
@@ -358,6 +383,7 @@ __device__ __forceinline__ void dict_walkers(DictSmem<CMAX>& S, uint32_t n, uint
             for (int q = 0; q < 8; q++)
                 f[q] = ffbl_raw((uint32_t)__builtin_amdgcn_alignbyte(w[q + 1], w[q], sh) ^ tg[q]) | (uint32_t)q << 5;
             const uint32_t fm = min(min(min(f[0], f[1]), min(f[2], f[3])), min(min(f[4], f[5]), min(f[6], f[7])));
+#endif
             const uint32_t L = v ? min(fm >> 3, look) : 0u;
             key = max(key, grp_max(v ? (L << 16 | (0xFFFFu - i)) : 0u));
             // ascending candidates: stop at the cap (the earliest reaching it
