@@ -124,9 +124,9 @@ __device__ __forceinline__ bool in_take(InBits& I, uint32_t n, uint32_t& v) {
 // kind: 0 = code-length code (incomplete sets are errors), 1 = literal/length
 // or distance (a single 1-bit code may be incomplete).  Returns false on an
 // over-subscribed or invalid incomplete set (zlib inflate_table's -1).
-template <uint32_t OUTMAX>
+template <int J, uint32_t OUTMAX>
 __device__ bool inf_build(InfSmem<OUTMAX>& S, int t, const uint8_t* len, int nsym, int kind, uint32_t lane) {
-    constexpr int J = 5;
+    // J: symbol blocks of 64 (nsym <= 64 J)
     uint32_t l[J];
 #pragma unroll
     for (int j = 0; j < J; j++) {
@@ -253,8 +253,8 @@ __device__ void fixed_tables_build(InfSmem<OUTMAX>& S, uint32_t lane) {
     for (uint32_t s = lane; s < 320; s += 64)
         S.lens[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : 5;
     wave_sync();
-    (void)inf_build(S, 0, S.lens, 288, 1, lane);
-    (void)inf_build(S, 1, S.lens + 288, 32, 1, lane);
+    (void)inf_build<5>(S, 0, S.lens, 288, 1, lane);
+    (void)inf_build<1>(S, 1, S.lens + 288, 32, 1, lane);
 }
 
 // table parts of InfSmem in the global layout of launch_inflate_fixed_tables:
@@ -540,6 +540,106 @@ __device__ int inflate_block_par(InfSmem<OUTMAX>& S, InBits& I, const uint8_t* g
     }
 }
 
+// ---- the dynamic block header's code lengths (RFC 1951 3.2.7), decoded like
+// the symbols: every lane decodes one code-length item (symbol 0..15, or 16 /
+// 17 / 18 with their 2 / 3 / 7 extra bits) at each of 4 bit positions of a
+// 256-bit window; the scalar unit follows the item chain (next position and
+// count per item, stopping when nlen + ndist lengths are known); the chain's
+// items are laid out by prefix sums of their counts, a 16 takes the value of
+// the last earlier non-16 item (a max scan), and lengths land at [0, nlen)
+// and [288, 288 + ndist) of lens[] (zeroed: 17 and 18 write nothing).
+// Same errors as the serial loop: a 16 first, a count past the total, a code
+// outside the table, a truncated payload.
+template <uint32_t OUTMAX>
+__device__ int inflate_lens_par(InfSmem<OUTMAX>& S, InBits& I, const uint8_t* g, uint32_t plen,
+                                uint32_t nlen, uint32_t ndist, uint32_t lane) {
+    const uint32_t nbits = plen * 8, tot = nlen + ndist;
+    uint32_t p0 = __builtin_amdgcn_readfirstlane(I.pos * 8 - I.cnt);
+    SpecWin W;
+    W.a0 = reinterpret_cast<const uint32_t*>(reinterpret_cast<uintptr_t>(g) & ~(uintptr_t)3);
+    W.boff = (uint32_t)(reinterpret_cast<uintptr_t>(g) & 3) * 8;
+    W.ndw = (W.boff / 8 + plen + 64) / 4;
+    spec_win_at(W, (p0 + W.boff) >> 5, lane);
+    uint32_t have = 0, last = 0x100u;   // last: the latest length + 1 (0x100: none yet)
+    for (;;) {
+        const uint32_t w0 = p0;
+        if (((w0 + W.boff) >> 5) + 11 > W.wbase + 64) spec_win_at(W, (w0 + W.boff) >> 5, lane);
+        uint32_t nx[4], sy[4], ct[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t p = w0 + lane + 64 * q;
+            const uint32_t P = p + W.boff;
+            const int di = (int)((P >> 5) - W.wbase) << 2;
+            const uint32_t sh = P & 31;
+            const uint32_t d0 = (uint32_t)__builtin_amdgcn_ds_bpermute(di, (int)W.v);
+            const uint32_t d1 = (uint32_t)__builtin_amdgcn_ds_bpermute(di + 4, (int)W.v);
+            uint32_t b = sh ? (d0 >> sh) | (d1 << (32 - sh)) : d0;   // 32 bits from p
+            const uint32_t avail = nbits > p ? nbits - p : 0u;
+            if (avail < 32) b &= (1u << avail) - 1u;
+            const uint32_t e = S.lut[0][b & ((1u << LUTB) - 1)];
+            const uint32_t c = (e >> 1) & 15, y = e >> 5;
+            const uint32_t eb = y == 16 ? 2u : y == 17 ? 3u : y == 18 ? 7u : 0u;
+            const uint32_t x = (b >> c) & ((1u << eb) - 1u);
+            sy[q] = y;
+            ct[q] = y < 16 ? 1u : y == 18 ? 11u + x : 3u + x;
+            nx[q] = (e & 1) && c + eb <= avail ? p + c + eb : IT_ERR;
+        }
+        // the chain through this window (scalar): stops at the total
+        uint64_t mk[4] = {0, 0, 0, 0};
+        uint32_t s = p0, h = have;
+        bool err = false;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t hi = w0 + 64u * (q + 1);
+            uint64_t m = 0;
+            while (!err && h < tot && s < hi) {
+                const uint32_t r = s - w0 - 64u * q;
+                const uint32_t t = readlane(nx[q], r);
+                const uint32_t k = readlane(ct[q], r);
+                if (t == IT_ERR || h + k > tot) { err = true; break; }
+                m |= 1ull << r;
+                h += k;
+                s = t;
+            }
+            mk[q] = m;
+        }
+        if (err) return -1;
+        // offsets (prefix sums of counts in bit order) and 16's values (the
+        // latest earlier non-16 item: a max scan of position | value + 1)
+        uint32_t base = have, lastv = last;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const bool me = (mk[q] >> lane) & 1u;
+            const uint32_t k = me ? ct[q] : 0u;
+            const uint32_t incl = wave_incl_sum(k);
+            const uint32_t off = base + incl - k;
+            base += readlane(incl, 63);
+            const uint32_t y = sy[q];
+            const uint32_t tag = me && y != 16 ? (lane + 1) << 9 | (y < 16 ? y + 1 : 1u) : 0u;
+            const uint32_t mx = (uint32_t)wave_excl_max((int)tag, 0);
+            const uint32_t val = mx ? (mx & 0x1FFu) : lastv;     // value + 1 (0x100: none)
+            if (__any(me && y == 16 && val == 0x100u)) return -1;   // 16 with no earlier length
+            const uint32_t v = (y == 16 ? val : y < 16 ? y + 1 : 1u) - 1;
+            if (me && v) {
+                for (uint32_t t = 0; t < k; t++) {
+                    const uint32_t o = off + t;
+                    S.lens[o < nlen ? o : 288 + (o - nlen)] = (uint8_t)v;
+                }
+            }
+            // carry: the value after this block of 64 positions
+            const uint32_t tall = (uint32_t)wave_max_i32((int)tag);
+            lastv = tall ? (tall & 0x1FFu) : lastv;
+        }
+        have = base;
+        last = lastv;
+        if (have >= tot) {
+            in_seek(I, s);
+            return 0;
+        }
+        p0 = s;
+    }
+}
+
 // the whole zlib stream; returns the decoded length, -1 invalid, -2 output
 // larger than OUTMAX (host path)
 #ifdef AMBC_STAMPS
@@ -605,62 +705,25 @@ __device__ int64_t inflate_stream(InfSmem<OUTMAX>& S, const uint8_t* g, uint32_t
                 if (nlen > 286 || ndist > 30) return -1;
                 for (uint32_t s = lane; s < 320; s += 64) S.lens[s] = 0;
                 wave_sync();
-                for (uint32_t i = 0; i < ncode; i++) {
-                    uint32_t c;
-                    if (!in_take(I, 3, c)) return -1;
-                    if (lane == 0) S.lens[c_clord2[i]] = (uint8_t)c;
-                }
+                // the ncode 3-bit code-length code lengths, at most 57 bits, in one read
+                uint32_t c0, c1 = 0;
+                if (!in_take(I, min(ncode, 10u) * 3, c0)) return -1;
+                if (ncode > 10 && !in_take(I, (ncode - 10) * 3, c1)) return -1;
+                if (lane < ncode) S.lens[c_clord2[lane]] = (uint8_t)((lane < 10 ? c0 >> (3 * lane) : c1 >> (3 * (lane - 10))) & 7u);
                 wave_sync();
-                if (!uniform_u32(inf_build(S, 0, S.lens, 19, 0, lane))) return -1;
-                // code-length codes are at most 7 bits: their 128 table entries
-                // in one register (lane l: entries 2l, 2l + 1), one v_readlane each
-                const uint32_t clut = reinterpret_cast<const uint32_t*>(S.lut[0])[lane];
-                uint32_t have = 0;
-                const uint32_t tot = nlen + ndist;
-                uint32_t lastlen = 0;
-                while (have < tot) {
-                    if (I.cnt < 15) in_fill(I);
-                    const uint32_t x = __builtin_amdgcn_readfirstlane((uint32_t)I.buf & 127u);
-                    const uint32_t e = (readlane(clut, x >> 1) >> ((x & 1) * 16)) & 0xFFFFu;
-                    if (!(e & 1) || ((e >> 1) & 15) > I.cnt) return -1;
-                    I.buf >>= (e >> 1) & 15;
-                    I.cnt -= (e >> 1) & 15;
-                    const int sy = (int)(e >> 5);
-                    uint32_t ln = 0, copy = 1;
-                    if (sy < 16) {
-                        ln = (uint32_t)sy;
-                    } else {
-                        uint32_t x;
-                        if (sy == 16) {
-                            if (have == 0) return -1;
-                            ln = lastlen;
-                            if (!in_take(I, 2, x)) return -1;
-                            copy = 3 + x;
-                        } else if (sy == 17) {
-                            if (!in_take(I, 3, x)) return -1;
-                            copy = 3 + x;
-                        } else {
-                            if (!in_take(I, 7, x)) return -1;
-                            copy = 11 + x;
-                        }
-                        if (have + copy > tot) return -1;
-                    }
-                    // code lengths into the literal/length (0..) and distance (288..) halves
-                    for (uint32_t c = lane; c < copy; c += 64) {
-                        const uint32_t q = have + c;
-                        S.lens[q < nlen ? q : 288 + (q - nlen)] = (uint8_t)ln;
-                    }
-                    lastlen = ln;
-                    have += copy;
-                }
+                if (!uniform_u32(inf_build<1>(S, 0, S.lens, 19, 0, lane))) return -1;
+                wave_sync();
+                for (uint32_t s = lane; s < 19; s += 64) S.lens[s] = 0;
+                wave_sync();
+                if (inflate_lens_par(S, I, g, plen, nlen, ndist, lane) < 0) return -1;
                 wave_sync();
                 // literal/length lengths live at [0, nlen) (rest 0 up to 288), distances at [288, 288+ndist)
                 for (uint32_t s = nlen + lane; s < 288; s += 64) S.lens[s] = 0;
                 for (uint32_t s = 288 + ndist + lane; s < 320; s += 64) S.lens[s] = 0;
                 wave_sync();
                 if (__builtin_amdgcn_readfirstlane(S.lens[256]) == 0) return -1;  // missing end-of-block code
-                if (!uniform_u32(inf_build(S, 0, S.lens, 288, 1, lane))) return -1;
-                if (!uniform_u32(inf_build(S, 1, S.lens + 288, 32, 1, lane))) return -1;
+                if (!uniform_u32(inf_build<5>(S, 0, S.lens, 288, 1, lane))) return -1;
+                if (!uniform_u32(inf_build<1>(S, 1, S.lens + 288, 32, 1, lane))) return -1;
             }
             ISTAMP(0);
             {

@@ -522,6 +522,111 @@ def test_gpu_inflate_zlib_corpus(ctx):
     assert st.kernel_ns > 0
 
 
+class _Bits:
+    """DEFLATE bit writer: fields LSB first, Huffman codes MSB first."""
+
+    def __init__(self):
+        self.v, self.n = 0, 0
+
+    def put(self, x, n):
+        self.v |= (x & ((1 << n) - 1)) << self.n
+        self.n += n
+
+    def code(self, c, n):
+        self.put(int(format(c, f"0{n}b")[::-1], 2), n)
+
+    def bytes(self):
+        return self.v.to_bytes((self.n + 7) // 8, "little")
+
+
+def _canon(lengths):
+    """canonical codes (RFC 1951 3.2.2) of {symbol: length}"""
+    codes, code = {}, 0
+    for ln in range(1, 16):
+        for s in sorted(k for k, v in lengths.items() if v == ln):
+            codes[s] = code
+            code += 1
+        code <<= 1
+    return codes
+
+
+def _dyn_stream(cl_lens, items, nlen, ndist, lit_lens, data_syms):
+    """one final dynamic block: code-length code lengths {sym: len}, the
+    code-length items [(sym, extra)], then data symbols coded with lit_lens"""
+    import zlib
+    b = _Bits()
+    b.put(0x78, 8)
+    b.put(0x9C, 8)
+    b.put(1, 1)
+    b.put(2, 2)
+    b.put(nlen - 257, 5)
+    b.put(ndist - 1, 5)
+    order = [16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15]
+    ncode = max(i for i, s in enumerate(order) if cl_lens.get(s, 0)) + 1
+    ncode = max(ncode, 4)
+    b.put(ncode - 4, 4)
+    for i in range(ncode):
+        b.put(cl_lens.get(order[i], 0), 3)
+    cc = _canon(cl_lens)
+    for sym, x in items:
+        b.code(cc[sym], cl_lens[sym])
+        if sym == 16:
+            b.put(x, 2)
+        elif sym == 17:
+            b.put(x, 3)
+        elif sym == 18:
+            b.put(x, 7)
+    lc = _canon(lit_lens)
+    for sym in data_syms:
+        b.code(lc[sym], lit_lens[sym])
+    raw = b.bytes()
+    text = bytes(s for s in data_syms if s < 256)
+    return raw + zlib.adler32(text).to_bytes(4, "big")
+
+
+def test_gpu_inflate_dynamic_headers(ctx):
+    """The dynamic header's code-length decode (speculative, RFC 1951 3.2.7)
+    against zlib semantics: a repeat (16) across the literal/distance boundary,
+    a 16 first, a 17/18 past the total, a missing end-of-block length, and
+    random bit flips in the headers of real level-9 streams."""
+    import zlib
+    cl = {1: 2, 2: 2, 16: 2, 18: 2}
+    # 0..96 zero, 97: 1, 98..254 zero, 255: 2, then a 16 repeats 2 over 256 and
+    # the four distance lengths (across the boundary)
+    ok_items = [(18, 97 - 11), (1, 0), (18, 127), (18, 157 - 138 - 11), (2, 0), (16, 2)]
+    lit = {97: 1, 255: 2, 256: 2}
+    good = _dyn_stream(cl, ok_items, 257, 4, lit, [97] * 5 + [256])
+    assert zlib.decompress(good) == b"aaaaa"
+    cases = [(good, 5),
+             (_dyn_stream(cl, [(16, 0)] + ok_items, 257, 4, lit, [97] * 5 + [256]), 5),          # 16 first
+             (_dyn_stream(cl, ok_items[:-1] + [(16, 3)], 257, 4, lit, [97] * 5 + [256]), 5),     # past the total
+             (_dyn_stream({1: 2, 2: 2, 17: 2, 18: 2},                                          # no EOB length
+                          ok_items[:3] + [(18, 156 - 138 - 11), (2, 0), (2, 0), (17, 2)],
+                          257, 4, {97: 1, 254: 2, 255: 2}, [97] * 5), 5)]
+    for z, n in cases[1:]:
+        with pytest.raises(zlib.error):
+            zlib.decompress(z)
+    rnd = random.Random(77)
+    mixed = synth.generate(1 << 20, 43)
+    for _ in range(300):
+        o = rnd.randrange(0, (1 << 20) - 4096)
+        z = bytearray(zlib.compress(mixed[o:o + 4096], 9))
+        for _ in range(rnd.randrange(1, 4)):
+            bit = rnd.randrange(16, min(len(z) * 8, 16 + 600))
+            z[bit >> 3] ^= 1 << (bit & 7)
+        cases.append((bytes(z), 4096))
+    parts, orig_total = [], 0
+    for z, n in cases:
+        parts.append(_chunk(5, z, n))
+        orig_total += n
+    body = b"".join(parts) + b"\xff\xff\x00\x00\x00\x00" + bytes(10)
+    want = orc.decompress_body(body, orig_total)
+    comp = _compressor()
+    got = comp._adaptive_decompress(body, orig_total)
+    assert got[:5] == b"aaaaa"
+    assert got == want
+
+
 # ---------------------------------------------------------------------------
 # the reference's multi-size walk (several CHUNK_SIZE_CANDIDATES)
 # ---------------------------------------------------------------------------
