@@ -351,6 +351,14 @@ __device__ int inf_item_serial(InfSmem<OUTMAX>& S, InBits& I, uint32_t& op, uint
     return 0;
 }
 
+#ifdef AMBC_STAMPS
+#define ISTAMP_PARAMS , uint64_t* _acc, uint64_t& _st_t
+#define ISTAMP_ARGS , _acc, _st_t
+#else
+#define ISTAMP_PARAMS
+#define ISTAMP_ARGS
+#endif
+
 // ---- speculative parallel symbol decode of one Huffman-coded block ----
 // Every lane decodes a whole item (literal, length + distance with their extra
 // bits, or end of block) at each of 4 bit positions of a 256-bit window
@@ -362,6 +370,9 @@ __device__ int inf_item_serial(InfSmem<OUTMAX>& S, InBits& I, uint32_t& op, uint
 // inf_item_serial in order.  Same results as the serial loop: any error in a
 // window is reported (an error and an overflow both end in orig zero bytes,
 // the overflow through the host zlib path).
+#ifndef INF_SHORT
+#define INF_SHORT 32u   // matches up to this length: one lane each; longer: the whole wave
+#endif
 constexpr uint32_t IT_EOB = 0xFFFFFFF0u, IT_SLOW = 0xFFFFFFF1u, IT_ERR = 0xFFFFFFF2u;
 enum : uint32_t { IK_LIT = 0, IK_MATCH = 1, IK_EOB = 2, IK_OTHER = 3 };
 
@@ -425,7 +436,7 @@ __device__ __forceinline__ uint32_t spec_item(const InfSmem<OUTMAX>& S, const Sp
 // code; the reader is left after it.  0 done, -1 invalid, -2 too large.
 template <uint32_t OUTMAX>
 __device__ int inflate_block_par(InfSmem<OUTMAX>& S, InBits& I, const uint8_t* g, uint32_t plen,
-                                 uint32_t& op, uint32_t lane) {
+                                 uint32_t& op, uint32_t lane ISTAMP_PARAMS) {
     const uint32_t nbits = plen * 8;
     uint32_t p0 = __builtin_amdgcn_readfirstlane(I.pos * 8 - I.cnt);
     SpecWin W;
@@ -441,6 +452,7 @@ __device__ int inflate_block_par(InfSmem<OUTMAX>& S, InBits& I, const uint8_t* g
         uint32_t nx[4], kd[4], vl[4], ln[4], dd[4];
 #pragma unroll
         for (int q = 0; q < 4; q++) nx[q] = spec_item(S, W, w0 + lane + 64 * q, nbits, kd[q], vl[q], ln[q], dd[q]);
+        ISTAMP(4);
         // the item chain through this window (scalar)
         uint64_t mk[4] = {0, 0, 0, 0};
         uint32_t s = p0, stop = 0;
@@ -461,6 +473,7 @@ __device__ int inflate_block_par(InfSmem<OUTMAX>& S, InBits& I, const uint8_t* g
             }
             mk[q] = m;
         }
+        ISTAMP(5);
         if (stop == IT_ERR) return -1;
         // the chain's items in bit order: output offsets, checks, entries
         uint32_t ko[4];
@@ -475,7 +488,7 @@ __device__ int inflate_block_par(InfSmem<OUTMAX>& S, InBits& I, const uint8_t* g
             base += readlane(incl, 63);
             if (me && kd[q] == IK_MATCH) {
                 bad |= dd[q] > ko[q];
-                lng |= ln[q] > 32;
+                lng |= ln[q] > INF_SHORT;
             }
             if (me && ol) big |= ko[q] + ol > OUTMAX;
         }
@@ -486,7 +499,7 @@ __device__ int inflate_block_par(InfSmem<OUTMAX>& S, InBits& I, const uint8_t* g
             if (!((mk[q] >> lane) & 1)) continue;
             if (kd[q] == IK_LIT) {
                 S.src[ko[q]] = (uint16_t)(IN_LIT | vl[q]);
-            } else if (kd[q] == IK_MATCH && ln[q] <= 32) {
+            } else if (kd[q] == IK_MATCH && ln[q] <= INF_SHORT) {
                 const uint32_t m0 = ko[q] - dd[q];
                 uint32_t c = 0;
                 for (uint32_t t = 0; t < ln[q]; t++) {
@@ -503,19 +516,23 @@ __device__ int inflate_block_par(InfSmem<OUTMAX>& S, InBits& I, const uint8_t* g
             for (int q = 0; q < 4; q++) {
                 if (!((mk[q] >> l) & 1) || readlane(kd[q], l) != IK_MATCH) continue;
                 const uint32_t Lm = readlane(ln[q], l);
-                if (Lm <= 32) continue;
+                if (Lm <= INF_SHORT) continue;
                 const uint32_t O = readlane(ko[q], l), Dm = readlane(dd[q], l), m0 = O - Dm;
-                const uint32_t lmod = lane % Dm;
-                uint32_t bmod = 0;
-                for (uint32_t b = 0; b < Lm; b += 64) {
-                    uint32_t c = bmod + lmod;
-                    if (c >= Dm) c -= Dm;
-                    if (b + lane < Lm) S.src[O + b + lane] = (uint16_t)(m0 + c);
-                    bmod = (bmod + 64) % Dm;
+                if (Dm >= Lm) {   // no overlap: the entries run along the source
+                    for (uint32_t b = lane; b < Lm; b += 64) S.src[O + b] = (uint16_t)(m0 + b);
+                } else {          // the period before the match: m0 + t mod D (rcp estimate, fixed up)
+                    const float rd = __builtin_amdgcn_rcpf((float)Dm);
+                    for (uint32_t b = lane; b < Lm; b += 64) {
+                        int r = (int)b - (int)((float)b * rd) * (int)Dm;
+                        r += r < 0 ? (int)Dm : 0;
+                        r -= r >= (int)Dm ? (int)Dm : 0;
+                        S.src[O + b] = (uint16_t)(m0 + (uint32_t)r);
+                    }
                 }
             }
         }
         op = base;
+        ISTAMP(6);
         if (stop == IT_EOB) {                    // the block ends after the end-of-block code
             const uint32_t r = s - w0;
             uint32_t c1;
@@ -642,13 +659,6 @@ __device__ int inflate_lens_par(InfSmem<OUTMAX>& S, InBits& I, const uint8_t* g,
 
 // the whole zlib stream; returns the decoded length, -1 invalid, -2 output
 // larger than OUTMAX (host path)
-#ifdef AMBC_STAMPS
-#define ISTAMP_PARAMS , uint64_t* _acc, uint64_t& _st_t
-#define ISTAMP_ARGS , _acc, _st_t
-#else
-#define ISTAMP_PARAMS
-#define ISTAMP_ARGS
-#endif
 template <uint32_t OUTMAX>
 __device__ int64_t inflate_stream(InfSmem<OUTMAX>& S, const uint8_t* g, uint32_t plen, const uint16_t* fixed,
                                   uint32_t lane ISTAMP_PARAMS) {
@@ -727,7 +737,7 @@ __device__ int64_t inflate_stream(InfSmem<OUTMAX>& S, const uint8_t* g, uint32_t
             }
             ISTAMP(0);
             {
-                const int rc = inflate_block_par(S, I, g, plen, op, lane);
+                const int rc = inflate_block_par(S, I, g, plen, op, lane ISTAMP_ARGS);
                 if (rc < 0) return rc;
             }
             ISTAMP(1);
@@ -785,7 +795,7 @@ __global__ __launch_bounds__(64) void k_decode_inflate(DecArgs A) {
     const uint32_t orig = uniform_u32(J.orig);
 #ifdef AMBC_STAMPS
     uint64_t _st_t = __builtin_amdgcn_s_memtime();
-    uint64_t _acc[4] = {0, 0, 0, 0};
+    uint64_t _acc[7] = {0, 0, 0, 0, 0, 0, 0};
 #endif
     const int64_t r = inflate_stream(S, uniform_ptr(A.body + J.body_off), uniform_u32(J.clen), A.inf_fixed,
                                      lane ISTAMP_ARGS);
@@ -814,7 +824,7 @@ __global__ __launch_bounds__(64) void k_decode_inflate(DecArgs A) {
 #ifdef AMBC_STAMPS
     ISTAMP(3);
     if (lane == 0 && A.stamps) {
-        for (int q = 0; q < 4; q++) A.stamps[(uint64_t)j * 8 + q] = _acc[q];
+        for (int q = 0; q < 7; q++) A.stamps[(uint64_t)j * 8 + q] = _acc[q];
         A.stamps[(uint64_t)j * 8 + 7] = 5;
     }
 #endif
