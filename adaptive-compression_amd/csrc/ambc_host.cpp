@@ -1284,7 +1284,7 @@ int ambc::decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t ori
                     if (sv[i * 8 + 7] == 5) for (int q = 0; q < 7; q++) g5[q] += (double)sv[i * 8 + q];
                 const double c5 = (double)tagged[5];
                 fprintf(stderr, "[ambc stamps] inflate jobs=%.0f cycles/job: tables %.0f symbols %.0f "
-                        "(spec %.0f chain %.0f layout+writes %.0f rest %.0f) resolve %.0f adler+out %.0f\n", c5,
+                        "(spec %.0f chain %.0f writes %.0f layout+rest %.0f) resolve %.0f adler+out %.0f\n", c5,
                         g5[0] / c5, (g5[1] + g5[4] + g5[5] + g5[6]) / c5, g5[4] / c5, g5[5] / c5, g5[6] / c5,
                         g5[1] / c5, g5[2] / c5, g5[3] / c5);
             }

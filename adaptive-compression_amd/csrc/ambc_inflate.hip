@@ -453,25 +453,39 @@ __device__ int inflate_block_par(InfSmem<OUTMAX>& S, InBits& I, const uint8_t* g
 #pragma unroll
         for (int q = 0; q < 4; q++) nx[q] = spec_item(S, W, w0 + lane + 64 * q, nbits, kd[q], vl[q], ln[q], dd[q]);
         ISTAMP(4);
-        // the item chain through this window (scalar)
+        // the item chain through this window (scalar): positions relative to
+        // the current 64-position block, next positions >= 2^31 are stops
+        // (items are shorter than 64 bits: a block's chain ends in the next)
+        uint32_t nr[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            nr[q] = nx[q] >= IT_EOB ? 0x80000000u | (nx[q] - IT_EOB) : nx[q] - (w0 + 64u * q);
         uint64_t mk[4] = {0, 0, 0, 0};
-        uint32_t s = p0, stop = 0;
+        uint32_t r = 0, rp = 0, qs = 0, stop = 0;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            const uint32_t hi = w0 + 64u * (q + 1);
-            uint64_t m = 0;
-            while (stop == 0 && s < hi) {
-                const uint32_t r = s - w0 - 64u * q;
-                const uint32_t t = readlane(nx[q], r);
-                if (t >= IT_EOB) {
-                    stop = t;
-                    if (t == IT_EOB) m |= 1ull << r;     // (no output; its end is read below)
-                } else {
+            if (r < 64) {
+                uint64_t m = 0;
+                do {
+                    const uint32_t t = readlane(nr[q], r);
                     m |= 1ull << r;
-                    s = t;
+                    rp = r;
+                    r = t;
+                } while (r < 64);
+                mk[q] = m;
+                if (r >= 0x80000000u) {
+                    stop = IT_EOB + (r & 0x7FFFFFFFu);
+                    qs = q;
+                } else {
+                    r -= 64;
                 }
             }
-            mk[q] = m;
+        }
+        // s: the stop item's position, else the first position past the window
+        uint32_t s = stop ? w0 + 64u * qs + rp : w0 + 256u + r;
+        if (stop == IT_SLOW) {   // (the serial decoder writes that item)
+#pragma unroll
+            for (int q = 0; q < 4; q++) mk[q] &= qs == (uint32_t)q ? ~(1ull << rp) : ~0ull;
         }
         ISTAMP(5);
         if (stop == IT_ERR) return -1;
@@ -494,6 +508,7 @@ __device__ int inflate_block_par(InfSmem<OUTMAX>& S, InBits& I, const uint8_t* g
         }
         if (__any(bad)) return -1;
         if (__any(big)) return -2;
+        ISTAMP(1);
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             if (!((mk[q] >> lane) & 1)) continue;
