@@ -1,0 +1,379 @@
+/* zlib9_model.c -- test infrastructure (oracle), never linked into the product.
+ *
+ * A plain-C restatement of what the reference's id-5 encoder computes:
+ * DeflateCompression.compress = zlib.compress(data, 9)
+ * (/root/reference/advanced_compression.py:76-81), i.e. zlib 1.2.11's
+ * compress2(level 9): deflate_slow (lazy matching) with good 32 / lazy 258 /
+ * nice 258 / chain 4096, windowBits 15, memLevel 8 (15-bit rolling hash of 3
+ * bytes, 16384-entry symbol buffer), and _tr_flush_block's stored / static /
+ * dynamic choice with zlib's heap-built Huffman trees, length limiting and
+ * code-length-tree RLE.  Written from the published algorithm (RFC 1950/1951
+ * and zlib's documented design); the product restates it again for the GPU
+ * (csrc/ambc_zlib9.hip) and both are checked byte for byte against the
+ * system zlib 1.2.11 by tests/test_zlib9.py.  Inputs up to 65536 bytes (the
+ * reference's id-5 chunk limit, adaptive_compressor.py:119).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define EXPORT __attribute__((visibility("default")))
+
+enum { WSZ = 32768, MAXM = 258, MINM = 3, MINLA = MAXM + MINM + 1, MAXD = WSZ - MINLA,
+       GOOD = 32, LAZY = 258, NICE = 258, CHAIN = 4096, TOOFAR = 4096, LITBUF = 16384,
+       LCODES = 286, DCODES = 30, BLCODES = 19, HEAPSZ = 2 * LCODES + 1 };
+
+static const uint8_t xl[29] = {0,0,0,0,0,0,0,0,1,1,1,1,2,2,2,2,3,3,3,3,4,4,4,4,5,5,5,5,0};
+static const uint8_t xd[30] = {0,0,0,0,1,1,2,2,3,3,4,4,5,5,6,6,7,7,8,8,9,9,10,10,11,11,12,12,13,13};
+static const uint8_t xb[19] = {0,0,0,0,0,0,0,0,0,0,0,0,0,0,0,0,2,3,7};
+static const uint8_t blord[19] = {16,17,18,0,8,7,9,6,10,5,11,4,12,3,13,2,14,1,15};
+
+static int lbase[29], dbase[30];
+static uint8_t lcode[256];        /* match length - 3 -> length code (0..28) */
+static void tables(void) {
+    int len = 0;
+    for (int c = 0; c < 28; c++) {
+        lbase[c] = len;
+        for (int k = 0; k < (1 << xl[c]); k++) lcode[len++] = (uint8_t)c;
+    }
+    lcode[255] = 28;              /* 258 has its own code; 227..257 keep 284 */
+    lbase[28] = 255;
+    int d = 0;
+    for (int c = 0; c < 30; c++) { dbase[c] = d; d += 1 << xd[c]; }
+}
+static int dcode(int dm1) {       /* distance - 1 -> distance code */
+    for (int c = 29; c >= 0; c--) if (dm1 >= dbase[c]) return c;
+    return 0;
+}
+
+typedef struct { uint16_t freq, code, len, dad; } Node;
+
+typedef struct {
+    const uint8_t* w;             /* input, read through wat(): zero past n */
+    uint32_t n;
+    uint32_t head[1 << 15];
+    uint32_t* prev;
+    /* symbols of the current block */
+    uint16_t sdist[LITBUF], slc[LITBUF];
+    uint32_t nsym;
+    Node lt[HEAPSZ], dt[2 * DCODES + 1], bt[2 * BLCODES + 1];
+    uint32_t opt_len, static_len;
+    int heap[HEAPSZ], heap_len, heap_max;
+    uint8_t depth[HEAPSZ];
+    uint16_t blc[16];
+    Node stl[288], std_[30];
+    /* output */
+    uint8_t* out;
+    uint64_t o;
+    uint32_t bb, bc;
+} Z;
+
+static inline uint8_t wat(const Z* z, uint32_t i) { return i < z->n ? z->w[i] : 0; }
+static inline uint32_t hsh(const Z* z, uint32_t p) {
+    return (((uint32_t)wat(z, p) << 10) ^ ((uint32_t)wat(z, p + 1) << 5) ^ wat(z, p + 2)) & 0x7FFF;
+}
+static uint32_t ins(Z* z, uint32_t p) {
+    const uint32_t h = hsh(z, p), r = z->head[h];
+    z->prev[p] = r;
+    z->head[h] = p;
+    return r;
+}
+
+static void bits(Z* z, uint32_t v, uint32_t n) {
+    z->bb |= v << z->bc;
+    z->bc += n;
+    while (z->bc >= 8) { z->out[z->o++] = (uint8_t)z->bb; z->bb >>= 8; z->bc -= 8; }
+}
+static void windup(Z* z) { if (z->bc) z->out[z->o++] = (uint8_t)z->bb; z->bb = 0; z->bc = 0; }
+static uint32_t rev(uint32_t c, int len) { uint32_t r = 0; while (len--) { r = (r << 1) | (c & 1); c >>= 1; } return r; }
+
+static void gen_codes(Node* t, int max_code, const uint16_t* blc) {
+    uint16_t next[16];
+    uint32_t code = 0;
+    for (int b = 1; b <= 15; b++) { code = (code + blc[b - 1]) << 1; next[b] = (uint16_t)code; }
+    for (int n = 0; n <= max_code; n++) {
+        const int len = t[n].len;
+        if (len) t[n].code = (uint16_t)rev(next[len]++, len);
+    }
+}
+
+/* freq, then depth: the heap order */
+static inline int smaller(const Z* z, const Node* t, int a, int b) {
+    return t[a].freq < t[b].freq || (t[a].freq == t[b].freq && z->depth[a] <= z->depth[b]);
+}
+static void down(Z* z, const Node* t, int k) {
+    const int v = z->heap[k];
+    int j = k << 1;
+    while (j <= z->heap_len) {
+        if (j < z->heap_len && smaller(z, t, z->heap[j + 1], z->heap[j])) j++;
+        if (smaller(z, t, v, z->heap[j])) break;
+        z->heap[k] = z->heap[j];
+        k = j;
+        j <<= 1;
+    }
+    z->heap[k] = v;
+}
+
+/* Huffman tree of t[0..elems) (max bit length maxlen); returns max_code.  stree:
+ * static lengths (for static_len), xbits / xbase: extra bits per symbol. */
+static int build(Z* z, Node* t, int elems, int maxlen, const Node* stree, const uint8_t* xbits, int xbase) {
+    int max_code = -1;
+    z->heap_len = 0;
+    z->heap_max = HEAPSZ;
+    for (int n = 0; n < elems; n++) {
+        if (t[n].freq) { z->heap[++z->heap_len] = max_code = n; z->depth[n] = 0; }
+        else t[n].len = 0;
+    }
+    while (z->heap_len < 2) {     /* at least two codes */
+        const int node = z->heap[++z->heap_len] = (max_code < 2 ? ++max_code : 0);
+        t[node].freq = 1;
+        z->depth[node] = 0;
+        z->opt_len--;
+        if (stree) z->static_len -= stree[node].len;
+    }
+    for (int n = z->heap_len / 2; n >= 1; n--) down(z, t, n);
+    int node = elems;
+    do {
+        const int n = z->heap[1];
+        z->heap[1] = z->heap[z->heap_len--];
+        down(z, t, 1);
+        const int m = z->heap[1];
+        z->heap[--z->heap_max] = n;
+        z->heap[--z->heap_max] = m;
+        t[node].freq = (uint16_t)(t[n].freq + t[m].freq);
+        z->depth[node] = (uint8_t)((z->depth[n] >= z->depth[m] ? z->depth[n] : z->depth[m]) + 1);
+        t[n].dad = t[m].dad = (uint16_t)node;
+        z->heap[1] = node++;
+        down(z, t, 1);
+    } while (z->heap_len >= 2);
+    z->heap[--z->heap_max] = z->heap[1];
+    /* bit lengths: parents before children (heap_max order), overflow fixed */
+    for (int b = 0; b <= 15; b++) z->blc[b] = 0;
+    t[z->heap[z->heap_max]].len = 0;
+    int overflow = 0, h;
+    for (h = z->heap_max + 1; h < HEAPSZ; h++) {
+        const int n = z->heap[h];
+        int b = t[t[n].dad].len + 1;
+        if (b > maxlen) { b = maxlen; overflow++; }
+        t[n].len = (uint16_t)b;       /* (the parent link is no longer needed) */
+        if (n > max_code) continue;
+        z->blc[b]++;
+        const int xb_ = n >= xbase ? xbits[n - xbase] : 0;
+        z->opt_len += t[n].freq * (uint32_t)(b + xb_);
+        if (stree) z->static_len += t[n].freq * (uint32_t)(stree[n].len + xb_);
+    }
+    if (overflow) {
+        do {
+            int b = maxlen - 1;
+            while (z->blc[b] == 0) b--;
+            z->blc[b]--;
+            z->blc[b + 1] += 2;
+            z->blc[maxlen]--;
+            overflow -= 2;
+        } while (overflow > 0);
+        h = HEAPSZ;
+        for (int b = maxlen; b != 0; b--) {
+            int k = z->blc[b];
+            while (k) {
+                const int m = z->heap[--h];
+                if (m > max_code) continue;
+                if (t[m].len != b) { z->opt_len += (uint32_t)((b - t[m].len) * t[m].freq); t[m].len = (uint16_t)b; }
+                k--;
+            }
+        }
+    }
+    gen_codes(t, max_code, z->blc);
+    return max_code;
+}
+
+/* the code-length RLE walk (scan: count into bt; send: emit) */
+static void rle_walk(Z* z, Node* t, int max_code, int send) {
+    int prevlen = -1, nextlen = t[0].len, count = 0, max_count = 7, min_count = 4;
+    if (nextlen == 0) { max_count = 138; min_count = 3; }
+    if (!send) t[max_code + 1].len = 0xFFFF;
+    for (int n = 0; n <= max_code; n++) {
+        const int curlen = nextlen;
+        nextlen = t[n + 1].len;
+        if (++count < max_count && curlen == nextlen) continue;
+        if (count < min_count) {
+            if (send) do { bits(z, z->bt[curlen].code, z->bt[curlen].len); } while (--count);
+            else z->bt[curlen].freq += (uint16_t)count;
+        } else if (curlen != 0) {
+            if (curlen != prevlen) {
+                if (send) { bits(z, z->bt[curlen].code, z->bt[curlen].len); count--; }
+                else z->bt[curlen].freq++;
+            }
+            if (send) { bits(z, z->bt[16].code, z->bt[16].len); bits(z, (uint32_t)count - 3, 2); }
+            else z->bt[16].freq++;
+        } else if (count <= 10) {
+            if (send) { bits(z, z->bt[17].code, z->bt[17].len); bits(z, (uint32_t)count - 3, 3); }
+            else z->bt[17].freq++;
+        } else {
+            if (send) { bits(z, z->bt[18].code, z->bt[18].len); bits(z, (uint32_t)count - 11, 7); }
+            else z->bt[18].freq++;
+        }
+        count = 0;
+        prevlen = curlen;
+        if (nextlen == 0) { max_count = 138; min_count = 3; }
+        else if (curlen == nextlen) { max_count = 6; min_count = 3; }
+        else { max_count = 7; min_count = 4; }
+    }
+}
+
+static void emit_symbols(Z* z, const Node* lt, const Node* dt) {
+    for (uint32_t i = 0; i < z->nsym; i++) {
+        const uint32_t d = z->sdist[i], lc = z->slc[i];
+        if (d == 0) { bits(z, lt[lc].code, lt[lc].len); continue; }
+        const int c = lcode[lc];
+        bits(z, lt[c + 257].code, lt[c + 257].len);
+        if (xl[c]) bits(z, lc - (uint32_t)lbase[c], xl[c]);
+        const int dc = dcode((int)d - 1);
+        bits(z, dt[dc].code, dt[dc].len);
+        if (xd[dc]) bits(z, (uint32_t)(d - 1 - (uint32_t)dbase[dc]), xd[dc]);
+    }
+    bits(z, lt[256].code, lt[256].len);
+}
+
+static void init_block(Z* z) {
+    for (int i = 0; i < HEAPSZ; i++) z->lt[i].freq = 0;
+    for (int i = 0; i < 2 * DCODES + 1; i++) z->dt[i].freq = 0;
+    for (int i = 0; i < 2 * BLCODES + 1; i++) z->bt[i].freq = 0;
+    z->lt[256].freq = 1;
+    z->opt_len = z->static_len = 0;
+    z->nsym = 0;
+}
+
+static void flush_block(Z* z, uint32_t start, uint32_t stored_len, int last) {
+    const int lmax = build(z, z->lt, LCODES, 15, z->stl, xl, 257);
+    const int dmax = build(z, z->dt, DCODES, 15, z->std_, xd, 0);
+    rle_walk(z, z->lt, lmax, 0);
+    rle_walk(z, z->dt, dmax, 0);
+    (void)build(z, z->bt, BLCODES, 7, NULL, xb, 0);
+    int maxbl;
+    for (maxbl = BLCODES - 1; maxbl >= 3; maxbl--) if (z->bt[blord[maxbl]].len != 0) break;
+    z->opt_len += 3 * ((uint32_t)maxbl + 1) + 5 + 5 + 4;
+    uint32_t opt_lenb = (z->opt_len + 3 + 7) >> 3;
+    const uint32_t static_lenb = (z->static_len + 3 + 7) >> 3;
+    if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
+    if (stored_len + 4 <= opt_lenb) {
+        bits(z, (uint32_t)last, 3);
+        windup(z);
+        z->out[z->o++] = (uint8_t)stored_len; z->out[z->o++] = (uint8_t)(stored_len >> 8);
+        z->out[z->o++] = (uint8_t)~stored_len; z->out[z->o++] = (uint8_t)(~stored_len >> 8);
+        for (uint32_t i = 0; i < stored_len; i++) z->out[z->o++] = z->w[start + i];
+    } else if (static_lenb == opt_lenb) {
+        bits(z, (1u << 1) + (uint32_t)last, 3);
+        emit_symbols(z, z->stl, z->std_);
+    } else {
+        bits(z, (2u << 1) + (uint32_t)last, 3);
+        bits(z, (uint32_t)lmax + 1 - 257, 5);
+        bits(z, (uint32_t)dmax + 1 - 1, 5);
+        bits(z, (uint32_t)maxbl + 1 - 4, 4);
+        for (int r = 0; r <= maxbl; r++) bits(z, z->bt[blord[r]].len, 3);
+        rle_walk(z, z->lt, lmax, 1);
+        rle_walk(z, z->dt, dmax, 1);
+        emit_symbols(z, z->lt, z->dt);
+    }
+    init_block(z);
+    if (last) windup(z);
+}
+
+static int tally(Z* z, uint32_t dist, uint32_t lc) {
+    z->sdist[z->nsym] = (uint16_t)dist;
+    z->slc[z->nsym++] = (uint16_t)lc;
+    if (dist == 0) z->lt[lc].freq++;
+    else { z->lt[lcode[lc] + 257].freq++; z->dt[dcode((int)dist - 1)].freq++; }
+    return z->nsym == LITBUF - 1;
+}
+
+/* the longest match at strstart from the chain at cur (most recent first) */
+static uint32_t longest(Z* z, uint32_t s, uint32_t cur, uint32_t prev_length, uint32_t lookahead,
+                        uint32_t* match_start) {
+    uint32_t chain = CHAIN, best = prev_length, nice = NICE;
+    const uint32_t limit = s > MAXD ? s - MAXD : 0;
+    if (prev_length >= GOOD) chain >>= 2;
+    if (nice > lookahead) nice = lookahead;
+    do {
+        /* bytes 0, 1 equal and the hash equal imply byte 2 equal; the scan
+         * compares from byte 3 up to 258, zeros past the input */
+        if (wat(z, cur + best) != wat(z, s + best) || wat(z, cur + best - 1) != wat(z, s + best - 1) ||
+            wat(z, cur) != wat(z, s) || wat(z, cur + 1) != wat(z, s + 1))
+            continue;
+        uint32_t len = 3;
+        while (len < MAXM && wat(z, cur + len) == wat(z, s + len)) len++;
+        if (len > best) {
+            *match_start = cur;
+            best = len;
+            if (len >= nice) break;
+        }
+    } while ((cur = z->prev[cur]) > limit && --chain != 0);
+    return best <= lookahead ? best : lookahead;
+}
+
+static uint32_t adler(const uint8_t* d, uint32_t n) {
+    uint32_t a = 1, b = 0;
+    for (uint32_t i = 0; i < n; i++) { a = (a + d[i]) % 65521; b = (b + a) % 65521; }
+    return b << 16 | a;
+}
+
+/* zlib.compress(in, 9); out needs n + n / 1000 + 64 bytes; returns the length */
+EXPORT int64_t orc_zlib9(const uint8_t* in, uint32_t n, uint8_t* out) {
+    static int init = 0;
+    if (!init) { tables(); init = 1; }
+    if (n > 65536) return -1;
+    Z* z = (Z*)calloc(1, sizeof(Z));
+    z->prev = (uint32_t*)calloc(n + 8, sizeof(uint32_t));
+    z->w = in;
+    z->n = n;
+    z->out = out;
+    for (int i = 0; i < 288; i++) z->stl[i].len = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : 8;
+    { uint16_t c[16] = {0}; for (int i = 0; i < 288; i++) c[z->stl[i].len]++; c[0] = 0;
+      uint16_t b[16] = {0}; memcpy(b, c, sizeof b); gen_codes(z->stl, 287, b); }
+    for (int i = 0; i < 30; i++) { z->std_[i].len = 5; z->std_[i].code = (uint16_t)rev((uint32_t)i, 5); }
+    out[0] = 0x78; out[1] = 0xDA;
+    z->o = 2;
+    init_block(z);
+    uint32_t s = 0, la = n, match_length = MINM - 1, prev_length, match_start = 0, prev_match;
+    int avail = 0;
+    uint32_t block_start = 0;
+    for (;;) {
+        if (la == 0) break;
+        uint32_t hh = 0;
+        if (la >= MINM) hh = ins(z, s);
+        prev_length = match_length;
+        prev_match = match_start;
+        match_length = MINM - 1;
+        if (hh != 0 && prev_length < LAZY && s - hh <= MAXD) {
+            match_length = longest(z, s, hh, prev_length, la, &match_start);
+            if (match_length == MINM && s - match_start > TOOFAR) match_length = MINM - 1;
+        }
+        if (prev_length >= MINM && match_length <= prev_length) {
+            const uint32_t max_insert = s + la - MINM;
+            const int fl = tally(z, s - 1 - prev_match, prev_length - MINM);
+            la -= prev_length - 1;
+            prev_length -= 2;
+            do { if (++s <= max_insert) ins(z, s); } while (--prev_length != 0);
+            avail = 0;
+            match_length = MINM - 1;
+            s++;
+            if (fl) { flush_block(z, block_start, s - block_start, 0); block_start = s; }
+        } else if (avail) {
+            if (tally(z, 0, wat(z, s - 1))) { flush_block(z, block_start, s - block_start, 0); block_start = s; }
+            s++;
+            la--;
+        } else {
+            avail = 1;
+            s++;
+            la--;
+        }
+    }
+    if (avail) (void)tally(z, 0, wat(z, s - 1));
+    flush_block(z, block_start, s - block_start, 1);
+    const uint32_t a = adler(in, n);
+    out[z->o++] = (uint8_t)(a >> 24); out[z->o++] = (uint8_t)(a >> 16);
+    out[z->o++] = (uint8_t)(a >> 8); out[z->o++] = (uint8_t)a;
+    const int64_t r = (int64_t)z->o;
+    free(z->prev);
+    free(z);
+    return r;
+}
