@@ -126,6 +126,20 @@ def test_dict_bodies_match_oracle(ctx, n, seed, chunk, methods, mode):
     assert comp._adaptive_decompress(body, n) == data
 
 
+@pytest.mark.parametrize("chunk", [4096, 8192])
+def test_dict_walkers_at_scale(ctx, chunk):
+    """The walker parse at scale (thousands of chunks, 64 walkers each): 8 MiB
+    of mixed and text-heavy input with {1,2,3,4}, every body byte against the
+    oracle's serial reference parse."""
+    from ambc import AdaptiveCompressor
+    for data in (synth.generate(8 << 20, 77), _text_heavy(8 << 20, 7)):
+        comp = AdaptiveCompressor(chunk_size=chunk, methods=(1, 2, 3, 4))
+        body = comp._adaptive_compress(data)
+        ref, st = orc.compress_body(data, orc.make_params(chunk, "native", (1, 2, 3, 4), n_total=len(data)))
+        assert body == ref
+        assert st.method_usage[2] > 0
+
+
 def test_dict_wins_and_ties(ctx):
     """Chunks where id 2 beats every other candidate, and the id-order tie rule."""
     from ambc import AdaptiveCompressor
