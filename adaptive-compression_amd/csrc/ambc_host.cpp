@@ -314,8 +314,9 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
     // Native mode over many chunks runs as NSEG pipelined segments: segment
     // i+1 encodes on the main stream while segment i is scanned and compacted
     // on d.cs (memory-bound work under the LDS-bound encoder).  Measured: one
-    // encode stream beats launches alternating over two, and 4 segments beat
-    // 5, 6 or 8 (the last segment's compaction stays exposed, ~0.4 ms).  Reference mode
+    // encode stream beats launches alternating over two, 4 segments beat 5, 6
+    // or 8 (the last segment's compaction stays exposed, ~0.4 ms), and equal
+    // segments beat a short last one (3:3:3:1, 3:3:3:2, 4:4:4:1: +3 % step).  Reference mode
     // needs every verdict before the scan (remainder-raw rule): one range.
     const uint32_t S = (p->mode != AMBC_MODE_REFERENCE && M >= 16384 && !ea.stamps) ? NSEG : 1;
     d.n_launch = S;
