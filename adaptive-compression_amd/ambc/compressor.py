@@ -72,7 +72,7 @@ class AdaptiveCompressor:
     REFERENCE_CHUNK_SIZE_CANDIDATES = list(REFERENCE_CHUNK_SIZE_CANDIDATES)
 
     def __init__(self, marker_max_length=32, sample_size=10000, *, chunk_size=None,
-                 mode="native", methods=None, devices=None):
+                 mode="native", methods=None, devices=None, deflate="v1"):
         self.marker_max_length = marker_max_length
         self.sample_size = sample_size
         self.marker_finder = None          # the reference's finder is never called (:303-310)
@@ -87,6 +87,12 @@ class AdaptiveCompressor:
         if mode not in ("native", "reference"):
             raise ValueError("mode must be 'native' or 'reference'")
         self.mode = mode
+        # id 5's GPU encoder: "v1" ("ambc-deflate v1", any chunk <= 16384) or
+        # "zlib9" (zlib.compress(data, 9)'s own bytes -- the reference's
+        # DeflateCompression, advanced_compression.py:76-81 -- chunks <= 4096)
+        if deflate not in ("v1", "zlib9"):
+            raise ValueError("deflate must be 'v1' or 'zlib9'")
+        self.deflate = deflate
         if chunk_size is not None:
             self.CHUNK_SIZE_CANDIDATES = [int(chunk_size)]
         ids = tuple(DEFAULT_METHODS if methods is None else [m for m in methods if m != 255])
@@ -144,6 +150,7 @@ class AdaptiveCompressor:
         p = _lib.Params()
         p.chunk_size = C_
         p.mode = _lib.MODE_REFERENCE if self.mode == "reference" else _lib.MODE_NATIVE
+        p.flags = _lib.FLAG_ZLIB9 if self.deflate == "zlib9" else 0
         p.method_mask = method_mask([m.type_id for m in self.compression_methods])
         for i in range(16):
             lo, hi = self.method_chunk_prefs.get(i, (1, 0))
@@ -170,6 +177,7 @@ class AdaptiveCompressor:
         ctx = self._ctx()
         cands = [int(c) for c in self.CHUNK_SIZE_CANDIDATES]
         p = _lib.Params()
+        p.flags = _lib.FLAG_ZLIB9 if self.deflate == "zlib9" else 0
         p.method_mask = method_mask([m.type_id for m in self.compression_methods])
         for i in range(16):
             lo, hi = self.method_chunk_prefs.get(i, (1, 0))

@@ -97,7 +97,7 @@ void ambc_destroy(ambc_ctx* ctx) {
         (void)hipStreamSynchronize(d.stream);
         for (Buf* b : {&d.in, &d.out, &d.slots, &d.plen, &d.ids, &d.sizes, &d.off, &d.scan_tmp,
                        &d.acc, &d.ent_full, &d.ent_tail, &d.body, &d.jobs, &d.produced, &d.dout,
-                       &d.scratch, &d.seg, &d.list, &d.bestpre, &d.gdseq, &d.pending, &d.segbase, &d.coll,
+                       &d.scratch, &d.seg, &d.list, &d.bestpre, &d.gdseq, &d.pending, &d.z9rec, &d.segbase, &d.coll,
                        &d.inffix})
             b->release();
         for (auto& b : d.msb) b.release();
@@ -141,6 +141,8 @@ int ambc::check_params(const ambc_params* p) {
         return fail(AMBC_E_INVAL, "method_mask holds ids without a GPU encoder (allowed: 1, 2, 3, 4, 5, 9)");
     if (((p->method_mask >> AMBC_M_DEFLATE) & 1) && C > 16384)
         return fail(AMBC_E_INVAL, "the GPU DEFLATE encoder supports chunk_size <= 16384");
+    if (((p->method_mask >> AMBC_M_DEFLATE) & 1) && (p->flags & AMBC_FLAG_ZLIB9) && z9_cmax(C) == 0)
+        return fail(AMBC_E_INVAL, "the GPU zlib-9 encoder (AMBC_FLAG_ZLIB9) supports chunk_size <= 4096");
     if (((p->method_mask >> AMBC_M_DICT) & 1) && p->pref_min[AMBC_M_DICT] <= dict_cmax(p) &&
         dict_cmax(p) > 8192)
         return fail(AMBC_E_INVAL, "the GPU Dictionary encoder takes chunks <= 8192 bytes "
@@ -272,6 +274,7 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
         ea.stamps = d.seg.as<unsigned long long>();
     }
     const bool deflate = (p->method_mask >> AMBC_M_DEFLATE) & 1;
+    const bool z9 = deflate && (p->flags & AMBC_FLAG_ZLIB9);   // id 5 = zlib-9's bytes
     uint32_t gd_cmax = 1024;                  // launch_deflate's template bucket
     while (gd_cmax < C) gd_cmax <<= 1;
     if (deflate) {
@@ -281,6 +284,10 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
         ea.gdseq = d.gdseq.as<uint8_t>();
         HIPCHK(d.pending.ensure((size_t)std::max<uint32_t>(M, 1)));
         ea.pending = d.pending.as<uint8_t>();
+        if (z9) {
+            HIPCHK(d.z9rec.ensure((size_t)std::max<uint32_t>(M, 1) * z9_rec_words(z9_cmax(C)) * 8));
+            ea.z9rec = d.z9rec.as<uint64_t>();
+        }
     }
     const bool dict = (p->method_mask >> AMBC_M_DICT) & 1;
     // the kernels of one chunk range [k0, k1): every per-chunk array offset to k0
@@ -296,13 +303,15 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
         if (e.bestpre) e.bestpre += k0;
         if (e.pending) e.pending += k0;
         if (e.gdseq) e.gdseq += (uint64_t)k0 * 2 * gd_cmax;
+        if (e.z9rec) e.z9rec += (uint64_t)k0 * z9_rec_words(z9_cmax(C));
         return e;
     };
     auto encode_range = [&](const EncArgs& e) -> int {
         HIPCHK(launch_encode(e, s));
         if (dict) HIPCHK(launch_dict(e, dict_cmax(p), s));   // id 2 against k_encode's winner
         if (deflate) {
-            HIPCHK(launch_deflate(e, s));   // id 5 after 1/2/3/4, against LZ4 (ties -> 5)
+            // id 5 after 1/2/3/4, against LZ4 (ties -> 5)
+            HIPCHK(z9 ? launch_zlib9(e, s) : launch_deflate(e, s));
             EncArgs ep = e;                 // RLE/Huffman payloads id 5 did not replace
             ep.flags |= ENC_EMIT_PENDING;
             ep.bestpre = nullptr;

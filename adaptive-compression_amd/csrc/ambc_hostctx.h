@@ -70,7 +70,7 @@ struct Buf {
 
 // device buffers of one multi-size walk batch (ambc_multisize.cpp)
 struct Batch {
-    Buf coff, clen, slots, plen, ids, sizes, bestpre, gdseq, pending, ent, off;
+    Buf coff, clen, slots, plen, ids, sizes, bestpre, gdseq, pending, ent, off, z9rec;
     uint32_t* hplen = nullptr;  // pinned copies of plen / ids for the host walk
     uint8_t* hids = nullptr;
     size_t hcap = 0;
@@ -85,7 +85,7 @@ struct Batch {
         return e;
     }
     void release() {
-        for (Buf* b : {&coff, &clen, &slots, &plen, &ids, &sizes, &bestpre, &gdseq, &pending, &ent, &off})
+        for (Buf* b : {&coff, &clen, &slots, &plen, &ids, &sizes, &bestpre, &gdseq, &pending, &ent, &off, &z9rec})
             b->release();
         if (hplen) (void)hipHostFree(hplen);
         if (hids) (void)hipHostFree(hids);
@@ -101,6 +101,7 @@ struct Dev {
     hipEvent_t xev[6] = {};     // h2d_done[2], comp_done[2], d2h_done[2]
     Buf in, out, slots, plen, ids, sizes, off, scan_tmp, acc, ent_full, ent_tail;
     Buf body, jobs, produced, dout, scratch, seg, list, bestpre, gdseq, pending;
+    Buf z9rec;                  // zlib-9 id 5: the parse's segments per chunk
     Buf coll;                   // small device buffers of the collectives (sizes, stats, flags)
     Buf inffix;                 // fixed-Huffman inflate tables (built on the first decode)
     bool inffix_ok = false;

@@ -55,6 +55,9 @@ int check_size(const ambc_params* p, uint32_t s) {
     if (eligible(p, s, AMBC_M_DEFLATE) && s > 16384)
         return fail(AMBC_E_INVAL, "a candidate chunk of " + std::to_string(s) +
                                       " bytes with DEFLATE eligible: the GPU DEFLATE encoder takes chunks up to 16384 bytes");
+    if (eligible(p, s, AMBC_M_DEFLATE) && (p->flags & AMBC_FLAG_ZLIB9) && z9_cmax(s) == 0)
+        return fail(AMBC_E_INVAL, "a candidate chunk of " + std::to_string(s) +
+                                      " bytes with DEFLATE eligible: the GPU zlib-9 encoder takes chunks up to 4096 bytes");
     if (eligible(p, s, AMBC_M_DICT) && s > 8192)
         return fail(AMBC_E_INVAL, "a candidate chunk of " + std::to_string(s) +
                                       " bytes with Dictionary eligible: the GPU Dictionary encoder takes chunks up to 8192 bytes");
@@ -112,11 +115,15 @@ int launch_batch(Batch& b, hipStream_t st, const uint8_t* d_in, uint64_t n, cons
         ea.bestpre = b.bestpre.as<uint32_t>();
         ea.gdseq = b.gdseq.as<uint8_t>();
         ea.pending = b.pending.as<uint8_t>();
+        if (p->flags & AMBC_FLAG_ZLIB9) {
+            HIPCHK(b.z9rec.ensure((size_t)cnt * z9_rec_words(z9_cmax(C)) * 8));
+            ea.z9rec = b.z9rec.as<uint64_t>();
+        }
     }
     HIPCHK(launch_encode(ea, st));
     if (dict) HIPCHK(launch_dict(ea, std::min<uint32_t>(C, p->pref_max[AMBC_M_DICT]), st));
     if (deflate) {
-        HIPCHK(launch_deflate(ea, st));
+        HIPCHK((p->flags & AMBC_FLAG_ZLIB9) ? launch_zlib9(ea, st) : launch_deflate(ea, st));
         EncArgs ep = ea;
         ep.flags |= ENC_EMIT_PENDING;
         ep.bestpre = nullptr;

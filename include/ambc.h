@@ -55,6 +55,9 @@ extern "C" {
 #define AMBC_MODE_REFERENCE 1 /* CHUNK_SIZE_CANDIDATES=[C] loop incl. the remainder-raw rule */
 
 #define AMBC_FLAG_NO_END_CHUNK 1u /* shard bodies for multi-GPU reassembly */
+#define AMBC_FLAG_ZLIB9 2u        /* id 5 = zlib.compress(data, 9)'s own bytes (the reference's,
+                                     advanced_compression.py:76-81; chunk_size <= 4096) instead
+                                     of "ambc-deflate v1" */
 
 /* GPU-routable method ids (bit i of method_mask = method id i) */
 #define AMBC_M_RLE 1

@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--out", default=None)
     ap.add_argument("--inputs", default="zero,random,ascii,mixed")
+    ap.add_argument("--flags", type=int, default=0, help="ambc_params.flags (2 = AMBC_FLAG_ZLIB9)")
     ap.add_argument("--msets", default="-;1;3;9;1,3,4,9",
                     help="method sets, ';'-separated ('-' = none)")
     args = ap.parse_args()
@@ -63,6 +64,7 @@ def main():
         for mset in msets:
             p = _lib.Params()
             p.chunk_size = args.chunk
+            p.flags = args.flags
             p.method_mask = method_mask(mset)
             for i in range(16):
                 lo, hi = METHOD_CHUNK_PREFS.get(i, (1, 0))

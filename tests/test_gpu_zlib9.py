@@ -1,0 +1,125 @@
+"""id 5 as the reference computes it -- zlib.compress(data, 9)
+(/root/reference/advanced_compression.py:76-81) -- on the GPU (ambc_zlib9.hip,
+AMBC_FLAG_ZLIB9 / AdaptiveCompressor(deflate="zlib9")): whole bodies against the
+oracle selector running the system zlib 1.2.11 for id 5, and every id-5 package
+against Python's zlib.compress(chunk, 9), byte for byte."""
+import random
+import zlib
+
+import pytest
+
+from oracle import oracle as orc
+from oracle import synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx(hip_lib):
+    from ambc import _lib
+    return _lib.default_context()
+
+
+def _comp(**kw):
+    from ambc import AdaptiveCompressor
+    return AdaptiveCompressor(deflate="zlib9", **kw)
+
+
+def _id5_packages(body, data):
+    """(chunk bytes, payload) of every id-5 package of a native/reference body"""
+    out = []
+    pos = off = 0
+    while pos + 18 <= len(body) and body[pos + 4] != 0:
+        t = body[pos + 4]
+        orig = int.from_bytes(body[pos + 10:pos + 14], "little")
+        clen = int.from_bytes(body[pos + 14:pos + 18], "little")
+        if t == 5:
+            out.append((data[off:off + orig], body[pos + 18:pos + 18 + clen]))
+        pos += 18 + clen
+        off += orig
+    return out
+
+
+def _check(data, chunk, methods, modes=("native", "reference")):
+    n = len(data)
+    seen = 0
+    for mode in modes:
+        comp = _comp(chunk_size=chunk, mode=mode, methods=methods)
+        body = comp._adaptive_compress(data)
+        ref, st = orc.compress_body(data, orc.make_params(chunk, mode, methods, n_total=n, deflate="zlib"),
+                                    nthreads=0)
+        assert body == ref, (mode, n, chunk, methods)
+        gst = comp._last_device_stats
+        assert gst.method_usage[5] == st.method_usage[5]
+        for raw, payload in _id5_packages(body, data):
+            assert payload == zlib.compress(raw, 9)
+            seen += 1
+        assert comp._adaptive_decompress(body, n) == data
+    return seen
+
+
+Z9_CASES = [((1 << 20) + 77, 20250418, 4096, (1, 3, 4, 5, 9)), ((1 << 20) + 5, 3, 1024, (1, 3, 5)),
+            (600001, 8, 4096, (5,)), (300000, 10, 2048, (3, 5, 9)), (250000, 12, 4096, (1, 2, 3, 4, 5)),
+            (123457, 13, 1008, (5,)), (200000, 14, 4000, (1, 3, 4, 5))]
+
+
+@pytest.mark.parametrize("n,seed,chunk,methods", Z9_CASES)
+def test_zlib9_bodies_match_zlib(ctx, n, seed, chunk, methods):
+    assert _check(synth.generate(n, seed), chunk, methods) > 0
+
+
+def _biased(n, p, seed):
+    rng = random.Random(seed)
+    return bytes(97 if rng.random() < p else 98 for _ in range(n))
+
+
+def _words(n, seed, vocab=40):
+    rng = random.Random(seed)
+    ws = ["".join(rng.choice("etaoinshrdlu") for _ in range(rng.randint(1, 9))) for _ in range(vocab)]
+    s = []
+    while sum(map(len, s)) < n:
+        s.append(rng.choice(ws) + rng.choice("  ,.\n"))
+    return "".join(s).encode()[:n]
+
+
+def test_zlib9_edge_chunks(ctx):
+    """zero runs and 258-long matches, short periods (overlapping copies),
+    biased binary data (hash chains past 1024 entries: the good_match chain cut
+    after a >= 32 match), words from a small vocabulary (lazy matches), random
+    bytes (stored blocks), tails below 64 bytes and odd lengths."""
+    edge = [bytes(8192), b"ab" * 4096, b"abc" * 3000 + b"x", bytes(range(256)) * 32,
+            b"\x07" * 5000 + bytes(range(256)) * 8, synth.random_bytes(12000, 4) + bytes(3000) + b"xyz" * 2000,
+            b"q" * 4159, _biased(16384, 0.9, 1), _biased(16384, 0.97, 2), _biased(12288, 0.8, 3),
+            _words(20000, 5), _words(16384, 6, vocab=6), synth.random_bytes(8193, 9),
+            bytes(range(256)) * 4 + synth.random_bytes(3000, 10) + bytes(range(256)) * 4]
+    seen = 0
+    for d in edge:
+        for chunk in (1024, 4096):
+            seen += _check(d, chunk, (1, 3, 5, 9), modes=("native",))
+    assert seen > 20
+
+
+def test_zlib9_random_small_chunks(ctx):
+    """many chunk contents from mixed generators at every size class"""
+    rng = random.Random(77)
+    parts = []
+    for i in range(120):
+        kind = rng.randrange(4)
+        m = rng.randint(64, 4096)
+        if kind == 0:
+            parts.append(_words(m, i, vocab=rng.randint(3, 60)))
+        elif kind == 1:
+            parts.append(_biased(m, rng.choice((0.6, 0.9, 0.99)), i))
+        elif kind == 2:
+            parts.append(synth.generate(m, i))
+        else:
+            parts.append(bytes([rng.randrange(4)]) * rng.randint(1, 300) + _words(m, i, vocab=5))
+    data = b"".join(parts)
+    for chunk in (1024, 2048, 4096):
+        assert _check(data, chunk, (5,), modes=("native",)) > 0
+
+
+def test_zlib9_rejects_large_chunks(ctx):
+    from ambc import _lib
+    with pytest.raises(_lib.AmbcError):
+        _comp(chunk_size=8192, methods=(5,))._adaptive_compress(synth.generate(100000, 1))
