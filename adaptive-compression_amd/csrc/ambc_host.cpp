@@ -285,8 +285,8 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
         HIPCHK(d.pending.ensure((size_t)std::max<uint32_t>(M, 1)));
         ea.pending = d.pending.as<uint8_t>();
         if (z9) {
-            HIPCHK(d.z9rec.ensure((size_t)std::max<uint32_t>(M, 1) * z9_rec_words(z9_cmax(C)) * 8));
-            ea.z9rec = d.z9rec.as<uint64_t>();
+            HIPCHK(d.z9rec.ensure((size_t)std::max<uint32_t>(M, 1) * z9_rec_words(z9_cmax(C)) * 4));
+            ea.z9rec = d.z9rec.as<uint32_t>();
         }
     }
     const bool dict = (p->method_mask >> AMBC_M_DICT) & 1;

@@ -31,7 +31,7 @@ struct EncArgs {
     unsigned long long* stamps;  // diagnostic build (-DAMBC_STAMPS): per-phase cycle sums
     uint32_t* bestpre;       // optional: best (len + 18) before LZ4 (k_deflate's threshold)
     uint8_t* gdseq;          // k_deflate: n_chunks x chunk-size scratch for the parse's matches
-    uint64_t* z9rec;         // k_z9_parse -> k_z9_code: per-chunk segments (ambc_zlib9.hip)
+    uint32_t* z9rec;         // k_z9_parse -> k_z9_code: per-chunk match starts + matches (ambc_zlib9.hip)
     uint8_t* pending;        // with k_deflate: 1 = the RLE/Huffman payload was not emitted (id 5 may win)
     uint32_t pref_min[16];
     uint32_t pref_max[16];
@@ -96,7 +96,7 @@ hipError_t launch_encode(const EncArgs& a, hipStream_t s);
 hipError_t launch_deflate(const EncArgs& a, hipStream_t s);   // ambc_deflate.hip
 hipError_t launch_dict(const EncArgs& a, uint32_t cmax, hipStream_t s);   // ambc_dict.hip
 // id 5 as zlib.compress(data, 9) (ambc_zlib9.hip): chunk_size <= z9 limit; the
-// record scratch is n_chunks x z9_rec_words(z9_cmax(chunk_size)) u64 words
+// record scratch is n_chunks x z9_rec_words(z9_cmax(chunk_size)) u32 words
 uint32_t z9_cmax(uint32_t chunk);   // 0: no zlib-9 encoder for this chunk size
 size_t z9_rec_words(uint32_t cmax);
 hipError_t launch_zlib9(const EncArgs& a, hipStream_t s);

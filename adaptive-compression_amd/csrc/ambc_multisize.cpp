@@ -116,8 +116,8 @@ int launch_batch(Batch& b, hipStream_t st, const uint8_t* d_in, uint64_t n, cons
         ea.gdseq = b.gdseq.as<uint8_t>();
         ea.pending = b.pending.as<uint8_t>();
         if (p->flags & AMBC_FLAG_ZLIB9) {
-            HIPCHK(b.z9rec.ensure((size_t)cnt * z9_rec_words(z9_cmax(C)) * 8));
-            ea.z9rec = b.z9rec.as<uint64_t>();
+            HIPCHK(b.z9rec.ensure((size_t)cnt * z9_rec_words(z9_cmax(C)) * 4));
+            ea.z9rec = b.z9rec.as<uint32_t>();
         }
     }
     HIPCHK(launch_encode(ea, st));

@@ -58,17 +58,8 @@ constexpr uint32_t Z_CHAIN = 4096;           // max_chain at level 9
 constexpr uint32_t Z_GOOD = 32;              // good_length: chain >> 2 beyond it
 constexpr uint32_t Z_TOOFAR = 4096;
 constexpr uint32_t Z_BLKSYM = 16383;         // lit_bufsize - 1 symbols per block
-constexpr uint32_t Z_NBLK = 8;               // record-area block starts (n <= 65536: <= 5 blocks)
+constexpr uint32_t Z_NBLK = 1;               // chunks <= 4096 bytes: < 16383 symbols, one block
 
-__constant__ uint16_t z_lbase[29] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  10,  12,  14,  16,  20, 24,
-                                     28, 32, 40, 48, 56, 64, 80, 96, 112, 128, 160, 192, 224, 255};
-__constant__ uint8_t z_xl[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2,
-                                 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
-__constant__ uint16_t z_dbase[30] = {0,    1,    2,    3,    4,    6,    8,     12,    16,    24,
-                                     32,   48,   64,   96,   128,  192,  256,   384,   512,   768,
-                                     1024, 1536, 2048, 3072, 4096, 6144, 8192, 12288, 16384, 24576};
-__constant__ uint8_t z_xd[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6,
-                                 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
 __constant__ uint8_t z_blord[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
 // length code (0..28) of a match length 3..258 (zlib's _length_code)
@@ -111,10 +102,11 @@ __device__ __forceinline__ bool z9_gate(const EncArgs& A, uint32_t k, uint32_t n
     return T > 18 + 6;
 }
 
-// per chunk: [0] = records | blocks << 32, [1 .. Z_NBLK] block starts, then
-// records c | L << 16 | dist << 32 (c literals, then a match of L, or L = 0 at the end)
+// per chunk (u32 words): [0] = matches, [1] unused, then the match-start
+// bitmask (CMAX / 32 words), then the matches in order, L | dist << 16
 template <int CMAX> struct Z9Rec {
-    static constexpr uint32_t STRIDE = 1 + Z_NBLK + CMAX / 3 + 3;   // u64 words
+    static constexpr uint32_t MASK = 2, MATCH = 2 + CMAX / 32;
+    static constexpr uint32_t STRIDE = MATCH + CMAX / 3 + 4;
 };
 
 template <int CMAX> struct Z9Cfg {
@@ -129,9 +121,13 @@ struct Z9Smem {
     alignas(16) uint16_t slot[CMAX];         // position -> its index in lst
     alignas(16) uint32_t bend32[ZNB / 2];    // bucket ends (u16 pairs)
     // the sort's per-range cursors [NR][ZNB] u16; then the parse: seg[q] = 0
-    // (not reached) or 1 << 31 | L << 16 | c for a fresh position q
+    // (not reached) or 1 << 31 | L << 16 | c for a clean position q: c
+    // literals, then a match of L (0: none); the next clean position is q + c + L
     alignas(16) uint32_t seg[CMAX];
     alignas(16) uint16_t sd[CMAX];           // the segment's match distance
+    uint16_t entry[CMAX / 64], rbase[CMAX / 64];   // the path: entry lane / match rank per window
+    uint32_t mask[CMAX / 32];                // the path's match starts
+    uint32_t nmatch;
     __device__ __forceinline__ uint16_t* bend() { return reinterpret_cast<uint16_t*>(bend32); }
     __device__ __forceinline__ uint32_t bstart(uint32_t h) { return h ? bend()[h - 1] : 0u; }
 };
@@ -224,10 +220,16 @@ __device__ __forceinline__ uint32_t grp_max8(uint32_t x) {
 }
 __device__ __forceinline__ uint32_t grp8(uint64_t m, uint32_t g) { return (uint32_t)(m >> (8 * g)) & 0xFFu; }
 
-// The lazy parse's walkers (deflate_slow).  Per 8-lane group: q = the fresh
-// position its current segment started at, s = the position being looked at,
-// P / Pd = the previous position's match (prev_length / distance), avail =
-// match_available.  One longest_match per iteration for every active group.
+// The lazy parse's walkers (deflate_slow).  A position is CLEAN when the
+// parser stands there with no pending match (prev_length < 3): right after a
+// match, or with a pending literal and no match at the previous position.
+// Everything zlib emits from a clean position on depends on the position only,
+// so walkers start anywhere, record seg[q] for every clean q they leave (one
+// literal, or the lazy chain's literals and the match that ends it) and stop
+// on one another walker recorded.  Per 8-lane group: q = the current clean
+// position, s = the position being looked at, P / Pd = the pending match at
+// s - 1 (prev_length / distance), c = literals since q.  One longest_match per
+// iteration for every active group.
 template <int CMAX>
 __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t wave, uint32_t lane) {
     constexpr uint32_t NWK = (uint32_t)Z9Cfg<CMAX>::NW * 8u;
@@ -237,11 +239,11 @@ __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t
     const uint32_t g = lane >> 3, r = lane & 7;
     const uint32_t wid = wave * 8u + g;
     uint32_t q = (uint32_t)(((uint64_t)n * wid) / NWK);
-    uint32_t s = q, P = 2, Pd = 0;
-    bool fresh = true, done = false;
+    uint32_t s = q, P = 2, Pd = 0, c = 0;
+    bool clean = true, done = false;
 #pragma unroll 1
     for (;;) {
-        if (fresh && !done && (q >= n || vs[q] != 0u)) done = true;
+        if (clean && !done && (q >= n || vs[q] != 0u)) done = true;
         if (__all(done)) break;
         const bool act = !done && s >= 1 && s + 3 <= n && P < 258;   // position 0 is zlib's NIL
         // ---- longest_match(s): k0 over the first 4096 chain entries, k1 over
@@ -286,7 +288,11 @@ __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t
 #pragma unroll
                 for (int t = 0; t < 4; t++) fm = min(fm, ffbl_raw(x[t] ^ tg[t]) | (uint32_t)t << 5);
                 uint32_t len = fm == ~0u ? 16u : fm >> 3;
-                bool ext = ok && fm == ~0u;
+                // zlib's scan_end test: a candidate whose byte at the current best
+                // length differs cannot be longer -- no full compare for it
+                const uint32_t best = k0 >> 16;
+                const bool can = best < 16 || S.ch[c + best] == S.ch[s + best];
+                bool ext = ok && fm == ~0u && can;
 #pragma unroll 1
                 while (__any(ext)) {
                     if (ext) {
@@ -305,7 +311,7 @@ __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t
                     }
                 }
                 const uint32_t Lp = min(min(len, Z_MAXM), nice);
-                const uint32_t key = ok ? (Lp << 16 | c) : 0u;
+                const uint32_t key = ok && can ? (Lp << 16 | c) : 0u;
                 k0 = max(k0, grp_max8(key));
                 k1 = max(k1, grp_max8(ok && kidx <= Z_CHAIN / 4 ? key : 0u));
                 cnt += (uint32_t)__popc(sm);
@@ -315,34 +321,41 @@ __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t
             }
         }
         if (!done) {
-            if (s >= n) {
-                // the input ends: the segment's literals run to n
-                if (r == 0) vs[q] = 0x80000000u | (n - q);
-                done = true;
-            } else {
-                uint32_t ML = 2, MD = 0;
-                if (act) {
-                    const uint32_t key = P >= Z_GOOD ? k1 : k0;
-                    const uint32_t L = key >> 16, d = s - (key & 0xFFFFu);
-                    if (L >= 3 && !(L == 3 && d > Z_TOOFAR)) { ML = L; MD = d; }
-                }
-                if (P >= 3 && ML <= P) {
-                    // the previous position's match: the segment ends with it
-                    const uint32_t ms = s - 1;
-                    if (r == 0) {
-                        S.sd[q] = (uint16_t)Pd;
-                        vs[q] = 0x80000000u | P << 16 | (ms - q);
-                    }
-                    q = ms + P;
+            uint32_t ML = 2, MD = 0;
+            if (act) {
+                const uint32_t key = P >= Z_GOOD ? k1 : k0;
+                const uint32_t L = key >> 16, d = s - (key & 0xFFFFu);
+                if (L >= 3 && !(L == 3 && d > Z_TOOFAR)) { ML = L; MD = d; }
+            }
+            if (clean) {
+                if (ML < 3) {
+                    // a literal; the next position is clean again
+                    if (r == 0) vs[q] = 0x80000000u | 1u;
+                    q++;
                     s = q;
-                    P = 2;
-                    fresh = true;
                 } else {
                     P = ML;
                     Pd = MD;
-                    s++;
-                    fresh = false;
+                    c = 0;
+                    s = q + 1;
+                    clean = false;
                 }
+            } else if (ML <= P) {
+                // the pending match at s - 1 is emitted: its end is clean
+                if (r == 0) {
+                    S.sd[q] = (uint16_t)Pd;
+                    vs[q] = 0x80000000u | P << 16 | c;
+                }
+                q = s - 1 + P;
+                s = q;
+                P = 2;
+                clean = true;
+            } else {
+                // a longer match at s: s - 1 goes out as a literal (lazy evaluation)
+                c++;
+                P = ML;
+                Pd = MD;
+                s++;
             }
         }
     }
@@ -378,37 +391,70 @@ __global__ __launch_bounds__(64 * Z9Cfg<CMAX>::NW) void k_z9_parse(EncArgs A) {
     __syncthreads();
     z9_walkers(S, n, wave, lane);
     __syncthreads();
-    // the path from 0, its segments and zlib's block starts
-    if (threadIdx.x == 0) {
-        uint64_t* R = A.z9rec + (uint64_t)k * Z9Rec<CMAX>::STRIDE;
-        uint64_t* rec = R + 1 + Z_NBLK;
-        uint32_t q = 0, i = 0, sym = 0, nb = Z_BLKSYM, nblk = 1;
-        R[1] = 0;
-        while (q < n) {
-            const uint32_t x = S.seg[q];
-            if (!(x >> 31)) { i = 0; nblk = 0; break; }   // (cannot happen: the path is complete)
-            const uint32_t c = x & 0xFFFFu, L = (x >> 16) & 0x1FFu;
-            const uint32_t d = L ? S.sd[q] : 0u;
-            rec[i++] = (uint64_t)(c | L << 16) | (uint64_t)d << 32;
-            // a block ends with its 16383rd symbol -- not with the final literal,
-            // tallied after deflate_slow's loop without the flush check
-            const uint32_t cl = L ? c : c - 1;
-            while (sym + cl >= nb && nblk < Z_NBLK) {
-                R[1 + nblk++] = q + (nb - sym);
-                nb += Z_BLKSYM;
-            }
-            sym += c;
-            if (L) {
-                sym++;
-                if (sym == nb && nblk < Z_NBLK) {
-                    R[1 + nblk++] = q + c + L;
-                    nb += Z_BLKSYM;
-                }
-            }
-            q += c + L;
+    // ---- the path from 0.  Per 64-position window, pointer doubling over the
+    // lanes gives every clean position's exit from the window (the first path
+    // position past it) and the matches on the way; thread 0 chains the windows
+    // (one step per visited window); then every window's path is walked on the
+    // scalar unit from its entry, and its matches are written at their ranks ----
+    constexpr uint32_t NWIN = (uint32_t)CMAX / 64;
+    const uint32_t nwin = (n + 63) / 64;
+    const uint64_t below = (1ull << lane) - 1ull;
+    uint16_t* xit = S.lst;    // the sort's lists are dead: exit position per position
+    uint16_t* xm = S.slot;    // and matches to the exit
+    for (uint32_t w = wave; w < nwin; w += NW) {
+        const uint32_t p = w * 64 + lane;
+        const uint32_t t = p < n ? S.seg[p] : 0u;
+        uint32_t J = t ? lane + (t & 0xFFFFu) + ((t >> 16) & 0x1FFu) : lane + 1;
+        uint32_t M = (t >> 16) & 0x1FFu ? 1u : 0u;
+#pragma unroll
+        for (int it = 0; it < 6; it++) {
+            const int src = (int)(min(J, 63u) << 2);
+            const uint32_t Jj = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)J);
+            const uint32_t Mj = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)M);
+            M = J < 64 ? M + Mj : M;
+            J = J < 64 ? Jj : J;
         }
-        R[0] = (uint64_t)i | (uint64_t)nblk << 32;
+        xit[p] = (uint16_t)(w * 64 + J);
+        xm[p] = (uint16_t)M;
     }
+    for (uint32_t i = threadIdx.x; i < NWIN; i += 64u * NW) S.entry[i] = 0xFFFFu;
+    for (uint32_t i = threadIdx.x; i < (uint32_t)CMAX / 32; i += 64u * NW) S.mask[i] = 0;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t cur = 0, mr = 0;
+        while (cur < n) {
+            S.entry[cur >> 6] = (uint16_t)(cur & 63u);
+            S.rbase[cur >> 6] = (uint16_t)mr;
+            mr += xm[cur];
+            cur = xit[cur];
+        }
+        S.nmatch = mr;
+    }
+    __syncthreads();
+    uint32_t* R = A.z9rec + (uint64_t)k * Z9Rec<CMAX>::STRIDE;
+    for (uint32_t w = wave; w < nwin; w += NW) {
+        const uint32_t e = S.entry[w];
+        if (e == 0xFFFFu) continue;
+        const uint32_t p = w * 64 + lane;
+        const uint32_t t = p < n ? S.seg[p] : 0u;
+        const uint32_t c = t & 0xFFFFu, L = (t >> 16) & 0x1FFu;
+        const uint32_t J1 = lane + max(1u, c + L);   // (t != 0 on the path; never stall)
+        uint64_t on = 0;
+        for (uint32_t q = e; q < 64;) {
+            on |= 1ull << q;
+            q = readlane(J1, q);
+        }
+        const bool mt = ((on >> lane) & 1u) && L != 0;
+        const uint64_t mm = __ballot(mt);
+        if (mt) {
+            const uint32_t ms = p + c;
+            atomicOr(&S.mask[ms >> 5], 1u << (ms & 31));
+            R[Z9Rec<CMAX>::MATCH + S.rbase[w] + (uint32_t)__popcll(mm & below)] = L | (uint32_t)S.sd[p] << 16;
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < (uint32_t)CMAX / 32; i += 64u * NW) R[Z9Rec<CMAX>::MASK + i] = S.mask[i];
+    if (threadIdx.x == 0) R[0] = S.nmatch;
 }
 
 // ---------------------------------------------------------------------------
@@ -431,9 +477,12 @@ struct Z9Tree {
     l16* blc;
 };
 
+// extra bits of length code lc / distance code dc (zlib's extra_lbits / extra_dbits)
+__device__ __forceinline__ uint32_t z_xlb(uint32_t lc) { return lc < 8 || lc == 28 ? 0u : (lc >> 2) - 1; }
+__device__ __forceinline__ uint32_t z_xdb(uint32_t dc) { return dc < 4 ? 0u : (dc >> 1) - 1; }
 __device__ __forceinline__ uint32_t z_xbits(int kind, int n) {
-    if (kind == 0) return n >= 257 ? z_xl[n - 257] : 0u;
-    if (kind == 1) return z_xd[n];
+    if (kind == 0) return n >= 257 ? z_xlb((uint32_t)n - 257) : 0u;
+    if (kind == 1) return z_xdb((uint32_t)n);
     return n == 16 ? 2u : n == 17 ? 3u : n == 18 ? 7u : 0u;
 }
 __device__ __forceinline__ uint32_t z_slen(int kind, int n) {
@@ -441,116 +490,310 @@ __device__ __forceinline__ uint32_t z_slen(int kind, int n) {
     return 5u;
 }
 
-__device__ __forceinline__ void z9_down(l32* heap, int heap_len, int k) {
-    const uint32_t v = heap[k];
-    int j = k << 1;
+// zlib's heap held in five VGPRs (entry i at lane i & 63 of register i >> 6):
+// the heap walk runs on the scalar unit (v_readlane / v_writelane), without
+// the LDS round trip per level a one-lane build pays
+struct VHeap {
+    uint32_t h[5];
+};
+__device__ __forceinline__ uint32_t vh_get(const VHeap& H, uint32_t i) {
+    const uint32_t l = i & 63u;
+    switch (i >> 6) {
+        case 0: return readlane(H.h[0], l);
+        case 1: return readlane(H.h[1], l);
+        case 2: return readlane(H.h[2], l);
+        case 3: return readlane(H.h[3], l);
+        default: return readlane(H.h[4], l);
+    }
+}
+__device__ __forceinline__ void vh_set(VHeap& H, uint32_t i, uint32_t v) {
+    const uint32_t l = i & 63u, me = __lane_id();   // v_writelane as a compare + select
+    switch (i >> 6) {
+        case 0: H.h[0] = me == l ? v : H.h[0]; break;
+        case 1: H.h[1] = me == l ? v : H.h[1]; break;
+        case 2: H.h[2] = me == l ? v : H.h[2]; break;
+        case 3: H.h[3] = me == l ? v : H.h[3]; break;
+        default: H.h[4] = me == l ? v : H.h[4]; break;
+    }
+}
+// pqdownheap: smaller() is the order of the packed keys' freq | depth bits
+__device__ __forceinline__ void vh_down(VHeap& H, uint32_t heap_len, uint32_t k) {
+    const uint32_t v = vh_get(H, k), kv = v >> 10;
+    uint32_t j = k << 1;
     while (j <= heap_len) {
-        uint32_t hj = heap[j];
+        uint32_t hj = vh_get(H, j);
         if (j < heap_len) {
-            const uint32_t hj1 = heap[j + 1];
+            const uint32_t hj1 = vh_get(H, j + 1);
             if ((hj1 >> 10) <= (hj >> 10)) { j++; hj = hj1; }
         }
-        if ((v >> 10) <= (hj >> 10)) break;
-        heap[k] = hj;
+        if (kv <= (hj >> 10)) break;
+        vh_set(H, k, hj);
         k = j;
         j <<= 1;
     }
-    heap[k] = v;
+    vh_set(H, k, v);
 }
 
-// zlib's build_tree + gen_bitlen + gen_codes (oracle/zlib9_model.c build()), on
-// the calling lane.  kind 0: literal/length (static lengths 8/9/7/8), 1:
-// distance (static 5), 2: bit lengths (no static tree).  Returns max_code.
-__device__ int z9_build(Z9Tree t, int elems, int maxlen, int kind, uint32_t& opt, uint32_t& stat) {
-    const int HSZ = 2 * elems + 1;
-    int heap_len = 0, heap_max = HSZ, max_code = -1;
-    for (int n = 0; n < elems; n++) {
-        const uint32_t f = t.freq[n];
-        if (f) { t.heap[++heap_len] = f << 16 | (uint32_t)n; max_code = n; }
-        else t.len[n] = 0;
+// zlib's build_tree + gen_bitlen + gen_codes with the whole wave (uniform
+// control flow; oracle/zlib9_model.c build() is the serial statement).  The
+// heap runs as above; gen_bitlen's depths come from pointer jumping over the
+// parent links (len = min(depth, maxlen), overflow = nodes deeper than maxlen,
+// exactly gen_bitlen's clamped recursion), its rare overflow repair runs on
+// lane 0; gen_codes ranks equal lengths by ballots.  pjd / pja: scratch of
+// 2 * elems + 1 entries; blc32: 16 u32.  Returns max_code.
+__device__ __forceinline__ int z9_build_w(Z9Tree t, l16* pjd, l16* pja, l32* blc32, l32* misc, int elems, int maxlen, int kind,
+                          uint32_t& opt, uint32_t& stat, uint32_t lane) {
+    const uint32_t HSZ = 2u * (uint32_t)elems + 1u;
+    const uint64_t below = (1ull << lane) - 1ull;
+    uint32_t cnt = 0;
+    int max_code = -1;
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+        const uint32_t n = 64u * j + lane;
+        const uint32_t f = n < (uint32_t)elems ? (uint32_t)t.freq[n] : 0u;
+        const uint64_t m = __ballot(f != 0);
+        if (f) t.heap[1 + cnt + (uint32_t)__popcll(m & below)] = f << 16 | n;
+        else if (n < (uint32_t)elems) t.len[n] = 0;
+        if (m) max_code = 64 * j + 63 - __clzll((long long)m);
+        cnt += (uint32_t)__popcll(m);
     }
-    while (heap_len < 2) {
+    if (lane < 16) blc32[lane] = 0;
+    wave_sync();
+    VHeap H;
+#pragma unroll
+    for (int j = 0; j < 5; j++) H.h[j] = 64u * j + lane <= cnt ? (uint32_t)t.heap[64 * j + lane] : 0u;
+    uint32_t heap_len = cnt;
+    while (heap_len < 2) {   // at least two codes
         const int node = max_code < 2 ? ++max_code : 0;
-        t.heap[++heap_len] = 1u << 16 | (uint32_t)node;
-        t.freq[node] = 1;
+        vh_set(H, ++heap_len, 1u << 16 | (uint32_t)node);
+        if (lane == 0) t.freq[node] = 1;
         opt--;
         if (kind < 2) stat -= z_slen(kind, node);
     }
-    for (int n = heap_len / 2; n >= 1; n--) z9_down(t.heap, heap_len, n);
-    int node = elems;
+    for (uint32_t k = heap_len / 2; k >= 1; k--) vh_down(H, heap_len, k);
+    uint32_t node = (uint32_t)elems, heap_max = HSZ;
     do {
-        const uint32_t hn = t.heap[1];
-        t.heap[1] = t.heap[heap_len--];
-        z9_down(t.heap, heap_len, 1);
-        const uint32_t hm = t.heap[1];
-        t.heap[--heap_max] = hn;
-        t.heap[--heap_max] = hm;
+        const uint32_t hn = vh_get(H, 1);
+        vh_set(H, 1, vh_get(H, heap_len));
+        heap_len--;
+        vh_down(H, heap_len, 1);
+        const uint32_t hm = vh_get(H, 1);
+        heap_max -= 2;
+        if (lane == 0) {
+            t.heap[heap_max + 1] = hn & 1023u;
+            t.heap[heap_max] = hm & 1023u;
+            t.dad[hn & 1023u] = (uint16_t)node;
+            t.dad[hm & 1023u] = (uint16_t)node;
+        }
         const uint32_t f = (hn >> 16) + (hm >> 16);
         const uint32_t dep = max((hn >> 10) & 63u, (hm >> 10) & 63u) + 1u;
-        t.freq[node] = (uint16_t)f;
-        t.dad[hn & 1023u] = (uint16_t)node;
-        t.dad[hm & 1023u] = (uint16_t)node;
-        t.heap[1] = f << 16 | dep << 10 | (uint32_t)node;
+        vh_set(H, 1, f << 16 | dep << 10 | node);
         node++;
-        z9_down(t.heap, heap_len, 1);
+        vh_down(H, heap_len, 1);
     } while (heap_len >= 2);
-    t.heap[--heap_max] = t.heap[1];
-    for (int b = 0; b <= 15; b++) t.blc[b] = 0;
-    t.len[t.heap[heap_max] & 1023u] = 0;
-    int overflow = 0;
-    for (int h = heap_max + 1; h < HSZ; h++) {
-        const int n = (int)(t.heap[h] & 1023u);
-        int b = t.len[t.dad[n]] + 1;
-        if (b > maxlen) { b = maxlen; overflow++; }
-        t.len[n] = (uint8_t)b;
-        if (n > max_code) continue;
-        t.blc[b]++;
-        const uint32_t xb = z_xbits(kind, n), f = t.freq[n];
-        opt += f * ((uint32_t)b + xb);
-        if (kind < 2) stat += f * (z_slen(kind, n) + xb);
+    const uint32_t root = vh_get(H, 1) & 1023u;
+    heap_max--;
+    if (lane == 0) t.heap[heap_max] = root;
+    wave_sync();
+    // ---- depths: pointer jumping over dad[] (nodes 0 .. node-1) ----
+    const uint32_t nn = node;
+    uint32_t d[9], a[9];
+    bool leaf_in[5];
+#pragma unroll
+    for (int j = 0; j < 9; j++) {
+        const uint32_t x = 64u * j + lane;
+        bool in = false;
+        if (x < (uint32_t)elems) {
+            in = (int)x <= max_code && t.freq[x] != 0;
+            if (j < 5) leaf_in[j] = in;
+        } else {
+            in = x < nn;
+        }
+        const bool nr = in && x != root;
+        d[j] = nr ? 1u : 0u;
+        a[j] = nr ? (uint32_t)t.dad[x] : x;
+        if (x < HSZ) { pjd[x] = (uint16_t)d[j]; pja[x] = (uint16_t)a[j]; }
     }
-    if (overflow) {
-        do {
-            int b = maxlen - 1;
-            while (t.blc[b] == 0) b--;
-            t.blc[b]--;
-            t.blc[b + 1] += 2;
-            t.blc[maxlen]--;
-            overflow -= 2;
-        } while (overflow > 0);
-        int h = HSZ;
-        for (int b = maxlen; b != 0; b--) {
-            int k = t.blc[b];
-            while (k) {
-                const int m = (int)(t.heap[--h] & 1023u);
-                if (m > max_code) continue;
-                if (t.len[m] != b) {
-                    opt += (uint32_t)((b - (int)t.len[m]) * (int)t.freq[m]);
-                    t.len[m] = (uint8_t)b;
+    wave_sync();
+#pragma unroll 1
+    for (int it = 0; it < 10; it++) {
+        uint32_t nd[9], na[9];
+#pragma unroll
+        for (int j = 0; j < 9; j++) {
+            const uint32_t x = 64u * j + lane;
+            nd[j] = x < nn ? d[j] + pjd[a[j]] : d[j];
+            na[j] = x < nn ? (uint32_t)pja[a[j]] : a[j];
+        }
+        wave_sync();
+#pragma unroll
+        for (int j = 0; j < 9; j++) {
+            const uint32_t x = 64u * j + lane;
+            d[j] = nd[j];
+            a[j] = na[j];
+            if (x < nn) { pjd[x] = (uint16_t)d[j]; pja[x] = (uint16_t)a[j]; }
+        }
+        wave_sync();
+    }
+    // ---- lengths, bl_count, opt_len / static_len, overflow ----
+    uint32_t ovf = 0, po = 0, ps = 0;
+#pragma unroll
+    for (int j = 0; j < 9; j++) {
+        const uint32_t x = 64u * j + lane;
+        const bool in = x < (uint32_t)elems ? (j < 5 && leaf_in[j]) : x < nn;
+        if (in && x != root && d[j] > (uint32_t)maxlen) ovf++;
+        if (j < 5 && x < (uint32_t)elems && leaf_in[j]) {
+            const uint32_t b = min(d[j], (uint32_t)maxlen);
+            t.len[x] = (uint8_t)b;
+            atomicAdd((uint32_t*)&blc32[b], 1u);
+            const uint32_t f = t.freq[x], xb = z_xbits(kind, (int)x);
+            po += f * (b + xb);
+            if (kind < 2) ps += f * (z_slen(kind, (int)x) + xb);
+        }
+    }
+    ovf = wave_sum_u32(ovf);
+    opt += wave_sum_u32(po);
+    stat += wave_sum_u32(ps);
+    wave_sync();
+    if (lane < 16) t.blc[lane] = (uint16_t)blc32[lane];
+    wave_sync();
+    if (ovf) {
+        // gen_bitlen's repair, serially on lane 0 (zlib's order over the heap's
+        // removed nodes, from the least frequent)
+        if (lane == 0) {
+            int overflow = (int)ovf;
+            uint32_t od = 0;
+            do {
+                int b = maxlen - 1;
+                while (t.blc[b] == 0) b--;
+                t.blc[b]--;
+                t.blc[b + 1] += 2;
+                t.blc[maxlen]--;
+                overflow -= 2;
+            } while (overflow > 0);
+            int h = (int)HSZ;
+            for (int b = maxlen; b != 0; b--) {
+                int k = t.blc[b];
+                while (k) {
+                    const int m = (int)(t.heap[--h] & 1023u);
+                    if (m > max_code) continue;
+                    if (t.len[m] != b) {
+                        od += (uint32_t)((b - (int)t.len[m]) * (int)t.freq[m]);
+                        t.len[m] = (uint8_t)b;
+                    }
+                    k--;
                 }
-                k--;
             }
+            misc[0] = od;
+        }
+        wave_sync();
+        opt += misc[0];
+    }
+    // ---- gen_codes: next_code per length, ranks among equal lengths ----
+    uint32_t nxt[16];
+    {
+        uint32_t code = 0;
+        nxt[0] = 0;
+#pragma unroll
+        for (int b = 1; b <= 15; b++) { code = (code + t.blc[b - 1]) << 1; nxt[b] = code; }
+    }
+    uint32_t ln[5], cd[5];
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+        const uint32_t x = 64u * j + lane;
+        ln[j] = (int)x <= max_code ? (uint32_t)t.len[x] : 0u;
+        cd[j] = 0;
+    }
+#pragma unroll
+    for (int b = 1; b <= 15; b++) {
+        uint32_t run = nxt[b];
+#pragma unroll
+        for (int j = 0; j < 5; j++) {
+            const uint64_t m = __ballot(ln[j] == (uint32_t)b);
+            if (ln[j] == (uint32_t)b) cd[j] = run + (uint32_t)__popcll(m & below);
+            run += (uint32_t)__popcll(m);
         }
     }
-    // gen_codes
-    uint32_t next[16], code = 0;
-    next[0] = 0;
-    for (int b = 1; b <= 15; b++) { code = (code + t.blc[b - 1]) << 1; next[b] = code; }
-    for (int n = 0; n <= max_code; n++) {
-        const int l = t.len[n];
-        if (l) {
-            uint32_t c = 0;
-            switch (l) {   // next[] indexed by a divergent value stays in registers
-#define Z_NX(B) case B: c = next[B]++; break;
-                Z_NX(1) Z_NX(2) Z_NX(3) Z_NX(4) Z_NX(5) Z_NX(6) Z_NX(7) Z_NX(8)
-                Z_NX(9) Z_NX(10) Z_NX(11) Z_NX(12) Z_NX(13) Z_NX(14) Z_NX(15)
-#undef Z_NX
-                default: break;
-            }
-            t.code[n] = (uint16_t)(__builtin_bitreverse32(c) >> (32 - l));
-        }
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+        const uint32_t x = 64u * j + lane;
+        if (ln[j]) t.code[x] = (uint16_t)(__builtin_bitreverse32(cd[j]) >> (32 - ln[j]));
     }
+    wave_sync();
     return max_code;
+}
+
+// the bit stream on the scalar unit: a 64-bit accumulator, whole words stored
+// by lane 0 (no read-modify-write); the stream starts word-aligned
+struct SBits {
+    uint64_t acc;
+    uint32_t n, w;
+};
+__device__ __forceinline__ void sb_put(SBits& b, l32* words, uint32_t v, uint32_t nb, uint32_t lane) {
+    b.acc |= (uint64_t)v << b.n;
+    b.n += nb;
+    if (b.n >= 32) {
+        if (lane == 0) words[b.w] = (uint32_t)b.acc;
+        b.w++;
+        b.acc >>= 32;
+        b.n -= 32;
+    }
+}
+
+// send_tree over len[0..max_code] with the bit-length codes bcl (lane i: code
+// | len << 16 of symbol i), on the scalar unit; lens: the lengths as VHeap-style
+// registers (symbol x at lane x & 63 of register x >> 6)
+__device__ __forceinline__ void z9_send_w(const VHeap& lens, int max_code, uint32_t bcl, SBits& sb, l32* W, uint32_t lane) {
+    int prevlen = -1, nextlen = (int)vh_get(lens, 0), count = 0, max_count = 7, min_count = 4;
+    if (nextlen == 0) { max_count = 138; min_count = 3; }
+    for (int n = 0; n <= max_code; n++) {
+        const int curlen = nextlen;
+        nextlen = n + 1 <= max_code ? (int)vh_get(lens, (uint32_t)n + 1) : 0xFFFF;
+        if (++count < max_count && curlen == nextlen) continue;
+        const uint32_t cc = readlane(bcl, (uint32_t)curlen);
+        if (count < min_count) {
+            do { sb_put(sb, W, cc & 0xFFFFu, cc >> 16, lane); } while (--count);
+        } else if (curlen != 0) {
+            if (curlen != prevlen) { sb_put(sb, W, cc & 0xFFFFu, cc >> 16, lane); count--; }
+            const uint32_t c16 = readlane(bcl, 16);
+            sb_put(sb, W, (c16 & 0xFFFFu) | ((uint32_t)count - 3) << (c16 >> 16), (c16 >> 16) + 2, lane);
+        } else if (count <= 10) {
+            const uint32_t c17 = readlane(bcl, 17);
+            sb_put(sb, W, (c17 & 0xFFFFu) | ((uint32_t)count - 3) << (c17 >> 16), (c17 >> 16) + 3, lane);
+        } else {
+            const uint32_t c18 = readlane(bcl, 18);
+            sb_put(sb, W, (c18 & 0xFFFFu) | ((uint32_t)count - 11) << (c18 >> 16), (c18 >> 16) + 7, lane);
+        }
+        count = 0;
+        prevlen = curlen;
+        if (nextlen == 0) { max_count = 138; min_count = 3; }
+        else if (curlen == nextlen) { max_count = 6; min_count = 3; }
+        else { max_count = 7; min_count = 4; }
+    }
+}
+
+// scan_tree on the scalar unit: the bit-length symbol counts into cnt (u32,
+// lane 0's fire-and-forget LDS adds)
+__device__ __forceinline__ void z9_scan_w(const VHeap& lens, int max_code, l32* cnt, uint32_t lane) {
+    int prevlen = -1, nextlen = (int)vh_get(lens, 0), count = 0, max_count = 7, min_count = 4;
+    if (nextlen == 0) { max_count = 138; min_count = 3; }
+    for (int n = 0; n <= max_code; n++) {
+        const int curlen = nextlen;
+        nextlen = n + 1 <= max_code ? (int)vh_get(lens, (uint32_t)n + 1) : 0xFFFF;
+        if (++count < max_count && curlen == nextlen) continue;
+        uint32_t sym, add;
+        if (count < min_count) { sym = (uint32_t)curlen; add = (uint32_t)count; }
+        else if (curlen != 0) {
+            if (curlen != prevlen && lane == 0) atomicAdd((uint32_t*)&cnt[curlen], 1u);
+            sym = 16; add = 1;
+        } else if (count <= 10) { sym = 17; add = 1; }
+        else { sym = 18; add = 1; }
+        if (lane == 0) atomicAdd((uint32_t*)&cnt[sym], add);
+        count = 0;
+        prevlen = curlen;
+        if (nextlen == 0) { max_count = 138; min_count = 3; }
+        else if (curlen == nextlen) { max_count = 6; min_count = 3; }
+        else { max_count = 7; min_count = 4; }
+    }
 }
 
 __device__ __forceinline__ void z_put(l32* w, uint32_t b, uint32_t v, uint32_t nb) {
@@ -567,53 +810,6 @@ __device__ __forceinline__ void z_put_atomic(uint32_t* w, uint32_t b, uint32_t v
 }
 
 
-// scan_tree (send = false: counts into cnt[0..19)) / send_tree (send = true:
-// the bits at bp with the bit-length codes bcode / blen) over len[0..max_code]
-__device__ void z9_rle(const l8* len, int max_code, bool send, l16* cnt, const l16* bcode, const l8* blen,
-                       l32* w, uint32_t& bp) {
-    int prevlen = -1, nextlen = len[0], count = 0, max_count = 7, min_count = 4;
-    if (nextlen == 0) { max_count = 138; min_count = 3; }
-    for (int n = 0; n <= max_code; n++) {
-        const int curlen = nextlen;
-        nextlen = n + 1 <= max_code ? (int)len[n + 1] : 0xFFFF;   // zlib's guard entry
-        if (++count < max_count && curlen == nextlen) continue;
-        if (count < min_count) {
-            if (!send) cnt[curlen] += (uint16_t)count;
-            else {
-                const uint32_t c = bcode[curlen], l = blen[curlen];
-                do { z_put(w, bp, c, l); bp += l; } while (--count);
-            }
-        } else if (curlen != 0) {
-            if (curlen != prevlen) {
-                if (!send) cnt[curlen]++;
-                else { z_put(w, bp, bcode[curlen], blen[curlen]); bp += blen[curlen]; count--; }
-            }
-            if (!send) cnt[16]++;
-            else {
-                z_put(w, bp, bcode[16], blen[16]); bp += blen[16];
-                z_put(w, bp, (uint32_t)count - 3, 2); bp += 2;
-            }
-        } else if (count <= 10) {
-            if (!send) cnt[17]++;
-            else {
-                z_put(w, bp, bcode[17], blen[17]); bp += blen[17];
-                z_put(w, bp, (uint32_t)count - 3, 3); bp += 3;
-            }
-        } else {
-            if (!send) cnt[18]++;
-            else {
-                z_put(w, bp, bcode[18], blen[18]); bp += blen[18];
-                z_put(w, bp, (uint32_t)count - 11, 7); bp += 7;
-            }
-        }
-        count = 0;
-        prevlen = curlen;
-        if (nextlen == 0) { max_count = 138; min_count = 3; }
-        else if (curlen == nextlen) { max_count = 6; min_count = 3; }
-        else { max_count = 7; min_count = 4; }
-    }
-}
-
 template <int CMAX>
 struct Z9CSmem {
     static constexpr int WORDS = (CMAX + 5 * (int)Z_NBLK + 64) / 4 + 4;
@@ -626,10 +822,30 @@ struct Z9CSmem {
     uint16_t dfreq[DT_N + 1], ddad[DT_N + 1], dcode[32];
     uint16_t bfreq[BT_N + 1], bdad[BT_N + 1], bcode[20];
     uint16_t blcL[16], blcD[16], blcB[16];
-    uint16_t cnt19[2][20];
+    uint16_t pjd[LT_N + 3], pja[LT_N + 3];   // z9_build_w's pointer-jumping scratch
+    uint32_t blc32[16], cnt32[20];
     uint8_t llen[LT_N + 1], dlen[DT_N + 1], blen[BT_N + 1];
     uint32_t misc[16];
 };
+
+#ifdef AMBC_STAMPS
+// diagnostic build only: k_z9_code's phase cycles per chunk in A.stamps[(M + k) * 8 + phase]
+#define ZSTAMP_DECL uint64_t _st_t = __builtin_amdgcn_s_memtime(); uint64_t _acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define ZSTAMP(ph)                                                 \
+    do {                                                           \
+        __builtin_amdgcn_s_waitcnt(0xC07F);                        \
+        const uint64_t _t = __builtin_amdgcn_s_memtime();          \
+        _acc[ph] += _t - _st_t;                                    \
+        _st_t = _t;                                                \
+    } while (0)
+#define ZSTAMP_FLUSH                                               \
+    if (lane == 0 && A.stamps)                                     \
+        for (int _p = 0; _p < 8; _p++) A.stamps[((uint64_t)A.n_chunks + k) * 8 + _p] = _acc[_p];
+#else
+#define ZSTAMP_DECL
+#define ZSTAMP(ph) do {} while (0)
+#define ZSTAMP_FLUSH
+#endif
 
 template <int CMAX>
 __global__ __launch_bounds__(64) void k_z9_code(EncArgs A) {
@@ -640,33 +856,22 @@ __global__ __launch_bounds__(64) void k_z9_code(EncArgs A) {
     const uint32_t n = A.coff ? A.clen[k] : (uint32_t)min((uint64_t)A.chunk_size, A.n_total - pos0);
     uint32_t T = 0;
     if (n > (uint32_t)CMAX || !z9_gate(A, k, n, T)) return;
+    ZSTAMP_DECL
     const uint8_t* src = A.in + pos0;
-    const uint64_t* R = A.z9rec + (uint64_t)k * Z9Rec<CMAX>::STRIDE;
-    const uint64_t hdr = R[0];
-    const uint32_t nrec = (uint32_t)hdr, nblk = (uint32_t)(hdr >> 32);
-    const uint64_t* rec = R + 1 + Z_NBLK;
+    const uint32_t* R = A.z9rec + (uint64_t)k * Z9Rec<CMAX>::STRIDE;
+    const uint32_t* rec = R + Z9Rec<CMAX>::MATCH;   // the path's matches, L | dist << 16
+    constexpr uint32_t nblk = Z_NBLK;
+    static_assert(CMAX < (int)Z_BLKSYM, "one block per chunk");
     const uint64_t below = (1ull << lane) - 1ull;
     l32* W = (l32*)S.bits;
     const Z9Tree LT{(l16*)S.lfreq, (l16*)S.ldad, (l8*)S.llen, (l16*)S.lcode, (l32*)S.heapL, (l16*)S.blcL};
     const Z9Tree DT{(l16*)S.dfreq, (l16*)S.ddad, (l8*)S.dlen, (l16*)S.dcode, (l32*)S.heapD, (l16*)S.blcD};
     const Z9Tree BT{(l16*)S.bfreq, (l16*)S.bdad, (l8*)S.blen, (l16*)S.bcode, (l32*)S.heapD, (l16*)S.blcB};
 
-    // ---- match starts from the segments ----
-    for (uint32_t i = lane; i < (uint32_t)CMAX / 32 + 2; i += 64) S.mstart[i] = 0;
+    // ---- the parse's match starts ----
+    for (uint32_t i = lane; i < (uint32_t)CMAX / 32 + 2; i += 64)
+        S.mstart[i] = i < (uint32_t)CMAX / 32 ? R[Z9Rec<CMAX>::MASK + i] : 0u;
     for (uint32_t i = lane; i < (uint32_t)Z9CSmem<CMAX>::WORDS; i += 64) S.bits[i] = 0;
-    wave_sync();
-    {
-        uint32_t carry = 0;
-        for (uint32_t e0 = 0; e0 < nrec; e0 += 64) {
-            const uint32_t e = e0 + lane;
-            const uint64_t x = e < nrec ? rec[e] : 0ull;
-            const uint32_t c = (uint32_t)x & 0xFFFFu, L = (uint32_t)(x >> 16) & 0x1FFu;
-            const uint32_t span = c + L, incl = wave_incl_sum(span);
-            const uint32_t p = carry + incl - span + c;
-            if (e < nrec && L) atomicOr(&S.mstart[p >> 5], 1u << (p & 31));
-            carry += readlane(incl, 63);
-        }
-    }
     wave_sync();
 
     // one position-major pass over [bs, be): emit = false counts the block's
@@ -674,24 +879,35 @@ __global__ __launch_bounds__(64) void k_z9_code(EncArgs A) {
     auto pass = [&](uint32_t bs, uint32_t be, uint32_t rank0, bool emit, uint32_t bp) -> uint32_t {
         uint32_t rank = rank0, out = 0;
         int carry = (int)bs;
+        // a round's global loads (its matches, its bytes) are issued one round
+        // ahead, so their latency hides behind the previous round's work
+        auto fetch = [&](uint32_t q0, uint32_t rk, uint64_t& bmo, uint32_t& xo, uint32_t& co) {
+            const uint32_t pos = q0 + lane;
+            const bool in = pos >= bs && pos < be;
+            const bool m = in && ((S.mstart[pos >> 5] >> (pos & 31)) & 1u);
+            bmo = __ballot(m);
+            xo = m ? rec[rk + (uint32_t)__popcll(bmo & below)] : 0u;
+            co = in ? (uint32_t)src[pos] : 0u;
+        };
+        uint64_t bmn = 0;
+        uint32_t xn = 0, cn = 0;
+        fetch(bs & ~63u, rank, bmn, xn, cn);
 #pragma unroll 1
         for (uint32_t p0 = bs & ~63u; p0 < be; p0 += 64) {
+            const uint64_t bm = bmn;
+            const uint32_t x = xn, cb = cn;
+            const uint32_t rank2 = rank + (uint32_t)__popcll(bm);
+            if (p0 + 64 < be) fetch(p0 + 64, rank2, bmn, xn, cn);
             const uint32_t pos = p0 + lane;
             const bool in = pos >= bs && pos < be;
-            const bool ms = in && ((S.mstart[pos >> 5] >> (pos & 31)) & 1u);
-            const uint64_t bm = __ballot(ms);
-            uint32_t L = 0, d = 0;
-            if (ms) {
-                const uint64_t x = rec[rank + (uint32_t)__popcll(bm & below)];
-                L = (uint32_t)(x >> 16) & 0x1FFu;
-                d = (uint32_t)(x >> 32);
-            }
+            const bool ms = (bm >> lane) & 1u;
+            const uint32_t L = ms ? x & 0xFFFFu : 0u, d = x >> 16;
             const int e = ms ? (int)(pos + L) : 0;
             const int E = max(carry, wave_incl_max_i32(e));
             carry = max(carry, wave_max_i32(e));
-            rank += (uint32_t)__popcll(bm);
+            rank = rank2;
             const bool lit = in && !ms && E <= (int)pos;
-            const uint32_t c = lit ? src[pos] : 0u;
+            const uint32_t c = lit ? cb : 0u;
             const uint32_t lc = ms ? z_lcode(L) : 0u, dc = ms ? z_dcode(d) : 0u;
             if (!emit) {
                 if (lit) atomicAdd(&S.lf32[c], 1u);
@@ -707,10 +923,13 @@ __global__ __launch_bounds__(64) void k_z9_code(EncArgs A) {
                 } else if (ms) {
                     const uint32_t a = S.ecl[257 + lc], b = S.ecd[dc];
                     const uint32_t la = a >> 16, lb = b >> 16;
-                    e1 = la + z_xl[lc];
-                    v1 = (a & 0xFFFFu) | (L - 3 - z_lbase[lc]) << la;
-                    e2 = lb + z_xd[dc];
-                    v2 = (b & 0xFFFFu) | (d - 1 - z_dbase[dc]) << lb;
+                    // the extra bits are the low bits of L - 3 / d - 1 (code bases
+                    // are multiples of their extra range)
+                    const uint32_t xl = z_xlb(lc), xd = z_xdb(dc);
+                    e1 = la + xl;
+                    v1 = (a & 0xFFFFu) | ((L - 3) & ((1u << xl) - 1u)) << la;
+                    e2 = lb + xd;
+                    v2 = (b & 0xFFFFu) | ((d - 1) & ((1u << xd) - 1u)) << lb;
                 }
                 cost = e1 + e2;
                 const uint32_t incl = wave_incl_sum(cost);
@@ -725,8 +944,7 @@ __global__ __launch_bounds__(64) void k_z9_code(EncArgs A) {
 
     uint32_t bp = 0;
     for (uint32_t b = 0; b < nblk; b++) {
-        const uint32_t bs = (uint32_t)R[1 + b];
-        const uint32_t be = b + 1 < nblk ? (uint32_t)R[2 + b] : n;
+        const uint32_t bs = 0, be = n;
         const uint32_t last = b + 1 == nblk ? 1u : 0u;
         // match starts before bs
         uint32_t rank0 = 0;
@@ -735,50 +953,52 @@ __global__ __launch_bounds__(64) void k_z9_code(EncArgs A) {
         rank0 = wave_sum_u32(rank0);
         for (uint32_t i = lane; i < 288; i += 64) S.lf32[i] = 0;
         if (lane < 32) S.df32[lane] = 0;
-        if (lane < 40) S.cnt19[lane / 20][lane % 20] = 0;
+        if (lane < 20) S.cnt32[lane] = 0;
         wave_sync();
+        ZSTAMP(0);
         pass(bs, be, rank0, false, 0);
         wave_sync();
+        ZSTAMP(1);
         for (uint32_t i = lane; i < 286; i += 64) S.lfreq[i] = (uint16_t)(S.lf32[i] + (i == 256 ? 1u : 0u));
         if (lane < 30) S.dfreq[lane] = (uint16_t)S.df32[lane];
-        if (lane < 19) S.bfreq[lane] = 0;
         wave_sync();
-        // ---- the trees (build_tree x 2 at once, scan_tree x 2, build_bl_tree) ----
-        if (lane < 2) {
-            uint32_t opt = 0, stat = 0;
-            const int mc = z9_build(lane ? DT : LT, lane ? 30 : 286, 15, (int)lane, opt, stat);
-            uint32_t dummy = 0;
-            z9_rle(lane ? (const l8*)S.dlen : (const l8*)S.llen, mc, false, (l16*)S.cnt19[lane],
-                   (const l16*)S.bcode, (const l8*)S.blen, W, dummy);
-            S.misc[lane] = (uint32_t)mc;
-            S.misc[2 + lane] = opt;
-            S.misc[4 + lane] = stat;
+        // ---- the trees: build_tree x 2, scan_tree x 2, build_bl_tree ----
+        l16* PJD = (l16*)S.pjd;
+        l16* PJA = (l16*)S.pja;
+        l32* BLC = (l32*)S.blc32;
+        l32* MISC = (l32*)(S.misc + 12);
+        uint32_t optL = 0, statL = 0, optD = 0, statD = 0, optB = 0, statB = 0;
+        const int lmax = z9_build_w(LT, PJD, PJA, BLC, MISC, 286, 15, 0, optL, statL, lane);
+        const int dmax = z9_build_w(DT, PJD, PJA, BLC, MISC, 30, 15, 1, optD, statD, lane);
+        VHeap LL, DL;
+#pragma unroll
+        for (int j = 0; j < 5; j++) {
+            const uint32_t x = 64u * j + lane;
+            LL.h[j] = (int)x <= lmax ? (uint32_t)S.llen[x] : 0u;
+            DL.h[j] = (int)x <= dmax ? (uint32_t)S.dlen[x] : 0u;
         }
+        z9_scan_w(LL, lmax, (l32*)S.cnt32, lane);
+        z9_scan_w(DL, dmax, (l32*)S.cnt32, lane);
         wave_sync();
-        if (lane == 0) {
-            for (int i = 0; i < 19; i++) S.bfreq[i] = (uint16_t)(S.cnt19[0][i] + S.cnt19[1][i]);
-            uint32_t opt = 0, stat = 0;
-            (void)z9_build(BT, 19, 7, 2, opt, stat);
-            int maxbl;
-            for (maxbl = 18; maxbl >= 3; maxbl--) if (S.blen[z_blord[maxbl]] != 0) break;
-            opt += S.misc[2] + S.misc[3] + 3u * (uint32_t)(maxbl + 1) + 5 + 5 + 4;
-            const uint32_t stl = S.misc[4] + S.misc[5];
-            uint32_t opt_lenb = (opt + 3 + 7) >> 3;
-            const uint32_t static_lenb = (stl + 3 + 7) >> 3;
-            if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
-            const uint32_t stored_len = be - bs;
-            const uint32_t kind = stored_len + 4 <= opt_lenb ? 0u : (static_lenb == opt_lenb ? 1u : 2u);
-            S.misc[6] = kind;
-            S.misc[7] = (uint32_t)maxbl;
-            S.misc[8] = kind == 2 ? opt : stl;   // the block's bits after its 3 header bits
-        }
+        if (lane < 19) S.bfreq[lane] = (uint16_t)S.cnt32[lane];
         wave_sync();
-        const uint32_t kind = S.misc[6];
+        (void)z9_build_w(BT, PJD, PJA, BLC, MISC, 19, 7, 2, optB, statB, lane);
+        ZSTAMP(2);
+        int maxbl;
+        for (maxbl = 18; maxbl >= 3; maxbl--) if (S.blen[z_blord[maxbl]] != 0) break;
+        const uint32_t opt = optL + optD + optB + 3u * (uint32_t)(maxbl + 1) + 5 + 5 + 4;
+        const uint32_t stl = statL + statD;
+        uint32_t opt_lenb = (opt + 3 + 7) >> 3;
+        const uint32_t static_lenb = (stl + 3 + 7) >> 3;
+        if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
+        ZSTAMP(3);
+        const uint32_t kind = be - bs + 4 <= opt_lenb ? 0u : (static_lenb == opt_lenb ? 1u : 2u);
+        S.misc[8] = kind == 2 ? opt : stl;   // the block's bits after its 3 header bits
         if (nblk == 1) {
             // the exact length before any bit is written
             const uint32_t bits = kind == 0 ? ((3 + 7) & ~7u) + 32 + 8 * n : 3 + S.misc[8];
             const uint32_t total = 2 + (bits + 7) / 8 + 4;
-            if (total + 18 >= T) return;
+            if (total + 18 >= T) { ZSTAMP_FLUSH; return; }
         }
         if (kind == 0) {
             // stored: the 3 header bits, byte alignment, LEN / NLEN, the bytes
@@ -813,21 +1033,25 @@ __global__ __launch_bounds__(64) void k_z9_code(EncArgs A) {
             for (uint32_t i = lane; i < 286; i += 64) S.ecl[i] = S.lcode[i] | (uint32_t)S.llen[i] << 16;
             if (lane < 30) S.ecd[lane] = S.dcode[lane] | (uint32_t)S.dlen[lane] << 16;
         }
-        if (lane == 0) {
-            z_put(W, bp, kind << 1 | last, 3);
-            uint32_t p = bp + 3;
+        {
+            // the block header on the scalar unit (the stream is word-aligned here)
+            SBits sb{0ull, bp & 31u, bp >> 5};
+            sb.acc = sb.n ? (uint64_t)(S.bits[sb.w] & ((1u << sb.n) - 1u)) : 0ull;
+            sb_put(sb, W, kind << 1 | last, 3, lane);
             if (kind == 2) {
-                const int lmax = (int)S.misc[0], dmax = (int)S.misc[1], maxbl = (int)S.misc[7];
-                z_put(W, p, (uint32_t)lmax + 1 - 257, 5); p += 5;
-                z_put(W, p, (uint32_t)dmax, 5); p += 5;
-                z_put(W, p, (uint32_t)maxbl + 1 - 4, 4); p += 4;
-                for (int r = 0; r <= maxbl; r++) { z_put(W, p, S.blen[z_blord[r]], 3); p += 3; }
-                z9_rle((const l8*)S.llen, lmax, true, (l16*)S.cnt19[0], (const l16*)S.bcode, (const l8*)S.blen, W, p);
-                z9_rle((const l8*)S.dlen, dmax, true, (l16*)S.cnt19[0], (const l16*)S.bcode, (const l8*)S.blen, W, p);
+                sb_put(sb, W, (uint32_t)lmax + 1 - 257, 5, lane);
+                sb_put(sb, W, (uint32_t)dmax, 5, lane);
+                sb_put(sb, W, (uint32_t)maxbl + 1 - 4, 4, lane);
+                for (int r = 0; r <= maxbl; r++) sb_put(sb, W, S.blen[z_blord[r]], 3, lane);
+                const uint32_t bcl = lane < 19 ? (uint32_t)S.bcode[lane] | (uint32_t)S.blen[lane] << 16 : 0u;
+                z9_send_w(LL, lmax, bcl, sb, W, lane);
+                z9_send_w(DL, dmax, bcl, sb, W, lane);
             }
-            S.misc[9] = p;
+            if (sb.n && lane == 0) W[sb.w] = (uint32_t)sb.acc;
+            S.misc[9] = sb.w * 32 + sb.n;
         }
         wave_sync();
+        ZSTAMP(4);
         bp = S.misc[9];
         bp += pass(bs, be, rank0, true, bp);
         wave_sync();
@@ -835,9 +1059,10 @@ __global__ __launch_bounds__(64) void k_z9_code(EncArgs A) {
         bp += S.ecl[256] >> 16;
         wave_sync();
     }
+    ZSTAMP(5);
     const uint32_t body = (bp + 7) >> 3;
     const uint32_t total = 2 + body + 4;
-    if (total + 18 >= T) return;
+    if (total + 18 >= T) { ZSTAMP_FLUSH; return; }
     // ---- Adler-32 of the chunk ----
     uint32_t adler;
     {
@@ -866,6 +1091,8 @@ __global__ __launch_bounds__(64) void k_z9_code(EncArgs A) {
         A.plen[k] = total;
         A.sizes[k] = 18ull + total;
     }
+    ZSTAMP(6);
+    ZSTAMP_FLUSH;
 }
 
 template <int CMAX>
