@@ -106,7 +106,9 @@ __device__ __forceinline__ bool z9_gate(const EncArgs& A, uint32_t k, uint32_t n
 // bitmask (CMAX / 32 words), then the matches in order, L | dist << 16
 template <int CMAX> struct Z9Rec {
     static constexpr uint32_t MASK = 2, MATCH = 2 + CMAX / 32;
-    static constexpr uint32_t STRIDE = MATCH + CMAX / 3 + 4;
+    static constexpr uint32_t FREQ = MATCH + CMAX / 3 + 4;   // 286 + 30 u16 symbol counts (EOB not counted)
+    static constexpr uint32_t MERGE = FREQ + 158;             // zlib's heap merges: lit 285 + dist 29, n | m << 16
+    static constexpr uint32_t STRIDE = MERGE + 316;
 };
 
 template <int CMAX> struct Z9Cfg {
@@ -127,6 +129,7 @@ struct Z9Smem {
     alignas(16) uint16_t sd[CMAX];           // the segment's match distance
     uint16_t entry[CMAX / 64], rbase[CMAX / 64];   // the path: entry lane / match rank per window
     uint32_t mask[CMAX / 32];                // the path's match starts
+    uint32_t cov[CMAX / 32];                 // positions the path's matches cover
     uint32_t nmatch;
     __device__ __forceinline__ uint16_t* bend() { return reinterpret_cast<uint16_t*>(bend32); }
     __device__ __forceinline__ uint32_t bstart(uint32_t h) { return h ? bend()[h - 1] : 0u; }
@@ -418,7 +421,9 @@ __global__ __launch_bounds__(64 * Z9Cfg<CMAX>::NW) void k_z9_parse(EncArgs A) {
         xm[p] = (uint16_t)M;
     }
     for (uint32_t i = threadIdx.x; i < NWIN; i += 64u * NW) S.entry[i] = 0xFFFFu;
-    for (uint32_t i = threadIdx.x; i < (uint32_t)CMAX / 32; i += 64u * NW) S.mask[i] = 0;
+    for (uint32_t i = threadIdx.x; i < (uint32_t)CMAX / 32; i += 64u * NW) { S.mask[i] = 0; S.cov[i] = 0; }
+    uint32_t* lf = S.bend32;   // the walkers are done: symbol counts (286 + 30 u32)
+    for (uint32_t i = threadIdx.x; i < 316; i += 64u * NW) lf[i] = 0;
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t cur = 0, mr = 0;
@@ -447,14 +452,100 @@ __global__ __launch_bounds__(64 * Z9Cfg<CMAX>::NW) void k_z9_parse(EncArgs A) {
         const bool mt = ((on >> lane) & 1u) && L != 0;
         const uint64_t mm = __ballot(mt);
         if (mt) {
-            const uint32_t ms = p + c;
+            const uint32_t ms = p + c, d = S.sd[p];
             atomicOr(&S.mask[ms >> 5], 1u << (ms & 31));
-            R[Z9Rec<CMAX>::MATCH + S.rbase[w] + (uint32_t)__popcll(mm & below)] = L | (uint32_t)S.sd[p] << 16;
+            R[Z9Rec<CMAX>::MATCH + S.rbase[w] + (uint32_t)__popcll(mm & below)] = L | d << 16;
+            for (uint32_t b = ms, e2 = ms + L; b < e2;) {
+                const uint32_t wd = b >> 5, hi = min(e2, (wd + 1) * 32);
+                const uint32_t bits = (hi - b == 32 ? ~0u : ((1u << (hi - b)) - 1u)) << (b & 31);
+                atomicOr(&S.cov[wd], bits);
+                b = hi;
+            }
+            atomicAdd(&lf[257 + z_lcode(L)], 1u);
+            atomicAdd(&lf[286 + z_dcode(d)], 1u);
         }
     }
     __syncthreads();
+    // the literals: every position no match covers
+    for (uint32_t i = threadIdx.x; i < n; i += 64u * NW)
+        if (!((S.cov[i >> 5] >> (i & 31)) & 1u)) atomicAdd(&lf[S.ch[i]], 1u);
     for (uint32_t i = threadIdx.x; i < (uint32_t)CMAX / 32; i += 64u * NW) R[Z9Rec<CMAX>::MASK + i] = S.mask[i];
     if (threadIdx.x == 0) R[0] = S.nmatch;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < 158; i += 64u * NW) R[Z9Rec<CMAX>::FREQ + i] = lf[2 * i] | lf[2 * i + 1] << 16;
+}
+
+// ---------------------------------------------------------------------------
+// k_z9_heap: zlib's build_tree heap for the literal/length and distance trees,
+// one chunk per LANE (64 chunks per wave), the heaps in LDS interleaved by lane
+// ([index][lane]: conflict-free).  The heap walk is inherently serial per tree;
+// across chunks it is plain SIMT.  Output: the merge sequence (the two nodes
+// each step pops) -- everything gen_bitlen needs (k_z9_code rebuilds the
+// parent links and the heap_max order from it).
+constexpr uint32_t ZH_N = 290;
+__device__ __forceinline__ void zh_down(uint32_t* H, uint32_t lane, uint32_t heap_len, uint32_t k) {
+    const uint32_t v = H[k * 64 + lane], kv = v >> 10;
+    uint32_t j = k << 1;
+    while (j <= heap_len) {
+        uint32_t hj = H[j * 64 + lane];
+        if (j < heap_len) {
+            const uint32_t hj1 = H[(j + 1) * 64 + lane];
+            if ((hj1 >> 10) <= (hj >> 10)) { j++; hj = hj1; }
+        }
+        if (kv <= (hj >> 10)) break;
+        H[k * 64 + lane] = hj;
+        k = j;
+        j <<= 1;
+    }
+    H[k * 64 + lane] = v;
+}
+
+template <int CMAX>
+__global__ __launch_bounds__(64) void k_z9_heap(EncArgs A) {
+    __shared__ uint32_t H[ZH_N * 64];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t k = blockIdx.x * 64 + lane;
+    if (k >= A.n_chunks) return;
+    const uint64_t pos0 = A.coff ? A.coff[k] : (uint64_t)k * A.chunk_size;
+    const uint32_t n = A.coff ? A.clen[k] : (uint32_t)min((uint64_t)A.chunk_size, A.n_total - pos0);
+    uint32_t T = 0;
+    if (n > (uint32_t)CMAX || !z9_gate(A, k, n, T)) return;
+    uint32_t* R = A.z9rec + (uint64_t)k * Z9Rec<CMAX>::STRIDE;
+    const uint16_t* F = reinterpret_cast<const uint16_t*>(R + Z9Rec<CMAX>::FREQ);
+    uint32_t* MG = R + Z9Rec<CMAX>::MERGE;
+#pragma unroll 1
+    for (int tree = 0; tree < 2; tree++) {
+        const uint32_t elems = tree ? 30u : 286u, fb = tree ? 286u : 0u, mb = tree ? 285u : 0u;
+        uint32_t heap_len = 0;
+        int max_code = -1;
+#pragma unroll 8
+        for (uint32_t s = 0; s < elems; s++) {
+            const uint32_t f = (uint32_t)F[fb + s] + (tree == 0 && s == 256 ? 1u : 0u);   // + the end of block
+            if (f) {
+                H[(++heap_len) * 64 + lane] = f << 16 | s;
+                max_code = (int)s;
+            }
+        }
+        while (heap_len < 2) {   // at least two codes
+            const int node = max_code < 2 ? ++max_code : 0;
+            H[(++heap_len) * 64 + lane] = 1u << 16 | (uint32_t)node;
+        }
+        for (uint32_t q = heap_len / 2; q >= 1; q--) zh_down(H, lane, heap_len, q);
+        uint32_t node = elems, i = 0;
+        do {
+            const uint32_t hn = H[64 + lane];
+            H[64 + lane] = H[heap_len * 64 + lane];
+            heap_len--;
+            zh_down(H, lane, heap_len, 1);
+            const uint32_t hm = H[64 + lane];
+            MG[mb + i++] = (hn & 1023u) | (hm & 1023u) << 16;
+            const uint32_t f = (hn >> 16) + (hm >> 16);
+            const uint32_t dep = max((hn >> 10) & 63u, (hm >> 10) & 63u) + 1u;
+            H[64 + lane] = f << 16 | dep << 10 | node;
+            node++;
+            zh_down(H, lane, heap_len, 1);
+        } while (heap_len >= 2);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -490,34 +581,34 @@ __device__ __forceinline__ uint32_t z_slen(int kind, int n) {
     return 5u;
 }
 
-// zlib's heap held in five VGPRs (entry i at lane i & 63 of register i >> 6):
-// the heap walk runs on the scalar unit (v_readlane / v_writelane), without
-// the LDS round trip per level a one-lane build pays
+// zlib's heap held in R VGPRs (entry i at lane i & 63 of register i >> 6):
+// the heap walk runs on the scalar unit (v_readlane, branch-free selects, a
+// compare-and-select write), without an LDS round trip per level
+template <int R>
 struct VHeap {
-    uint32_t h[5];
+    uint32_t h[R];
 };
-__device__ __forceinline__ uint32_t vh_get(const VHeap& H, uint32_t i) {
-    const uint32_t l = i & 63u;
-    switch (i >> 6) {
-        case 0: return readlane(H.h[0], l);
-        case 1: return readlane(H.h[1], l);
-        case 2: return readlane(H.h[2], l);
-        case 3: return readlane(H.h[3], l);
-        default: return readlane(H.h[4], l);
+template <int R>
+__device__ __forceinline__ uint32_t vh_get(const VHeap<R>& H, uint32_t i) {
+    const uint32_t l = i & 63u, r = i >> 6;
+    uint32_t x = readlane(H.h[0], l);
+#pragma unroll
+    for (int q = 1; q < R; q++) {
+        const uint32_t y = readlane(H.h[q], l);
+        x = r >= (uint32_t)q ? y : x;
     }
+    return x;
 }
-__device__ __forceinline__ void vh_set(VHeap& H, uint32_t i, uint32_t v) {
-    const uint32_t l = i & 63u, me = __lane_id();   // v_writelane as a compare + select
-    switch (i >> 6) {
-        case 0: H.h[0] = me == l ? v : H.h[0]; break;
-        case 1: H.h[1] = me == l ? v : H.h[1]; break;
-        case 2: H.h[2] = me == l ? v : H.h[2]; break;
-        case 3: H.h[3] = me == l ? v : H.h[3]; break;
-        default: H.h[4] = me == l ? v : H.h[4]; break;
-    }
+template <int R>
+__device__ __forceinline__ void vh_set(VHeap<R>& H, uint32_t i, uint32_t v) {
+    const uint32_t l = i & 63u, r = i >> 6;
+    const bool me = __lane_id() == l;
+#pragma unroll
+    for (int q = 0; q < R; q++) H.h[q] = me && r == (uint32_t)q ? v : H.h[q];
 }
 // pqdownheap: smaller() is the order of the packed keys' freq | depth bits
-__device__ __forceinline__ void vh_down(VHeap& H, uint32_t heap_len, uint32_t k) {
+template <int R>
+__device__ __forceinline__ void vh_down(VHeap<R>& H, uint32_t heap_len, uint32_t k) {
     const uint32_t v = vh_get(H, k), kv = v >> 10;
     uint32_t j = k << 1;
     while (j <= heap_len) {
@@ -541,8 +632,9 @@ __device__ __forceinline__ void vh_down(VHeap& H, uint32_t heap_len, uint32_t k)
 // exactly gen_bitlen's clamped recursion), its rare overflow repair runs on
 // lane 0; gen_codes ranks equal lengths by ballots.  pjd / pja: scratch of
 // 2 * elems + 1 entries; blc32: 16 u32.  Returns max_code.
+template <int R, bool MERGED>
 __device__ __forceinline__ int z9_build_w(Z9Tree t, l16* pjd, l16* pja, l32* blc32, l32* misc, int elems, int maxlen, int kind,
-                          uint32_t& opt, uint32_t& stat, uint32_t lane) {
+                          uint32_t& opt, uint32_t& stat, uint32_t lane, const uint32_t* MG = nullptr) {
     const uint32_t HSZ = 2u * (uint32_t)elems + 1u;
     const uint64_t below = (1ull << lane) - 1ull;
     uint32_t cnt = 0;
@@ -559,42 +651,68 @@ __device__ __forceinline__ int z9_build_w(Z9Tree t, l16* pjd, l16* pja, l32* blc
     }
     if (lane < 16) blc32[lane] = 0;
     wave_sync();
-    VHeap H;
-#pragma unroll
-    for (int j = 0; j < 5; j++) H.h[j] = 64u * j + lane <= cnt ? (uint32_t)t.heap[64 * j + lane] : 0u;
-    uint32_t heap_len = cnt;
-    while (heap_len < 2) {   // at least two codes
-        const int node = max_code < 2 ? ++max_code : 0;
-        vh_set(H, ++heap_len, 1u << 16 | (uint32_t)node);
-        if (lane == 0) t.freq[node] = 1;
-        opt--;
-        if (kind < 2) stat -= z_slen(kind, node);
-    }
-    for (uint32_t k = heap_len / 2; k >= 1; k--) vh_down(H, heap_len, k);
-    uint32_t node = (uint32_t)elems, heap_max = HSZ;
-    do {
-        const uint32_t hn = vh_get(H, 1);
-        vh_set(H, 1, vh_get(H, heap_len));
-        heap_len--;
-        vh_down(H, heap_len, 1);
-        const uint32_t hm = vh_get(H, 1);
-        heap_max -= 2;
-        if (lane == 0) {
-            t.heap[heap_max + 1] = hn & 1023u;
-            t.heap[heap_max] = hm & 1023u;
-            t.dad[hn & 1023u] = (uint16_t)node;
-            t.dad[hm & 1023u] = (uint16_t)node;
+    uint32_t node, root;
+    if (MERGED) {
+        // k_z9_heap's merge sequence: the heap_max order and the parent links
+        uint32_t heap_len = cnt;
+        while (heap_len < 2) {   // at least two codes (k_z9_heap forced the same nodes)
+            const int nd = max_code < 2 ? ++max_code : 0;
+            heap_len++;
+            if (lane == 0) t.freq[nd] = 1;
+            opt--;
+            if (kind < 2) stat -= z_slen(kind, nd);
         }
-        const uint32_t f = (hn >> 16) + (hm >> 16);
-        const uint32_t dep = max((hn >> 10) & 63u, (hm >> 10) & 63u) + 1u;
-        vh_set(H, 1, f << 16 | dep << 10 | node);
-        node++;
-        vh_down(H, heap_len, 1);
-    } while (heap_len >= 2);
-    const uint32_t root = vh_get(H, 1) & 1023u;
-    heap_max--;
-    if (lane == 0) t.heap[heap_max] = root;
-    wave_sync();
+        const uint32_t nm = heap_len - 1;
+        for (uint32_t i = lane; i < nm; i += 64) {
+            const uint32_t x = MG[i], a = x & 1023u, b = x >> 16;
+            t.heap[HSZ - 1 - 2 * i] = a;
+            t.heap[HSZ - 2 - 2 * i] = b;
+            t.dad[a] = (uint16_t)(elems + i);
+            t.dad[b] = (uint16_t)(elems + i);
+        }
+        node = (uint32_t)elems + nm;
+        root = node - 1;
+        if (lane == 0) t.heap[HSZ - 1 - 2 * nm] = root;
+        wave_sync();
+    } else {
+        VHeap<R> H;
+    #pragma unroll
+        for (int j = 0; j < R; j++) H.h[j] = 64u * j + lane <= cnt ? (uint32_t)t.heap[64 * j + lane] : 0u;
+        uint32_t heap_len = cnt;
+        while (heap_len < 2) {   // at least two codes
+            const int nd = max_code < 2 ? ++max_code : 0;
+            vh_set(H, ++heap_len, 1u << 16 | (uint32_t)nd);
+            if (lane == 0) t.freq[nd] = 1;
+            opt--;
+            if (kind < 2) stat -= z_slen(kind, nd);
+        }
+        for (uint32_t k = heap_len / 2; k >= 1; k--) vh_down(H, heap_len, k);
+        node = (uint32_t)elems;
+        uint32_t heap_max = HSZ;
+        do {
+            const uint32_t hn = vh_get(H, 1);
+            vh_set(H, 1, vh_get(H, heap_len));
+            heap_len--;
+            vh_down(H, heap_len, 1);
+            const uint32_t hm = vh_get(H, 1);
+            heap_max -= 2;
+            if (lane == 0) {
+                t.heap[heap_max + 1] = hn & 1023u;
+                t.heap[heap_max] = hm & 1023u;
+                t.dad[hn & 1023u] = (uint16_t)node;
+                t.dad[hm & 1023u] = (uint16_t)node;
+            }
+            const uint32_t f = (hn >> 16) + (hm >> 16);
+            const uint32_t dep = max((hn >> 10) & 63u, (hm >> 10) & 63u) + 1u;
+            vh_set(H, 1, f << 16 | dep << 10 | node);
+            node++;
+            vh_down(H, heap_len, 1);
+        } while (heap_len >= 2);
+        root = vh_get(H, 1) & 1023u;
+        heap_max--;
+        if (lane == 0) t.heap[heap_max] = root;
+        wave_sync();
+    }
     // ---- depths: pointer jumping over dad[] (nodes 0 .. node-1) ----
     const uint32_t nn = node;
     uint32_t d[9], a[9];
@@ -739,63 +857,6 @@ __device__ __forceinline__ void sb_put(SBits& b, l32* words, uint32_t v, uint32_
     }
 }
 
-// send_tree over len[0..max_code] with the bit-length codes bcl (lane i: code
-// | len << 16 of symbol i), on the scalar unit; lens: the lengths as VHeap-style
-// registers (symbol x at lane x & 63 of register x >> 6)
-__device__ __forceinline__ void z9_send_w(const VHeap& lens, int max_code, uint32_t bcl, SBits& sb, l32* W, uint32_t lane) {
-    int prevlen = -1, nextlen = (int)vh_get(lens, 0), count = 0, max_count = 7, min_count = 4;
-    if (nextlen == 0) { max_count = 138; min_count = 3; }
-    for (int n = 0; n <= max_code; n++) {
-        const int curlen = nextlen;
-        nextlen = n + 1 <= max_code ? (int)vh_get(lens, (uint32_t)n + 1) : 0xFFFF;
-        if (++count < max_count && curlen == nextlen) continue;
-        const uint32_t cc = readlane(bcl, (uint32_t)curlen);
-        if (count < min_count) {
-            do { sb_put(sb, W, cc & 0xFFFFu, cc >> 16, lane); } while (--count);
-        } else if (curlen != 0) {
-            if (curlen != prevlen) { sb_put(sb, W, cc & 0xFFFFu, cc >> 16, lane); count--; }
-            const uint32_t c16 = readlane(bcl, 16);
-            sb_put(sb, W, (c16 & 0xFFFFu) | ((uint32_t)count - 3) << (c16 >> 16), (c16 >> 16) + 2, lane);
-        } else if (count <= 10) {
-            const uint32_t c17 = readlane(bcl, 17);
-            sb_put(sb, W, (c17 & 0xFFFFu) | ((uint32_t)count - 3) << (c17 >> 16), (c17 >> 16) + 3, lane);
-        } else {
-            const uint32_t c18 = readlane(bcl, 18);
-            sb_put(sb, W, (c18 & 0xFFFFu) | ((uint32_t)count - 11) << (c18 >> 16), (c18 >> 16) + 7, lane);
-        }
-        count = 0;
-        prevlen = curlen;
-        if (nextlen == 0) { max_count = 138; min_count = 3; }
-        else if (curlen == nextlen) { max_count = 6; min_count = 3; }
-        else { max_count = 7; min_count = 4; }
-    }
-}
-
-// scan_tree on the scalar unit: the bit-length symbol counts into cnt (u32,
-// lane 0's fire-and-forget LDS adds)
-__device__ __forceinline__ void z9_scan_w(const VHeap& lens, int max_code, l32* cnt, uint32_t lane) {
-    int prevlen = -1, nextlen = (int)vh_get(lens, 0), count = 0, max_count = 7, min_count = 4;
-    if (nextlen == 0) { max_count = 138; min_count = 3; }
-    for (int n = 0; n <= max_code; n++) {
-        const int curlen = nextlen;
-        nextlen = n + 1 <= max_code ? (int)vh_get(lens, (uint32_t)n + 1) : 0xFFFF;
-        if (++count < max_count && curlen == nextlen) continue;
-        uint32_t sym, add;
-        if (count < min_count) { sym = (uint32_t)curlen; add = (uint32_t)count; }
-        else if (curlen != 0) {
-            if (curlen != prevlen && lane == 0) atomicAdd((uint32_t*)&cnt[curlen], 1u);
-            sym = 16; add = 1;
-        } else if (count <= 10) { sym = 17; add = 1; }
-        else { sym = 18; add = 1; }
-        if (lane == 0) atomicAdd((uint32_t*)&cnt[sym], add);
-        count = 0;
-        prevlen = curlen;
-        if (nextlen == 0) { max_count = 138; min_count = 3; }
-        else if (curlen == nextlen) { max_count = 6; min_count = 3; }
-        else { max_count = 7; min_count = 4; }
-    }
-}
-
 __device__ __forceinline__ void z_put(l32* w, uint32_t b, uint32_t v, uint32_t nb) {
     if (!nb) return;
     const uint32_t i = b >> 5, o = b & 31;
@@ -809,13 +870,102 @@ __device__ __forceinline__ void z_put_atomic(uint32_t* w, uint32_t b, uint32_t v
     if (o + nb > 32) atomicOr(&w[i + 1], v >> (32 - o));
 }
 
+// scan_tree / send_tree (the code-length RLE) one lane per maximal run of
+// equal lengths.  zlib's loop cuts a run of value v and length r into chunks:
+// v != 0: the first chunk takes min(r, 7) (below 4: v raw each; else v once and
+// 16 for the rest), later chunks 6 each as 16 (a tail below 3 goes raw); v == 0:
+// chunks of 138 as 18, the tail as 17 (3..10), 18 (11+) or raw (< 3).  A run
+// start resets the chunk limits exactly as zlib's transition does (the previous
+// value differs).  send = false: the symbol counts into cnt (u32); send = true:
+// the bits from bit bp (codes bcl: lane i = code | len << 16 of symbol i).
+// Returns the bits of the send.
+template <int R>
+__device__ __forceinline__ uint32_t z9_rle_par(const VHeap<R>& L, int max_code, bool send, l32* cnt, uint32_t bcl,
+                                               uint32_t* words, uint32_t bp, uint32_t lane) {
+    const uint32_t N = (uint32_t)(max_code + 1);
+    uint64_t st[R];
+#pragma unroll
+    for (int j = 0; j < R; j++) {
+        const uint32_t e = 64u * j + lane;
+        uint32_t prev = AMBC_DPP(0xFFFFu, L.h[j], 0x138, 0xF, 0xF, false);   // wave_shr:1
+        if (lane == 0) prev = j ? readlane(L.h[j > 0 ? j - 1 : 0], 63) : 0xFFFFu;
+        st[j] = __ballot(e < N && L.h[j] != prev);
+    }
+    const uint32_t c16 = readlane(bcl, 16), c17 = readlane(bcl, 17), c18 = readlane(bcl, 18);
+    uint32_t carry = 0;
+#pragma unroll
+    for (int j = 0; j < R; j++) {
+        const uint32_t e = 64u * j + lane;
+        const bool run = (st[j] >> lane) & 1u;
+        const uint32_t v = L.h[j];
+        uint32_t end = N;
+        {
+            const uint64_t above = lane < 63 ? st[j] >> (lane + 1) : 0ull;
+            if (above) end = e + 1 + (uint32_t)__builtin_ctzll(above);
+            else {
+#pragma unroll
+                for (int q = R - 1; q > j; q--)
+                    if (st[q]) end = 64u * q + (uint32_t)__builtin_ctzll(st[q]);
+            }
+        }
+        const uint32_t r = run ? end - e : 0u;
+        // the run's chunks: rawA raw v, a16 (16 with extra x16a), k full chunks
+        // (16 x 3 / 18 x 127), the tail (raw rawC, or one 16 / 17 / 18 with extra xt)
+        uint32_t rawA = 0, a16 = 0, x16a = 0, kf = 0, rawC = 0, tsym = 0, xt = 0;
+        if (run) {
+            if (v != 0) {
+                const uint32_t c1 = min(r, 7u);
+                if (c1 < 4) rawA = c1;
+                else { rawA = 1; a16 = 1; x16a = c1 - 4; }
+                const uint32_t r1 = r - c1;
+                kf = r1 / 6;
+                const uint32_t rem = r1 % 6;
+                if (rem >= 3) { tsym = 16; xt = rem - 3; }
+                else rawC = rem;
+            } else {
+                kf = r / 138;
+                const uint32_t rem = r % 138;
+                if (rem < 3) rawC = rem;
+                else if (rem <= 10) { tsym = 17; xt = rem - 3; }
+                else { tsym = 18; xt = rem - 11; }
+            }
+        }
+        const uint32_t ksym = v != 0 ? 16u : 18u;
+        if (!send) {
+            if (run) {
+                if (rawA + rawC) atomicAdd((uint32_t*)&cnt[v], rawA + rawC);
+                if (a16) atomicAdd((uint32_t*)&cnt[16], 1u);
+                if (kf) atomicAdd((uint32_t*)&cnt[ksym], kf);
+                if (tsym) atomicAdd((uint32_t*)&cnt[tsym], 1u);
+            }
+        } else {
+            const uint32_t cv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(min(v, 18u) << 2), (int)bcl);   // v's code
+            const uint32_t lv = cv >> 16, l16 = c16 >> 16;
+            const uint32_t ck = v != 0 ? c16 : c18, lk = (ck >> 16) + (v != 0 ? 2u : 7u);
+            const uint32_t ct = tsym == 16 ? c16 : tsym == 17 ? c17 : c18;
+            const uint32_t lt = tsym ? (ct >> 16) + (tsym == 16 ? 2u : tsym == 17 ? 3u : 7u) : 0u;
+            const uint32_t bits = run ? (rawA + rawC) * lv + a16 * (l16 + 2) + kf * lk + lt : 0u;
+            const uint32_t incl = wave_incl_sum(bits);
+            uint32_t b = bp + carry + incl - bits;
+            carry += readlane(incl, 63);
+            if (run) {
+                for (uint32_t i = 0; i < rawA; i++) { z_put_atomic(words, b, cv & 0xFFFFu, lv); b += lv; }
+                if (a16) { z_put_atomic(words, b, (c16 & 0xFFFFu) | x16a << l16, l16 + 2); b += l16 + 2; }
+                const uint32_t kv = (ck & 0xFFFFu) | (v != 0 ? 3u : 127u) << (ck >> 16);
+                for (uint32_t i = 0; i < kf; i++) { z_put_atomic(words, b, kv, lk); b += lk; }
+                for (uint32_t i = 0; i < rawC; i++) { z_put_atomic(words, b, cv & 0xFFFFu, lv); b += lv; }
+                if (tsym) z_put_atomic(words, b, (ct & 0xFFFFu) | xt << (ct >> 16), lt);
+            }
+        }
+    }
+    return carry;
+}
 
 template <int CMAX>
 struct Z9CSmem {
     static constexpr int WORDS = (CMAX + 5 * (int)Z_NBLK + 64) / 4 + 4;
     alignas(16) uint32_t bits[WORDS];        // the deflate body, LSB first
     uint32_t mstart[CMAX / 32 + 2];          // match starts (bitmask by position)
-    uint32_t lf32[288], df32[32];            // block frequencies (counted with atomics)
     uint32_t ecl[288], ecd[32];              // emission codes: code | len << 16
     uint32_t heapL[LT_N + 1], heapD[DT_N + 1];
     uint16_t lfreq[LT_N + 1], ldad[LT_N + 1], lcode[288];
@@ -874,9 +1024,9 @@ __global__ __launch_bounds__(64) void k_z9_code(EncArgs A) {
     for (uint32_t i = lane; i < (uint32_t)Z9CSmem<CMAX>::WORDS; i += 64) S.bits[i] = 0;
     wave_sync();
 
-    // one position-major pass over [bs, be): emit = false counts the block's
-    // symbols, emit = true writes them at bit bp (returns the bits written)
-    auto pass = [&](uint32_t bs, uint32_t be, uint32_t rank0, bool emit, uint32_t bp) -> uint32_t {
+    // the block's symbols over [bs, be), position-major, written from bit bp
+    // (returns the bits written)
+    auto pass = [&](uint32_t bs, uint32_t be, uint32_t rank0, uint32_t bp) -> uint32_t {
         uint32_t rank = rank0, out = 0;
         int carry = (int)bs;
         // a round's global loads (its matches, its bytes) are issued one round
@@ -909,13 +1059,7 @@ __global__ __launch_bounds__(64) void k_z9_code(EncArgs A) {
             const bool lit = in && !ms && E <= (int)pos;
             const uint32_t c = lit ? cb : 0u;
             const uint32_t lc = ms ? z_lcode(L) : 0u, dc = ms ? z_dcode(d) : 0u;
-            if (!emit) {
-                if (lit) atomicAdd(&S.lf32[c], 1u);
-                if (ms) {
-                    atomicAdd(&S.lf32[257 + lc], 1u);
-                    atomicAdd(&S.df32[dc], 1u);
-                }
-            } else {
+            {
                 uint32_t cost = 0, e1 = 0, e2 = 0, v1 = 0, v2 = 0;
                 if (lit) {
                     e1 = S.ecl[c] >> 16;
@@ -951,38 +1095,37 @@ __global__ __launch_bounds__(64) void k_z9_code(EncArgs A) {
         for (uint32_t i = lane; i < (bs >> 5); i += 64) rank0 += (uint32_t)__popc(S.mstart[i]);
         if (lane == 0 && (bs & 31)) rank0 += (uint32_t)__popc(S.mstart[bs >> 5] & ((1u << (bs & 31)) - 1u));
         rank0 = wave_sum_u32(rank0);
-        for (uint32_t i = lane; i < 288; i += 64) S.lf32[i] = 0;
-        if (lane < 32) S.df32[lane] = 0;
+        // the block's symbol counts (k_z9_parse) + the end of block
+        const uint16_t* F = reinterpret_cast<const uint16_t*>(R + Z9Rec<CMAX>::FREQ);
         if (lane < 20) S.cnt32[lane] = 0;
+        for (uint32_t i = lane; i < 286; i += 64) S.lfreq[i] = (uint16_t)(F[i] + (i == 256 ? 1u : 0u));
+        if (lane < 30) S.dfreq[lane] = F[286 + lane];
         wave_sync();
         ZSTAMP(0);
-        pass(bs, be, rank0, false, 0);
-        wave_sync();
-        ZSTAMP(1);
-        for (uint32_t i = lane; i < 286; i += 64) S.lfreq[i] = (uint16_t)(S.lf32[i] + (i == 256 ? 1u : 0u));
-        if (lane < 30) S.dfreq[lane] = (uint16_t)S.df32[lane];
-        wave_sync();
         // ---- the trees: build_tree x 2, scan_tree x 2, build_bl_tree ----
         l16* PJD = (l16*)S.pjd;
         l16* PJA = (l16*)S.pja;
         l32* BLC = (l32*)S.blc32;
         l32* MISC = (l32*)(S.misc + 12);
         uint32_t optL = 0, statL = 0, optD = 0, statD = 0, optB = 0, statB = 0;
-        const int lmax = z9_build_w(LT, PJD, PJA, BLC, MISC, 286, 15, 0, optL, statL, lane);
-        const int dmax = z9_build_w(DT, PJD, PJA, BLC, MISC, 30, 15, 1, optD, statD, lane);
-        VHeap LL, DL;
+        const int lmax = z9_build_w<5, true>(LT, PJD, PJA, BLC, MISC, 286, 15, 0, optL, statL, lane,
+                                               R + Z9Rec<CMAX>::MERGE);
+        const int dmax = z9_build_w<1, true>(DT, PJD, PJA, BLC, MISC, 30, 15, 1, optD, statD, lane,
+                                              R + Z9Rec<CMAX>::MERGE + 285);
+        VHeap<5> LL;
+        VHeap<1> DL;
 #pragma unroll
         for (int j = 0; j < 5; j++) {
             const uint32_t x = 64u * j + lane;
             LL.h[j] = (int)x <= lmax ? (uint32_t)S.llen[x] : 0u;
-            DL.h[j] = (int)x <= dmax ? (uint32_t)S.dlen[x] : 0u;
         }
-        z9_scan_w(LL, lmax, (l32*)S.cnt32, lane);
-        z9_scan_w(DL, dmax, (l32*)S.cnt32, lane);
+        DL.h[0] = (int)lane <= dmax ? (uint32_t)S.dlen[lane] : 0u;
+        (void)z9_rle_par(LL, lmax, false, (l32*)S.cnt32, 0u, S.bits, 0u, lane);
+        (void)z9_rle_par(DL, dmax, false, (l32*)S.cnt32, 0u, S.bits, 0u, lane);
         wave_sync();
         if (lane < 19) S.bfreq[lane] = (uint16_t)S.cnt32[lane];
         wave_sync();
-        (void)z9_build_w(BT, PJD, PJA, BLC, MISC, 19, 7, 2, optB, statB, lane);
+        (void)z9_build_w<1, false>(BT, PJD, PJA, BLC, MISC, 19, 7, 2, optB, statB, lane);
         ZSTAMP(2);
         int maxbl;
         for (maxbl = 18; maxbl >= 3; maxbl--) if (S.blen[z_blord[maxbl]] != 0) break;
@@ -1044,16 +1187,23 @@ __global__ __launch_bounds__(64) void k_z9_code(EncArgs A) {
                 sb_put(sb, W, (uint32_t)maxbl + 1 - 4, 4, lane);
                 for (int r = 0; r <= maxbl; r++) sb_put(sb, W, S.blen[z_blord[r]], 3, lane);
                 const uint32_t bcl = lane < 19 ? (uint32_t)S.bcode[lane] | (uint32_t)S.blen[lane] << 16 : 0u;
-                z9_send_w(LL, lmax, bcl, sb, W, lane);
-                z9_send_w(DL, dmax, bcl, sb, W, lane);
+                if (sb.n && lane == 0) W[sb.w] = (uint32_t)sb.acc;
+                wave_sync();
+                uint32_t p = sb.w * 32 + sb.n;
+                p += z9_rle_par(LL, lmax, true, (l32*)S.cnt32, bcl, S.bits, p, lane);
+                p += z9_rle_par(DL, dmax, true, (l32*)S.cnt32, bcl, S.bits, p, lane);
+                sb.w = p >> 5;
+                sb.n = p & 31u;
+                sb.acc = 0;   // (the partial word is in LDS already)
+            } else if (sb.n && lane == 0) {
+                W[sb.w] = (uint32_t)sb.acc;
             }
-            if (sb.n && lane == 0) W[sb.w] = (uint32_t)sb.acc;
             S.misc[9] = sb.w * 32 + sb.n;
         }
         wave_sync();
         ZSTAMP(4);
         bp = S.misc[9];
-        bp += pass(bs, be, rank0, true, bp);
+        bp += pass(bs, be, rank0, bp);
         wave_sync();
         if (lane == 0) z_put(W, bp, S.ecl[256] & 0xFFFFu, S.ecl[256] >> 16);
         bp += S.ecl[256] >> 16;
@@ -1098,6 +1248,7 @@ __global__ __launch_bounds__(64) void k_z9_code(EncArgs A) {
 template <int CMAX>
 hipError_t launch_z9_t(const EncArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_z9_parse<CMAX>, dim3(a.n_chunks), dim3(64 * Z9Cfg<CMAX>::NW), 0, s, a);
+    hipLaunchKernelGGL(k_z9_heap<CMAX>, dim3((a.n_chunks + 63) / 64), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_z9_code<CMAX>, dim3(a.n_chunks), dim3(64), 0, s, a);
     return hipGetLastError();
 }
