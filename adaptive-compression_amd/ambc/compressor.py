@@ -72,7 +72,7 @@ class AdaptiveCompressor:
     REFERENCE_CHUNK_SIZE_CANDIDATES = list(REFERENCE_CHUNK_SIZE_CANDIDATES)
 
     def __init__(self, marker_max_length=32, sample_size=10000, *, chunk_size=None,
-                 mode="native", methods=None, devices=None, deflate="v1"):
+                 mode="native", methods=None, devices=None, deflate=None):
         self.marker_max_length = marker_max_length
         self.sample_size = sample_size
         self.marker_finder = None          # the reference's finder is never called (:303-310)
@@ -87,12 +87,14 @@ class AdaptiveCompressor:
         if mode not in ("native", "reference"):
             raise ValueError("mode must be 'native' or 'reference'")
         self.mode = mode
-        # id 5's GPU encoder: "v1" ("ambc-deflate v1", any chunk <= 16384) or
-        # "zlib9" (zlib.compress(data, 9)'s own bytes -- the reference's
-        # DeflateCompression, advanced_compression.py:76-81 -- chunks <= 4096)
-        if deflate not in ("v1", "zlib9"):
-            raise ValueError("deflate must be 'v1' or 'zlib9'")
-        self.deflate = deflate
+        # id 5's GPU encoder: "zlib9" (zlib.compress(data, 9)'s own bytes -- the
+        # reference's DeflateCompression, advanced_compression.py:76-81 -- chunks
+        # <= 4096) or "v1" ("ambc-deflate v1": valid zlib streams of this
+        # engine's own parse, chunks <= 16384, faster).  None: "zlib9" in
+        # reference mode when every chunk size allows it, else "v1".
+        if deflate not in (None, "v1", "zlib9"):
+            raise ValueError("deflate must be None, 'v1' or 'zlib9'")
+        self._deflate = deflate
         if chunk_size is not None:
             self.CHUNK_SIZE_CANDIDATES = [int(chunk_size)]
         ids = tuple(DEFAULT_METHODS if methods is None else [m for m in methods if m != 255])
@@ -107,6 +109,14 @@ class AdaptiveCompressor:
         self.method_chunk_prefs = dict(METHOD_CHUNK_PREFS)
         self.devices = list(devices) if devices else None
         self.chunk_stats = None
+
+    @property
+    def deflate(self):
+        if self._deflate is not None:
+            return self._deflate
+        if self.mode == "reference" and max(int(c) for c in self.CHUNK_SIZE_CANDIDATES) <= 4096:
+            return "zlib9"
+        return "v1"
 
     # -- API parity helpers (adaptive_compressor.py:179-194) --------------------
     def set_progress_callback(self, callback):

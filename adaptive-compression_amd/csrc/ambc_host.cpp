@@ -401,6 +401,18 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
                     "buckets %.0f clear %.0f walk %.0f wait %.0f path+out %.0f\n", gs[7], gs[0] / c, gs[1] / c,
                     gs[2] / c, gs[3] / c, gs[4] / c, gs[5] / c, gs[6] / c);
         }
+        if (z9 && !((p->method_mask >> AMBC_M_DICT) & 1)) {
+            std::vector<unsigned long long> g((size_t)M * 8);
+            HIPCHK(hipMemcpyAsync(g.data(), d.seg.as<unsigned long long>() + (size_t)M * 16, (size_t)M * 64,
+                                  hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            double gs[8] = {0};
+            for (size_t q = 0; q < g.size(); q++) gs[q & 7] += (double)g[q];
+            const double c = std::max(gs[7], 1.0);
+            fprintf(stderr, "[ambc stamps] z9 parsed=%.0f wave-0 cycles/chunk: load %.0f sort %.0f walk %.0f "
+                    "wait %.0f path %.0f out %.0f\n", gs[7], gs[0] / c, gs[1] / c, gs[2] / c, gs[3] / c,
+                    gs[4] / c, gs[5] / c);
+        }
         if (deflate) {
             std::vector<unsigned long long> g((size_t)M * 8);
             HIPCHK(hipMemcpyAsync(g.data(), d.seg.as<unsigned long long>() + (size_t)M * 8, (size_t)M * 64,

@@ -364,6 +364,28 @@ __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t
     }
 }
 
+#ifdef AMBC_STAMPS
+// diagnostic build only: wave 0's phase cycles per parsed chunk in
+// A.stamps[(2 M + k) * 8 + phase] (k_dict's slots; phase 7 = 1 marks a parse)
+#define PSTAMP_DECL uint64_t _pt = __builtin_amdgcn_s_memtime(); uint64_t _pa[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define PSTAMP(ph)                                                 \
+    do {                                                           \
+        __builtin_amdgcn_s_waitcnt(0xC07F);                        \
+        const uint64_t _t = __builtin_amdgcn_s_memtime();          \
+        _pa[ph] += _t - _pt;                                       \
+        _pt = _t;                                                  \
+    } while (0)
+#define PSTAMP_FLUSH                                                                  \
+    if (threadIdx.x == 0 && A.stamps) {                                               \
+        _pa[7] = 1;                                                                   \
+        for (int _p = 0; _p < 8; _p++) A.stamps[(2ull * A.n_chunks + k) * 8 + _p] = _pa[_p]; \
+    }
+#else
+#define PSTAMP_DECL
+#define PSTAMP(ph) do {} while (0)
+#define PSTAMP_FLUSH
+#endif
+
 template <int CMAX>
 __global__ __launch_bounds__(64 * Z9Cfg<CMAX>::NW) void k_z9_parse(EncArgs A) {
     constexpr int NW = Z9Cfg<CMAX>::NW;
@@ -375,6 +397,7 @@ __global__ __launch_bounds__(64 * Z9Cfg<CMAX>::NW) void k_z9_parse(EncArgs A) {
     const uint32_t n = A.coff ? A.clen[k] : (uint32_t)min((uint64_t)A.chunk_size, A.n_total - pos0);
     uint32_t T = 0;
     if (n > (uint32_t)CMAX || !z9_gate(A, k, n, T)) return;
+    PSTAMP_DECL
     const uint8_t* src = A.in + pos0;
     {
         const uint32_t TT = 64u * NW;
@@ -389,11 +412,15 @@ __global__ __launch_bounds__(64 * Z9Cfg<CMAX>::NW) void k_z9_parse(EncArgs A) {
         for (uint32_t i = n + threadIdx.x; i < (uint32_t)CMAX + 320; i += TT) S.ch[i] = 0;
     }
     __syncthreads();
+    PSTAMP(0);
     z9_sort(S, n - 2, wave, lane);
     for (uint32_t i = threadIdx.x; i < (uint32_t)CMAX; i += 64u * NW) S.seg[i] = 0;
     __syncthreads();
+    PSTAMP(1);
     z9_walkers(S, n, wave, lane);
+    PSTAMP(2);
     __syncthreads();
+    PSTAMP(3);
     // ---- the path from 0.  Per 64-position window, pointer doubling over the
     // lanes gives every clean position's exit from the window (the first path
     // position past it) and the matches on the way; thread 0 chains the windows
@@ -436,6 +463,7 @@ __global__ __launch_bounds__(64 * Z9Cfg<CMAX>::NW) void k_z9_parse(EncArgs A) {
         S.nmatch = mr;
     }
     __syncthreads();
+    PSTAMP(4);
     uint32_t* R = A.z9rec + (uint64_t)k * Z9Rec<CMAX>::STRIDE;
     for (uint32_t w = wave; w < nwin; w += NW) {
         const uint32_t e = S.entry[w];
@@ -473,6 +501,8 @@ __global__ __launch_bounds__(64 * Z9Cfg<CMAX>::NW) void k_z9_parse(EncArgs A) {
     if (threadIdx.x == 0) R[0] = S.nmatch;
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < 158; i += 64u * NW) R[Z9Rec<CMAX>::FREQ + i] = lf[2 * i] | lf[2 * i + 1] << 16;
+    PSTAMP(5);
+    PSTAMP_FLUSH
 }
 
 // ---------------------------------------------------------------------------

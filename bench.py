@@ -67,9 +67,10 @@ def parse():
     ap.add_argument("--py-seconds", type=float, default=12.0,
                     help="budget of the single-core pure-Python restatement leg")
     ap.add_argument("--no-e2e", action="store_true", help="skip the pinned host-to-host leg")
-    ap.add_argument("--alt-methods", default="1,3,4,5;1,2,3,4",
+    ap.add_argument("--alt-methods", default="1,3,4,5;1,2,3,4;1,3,4,5z",
                     help="';'-separated method sets reported beside the headline ('' to skip): "
                          "1,3,4,5 = every package decodable by the stdlib-only reference; "
+                         "a trailing z = id 5 as zlib.compress(data, 9)'s own bytes; "
                          "1,2,3,4 = the reference's own bytes (byte-pinned set)")
     ap.add_argument("--api-bytes", type=int, default=256 << 20,
                     help="input size of the AdaptiveCompressor.compress(path, path) leg (0: skip)")
@@ -246,11 +247,15 @@ def api_leg(nbytes, chunk, mode, methods, seed):
             "ratio": round(stats["compressed_size"] / nbytes, 5) if "compressed_size" in stats else None}
 
 
-def alt_leg(lib, ctx, d_in, n, args, methods, steps):
+def alt_leg(lib, ctx, d_in, n, args, methods, steps, zlib9=False):
     """The same input under another method set (device-resident, same clock
-    discipline as the headline), its ratio and a bit-exact decode."""
+    discipline as the headline), its ratio and a bit-exact decode.  zlib9: id 5
+    as zlib.compress(data, 9)'s own bytes (AMBC_FLAG_ZLIB9); the id-5 packages
+    of a 16 MiB prefix are compared with Python's zlib.compress(chunk, 9)."""
     from ambc import _lib, AdaptiveCompressor
     p = make_params(args, methods, n)
+    if zlib9:
+        p.flags |= _lib.FLAG_ZLIB9
     cap = lib.ambc_compress_bound(n, args.chunk)
     d_out = _lib.DeviceBuffer(ctx, cap + 64)
     olen = C.c_uint64()
@@ -283,7 +288,24 @@ def alt_leg(lib, ctx, d_in, n, args, methods, steps):
     dwall = time.perf_counter() - t
     ok = device_equals_host(ctx, back, n, d_in)
     ds = comp._last_device_stats
-    return {"methods": methods, "GBps": round(n / dt / 1e9, 3), "ms_per_step": round(dt * 1e3, 3),
+    z9 = None
+    if zlib9:
+        import zlib
+        pre = d_in.download(min(n, 16 << 20))
+        pos = off = checked = same = 0
+        while pos + 18 <= len(body) and body[pos + 4] != 0 and off + args.chunk <= len(pre):
+            orig = int.from_bytes(body[pos + 10:pos + 14], "little")
+            clen = int.from_bytes(body[pos + 14:pos + 18], "little")
+            if body[pos + 4] == 5:
+                checked += 1
+                same += body[pos + 18:pos + 18 + clen] == zlib.compress(bytes(pre[off:off + orig]), 9)
+            pos += 18 + clen
+            off += orig
+        z9 = {"id5_encoder": "zlib.compress(data, 9) bytes (AMBC_FLAG_ZLIB9)",
+              "id5_packages_checked_vs_python_zlib": checked, "identical": same,
+              "zlib_version": zlib.ZLIB_RUNTIME_VERSION}
+    return {"methods": methods, **({"zlib9": z9} if z9 else {}),
+            "GBps": round(n / dt / 1e9, 3), "ms_per_step": round(dt * 1e3, 3),
             "steps": steps, "ratio": round(olen.value / n, 5), "method_usage": usage,
             "kernels_ms": round(sum(enc) / len(enc) / 1e6, 3), "round_trip_bit_exact": ok,
             "decode": {"kernel_ms": round(ds.kernel_ns / 1e6, 3), "host_zlib_ms": round(ds.host_codec_ns / 1e6, 3),
@@ -447,7 +469,9 @@ def main():
     if rank == 0 and world == 1 and args.alt_methods:
         for ms in args.alt_methods.split(";"):
             if ms.strip():
-                alt = alt_leg(lib, ctx, d_in, n, args, [int(x) for x in ms.split(",")], max(2, args.steps // 2))
+                z = ms.strip().endswith("z")   # "...z": id 5 as zlib-9's own bytes
+                alt = alt_leg(lib, ctx, d_in, n, args, [int(x) for x in ms.strip().rstrip("z").split(",")],
+                              max(2, args.steps // 2), zlib9=z)
                 log(f"alt: {alt}")
                 alts.append(alt)
     if rank == 0 and world == 1 and args.api_bytes:

@@ -65,14 +65,19 @@ def analyze(ctx, data, chunk, methods=(1, 3, 4, 9), prefs=None):
 # whole files vs the reference's own .ambc outputs
 # ---------------------------------------------------------------------------
 def test_golden_files_bit_exact(ctx):
-    n = 0
+    n = n5 = 0
     for rec in load_golden("files.json"):
         if rec["mode"] not in ("native", "reference"):
             continue
-        if set(rec["methods"]) - {1, 3, 4, 9, 255}:
+        ms = set(rec["methods"])
+        # id 5 is zlib.compress(data, 9) in the reference: the zlib-9 GPU encoder
+        # (chunks <= 4096) reproduces those packages byte for byte
+        z9 = 5 in ms and rec["chunk"] <= 4096
+        if ms - {1, 3, 4, 9, 255} - ({5} if z9 else set()):
             continue
         data = synth.generate(rec["size"], rec["seed"])
-        comp = _compressor(chunk_size=rec["chunk"], mode=rec["mode"], methods=rec["methods"])
+        comp = _compressor(chunk_size=rec["chunk"], mode=rec["mode"], methods=rec["methods"],
+                           **({"deflate": "zlib9"} if z9 else {}))
         blob, stats = comp.compress_bytes(data)
         with open(os.path.join(GOLDEN, rec["file"]), "rb") as f:
             ref = f.read()
@@ -80,7 +85,8 @@ def test_golden_files_bit_exact(ctx):
         assert blob == ref
         assert _norm(stats) == rec["stats"], rec["name"]
         n += 1
-    assert n >= 20
+        n5 += z9
+    assert n >= 21 and n5 >= 1
 
 
 def test_golden_files_decode(ctx):
@@ -436,7 +442,8 @@ def test_deflate_chunks_decode(ctx):
 
 # ---------------------------------------------------------------------------
 # id 5 on the GPU: "ambc-deflate v1" (k_deflate) against the oracle's
-# restatement, byte for byte, inside the whole selector; every stream inflates
+# restatement, byte for byte, inside the whole selector (reference mode at
+# chunks <= 4096: zlib-9's bytes against the system zlib); every stream inflates
 # with zlib (what the reference's DeflateCompression.decompress calls)
 # ---------------------------------------------------------------------------
 GD_CASES = [((1 << 20) + 77, 20250418, 4096, (1, 3, 4, 5, 9)), ((1 << 20) + 5, 3, 1024, (1, 3, 5)),
@@ -451,7 +458,10 @@ def test_gdeflate_bodies_match_oracle(ctx, n, seed, chunk, methods):
     for mode in ("native", "reference"):
         comp = _compressor(chunk_size=chunk, mode=mode, methods=methods)
         body = comp._adaptive_compress(data)
-        p = orc.make_params(chunk, mode, methods, n_total=n, deflate="gd")
+        # reference mode at chunks <= 4096 defaults to zlib-9's own bytes
+        z9 = mode == "reference" and chunk <= 4096
+        assert comp.deflate == ("zlib9" if z9 else "v1")
+        p = orc.make_params(chunk, mode, methods, n_total=n, deflate="zlib" if z9 else "gd")
         ref, st = orc.compress_body(data, p, nthreads=0)
         assert body == ref, (mode, n, chunk, methods)
         gst = comp._last_device_stats
