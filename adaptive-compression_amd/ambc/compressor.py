@@ -90,7 +90,7 @@ class AdaptiveCompressor:
         # id 5's GPU encoder: "zlib9" (zlib.compress(data, 9)'s own bytes -- the
         # reference's DeflateCompression, advanced_compression.py:76-81 -- chunks
         # <= 4096) or "v1" ("ambc-deflate v1": valid zlib streams of this
-        # engine's own parse, chunks <= 16384, faster).  None: "zlib9" in
+        # engine's own parse, chunks <= 65536, faster).  None: "zlib9" in
         # reference mode when every chunk size allows it, else "v1".
         if deflate not in (None, "v1", "zlib9"):
             raise ValueError("deflate must be None, 'v1' or 'zlib9'")

@@ -924,7 +924,11 @@ hipError_t launch_deflate(const EncArgs& a, hipStream_t s) {
     if (C <= 2048) return launch_deflate_t<2048>(a, s);
     if (C <= 4096) return launch_deflate_t<4096>(a, s);
     if (C <= 8192) return launch_deflate_t<8192>(a, s);
-    return launch_deflate_t<16384>(a, s);
+    if (C <= 16384) return launch_deflate_t<16384>(a, s);
+    // the reference's prefs allow id 5 up to 65536 (adaptive_compressor.py:119):
+    // 73 KB / 145 KB of LDS, 2 / 1 workgroups per CU
+    if (C <= 32768) return launch_deflate_t<32768>(a, s);
+    return launch_deflate_t<65536>(a, s);
 }
 
 }  // namespace ambc

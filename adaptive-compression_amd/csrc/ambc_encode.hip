@@ -728,7 +728,9 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         for (uint32_t i = lane; i < n; i += 64)
             slot[i] = i ? (uint8_t)(S.chunk[i] - S.chunk[i - 1]) : S.chunk[0];
     } else if (win == 255) {
-        const uint32_t nv = (n + 15) >> 4;
+        // in place: k_compact copies the chunk from the input (saves writing and
+        // re-reading a third of a mixed input's bytes through the slots)
+        const uint32_t nv = (A.flags & ENC_RAW_IN_PLACE) ? 0u : (n + 15) >> 4;
         for (uint32_t v = lane; v < nv; v += 64)
             reinterpret_cast<uint4*>(slot)[v] = reinterpret_cast<const uint4*>(S.chunk)[v];
     } else if (win == 1 && S.hist()[S.chunk[0]] == n) {
@@ -891,7 +893,7 @@ __device__ __forceinline__ void compact_package(const CompactArgs& A, uint32_t k
     const uint32_t type = A.ids[k];
     const uint64_t p0 = (uint64_t)k * A.chunk_size;
     const uint32_t n = A.clen ? A.clen[k] : (uint32_t)min((uint64_t)A.chunk_size, A.n_total - p0);
-    const uint8_t* __restrict__ sl = A.slots + (uint64_t)k * A.slot_stride;
+    const uint8_t* __restrict__ sl = type == 255 && A.in ? A.in + p0 : A.slots + (uint64_t)k * A.slot_stride;
     const uint64_t d0 = o >> 2, d1 = (o + P - 1) >> 2;
     uint32_t* __restrict__ out32 = reinterpret_cast<uint32_t*>(A.out);
     const uint32_t sh = (uint32_t)((0 - o - HDR) & 3u);   // payload byte offset inside a source dword

@@ -139,8 +139,6 @@ int ambc::check_params(const ambc_params* p) {
                              (1u << AMBC_M_DELTA) | (1u << AMBC_M_DEFLATE) | (1u << AMBC_M_LZ4);
     if (p->method_mask & ~allowed)
         return fail(AMBC_E_INVAL, "method_mask holds ids without a GPU encoder (allowed: 1, 2, 3, 4, 5, 9)");
-    if (((p->method_mask >> AMBC_M_DEFLATE) & 1) && C > 16384)
-        return fail(AMBC_E_INVAL, "the GPU DEFLATE encoder supports chunk_size <= 16384");
     if (((p->method_mask >> AMBC_M_DEFLATE) & 1) && (p->flags & AMBC_FLAG_ZLIB9) && z9_cmax(C) == 0)
         return fail(AMBC_E_INVAL, "the GPU zlib-9 encoder (AMBC_FLAG_ZLIB9) supports chunk_size <= 4096");
     if (((p->method_mask >> AMBC_M_DICT) & 1) && p->pref_min[AMBC_M_DICT] <= dict_cmax(p) &&
@@ -265,6 +263,9 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
     ea.ent_full = ef;
     ea.ent_tail = et;
     for (int i = 0; i < 16; i++) { ea.pref_min[i] = p->pref_min[i]; ea.pref_max[i] = p->pref_max[i]; }
+    // raw packages go from the input straight to the body (aligned inputs: k_compact's dword loads)
+    const bool raw_in_place = ((uintptr_t)d_in & 3) == 0 && !getenv("AMBC_RAW_VIA_SLOT");
+    if (raw_in_place) ea.flags |= ENC_RAW_IN_PLACE;
 
     TRACE("compress_on n=%llu M=%u C=%u", (unsigned long long)n, M, C);
     std::vector<unsigned long long> stamps;
@@ -360,6 +361,7 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
             ca.n_total = std::min<uint64_t>(n - (uint64_t)k0 * C, (uint64_t)(k1 - k0) * C);
             ca.chunk_size = C;
             ca.out = d_out;
+            ca.in = raw_in_place ? d_in + (uint64_t)k0 * C : nullptr;
             // beside the next segment's encoder the compaction runs as a resident
             // grid (per-package-group workgroups would wait behind the encoder's
             // queued workgroups for every dispatch); the last one runs alone
@@ -479,6 +481,7 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
     ca.n_total = n;
     ca.chunk_size = C;
     ca.out = d_out;
+    ca.in = raw_in_place ? d_in : nullptr;
     HIPCHK(launch_compact(ca, s));
     HIPCHK(hipEventRecord(d.ev[3], s));
     if (trace_on()) { HIPCHK(hipStreamSynchronize(s)); TRACE("compact done"); }
@@ -812,10 +815,12 @@ bool make_job(const uint8_t* body, uint64_t blen, uint64_t hp, uint32_t ord, con
     if (!registered_id(reg, t)) {
         j.type = DEC_VERBATIM;
         kind = DEC_KIND_LIGHT;
-    } else if (t == 5 && clen && orig <= 16384) {
-        // zlib payload: inflated on the GPU (host zlib if it decodes past the map)
+    } else if (t == 5 && clen && orig <= 32768) {
+        // zlib payload: inflated on the GPU (host zlib if it decodes past the map;
+        // the u16 source map indexes at most 32768 output bytes)
         j.type = 5;
-        kind = orig <= 4096 ? DEC_KIND_INFLATE_4K : orig <= 8192 ? DEC_KIND_INFLATE_8K : DEC_KIND_INFLATE_16K;
+        kind = orig <= 4096 ? DEC_KIND_INFLATE_4K : orig <= 8192 ? DEC_KIND_INFLATE_8K
+             : orig <= 16384 ? DEC_KIND_INFLATE_16K : DEC_KIND_INFLATE_32K;
     } else if (t == 5 || t == 6 || t == 7) {
         j.type = DEC_SKIP;
         kind = DEC_KIND_LIGHT;

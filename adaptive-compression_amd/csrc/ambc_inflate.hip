@@ -858,8 +858,10 @@ hipError_t launch_inflate(int kind, const DecArgs& a, hipStream_t s) {
         hipLaunchKernelGGL(k_decode_inflate<4096>, dim3(a.n_list), dim3(64), 0, s, a);
     else if (kind == DEC_KIND_INFLATE_8K)
         hipLaunchKernelGGL(k_decode_inflate<8192>, dim3(a.n_list), dim3(64), 0, s, a);
-    else
+    else if (kind == DEC_KIND_INFLATE_16K)
         hipLaunchKernelGGL(k_decode_inflate<16384>, dim3(a.n_list), dim3(64), 0, s, a);
+    else  // 64 KB source map + tables: 2 workgroups per CU
+        hipLaunchKernelGGL(k_decode_inflate<32768>, dim3(a.n_list), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 

@@ -11,6 +11,7 @@ constexpr uint32_t LZ4_HASH_BITS = 10;   // "ambc-lz4 greedy v2" hash width
 constexpr uint32_t ENC_FORCE = 1;    // CompressionMethod.compress(chunk) semantics
 constexpr uint32_t ENC_ANALYZE = 2;  // also evaluate every should_use
 constexpr uint32_t ENC_EMIT_PENDING = 4;  // emit only the chunks the first pass deferred and id 5 did not take
+constexpr uint32_t ENC_RAW_IN_PLACE = 8;  // raw (255) payloads are not copied to the slot: k_compact reads the input
 
 // per-chunk encode: one 64-lane workgroup per chunk
 struct EncArgs {
@@ -53,6 +54,7 @@ struct CompactArgs {
     uint64_t n_total;
     uint32_t chunk_size;
     uint8_t* out;
+    const uint8_t* in;       // optional (ENC_RAW_IN_PLACE): raw packages read from in + k * chunk_size
 };
 
 // one decode job per chunk package (built by the host header walk)
@@ -85,7 +87,7 @@ struct DecArgs {
 enum : int { DEC_KIND_LIGHT = 0, DEC_KIND_LZ4_4K = 1, DEC_KIND_LZ4_8K = 2, DEC_KIND_LZ4_16K = 3,
              DEC_KIND_LZ4_G = 4, DEC_KIND_INFLATE_4K = 5, DEC_KIND_INFLATE_8K = 6,
              DEC_KIND_INFLATE_16K = 7, DEC_KIND_HEAVY = 8, DEC_KIND_DICT_4K = 9, DEC_KIND_DICT_8K = 10,
-             DEC_KIND_DICT_16K = 11, DEC_KINDS = 12 };
+             DEC_KIND_DICT_16K = 11, DEC_KIND_INFLATE_32K = 12, DEC_KINDS = 13 };
 constexpr uint32_t DEC_PRODUCED_HOST = 0xFFFFFFFEu;  // k_decode_inflate: output too large, inflate on host
 
 constexpr uint32_t DEC_VERBATIM = 256;

@@ -47,14 +47,11 @@ bool any_eligible(const ambc_params* p, uint32_t s) {
     return false;
 }
 
-// the sizes the GPU encoders take (k_encode <= 65536, k_deflate <= 16384, k_dict <= 8192)
+// the sizes the GPU encoders take (k_encode <= 65536, k_deflate <= 65536, k_dict <= 8192)
 int check_size(const ambc_params* p, uint32_t s) {
     if (s > AMBC_MAX_CHUNK)
         return fail(AMBC_E_INVAL, "a candidate chunk of " + std::to_string(s) +
                                       " bytes with eligible methods: the GPU encoders take chunks up to 65536 bytes");
-    if (eligible(p, s, AMBC_M_DEFLATE) && s > 16384)
-        return fail(AMBC_E_INVAL, "a candidate chunk of " + std::to_string(s) +
-                                      " bytes with DEFLATE eligible: the GPU DEFLATE encoder takes chunks up to 16384 bytes");
     if (eligible(p, s, AMBC_M_DEFLATE) && (p->flags & AMBC_FLAG_ZLIB9) && z9_cmax(s) == 0)
         return fail(AMBC_E_INVAL, "a candidate chunk of " + std::to_string(s) +
                                       " bytes with DEFLATE eligible: the GPU zlib-9 encoder takes chunks up to 4096 bytes");

@@ -64,7 +64,8 @@ extern "C" {
 #define AMBC_M_DICT 2  /* GPU encoder k_dict: the reference's bytes; chunks <= 8192 */
 #define AMBC_M_HUFFMAN 3
 #define AMBC_M_DELTA 4 /* never selected: payload length == n (compression_methods.py:598-608) */
-#define AMBC_M_DEFLATE 5 /* GPU encoder "ambc-deflate v1" (chunk_size <= 16384); decode: host zlib */
+#define AMBC_M_DEFLATE 5 /* GPU encoder "ambc-deflate v1" (chunk_size <= 65536) or zlib-9 (AMBC_FLAG_ZLIB9,
+                           <= 4096); decode: GPU inflate (packages <= 32768), else host zlib */
 #define AMBC_M_LZ4 9
 #define AMBC_M_RAW 255
 
@@ -128,7 +129,7 @@ int ambc_compress_batch(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const ambc
  * ignored).  ent_sizes/ent_tabs: optional numpy-exact p*log2(p) tables for the
  * chunk sizes Huffman may take (see ambc_params.ent_full).  Writes the .ambc
  * body (packages + end chunk); AMBC_E_INVAL when a size the walk needs has an
- * eligible method the GPU encoders do not take at that size (DEFLATE > 16384,
+ * eligible method the GPU encoders do not take at that size (zlib-9 DEFLATE > 4096,
  * Dictionary > 8192, any > 65536), AMBC_E_RANGE for a raw remainder > 4 GiB. */
 int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const ambc_params* p,
                             const uint32_t* cands, uint32_t n_cands, const uint32_t* ent_sizes,

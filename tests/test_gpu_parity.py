@@ -448,7 +448,9 @@ def test_deflate_chunks_decode(ctx):
 # ---------------------------------------------------------------------------
 GD_CASES = [((1 << 20) + 77, 20250418, 4096, (1, 3, 4, 5, 9)), ((1 << 20) + 5, 3, 1024, (1, 3, 5)),
             (600000, 8, 8192, (5,)), (700001, 9, 16384, (1, 3, 4, 5, 9)), (300000, 10, 2048, (3, 5, 9)),
-            (250000, 12, 4096, (5, 9))]
+            (250000, 12, 4096, (5, 9)),
+            # the reference's prefs allow id 5 up to 65536 (adaptive_compressor.py:119)
+            (300007, 14, 32768, (1, 3, 4, 5, 9)), (400000, 15, 65536, (5, 9)), (200000, 16, 65536, (5,))]
 
 
 @pytest.mark.parametrize("n,seed,chunk,methods", GD_CASES)
@@ -530,6 +532,33 @@ def test_gpu_inflate_zlib_corpus(ctx):
     assert comp._adaptive_decompress(body, orig_total) == want
     st = comp._last_device_stats
     assert st.kernel_ns > 0
+
+
+def test_gpu_inflate_large_packages(ctx):
+    """id-5 packages of 16-32 KiB (k_decode_inflate<32768>, a 64 KB source map)
+    and of 64 KiB (host zlib): zlib levels 1/6/9, matches at distance 32768,
+    streams that decode past the package's orig, a truncated one."""
+    import zlib
+    mixed = synth.generate(1 << 20, 43)
+    blk = synth.random_bytes(2000, 44)
+    far = blk + synth.random_bytes(30768, 45) + blk
+    payloads = []
+    for lvl in (1, 6, 9):
+        for o, n in ((0, 32768), (100000, 20000), (300000, 16385), (500000, 65536)):
+            payloads.append((zlib.compress(mixed[o:o + n], lvl), n))
+        payloads.append((zlib.compress(far, lvl), len(far)))
+    payloads.append((zlib.compress(bytes(40000), 9), 32768))         # decodes past the package
+    good = zlib.compress(mixed[700000:730000], 9)
+    payloads.append((good[:len(good) // 2], 30000))                  # unfinished stream
+    parts, orig_total = [], 0
+    for z, n in payloads:
+        parts.append(_chunk(5, z, n))
+        orig_total += n
+    body = b"".join(parts) + b"\xff\xff\x00\x00\x00\x00" + bytes(10)
+    want = orc.decompress_body(body, orig_total)
+    comp = _compressor()
+    assert comp._adaptive_decompress(body, orig_total) == want
+    assert want[:32768] == mixed[:32768]
 
 
 class _Bits:
@@ -651,7 +680,9 @@ def _zero_then_random():
 @pytest.mark.parametrize("methods,cands", [((1, 3, 4), REF_CANDS), ((1, 3, 4, 9), REF_CANDS),
                                            ((1, 2, 3, 4), REF_CANDS),           # Dictionary: <= 8192 by prefs
                                            ((1, 2, 3, 4, 9), REF_CANDS),
-                                           ((1, 3, 4, 5), [16384, 8192, 4096, 2048, 1024])])
+                                           ((1, 3, 4, 5), [16384, 8192, 4096, 2048, 1024]),
+                                           ((1, 3, 4, 5), REF_CANDS),           # DEFLATE up to 65536
+                                           ((1, 2, 3, 4, 5, 9), REF_CANDS)])
 def test_multisize_walk_matches_oracle(ctx, methods, cands):
     inputs = [synth.generate(12288, 3), synth.generate(65536, 21), synth.generate(200000, 22),
               _zero_then_random(), bytes(7)]
@@ -699,10 +730,33 @@ def test_multisize_many_walks_match_oracle(ctx):
 
 
 def test_multisize_rejects_oversize_gpu_chunks(ctx):
-    comp = _compressor(methods=(1, 3, 4, 5))
+    # the zlib-9 encoder's walkers keep their tables in LDS: chunks <= 4096
+    comp = _compressor(methods=(1, 3, 4, 5), deflate="zlib9")
     comp.CHUNK_SIZE_CANDIDATES = list(REF_CANDS)
     with pytest.raises(NotImplementedError):
         comp._adaptive_compress(synth.generate(100000, 5))
+
+
+def test_gdeflate_large_chunks_edge(ctx):
+    """k_deflate<32768> / <65536>: distances at the 32768 window limit (a block
+    repeated 32768 and 32769 bytes later), 258-splits over a 64 KiB zero chunk,
+    positions past 65280 in the u16 hash table, one-symbol chunks."""
+    import zlib
+    blk = synth.random_bytes(3000, 77)
+    edge = [bytes(65536), b"xy" * 32768, blk + synth.random_bytes(29768, 78) + blk + b"!" + blk,
+            synth.random_bytes(60000, 79) + synth.generate(5536, 80) + synth.generate(40000, 81),
+            synth.generate(65536, 82)[:65000] + bytes(536), b"\x05" * 40000]
+    for d in edge:
+        for chunk in (32768, 65536):
+            comp = _compressor(chunk_size=chunk, methods=(5, 9))
+            body = comp._adaptive_compress(d)
+            ref, _ = orc.compress_body(d, orc.make_params(chunk, "native", (5, 9), n_total=len(d),
+                                                           deflate="gd"), nthreads=0)
+            assert body == ref, (len(d), chunk)
+            assert comp._adaptive_decompress(body, len(d)) == d
+            if body[4] == 5:
+                clen = int.from_bytes(body[14:18], "little")
+                assert zlib.decompress(body[18:18 + clen]) == d[:min(chunk, len(d))]
 
 
 def _pkg(t, orig, payload):
