@@ -2,6 +2,7 @@
 GPU (ambc_compress_multisize) and check the body against the oracle's walk.
 
     python scripts/multisize_bench.py [MiB ...]      (default: 32 256)
+    MS_SETS="mixed:1,3,4,5;mixed:1,2,3,4,5,9" python scripts/multisize_bench.py 32
 
 Input: runs, text-like bytes and skewed random bytes in 8-64 KiB segments, so
 every position compresses and the walk never ends in the remainder-raw rule."""
@@ -43,7 +44,11 @@ def text(n, seed):
 
 def main():
     sizes = [float(x) for x in sys.argv[1:]] or [32, 256]
-    for kind, methods in (("mixed", (1, 3, 4, 9)), ("mixed", (1, 2, 3, 4)), ("text", (1, 3, 4, 9))):
+    sets = (("mixed", (1, 3, 4, 9)), ("mixed", (1, 2, 3, 4)), ("text", (1, 3, 4, 9)))
+    if os.environ.get("MS_SETS"):
+        sets = [(k, tuple(int(x) for x in m.split(","))) for k, m in
+                (e.split(":") for e in os.environ["MS_SETS"].split(";"))]
+    for kind, methods in sets:
         for mib in sizes:
             data = (mixed if kind == "mixed" else text)(int(mib * (1 << 20)), 7)
             comp = ambc.AdaptiveCompressor(methods=methods)
