@@ -89,7 +89,7 @@ class AdaptiveCompressor:
         self.mode = mode
         # id 5's GPU encoder: "zlib9" (zlib.compress(data, 9)'s own bytes -- the
         # reference's DeflateCompression, advanced_compression.py:76-81 -- chunks
-        # <= 4096) or "v1" ("ambc-deflate v1": valid zlib streams of this
+        # <= 8192) or "v1" ("ambc-deflate v1": valid zlib streams of this
         # engine's own parse, chunks <= 65536, faster).  None: "zlib9" in
         # reference mode when every chunk size allows it, else "v1".
         if deflate not in (None, "v1", "zlib9"):
@@ -114,7 +114,7 @@ class AdaptiveCompressor:
     def deflate(self):
         if self._deflate is not None:
             return self._deflate
-        if self.mode == "reference" and max(int(c) for c in self.CHUNK_SIZE_CANDIDATES) <= 4096:
+        if self.mode == "reference" and max(int(c) for c in self.CHUNK_SIZE_CANDIDATES) <= 8192:
             return "zlib9"
         return "v1"
 

@@ -118,14 +118,19 @@ __device__ __forceinline__ void put_bits_plain(uint32_t* words, uint32_t b, uint
 
 template <int CMAX>
 struct GdSmem {
-    // parse: last[] (4 KB) + 64 bucket masks (512 B); trees: 5 KB; emit: bit staging
-    static constexpr int REGION = (CMAX > 5120 ? CMAX : 5120) + 64;
+    // parse: last[] (4 KB) + 64 bucket masks (512 B); trees: 5 KB; emit: bit staging.
+    // Chunks of 16 KiB and more stage their bits over the chunk itself (the
+    // emission then reads literals from the input) and keep the match-start
+    // masks in device scratch: 74 / 41 KB at 64 / 32 KiB, 2 / 3 workgroups per
+    // CU (1 / 1 with LDS staging)
+    static constexpr bool BIG = CMAX >= 16384;
+    static constexpr int REGION = (CMAX > 5120 && !BIG ? CMAX : 5120) + 64;
     static constexpr int ROUNDS = (CMAX + 63) / 64;
     alignas(16) uint8_t chunk[CMAX + 64];  // zero padded
     // parse: last[] (u16 x 2048) | trees: sorted/weights/parents | emit: bit staging
     alignas(16) uint32_t region[REGION / 4];
-    uint64_t sel[ROUNDS];                  // match-start positions, per 64-position round
-    uint16_t sbase[ROUNDS + 1];            // first match index of every round
+    uint64_t sel[BIG ? 1 : ROUNDS];        // match-start positions, per 64-position round
+                                           // (BIG: in the chunk's device scratch, gd_seq_bytes)
     uint32_t lf[288], df[32], cf[20];      // symbol frequencies
     uint8_t ll[288], dl[32], cl[20];       // code lengths
     uint16_t lc[288], dc[32], cc[20];      // bit-reversed canonical codes
@@ -427,7 +432,9 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     // the parse's matches, in order, as (position | length << 16 | distance << 32)
     // in the chunk's window of the device scratch A.gdseq (2 CMAX bytes: at most
     // n/4 matches)
-    uint64_t* seq = reinterpret_cast<uint64_t*>(A.gdseq + (uint64_t)k * 2 * CMAX);
+    uint8_t* const scr = A.gdseq + (uint64_t)k * gd_seq_bytes(CMAX);
+    uint64_t* seq = reinterpret_cast<uint64_t*>(scr);
+    uint64_t* const selp = GdSmem<CMAX>::BIG ? reinterpret_cast<uint64_t*>(scr + 2 * CMAX) : S.sel;
     uint32_t mcov = 0;  // bytes the matches cover
     unsigned long long* bk = reinterpret_cast<unsigned long long*>(S.region + 1024);  // after last[]
     uint32_t ns = 0;
@@ -438,17 +445,16 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
         // one byte value: the greedy parse is a literal at 0, then distance-1
         // matches of min(258, n - p) at p = 1 + 258 j while p + 4 <= n
         const uint32_t M = n >= 5 ? (n - 5) / 258 + 1 : 0;
+        // (258 > 64: at most one match start per round)
         for (uint32_t r = lane; r < (n + 63) / 64; r += 64) {
-            S.sel[r] = 0;
-            S.sbase[r] = (uint16_t)(64 * r <= 1 ? 0u : min(M, (64 * r - 2) / 258 + 1));
+            const uint32_t p0 = 64 * r, j = p0 <= 1 ? 0u : (p0 - 1 + 257) / 258, pj = 1 + 258 * j;
+            selp[r] = j < M && pj < p0 + 64 ? 1ull << (pj - p0) : 0ull;
         }
-        wave_sync();
         for (uint32_t j = lane; j < M; j += 64) {
             const uint32_t pj = 1 + 258 * j;
             const uint32_t Lj = min(258u, n - pj);
             seq[j] = pj | (uint64_t)Lj << 16 | 1ull << 32;
             mcov += Lj;
-            atomicOr(&S.sel[pj >> 6], 1ull << (pj & 63));
         }
         ns = M;
         mcov = wave_sum_u32(mcov);
@@ -614,7 +620,7 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
             mcov += wave_sum_u32(st ? L : 0u);
         }
         ns = ns0 + (uint32_t)__popcll(selm);
-        if (lane == 0) { S.sel[r] = selm; S.sbase[r] = (uint16_t)ns0; }
+        if (lane == 0) selp[r] = selm;
     }
     }
     const uint32_t nrounds = (n + 63) / 64;
@@ -758,6 +764,23 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     const uint32_t total = 2 + body + 4;
     if (kind == 0 || total + 18 >= T) GRET;  // a stored block never beats raw
 
+    // ---- Adler-32 of the chunk (before a BIG chunk's bits overwrite it) ----
+    uint32_t adler;
+    {
+        uint64_t asum = 0, bsum = 0;
+        for (uint32_t i = lane; i < n; i += 64) {
+            const uint32_t c = S.chunk[i];
+            asum += c;
+            bsum += (uint64_t)(n - i) * c;
+        }
+        asum = wave_sum<uint64_t>(asum);
+        bsum = wave_sum<uint64_t>(bsum);
+        adler = (uint32_t)(((n + bsum) % 65521) << 16 | ((1 + asum) % 65521));
+    }
+    // literal bytes during the emission: LDS, or the input (L2) for BIG chunks
+    constexpr bool BIG = GdSmem<CMAX>::BIG;
+    auto chb = [&](uint32_t q) -> uint32_t { return BIG ? (uint32_t)src[q] : (uint32_t)S.chunk[q]; };
+
     // ---- emission (this chunk's winner) ----
     if (kind == 1) {  // fixed tables
         for (uint32_t s = lane; s < 288; s += 64) S.ll[s] = s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : 8;
@@ -770,7 +793,7 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
         gd_codes<30>(S.dl, S.dc, S.blc, lane);
         gd_codes<19>(S.cl, S.cc, S.blc, lane);
     }
-    uint32_t* bits = S.region;
+    uint32_t* bits = BIG ? reinterpret_cast<uint32_t*>(S.chunk) : S.region;
     const uint32_t nwords = (body + 8) / 4 + 1;
     for (uint32_t i = lane; i < nwords; i += 64) bits[i] = 0;
     wave_sync();
@@ -810,7 +833,7 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
             if (lane == 0) pe = pe_carry;
             uint32_t cost = 0, lcd = 0, dcd = 0;
             if (has)
-                for (uint32_t q = pe; q < pos; q++) cost += S.ll[S.chunk[q]];
+                for (uint32_t q = pe; q < pos; q++) cost += S.ll[chb(q)];
             if (mt) {
                 lcd = gd_lcode(Lx);
                 dcd = gd_dcode(Dx);
@@ -820,7 +843,7 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
             uint32_t b = bp + incl - cost;
             if (has) {
                 for (uint32_t q = pe; q < pos; q++) {
-                    const uint32_t c = S.chunk[q];
+                    const uint32_t c = chb(q);
                     put_bits_atomic(bits, b, S.lc[c], S.ll[c]);
                     b += S.ll[c];
                 }
@@ -837,17 +860,20 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     } else {
         // position-major (literal-heavy chunks)
         int carry = 0;
+        uint32_t sb = 0;   // matches before this round
         const uint64_t lt = (1ull << lane) - 1;
 #pragma unroll 1
         for (uint32_t r = 0; r < nrounds; r++) {
             const uint32_t i = r * 64 + lane;
-            const uint64_t sm = S.sel[r];
+            const uint64_t sv = selp[r];
+            const uint64_t sm = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)sv) |
+                                (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(sv >> 32)) << 32;
             if (!sm && carry >= (int)(r * 64 + 64)) continue;  // inside one match
             const bool st = (sm >> lane) & 1;
             int e = 0;
             uint32_t Lx = 0, Dx = 0, lcd = 0, dcd = 0, cost = 0;
             if (st) {
-                const uint32_t si = S.sbase[r] + (uint32_t)__popcll(sm & lt);
+                const uint32_t si = sb + (uint32_t)__popcll(sm & lt);
                 const uint64_t sq = seq[si];
                 Lx = (uint32_t)(sq >> 16) & 0xFFFF;
                 Dx = (uint32_t)(sq >> 32);
@@ -859,7 +885,7 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
             const int E = max(carry, wave_incl_max_i32(e));
             carry = max(carry, wave_max_i32(e));
             const bool lit = i < n && E <= (int)i;
-            const uint32_t c = lit ? S.chunk[i] : 0u;
+            const uint32_t c = lit ? chb(i) : 0u;
             if (lit) cost = S.ll[c];
             const uint32_t incl = wave_incl_sum(cost);
             uint32_t b = bp + incl - cost;
@@ -872,24 +898,12 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
                 put_bits_atomic(bits, b, S.dc[dcd] | (Dx - c_dbase[dcd]) << l2, l2 + c_dext[dcd]);
             }
             bp += readlane(incl, 63);
+            sb += (uint32_t)__popcll(sm);
         }
     }
     wave_sync();
     if (lane == 0) put_bits_plain(bits, bp, S.lc[256], S.ll[256]);
     wave_sync();
-    // ---- Adler-32 of the chunk ----
-    uint32_t adler;
-    {
-        uint64_t asum = 0, bsum = 0;
-        for (uint32_t i = lane; i < n; i += 64) {
-            const uint32_t c = S.chunk[i];
-            asum += c;
-            bsum += (uint64_t)(n - i) * c;
-        }
-        asum = wave_sum<uint64_t>(asum);
-        bsum = wave_sum<uint64_t>(bsum);
-        adler = (uint32_t)(((n + bsum) % 65521) << 16 | ((1 + asum) % 65521));
-    }
     // ---- the zlib stream into the slot ----
     const uint8_t* bb = reinterpret_cast<const uint8_t*>(bits);
     for (uint32_t i = lane; i < total; i += 64) {

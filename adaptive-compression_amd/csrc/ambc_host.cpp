@@ -140,7 +140,7 @@ int ambc::check_params(const ambc_params* p) {
     if (p->method_mask & ~allowed)
         return fail(AMBC_E_INVAL, "method_mask holds ids without a GPU encoder (allowed: 1, 2, 3, 4, 5, 9)");
     if (((p->method_mask >> AMBC_M_DEFLATE) & 1) && (p->flags & AMBC_FLAG_ZLIB9) && z9_cmax(C) == 0)
-        return fail(AMBC_E_INVAL, "the GPU zlib-9 encoder (AMBC_FLAG_ZLIB9) supports chunk_size <= 4096");
+        return fail(AMBC_E_INVAL, "the GPU zlib-9 encoder (AMBC_FLAG_ZLIB9) supports chunk_size <= 8192");
     if (((p->method_mask >> AMBC_M_DICT) & 1) && p->pref_min[AMBC_M_DICT] <= dict_cmax(p) &&
         dict_cmax(p) > 8192)
         return fail(AMBC_E_INVAL, "the GPU Dictionary encoder takes chunks <= 8192 bytes "
@@ -281,7 +281,7 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
     if (deflate) {
         HIPCHK(d.bestpre.ensure((size_t)std::max<uint32_t>(M, 1) * 4));
         ea.bestpre = d.bestpre.as<uint32_t>();
-        HIPCHK(d.gdseq.ensure((size_t)std::max<uint32_t>(M, 1) * 2 * gd_cmax));
+        HIPCHK(d.gdseq.ensure((size_t)std::max<uint32_t>(M, 1) * gd_seq_bytes(gd_cmax)));
         ea.gdseq = d.gdseq.as<uint8_t>();
         HIPCHK(d.pending.ensure((size_t)std::max<uint32_t>(M, 1)));
         ea.pending = d.pending.as<uint8_t>();
@@ -303,7 +303,7 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
         e.sizes += k0;
         if (e.bestpre) e.bestpre += k0;
         if (e.pending) e.pending += k0;
-        if (e.gdseq) e.gdseq += (uint64_t)k0 * 2 * gd_cmax;
+        if (e.gdseq) e.gdseq += (uint64_t)k0 * gd_seq_bytes(gd_cmax);
         if (e.z9rec) e.z9rec += (uint64_t)k0 * z9_rec_words(z9_cmax(C));
         return e;
     };

@@ -13,6 +13,10 @@ constexpr uint32_t ENC_ANALYZE = 2;  // also evaluate every should_use
 constexpr uint32_t ENC_EMIT_PENDING = 4;  // emit only the chunks the first pass deferred and id 5 did not take
 constexpr uint32_t ENC_RAW_IN_PLACE = 8;  // raw (255) payloads are not copied to the slot: k_compact reads the input
 
+// k_deflate's per-chunk device scratch: the parse's matches (2 cmax bytes), then
+// for chunks above 16 KiB the match-start masks (cmax / 8 bytes)
+constexpr uint64_t gd_seq_bytes(uint32_t cmax) { return 2ull * cmax + cmax / 8; }
+
 // per-chunk encode: one 64-lane workgroup per chunk
 struct EncArgs {
     const uint8_t* in;       // device input

@@ -54,7 +54,7 @@ int check_size(const ambc_params* p, uint32_t s) {
                                       " bytes with eligible methods: the GPU encoders take chunks up to 65536 bytes");
     if (eligible(p, s, AMBC_M_DEFLATE) && (p->flags & AMBC_FLAG_ZLIB9) && z9_cmax(s) == 0)
         return fail(AMBC_E_INVAL, "a candidate chunk of " + std::to_string(s) +
-                                      " bytes with DEFLATE eligible: the GPU zlib-9 encoder takes chunks up to 4096 bytes");
+                                      " bytes with DEFLATE eligible: the GPU zlib-9 encoder takes chunks up to 8192 bytes");
     if (eligible(p, s, AMBC_M_DICT) && s > 8192)
         return fail(AMBC_E_INVAL, "a candidate chunk of " + std::to_string(s) +
                                       " bytes with Dictionary eligible: the GPU Dictionary encoder takes chunks up to 8192 bytes");
@@ -107,7 +107,7 @@ int launch_batch(Batch& b, hipStream_t st, const uint8_t* d_in, uint64_t n, cons
     while (gd_cmax < C) gd_cmax <<= 1;
     if (deflate) {
         HIPCHK(b.bestpre.ensure((size_t)cnt * 4));
-        HIPCHK(b.gdseq.ensure((size_t)cnt * 2 * gd_cmax));
+        HIPCHK(b.gdseq.ensure((size_t)cnt * gd_seq_bytes(gd_cmax)));
         HIPCHK(b.pending.ensure((size_t)cnt));
         ea.bestpre = b.bestpre.as<uint32_t>();
         ea.gdseq = b.gdseq.as<uint8_t>();

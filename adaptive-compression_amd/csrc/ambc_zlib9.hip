@@ -1286,7 +1286,7 @@ hipError_t launch_z9_t(const EncArgs& a, hipStream_t s) {
 }  // namespace
 
 uint32_t z9_cmax(uint32_t chunk) {
-    return chunk <= 1024 ? 1024u : chunk <= 2048 ? 2048u : chunk <= 4096 ? 4096u : 0u;
+    return chunk <= 1024 ? 1024u : chunk <= 2048 ? 2048u : chunk <= 4096 ? 4096u : chunk <= 8192 ? 8192u : 0u;
 }
 
 size_t z9_rec_words(uint32_t cmax) {
@@ -1294,6 +1294,7 @@ size_t z9_rec_words(uint32_t cmax) {
         case 1024: return Z9Rec<1024>::STRIDE;
         case 2048: return Z9Rec<2048>::STRIDE;
         case 4096: return Z9Rec<4096>::STRIDE;
+        case 8192: return Z9Rec<8192>::STRIDE;
         default: return 0;
     }
 }
@@ -1304,6 +1305,7 @@ hipError_t launch_zlib9(const EncArgs& a, hipStream_t s) {
         case 1024: return launch_z9_t<1024>(a, s);
         case 2048: return launch_z9_t<2048>(a, s);
         case 4096: return launch_z9_t<4096>(a, s);
+        case 8192: return launch_z9_t<8192>(a, s);
         default: return hipErrorInvalidValue;
     }
 }

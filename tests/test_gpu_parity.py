@@ -71,8 +71,8 @@ def test_golden_files_bit_exact(ctx):
             continue
         ms = set(rec["methods"])
         # id 5 is zlib.compress(data, 9) in the reference: the zlib-9 GPU encoder
-        # (chunks <= 4096) reproduces those packages byte for byte
-        z9 = 5 in ms and rec["chunk"] <= 4096
+        # (chunks <= 8192) reproduces those packages byte for byte
+        z9 = 5 in ms and rec["chunk"] <= 8192
         if ms - {1, 3, 4, 9, 255} - ({5} if z9 else set()):
             continue
         data = synth.generate(rec["size"], rec["seed"])
@@ -460,8 +460,8 @@ def test_gdeflate_bodies_match_oracle(ctx, n, seed, chunk, methods):
     for mode in ("native", "reference"):
         comp = _compressor(chunk_size=chunk, mode=mode, methods=methods)
         body = comp._adaptive_compress(data)
-        # reference mode at chunks <= 4096 defaults to zlib-9's own bytes
-        z9 = mode == "reference" and chunk <= 4096
+        # reference mode at chunks <= 8192 defaults to zlib-9's own bytes
+        z9 = mode == "reference" and chunk <= 8192
         assert comp.deflate == ("zlib9" if z9 else "v1")
         p = orc.make_params(chunk, mode, methods, n_total=n, deflate="zlib" if z9 else "gd")
         ref, st = orc.compress_body(data, p, nthreads=0)

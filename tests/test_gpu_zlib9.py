@@ -60,7 +60,10 @@ def _check(data, chunk, methods, modes=("native", "reference")):
 
 Z9_CASES = [((1 << 20) + 77, 20250418, 4096, (1, 3, 4, 5, 9)), ((1 << 20) + 5, 3, 1024, (1, 3, 5)),
             (600001, 8, 4096, (5,)), (300000, 10, 2048, (3, 5, 9)), (250000, 12, 4096, (1, 2, 3, 4, 5)),
-            (123457, 13, 1008, (5,)), (200000, 14, 4000, (1, 3, 4, 5))]
+            (123457, 13, 1008, (5,)), (200000, 14, 4000, (1, 3, 4, 5)),
+            # 8 KiB chunks: distances past TOO_FAR (4096), chains of 8192 positions
+            (600000, 21, 8192, (1, 3, 4, 5, 9)), (300001, 22, 8192, (5,)), (250000, 23, 8192, (1, 2, 3, 4, 5)),
+            (123456, 24, 6000, (1, 3, 5))]
 
 
 @pytest.mark.parametrize("n,seed,chunk,methods", Z9_CASES)
@@ -71,6 +74,13 @@ def test_zlib9_bodies_match_zlib(ctx, n, seed, chunk, methods):
 def _biased(n, p, seed):
     rng = random.Random(seed)
     return bytes(97 if rng.random() < p else 98 for _ in range(n))
+
+
+def _alphabet(n, k, seed):
+    """k random symbols: many length-3 matches, some only further back than TOO_FAR"""
+    rng = random.Random(seed)
+    sym = bytes(rng.sample(range(256), k))
+    return bytes(rng.choice(sym) for _ in range(n))
 
 
 def _words(n, seed, vocab=40):
@@ -91,10 +101,11 @@ def test_zlib9_edge_chunks(ctx):
             b"\x07" * 5000 + bytes(range(256)) * 8, synth.random_bytes(12000, 4) + bytes(3000) + b"xyz" * 2000,
             b"q" * 4159, _biased(16384, 0.9, 1), _biased(16384, 0.97, 2), _biased(12288, 0.8, 3),
             _words(20000, 5), _words(16384, 6, vocab=6), synth.random_bytes(8193, 9),
-            bytes(range(256)) * 4 + synth.random_bytes(3000, 10) + bytes(range(256)) * 4]
+            bytes(range(256)) * 4 + synth.random_bytes(3000, 10) + bytes(range(256)) * 4,
+            _alphabet(16384, 24, 11), _alphabet(8192, 40, 12), _alphabet(12000, 64, 13)]
     seen = 0
     for d in edge:
-        for chunk in (1024, 4096):
+        for chunk in (1024, 4096, 8192):
             seen += _check(d, chunk, (1, 3, 5, 9), modes=("native",))
     assert seen > 20
 
@@ -115,11 +126,11 @@ def test_zlib9_random_small_chunks(ctx):
         else:
             parts.append(bytes([rng.randrange(4)]) * rng.randint(1, 300) + _words(m, i, vocab=5))
     data = b"".join(parts)
-    for chunk in (1024, 2048, 4096):
+    for chunk in (1024, 2048, 4096, 8192):
         assert _check(data, chunk, (5,), modes=("native",)) > 0
 
 
 def test_zlib9_rejects_large_chunks(ctx):
     from ambc import _lib
     with pytest.raises(_lib.AmbcError):
-        _comp(chunk_size=8192, methods=(5,))._adaptive_compress(synth.generate(100000, 1))
+        _comp(chunk_size=16384, methods=(5,))._adaptive_compress(synth.generate(100000, 1))
