@@ -1187,7 +1187,8 @@ hipError_t launch_decode(int kind, const DecArgs& a, hipStream_t s) {
     case DEC_KIND_INFLATE_4K:
     case DEC_KIND_INFLATE_8K:
     case DEC_KIND_INFLATE_16K:
-    case DEC_KIND_INFLATE_32K: return launch_inflate(kind, a, s);
+    case DEC_KIND_INFLATE_32K:
+    case DEC_KIND_INFLATE_G: return launch_inflate(kind, a, s);
     default: hipLaunchKernelGGL(k_decode, dim3(a.n_list), dim3(64), 0, s, a); break;
     }
     return hipGetLastError();

@@ -815,12 +815,17 @@ bool make_job(const uint8_t* body, uint64_t blen, uint64_t hp, uint32_t ord, con
     if (!registered_id(reg, t)) {
         j.type = DEC_VERBATIM;
         kind = DEC_KIND_LIGHT;
-    } else if (t == 5 && clen && orig <= 32768) {
+    } else if (t == 5 && clen && orig <= AMBC_MAX_CHUNK) {
         // zlib payload: inflated on the GPU (host zlib if it decodes past the map;
-        // the u16 source map indexes at most 32768 output bytes)
+        // the LDS map of u16 entries indexes at most 32768 output bytes, larger
+        // packages keep a u32 map of orig entries in device scratch)
         j.type = 5;
         kind = orig <= 4096 ? DEC_KIND_INFLATE_4K : orig <= 8192 ? DEC_KIND_INFLATE_8K
-             : orig <= 16384 ? DEC_KIND_INFLATE_16K : DEC_KIND_INFLATE_32K;
+             : orig <= 16384 ? DEC_KIND_INFLATE_16K : orig <= 32768 ? DEC_KIND_INFLATE_32K : DEC_KIND_INFLATE_G;
+        if (kind == DEC_KIND_INFLATE_G) {
+            j.scratch_cap = orig;
+            sneed = (4ull * orig + 15) & ~15ull;
+        }
     } else if (t == 5 || t == 6 || t == 7) {
         j.type = DEC_SKIP;
         kind = DEC_KIND_LIGHT;

@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "ambc_internal.h"
 #include "ambc_wave.h"
 
@@ -47,9 +49,23 @@ constexpr uint16_t LUT_LONG = 2;
 
 __constant__ uint8_t c_clord2[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
+// packages above 32 KiB (OUTMAX 65536): the map lives in the job's device
+// scratch window with u32 entries (bit 31 = literal), its capacity the job's orig
+template <uint32_t OUTMAX> using inf_map_t = typename std::conditional<(OUTMAX > 32768), uint32_t, uint16_t>::type;
+template <uint32_t OUTMAX> constexpr uint32_t inf_lit = OUTMAX > 32768 ? 0x80000000u : IN_LIT;
+
 template <uint32_t OUTMAX>
 struct InfSmem {
-    uint16_t src[OUTMAX];             // output source map
+    static constexpr bool G = OUTMAX > 32768;
+    inf_map_t<OUTMAX> srcl[G ? 1 : OUTMAX];   // output source map (LDS)
+    inf_map_t<OUTMAX>* srcg;                  // G: the map in device scratch
+    uint32_t capg;                            // G: its entries
+    __device__ __forceinline__ inf_map_t<OUTMAX>* src() {
+        if constexpr (G) return srcg; else return srcl;
+    }
+    __device__ __forceinline__ uint32_t cap() const {
+        if constexpr (G) return capg; else return OUTMAX;
+    }
     uint16_t lut[2][1 << LUTB];       // [0] literal/length (or code lengths), [1] distance
     uint16_t sorted[2][288];          // symbols in canonical (length, symbol) order
     uint16_t first[2][16], cnt[2][16], offs[2][16];
@@ -300,8 +316,8 @@ __device__ int inf_item_serial(InfSmem<OUTMAX>& S, InBits& I, uint32_t& op, uint
     const int sy = inf_sym(S, 0, I);
     if (sy < 0) return -1;
     if (sy < 256) {
-        if (op >= OUTMAX) return -2;
-        if (lane == 0) S.src[op] = (uint16_t)(IN_LIT | (uint32_t)sy);
+        if (op >= S.cap()) return -2;
+        if (lane == 0) S.src()[op] = (inf_map_t<OUTMAX>)(inf_lit<OUTMAX> | (uint32_t)sy);
         op++;
         return 0;
     }
@@ -331,19 +347,19 @@ __device__ int inf_item_serial(InfSmem<OUTMAX>& S, InBits& I, uint32_t& op, uint
         D = base + x;
     }
     if (D > op) return -1;  // invalid distance too far back
-    if (op + L > OUTMAX) return -2;
+    if (op + L > S.cap()) return -2;
     // entries point into the period before the match (chains stay short)
     const uint32_t m0 = op - D;
     if (D >= L) {
         for (uint32_t b = 0; b < L; b += 64)
-            if (b + lane < L) S.src[op + b + lane] = (uint16_t)(m0 + b + lane);
+            if (b + lane < L) S.src()[op + b + lane] = (inf_map_t<OUTMAX>)(m0 + b + lane);
     } else {
         const uint32_t lmod = lane % D;
         uint32_t bmod = 0;
         for (uint32_t b = 0; b < L; b += 64) {
             uint32_t c = bmod + lmod;
             if (c >= D) c -= D;
-            if (b + lane < L) S.src[op + b + lane] = (uint16_t)(m0 + c);
+            if (b + lane < L) S.src()[op + b + lane] = (inf_map_t<OUTMAX>)(m0 + c);
             bmod = (bmod + 64) % D;
         }
     }
@@ -504,7 +520,7 @@ __device__ int inflate_block_par(InfSmem<OUTMAX>& S, InBits& I, const uint8_t* g
                 bad |= dd[q] > ko[q];
                 lng |= ln[q] > INF_SHORT;
             }
-            if (me && ol) big |= ko[q] + ol > OUTMAX;
+            if (me && ol) big |= ko[q] + ol > S.cap();
         }
         if (__any(bad)) return -1;
         if (__any(big)) return -2;
@@ -513,12 +529,12 @@ __device__ int inflate_block_par(InfSmem<OUTMAX>& S, InBits& I, const uint8_t* g
         for (int q = 0; q < 4; q++) {
             if (!((mk[q] >> lane) & 1)) continue;
             if (kd[q] == IK_LIT) {
-                S.src[ko[q]] = (uint16_t)(IN_LIT | vl[q]);
+                S.src()[ko[q]] = (inf_map_t<OUTMAX>)(inf_lit<OUTMAX> | vl[q]);
             } else if (kd[q] == IK_MATCH && ln[q] <= INF_SHORT) {
                 const uint32_t m0 = ko[q] - dd[q];
                 uint32_t c = 0;
                 for (uint32_t t = 0; t < ln[q]; t++) {
-                    S.src[ko[q] + t] = (uint16_t)(m0 + c);
+                    S.src()[ko[q] + t] = (inf_map_t<OUTMAX>)(m0 + c);
                     if (++c == dd[q]) c = 0;
                 }
             }
@@ -534,14 +550,14 @@ __device__ int inflate_block_par(InfSmem<OUTMAX>& S, InBits& I, const uint8_t* g
                 if (Lm <= INF_SHORT) continue;
                 const uint32_t O = readlane(ko[q], l), Dm = readlane(dd[q], l), m0 = O - Dm;
                 if (Dm >= Lm) {   // no overlap: the entries run along the source
-                    for (uint32_t b = lane; b < Lm; b += 64) S.src[O + b] = (uint16_t)(m0 + b);
+                    for (uint32_t b = lane; b < Lm; b += 64) S.src()[O + b] = (inf_map_t<OUTMAX>)(m0 + b);
                 } else {          // the period before the match: m0 + t mod D (rcp estimate, fixed up)
                     const float rd = __builtin_amdgcn_rcpf((float)Dm);
                     for (uint32_t b = lane; b < Lm; b += 64) {
                         int r = (int)b - (int)((float)b * rd) * (int)Dm;
                         r += r < 0 ? (int)Dm : 0;
                         r -= r >= (int)Dm ? (int)Dm : 0;
-                        S.src[O + b] = (uint16_t)(m0 + (uint32_t)r);
+                        S.src()[O + b] = (inf_map_t<OUTMAX>)(m0 + (uint32_t)r);
                     }
                 }
             }
@@ -704,18 +720,18 @@ __device__ int64_t inflate_stream(InfSmem<OUTMAX>& S, const uint8_t* g, uint32_t
             uint32_t ln, nl;
             if (!in_take(I, 16, ln) || !in_take(I, 16, nl)) return -1;
             if (ln != (~nl & 0xFFFF)) return -1;
-            if (op + ln > OUTMAX) return -2;
+            if (op + ln > S.cap()) return -2;
             // the buffered bytes first, then straight from the payload
             uint32_t k = 0;
             while (k < ln && I.cnt >= 8) {
-                if (lane == 0) S.src[op + k] = (uint16_t)(IN_LIT | (I.buf & 0xFF));
+                if (lane == 0) S.src()[op + k] = (inf_map_t<OUTMAX>)(inf_lit<OUTMAX> | (I.buf & 0xFF));
                 I.buf >>= 8;
                 I.cnt -= 8;
                 k++;
             }
             if (I.pos + (ln - k) > plen) return -1;
             for (uint32_t b = 0; b < ln - k; b += 64)
-                if (b + lane < ln - k) S.src[op + k + b + lane] = (uint16_t)(IN_LIT | g[I.pos + b + lane]);
+                if (b + lane < ln - k) S.src()[op + k + b + lane] = (inf_map_t<OUTMAX>)(inf_lit<OUTMAX> | g[I.pos + b + lane]);
             I.pos += ln - k;
             op += ln;
         } else if (btype == 1 || btype == 2) {
@@ -774,13 +790,13 @@ __device__ int64_t inflate_stream(InfSmem<OUTMAX>& S, const uint8_t* g, uint32_t
         for (uint32_t q0 = lane * 4; q0 < op; q0 += 256) {
             uint32_t w[4];
 #pragma unroll
-            for (int t = 0; t < 4; t++) w[t] = q0 + t < op ? S.src[q0 + t] : IN_LIT;
+            for (int t = 0; t < 4; t++) w[t] = q0 + t < op ? S.src()[q0 + t] : inf_lit<OUTMAX>;
 #pragma unroll
             for (int t = 0; t < 4; t++)
-                if (!(w[t] & IN_LIT)) {
-                    w[t] = S.src[w[t]];
-                    S.src[q0 + t] = (uint16_t)w[t];
-                    more |= !(w[t] & IN_LIT);
+                if (!(w[t] & inf_lit<OUTMAX>)) {
+                    w[t] = S.src()[w[t]];
+                    S.src()[q0 + t] = (inf_map_t<OUTMAX>)w[t];
+                    more |= !(w[t] & inf_lit<OUTMAX>);
                 }
         }
         wave_sync();
@@ -788,7 +804,7 @@ __device__ int64_t inflate_stream(InfSmem<OUTMAX>& S, const uint8_t* g, uint32_t
     }
     uint64_t asum = 0, bsum = 0;
     for (uint32_t q = lane; q < op; q += 64) {
-        const uint32_t c = S.src[q] & 0xFF;
+        const uint32_t c = S.src()[q] & 0xFF;
         asum += c;
         bsum += (uint64_t)(op - q) * c;
     }
@@ -808,6 +824,10 @@ __global__ __launch_bounds__(64) void k_decode_inflate(DecArgs A) {
     const DecJob J = A.jobs[j];
     uint8_t* out = uniform_ptr(A.out + J.out_off);
     const uint32_t orig = uniform_u32(J.orig);
+    if constexpr (InfSmem<OUTMAX>::G) {
+        S.srcg = reinterpret_cast<inf_map_t<OUTMAX>*>(A.scratch + J.scratch_off);
+        S.capg = uniform_u32((uint32_t)J.scratch_cap);
+    }
 #ifdef AMBC_STAMPS
     uint64_t _st_t = __builtin_amdgcn_s_memtime();
     uint64_t _acc[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -824,15 +844,15 @@ __global__ __launch_bounds__(64) void k_decode_inflate(DecArgs A) {
     } else {
         const uint32_t m = min((uint32_t)r, orig);
         const uint32_t head = min((uint32_t)((4 - (reinterpret_cast<uintptr_t>(out) & 3)) & 3), m);
-        if (lane < head) out[lane] = (uint8_t)(S.src[lane] & 0xFF);
+        if (lane < head) out[lane] = (uint8_t)(S.src()[lane] & 0xFF);
         const uint32_t nw = (m - head) >> 2;
         uint32_t* o32 = reinterpret_cast<uint32_t*>(out + head);
         for (uint32_t w = lane; w < nw; w += 64) {
             const uint32_t q = head + 4 * w;
-            o32[w] = (S.src[q] & 0xFFu) | (S.src[q + 1] & 0xFFu) << 8 | (S.src[q + 2] & 0xFFu) << 16 |
-                     (S.src[q + 3] & 0xFFu) << 24;
+            o32[w] = (S.src()[q] & 0xFFu) | (S.src()[q + 1] & 0xFFu) << 8 | (S.src()[q + 2] & 0xFFu) << 16 |
+                     (S.src()[q + 3] & 0xFFu) << 24;
         }
-        for (uint32_t q = head + (nw << 2) + lane; q < m; q += 64) out[q] = (uint8_t)(S.src[q] & 0xFF);
+        for (uint32_t q = head + (nw << 2) + lane; q < m; q += 64) out[q] = (uint8_t)(S.src()[q] & 0xFF);
         for (uint32_t q = m + lane; q < orig; q += 64) out[q] = 0;
     }
     if (lane == 0) A.produced[j] = orig;
@@ -860,8 +880,10 @@ hipError_t launch_inflate(int kind, const DecArgs& a, hipStream_t s) {
         hipLaunchKernelGGL(k_decode_inflate<8192>, dim3(a.n_list), dim3(64), 0, s, a);
     else if (kind == DEC_KIND_INFLATE_16K)
         hipLaunchKernelGGL(k_decode_inflate<16384>, dim3(a.n_list), dim3(64), 0, s, a);
-    else  // 64 KB source map + tables: 2 workgroups per CU
+    else if (kind == DEC_KIND_INFLATE_32K)  // 64 KB source map + tables: 2 workgroups per CU
         hipLaunchKernelGGL(k_decode_inflate<32768>, dim3(a.n_list), dim3(64), 0, s, a);
+    else  // the map in device scratch
+        hipLaunchKernelGGL(k_decode_inflate<65536>, dim3(a.n_list), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 

@@ -91,7 +91,8 @@ struct DecArgs {
 enum : int { DEC_KIND_LIGHT = 0, DEC_KIND_LZ4_4K = 1, DEC_KIND_LZ4_8K = 2, DEC_KIND_LZ4_16K = 3,
              DEC_KIND_LZ4_G = 4, DEC_KIND_INFLATE_4K = 5, DEC_KIND_INFLATE_8K = 6,
              DEC_KIND_INFLATE_16K = 7, DEC_KIND_HEAVY = 8, DEC_KIND_DICT_4K = 9, DEC_KIND_DICT_8K = 10,
-             DEC_KIND_DICT_16K = 11, DEC_KIND_INFLATE_32K = 12, DEC_KINDS = 13 };
+             DEC_KIND_DICT_16K = 11, DEC_KIND_INFLATE_32K = 12,
+             DEC_KIND_INFLATE_G = 13, DEC_KINDS = 14 };
 constexpr uint32_t DEC_PRODUCED_HOST = 0xFFFFFFFEu;  // k_decode_inflate: output too large, inflate on host
 
 constexpr uint32_t DEC_VERBATIM = 256;

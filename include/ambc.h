@@ -65,7 +65,7 @@ extern "C" {
 #define AMBC_M_HUFFMAN 3
 #define AMBC_M_DELTA 4 /* never selected: payload length == n (compression_methods.py:598-608) */
 #define AMBC_M_DEFLATE 5 /* GPU encoder "ambc-deflate v1" (chunk_size <= 65536) or zlib-9 (AMBC_FLAG_ZLIB9,
-                           <= 8192); decode: GPU inflate (packages <= 32768), else host zlib */
+                           <= 8192); decode: GPU inflate (packages <= 65536) */
 #define AMBC_M_LZ4 9
 #define AMBC_M_RAW 255
 

@@ -535,9 +535,10 @@ def test_gpu_inflate_zlib_corpus(ctx):
 
 
 def test_gpu_inflate_large_packages(ctx):
-    """id-5 packages of 16-32 KiB (k_decode_inflate<32768>, a 64 KB source map)
-    and of 64 KiB (host zlib): zlib levels 1/6/9, matches at distance 32768,
-    streams that decode past the package's orig, a truncated one."""
+    """id-5 packages of 16-32 KiB (k_decode_inflate<32768>, a 64 KB LDS source
+    map) and of 32-64 KiB (k_decode_inflate<65536>, a u32 map in device
+    scratch): zlib levels 1/6/9, matches at distance 32768, streams that decode
+    past the package's orig, truncated ones."""
     import zlib
     mixed = synth.generate(1 << 20, 43)
     blk = synth.random_bytes(2000, 44)
@@ -548,6 +549,8 @@ def test_gpu_inflate_large_packages(ctx):
             payloads.append((zlib.compress(mixed[o:o + n], lvl), n))
         payloads.append((zlib.compress(far, lvl), len(far)))
     payloads.append((zlib.compress(bytes(40000), 9), 32768))         # decodes past the package
+    payloads.append((zlib.compress(bytes(70000), 9), 65536))         # past a device-scratch map
+    payloads.append((zlib.compress(mixed[800000:850000], 9)[:-1], 50000))   # bad Adler-32 length
     good = zlib.compress(mixed[700000:730000], 9)
     payloads.append((good[:len(good) // 2], 30000))                  # unfinished stream
     parts, orig_total = [], 0
