@@ -23,6 +23,14 @@ With several ``CHUNK_SIZE_CANDIDATES`` (e.g. the reference's default
 ``REFERENCE_CHUNK_SIZE_CANDIDATES``) the reference's multi-size walk runs
 instead, on the device (``_adaptive_compress_multisize`` ->
 ambc_compress_multisize).
+
+Defaults differ from the reference's ``AdaptiveCompressor()`` (8-candidate
+walk, every stdlib codec): this class defaults to one 4096-byte chunk size,
+native mode and methods {1, 3, 4, 9} (the throughput configuration; id 9 needs
+an LZ4 decoder on the reading side).  The first compress of an instance built
+with those defaults says so once (``DefaultsWarning``);
+``AdaptiveCompressor.like_reference()`` builds the closest GPU configuration to
+the reference's default instead.
 """
 import ctypes as C
 import hashlib
@@ -32,6 +40,7 @@ import struct
 import sys
 import threading
 import time
+import warnings
 
 import numpy as np
 
@@ -61,6 +70,10 @@ def entropy_terms(n):
         if len(_TERMS) < 16:
             _TERMS[n] = t
     return t
+
+
+class DefaultsWarning(UserWarning):
+    """An instance with this engine's (not the reference's) encode defaults compresses."""
 
 
 class AdaptiveCompressor:
@@ -95,6 +108,8 @@ class AdaptiveCompressor:
         if deflate not in (None, "v1", "zlib9"):
             raise ValueError("deflate must be None, 'v1' or 'zlib9'")
         self._deflate = deflate
+        # encode defaults left as they are: the first compress says they are not the reference's
+        self._warn_defaults = chunk_size is None and mode == "native" and methods is None
         if chunk_size is not None:
             self.CHUNK_SIZE_CANDIDATES = [int(chunk_size)]
         ids = tuple(DEFAULT_METHODS if methods is None else [m for m in methods if m != 255])
@@ -109,6 +124,25 @@ class AdaptiveCompressor:
         self.method_chunk_prefs = dict(METHOD_CHUNK_PREFS)
         self.devices = list(devices) if devices else None
         self.chunk_stats = None
+
+    @classmethod
+    def like_reference(cls, **kw):
+        """The closest GPU configuration to the reference's ``AdaptiveCompressor()``
+        (adaptive_compressor.py:61-62,64-178): its 8-candidate walk, reference mode,
+        and its stdlib codecs that have GPU encoders -- RLE, Dictionary, Huffman,
+        Delta, DEFLATE (ids 6/7, bz2/lzma, have no GPU encoder: files where the
+        reference would pick them differ; every package stays decodable by it)."""
+        comp = cls(mode="reference", methods=(1, 2, 3, 4, 5), **kw)
+        comp.CHUNK_SIZE_CANDIDATES = list(REFERENCE_CHUNK_SIZE_CANDIDATES)
+        return comp
+
+    def _note_defaults(self):
+        if self._warn_defaults and self.CHUNK_SIZE_CANDIDATES == [DEFAULT_CHUNK_SIZE]:
+            self._warn_defaults = False
+            warnings.warn("AdaptiveCompressor() defaults here are chunk_size=4096, mode='native', "
+                          "methods (1, 3, 4, 9) -- not the reference's 8-candidate walk with its stdlib "
+                          "codecs; use AdaptiveCompressor.like_reference() for the closest match",
+                          DefaultsWarning, stacklevel=3)
 
     @property
     def deflate(self):
@@ -231,6 +265,7 @@ class AdaptiveCompressor:
         return out[:olen.value].tobytes()
 
     def _adaptive_compress(self, file_data):
+        self._note_defaults()
         """One C-ABI call: input bytes -> .ambc body (packages + end chunk)."""
         if len(self.CHUNK_SIZE_CANDIDATES) != 1:
             return self._adaptive_compress_multisize(file_data)

@@ -732,6 +732,28 @@ def test_multisize_many_walks_match_oracle(ctx):
         assert comp._adaptive_decompress(body, len(data)) == data
 
 
+def test_like_reference_and_defaults_warning(ctx):
+    """AdaptiveCompressor.like_reference(): the reference's 8-candidate walk with
+    its GPU-encodable stdlib codecs, body equal to the oracle's walk; an instance
+    with this engine's defaults warns once, at its first compress."""
+    import warnings
+    from ambc import AdaptiveCompressor, DefaultsWarning
+    data = synth.generate(150000, 31)
+    comp = AdaptiveCompressor.like_reference()
+    assert comp.CHUNK_SIZE_CANDIDATES == REF_CANDS and comp.mode == "reference"
+    body = comp._adaptive_compress(data)
+    ref, _ = orc.compress_body_multisize(data, REF_CANDS, (1, 2, 3, 4, 5, 255))
+    assert body == ref
+    assert comp._adaptive_decompress(body, len(data)) == data
+    plain = AdaptiveCompressor()
+    with pytest.warns(DefaultsWarning):
+        plain._adaptive_compress(data[:8192])
+    with warnings.catch_warnings():
+        warnings.simplefilter("error", DefaultsWarning)
+        plain._adaptive_compress(data[:8192])                       # once per instance
+        AdaptiveCompressor(chunk_size=4096)._adaptive_compress(data[:8192])
+
+
 def test_multisize_rejects_oversize_gpu_chunks(ctx):
     # the zlib-9 encoder's walkers keep their tables in LDS: chunks <= 4096
     comp = _compressor(methods=(1, 3, 4, 5), deflate="zlib9")
