@@ -214,6 +214,16 @@ static int finish_compress(Dev& d, const ambc_params* p, uint32_t R, const Remai
     return AMBC_OK;
 }
 
+// workgroups of the compaction grid that runs beside the next segment's encoder
+// (AMBC_COMPACT_RESIDENT overrides, for measurements)
+static uint32_t compact_resident() {
+    static const uint32_t r = [] {
+        const char* e = getenv("AMBC_COMPACT_RESIDENT");
+        return e && atoi(e) > 0 ? (uint32_t)atoi(e) : 1024u;
+    }();
+    return r;
+}
+
 int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params* p, uint8_t* d_out,
                       uint64_t out_cap, uint64_t* out_len, ambc_stats* st, const ShardInfo* si) {
     int rc = check_params(p);
@@ -337,6 +347,7 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
         HIPCHK(d.scan_tmp.ensure(tmpb));
         HIPCHK(d.segbase.ensure((S + 1) * 8));
         HIPCHK(hipMemsetAsync(d.segbase.p, 0, 8, d.cs));
+        HIPCHK(hipMemsetAsync(d.acc.p, 0, 260 * 8, d.cs));
         uint64_t* sb = d.segbase.as<uint64_t>();
         for (uint32_t i = 0; i < S; i++) {
             const uint32_t k0 = (uint32_t)((uint64_t)M * i / S), k1 = (uint32_t)((uint64_t)M * (i + 1) / S);
@@ -365,13 +376,14 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
             // beside the next segment's encoder the compaction runs as a resident
             // grid (per-package-group workgroups would wait behind the encoder's
             // queued workgroups for every dispatch); the last one runs alone
-            ca.resident = i + 1 < S ? 1024 : 0;
+            ca.resident = i + 1 < S ? compact_resident() : 0;
             HIPCHK(launch_compact(ca, d.cs));
+            // the segment's statistics beside the next encode too (acc[] accumulates)
+            HIPCHK(launch_stats(d.ids.as<uint8_t>() + k0, d.plen.as<uint32_t>() + k0, k1 - k0, ca.n_total, C,
+                                d.acc.as<uint64_t>(), d.cs));
         }
         HIPCHK(hipEventRecord(d.ev[3], d.cs));
         HIPCHK(hipStreamWaitEvent(s, d.ev[3], 0));
-        HIPCHK(hipMemsetAsync(d.acc.p, 0, 260 * 8, s));
-        HIPCHK(launch_stats(d.ids.as<uint8_t>(), d.plen.as<uint32_t>(), M, n, C, d.acc.as<uint64_t>(), s));
         uint64_t body_len = 0;
         HIPCHK(hipMemcpyAsync(&body_len, sb + S, 8, hipMemcpyDeviceToHost, s));
         std::vector<uint64_t> acc(260);

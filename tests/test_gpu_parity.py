@@ -210,7 +210,11 @@ def test_pipelined_segments_match_oracle(ctx, n, chunk, methods):
     ref, st = orc.compress_body(data, orc.make_params(chunk, "native", methods, n_total=n,
                                                       deflate="gd" if 5 in methods else "zlib"))
     assert body == ref
+    # statistics accumulate per segment beside the next segment's encode
     assert comp.chunk_stats["compressed_chunks"] == st.compressed_chunks
+    gst = comp._last_device_stats
+    assert [gst.method_usage[i] for i in range(256)] == [st.method_usage[i] for i in range(256)]
+    assert (gst.payload_bytes, gst.bytes_saved) == (st.payload_bytes, st.bytes_saved)
     assert comp._adaptive_decompress(body, n) == data
 
 
