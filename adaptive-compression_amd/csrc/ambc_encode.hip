@@ -521,10 +521,10 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
             // the walk extends the selected longer ones with the whole wave
             const bool run_l = valid && (uint32_t)i >= nextp;
             const uint32_t lim = run_l ? n - 5 - (uint32_t)i : 0u;
-            uint32_t L;
-            {
+            uint32_t L = 0;
+            if (run_l) {   // only possible match starts read their 12 bytes (fewer LDS bank conflicts)
                 const uint32_t* c32 = reinterpret_cast<const uint32_t*>(S.chunk);
-                const uint32_t cs = (uint32_t)max(cand, 0);
+                const uint32_t cs = (uint32_t)cand;
                 const uint32_t si = (uint32_t)i & 3u, sc = cs & 3u;
                 const uint32_t ai = ((uint32_t)i + 4) >> 2, ac = (cs + 4) >> 2;
                 uint32_t wi[4], wc[4];
@@ -537,7 +537,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                                        __builtin_amdgcn_alignbyte(wc[t + 1], wc[t], sc);
                     if (x) add = 4 * t + ((uint32_t)__builtin_ctz(x) >> 3);
                 }
-                L = run_l ? 4 + add : 0u;
+                L = 4 + add;
             }
             L = min(L, lim);
             STAMP(3);
