@@ -176,6 +176,19 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
     // 255-byte splits of the run carried into the lane (a run that starts inside
     // a lane is shorter than 255 there); the should_use samples at step 4 are
     // byte 0 against byte 1 of each dword; the histogram adds whole runs.
+    const uint32_t mm = A.method_mask;
+    const bool force = A.flags & ENC_FORCE;
+    const bool analyze = A.flags & ENC_ANALYZE;
+    auto eligible = [&](int id) {
+        return ((mm >> id) & 1u) && (force || (A.pref_min[id] <= n && n <= A.pref_max[id]));
+    };
+    // pass A feeds RLE, Huffman, Delta, the should_use report and k_deflate's
+    // gates; chunks only LZ4 may take (above Huffman's 8192 by the prefs) skip it
+    const bool need_a = force || analyze || A.bestpre || eligible(1) || eligible(3) || eligible(4);
+    // within it: RLE's pair count, and the RLE / Delta should_use samples (chunks
+    // above 4096 -- C4's 8192 -- keep only Huffman's histogram)
+    const bool need_p = force || analyze || eligible(1);
+    const bool need_s = need_p || eligible(4);
     const uint32_t ss = n < 1000 ? n : 1000;
     const uint32_t step = max(1u, n / ss);
     const bool fast_samples = step == 4;
@@ -183,7 +196,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
     int rs_carry = -1;
     const uint32_t* c32 = reinterpret_cast<const uint32_t*>(S.chunk);
 #pragma unroll 1
-    for (int r = 0; r < ROUNDS; r++) {
+    for (int r = 0; r < (need_a ? ROUNDS : 0); r++) {
         const uint32_t b0 = (uint32_t)(r * 64 + lane) * BS;
         // previous byte; position 0 always starts a run (the reference's prev = None)
         uint32_t pw = b0 ? c32[(b0 >> 2) - 1] : ~((uint32_t)S.chunk[0] << 24);
@@ -201,12 +214,14 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                 const uint32_t nv = p < n ? min(n - p, 4u) : 0u;       // valid bytes
                 const uint32_t vmask = nv >= 4 ? 0xFFFFFFFFu : (1u << (8 * nv)) - 1u;
                 const uint32_t chg = (x | ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu)) & 0x80808080u & vmask;
-                starts += __builtin_popcount(chg);
-                if (chg) {
-                    lb = (int)(p + ((31 - __builtin_clz(chg)) >> 3));
-                    if (fc < 0) fc = (int)(p + ((uint32_t)__builtin_ctz(chg) >> 3));
+                if (need_p) {
+                    starts += __builtin_popcount(chg);
+                    if (chg) {
+                        lb = (int)(p + ((31 - __builtin_clz(chg)) >> 3));
+                        if (fc < 0) fc = (int)(p + ((uint32_t)__builtin_ctz(chg) >> 3));
+                    }
                 }
-                if (fast_samples && p + 1 < n) {      // sample p: byte 0 against byte 1
+                if (need_s && fast_samples && p + 1 < n) {      // sample p: byte 0 against byte 1
                     const uint32_t a0 = w & 0xFFu, a1 = (w >> 8) & 0xFFu;
                     samp += (chg & 0x8000u) == 0;
                     dsamp += (a0 > a1 ? a0 - a1 : a1 - a0) < 32u;
@@ -228,13 +243,15 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
             }
         }
         if (rc) atomicAdd(&S.hist()[cur], rc);
-        const int rs = wave_excl_max(lb, rs_carry);  // run start of position b0-1
-        rs_carry = max(rs_carry, wave_max_i32(lb));
-        // 255-byte splits of the carried-in run inside [b0, first run start)
-        const int end = fc >= 0 ? fc : (int)min(b0 + BS, n);
-        if (b0 && end > (int)b0) starts += (uint32_t)((end - 1 - rs) / 255 - ((int)b0 - 1 - rs) / 255);
-        pairs += starts;
-        if (!fast_samples) {
+        if (need_p) {
+            const int rs = wave_excl_max(lb, rs_carry);  // run start of position b0-1
+            rs_carry = max(rs_carry, wave_max_i32(lb));
+            // 255-byte splits of the carried-in run inside [b0, first run start)
+            const int end = fc >= 0 ? fc : (int)min(b0 + BS, n);
+            if (b0 && end > (int)b0) starts += (uint32_t)((end - 1 - rs) / 255 - ((int)b0 - 1 - rs) / 255);
+            pairs += starts;
+        }
+        if (need_s && !fast_samples) {
             // other steps: positions p = step * i in the lane's block
 #pragma unroll 1
             for (uint32_t p = (b0 + step - 1) / step * step; p < b0 + BS && p + 1 < n; p += step) {
@@ -249,13 +266,6 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
     dsamp = wave_sum_u32(dsamp);
     wave_sync();
     STAMP(0);
-
-    const uint32_t mm = A.method_mask;
-    const bool force = A.flags & ENC_FORCE;
-    const bool analyze = A.flags & ENC_ANALYZE;
-    auto eligible = [&](int id) {
-        return ((mm >> id) & 1u) && (force || (A.pref_min[id] <= n && n <= A.pref_max[id]));
-    };
 
     // best (len + 18); (len+18)/n < 1.0  <=>  len + 18 < n (adaptive_compressor.py:573-577)
     uint32_t best = force ? 0xFFFFFFFFu : n;
