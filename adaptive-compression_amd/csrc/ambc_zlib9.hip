@@ -112,7 +112,7 @@ template <int CMAX> struct Z9Rec {
 };
 
 template <int CMAX> struct Z9Cfg {
-    static constexpr int NW = CMAX <= 1024 ? 2 : (CMAX <= 2048 ? 4 : 8);
+    static constexpr int NW = CMAX <= 1024 ? 2 : (CMAX <= 2048 ? 4 : (CMAX <= 4096 ? 8 : 16));
 };
 
 template <int CMAX>
