@@ -111,8 +111,11 @@ template <int CMAX> struct Z9Rec {
     static constexpr uint32_t STRIDE = MERGE + 316;
 };
 
+#ifndef AMBC_Z9_NW4096
+#define AMBC_Z9_NW4096 8
+#endif
 template <int CMAX> struct Z9Cfg {
-    static constexpr int NW = CMAX <= 1024 ? 2 : (CMAX <= 2048 ? 4 : (CMAX <= 4096 ? 8 : 16));
+    static constexpr int NW = CMAX <= 1024 ? 2 : (CMAX <= 2048 ? 4 : (CMAX <= 4096 ? AMBC_Z9_NW4096 : 16));
 };
 
 template <int CMAX>
