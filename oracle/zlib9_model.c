@@ -12,9 +12,24 @@
  * (adaptive-compression_amd/csrc/ambc_zlib9.hip) and both are checked byte for
  * byte against the system zlib 1.2.11 (tests/test_zlib9_model.py,
  * tests/test_gpu_zlib9.py).  Inputs up to 65536 bytes (the reference's id-5
- * chunk limit, adaptive_compressor.py:119); the window slide zlib performs past
- * 65274 bytes (which only forbids a stored block that started before 32768) is
- * not modelled.
+ * chunk limit, adaptive_compressor.py:119).
+ *
+ * The window slide.  zlib's window is 2 x 32768 bytes; fill_window (called at
+ * the top of every deflate_slow step whose lookahead is below MIN_LOOKAHEAD =
+ * 262, before the lookahead == 0 exit) slides it down by 32768 once strstart
+ * reaches w_size + MAX_DIST = 65274.  For inputs <= 65536 that happens at most
+ * once, at the first step top s >= 65274 with n - s < 262 (s = n included), and
+ * it changes exactly two things a model in input coordinates must restate:
+ *   - head/prev entries below 32768 become NIL, and the entry 32768 becomes
+ *     window position 0 = NIL: a hash head equal to 32768 at the slide step
+ *     itself (s = 65274, reachable when n < 65536) starts no match search;
+ *     deeper chain entries are cut by MAX_DIST either way;
+ *   - block_start drops below 0 for a block that began before 32768, and
+ *     FLUSH_BLOCK then passes no buffer to _tr_flush_block: such a block
+ *     flushed after the slide cannot be stored.
+ * (Bytes past the input in the slid window are stale instead of zero: they can
+ * only lengthen a match that already reaches the end of the input, and every
+ * such length is capped to the lookahead before it is used.)
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -69,6 +84,7 @@ typedef struct {
     uint8_t* out;
     uint64_t o;
     uint32_t bb, bc;
+    int slid;                     /* the window has slid (see the header) */
 } Z;
 
 static inline uint8_t wat(const Z* z, uint32_t i) { return i < z->n ? z->w[i] : 0; }
@@ -258,7 +274,9 @@ static void flush_block(Z* z, uint32_t start, uint32_t stored_len, int last) {
     uint32_t opt_lenb = (z->opt_len + 3 + 7) >> 3;
     const uint32_t static_lenb = (z->static_len + 3 + 7) >> 3;
     if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
-    if (stored_len + 4 <= opt_lenb) {
+    /* a block that began before the slid window's start has no buffer */
+    const int have_buf = !(z->slid && start < WSZ);
+    if (stored_len + 4 <= opt_lenb && have_buf) {
         bits(z, (uint32_t)last, 3);
         windup(z);
         z->out[z->o++] = (uint8_t)stored_len; z->out[z->o++] = (uint8_t)(stored_len >> 8);
@@ -340,9 +358,14 @@ EXPORT int64_t orc_zlib9(const uint8_t* in, uint32_t n, uint8_t* out) {
     int avail = 0;
     uint32_t block_start = 0;
     for (;;) {
-        if (la == 0) break;
+        if (la < MINLA) {
+            /* fill_window: the slide, before the end-of-input exit */
+            if (!z->slid && s >= WSZ + MAXD) z->slid = 1;
+            if (la == 0) break;
+        }
         uint32_t hh = 0;
         if (la >= MINM) hh = ins(z, s);
+        if (z->slid && hh == WSZ) hh = 0;   /* window position 0 after the slide: NIL */
         prev_length = match_length;
         prev_match = match_start;
         match_length = MINM - 1;

@@ -61,3 +61,47 @@ def test_zlib9_model_matches_zlib():
     cases += [bytes(rnd.randrange(256) for _ in range(n)) for n in (16383, 16384, 40000)]
     for c in cases:
         assert _z9(c) == zlib.compress(c, 9), len(c)
+
+
+def _h15(b, p):
+    return ((b[p] << 10) ^ (b[p + 1] << 5) ^ b[p + 2]) & 0x7FFF
+
+
+def slide_head_case(seed, n, L=40):
+    """Input where zlib's window slide decides a match: compressible bytes
+    (0..127, geometric) with a 40-byte pattern of bytes >= 128 at 32768 and again
+    at 65274, the slide step of an input shorter than 65536, and no position in
+    between with the pattern's 15-bit hash -- so 65274's hash head is 32768,
+    which the slid window reads as NIL (no match there; the copy is found one
+    byte later, against 32769)."""
+    rnd = random.Random(seed)
+    while True:
+        b = bytearray(min(int(rnd.expovariate(0.05)), 127) for _ in range(n))
+        pat = bytes(rnd.randrange(128, 256) for _ in range(L))
+        b[32768:32768 + L] = pat
+        b[65274:65274 + L] = pat
+        hh = _h15(b, 65274)
+        if not any(_h15(b, p) == hh for p in range(32769, 65274)):
+            return bytes(b)
+
+
+def test_zlib9_model_window_slide():
+    """8..64 KiB inputs (the reference's id-5 chunk sizes up to its 65536 prefs
+    maximum, adaptive_compressor.py:119), the multi-block split there, and the
+    window slide past 65274 bytes: the slide step's NIL head (inputs a model
+    without the slide gets wrong) and sizes 65200..65536 of every class."""
+    rnd = random.Random(65274)
+    mixed = synth.generate(1 << 20, 13)
+    cases = [slide_head_case(n, n) for n in (65317, 65400, 65535)]
+    for n in (8193, 12288, 16384, 20000, 32767, 32768, 32769, 49152, 65273, 65274, 65275, 65276,
+              65277, 65535, 65536):
+        o = rnd.randrange(0, len(mixed) - n)
+        cases += [mixed[o:o + n], _gen(rnd, n)]
+    for _ in range(24):
+        n = rnd.randrange(65200, 65537)
+        cases.append(_gen(rnd, n))
+        o = rnd.randrange(0, len(mixed) - n)
+        cases.append(mixed[o:o + n])
+    cases += [bytes(65536), b"xy" * 32768, bytes(range(256)) * 256]
+    for c in cases:
+        assert _z9(c) == zlib.compress(c, 9), len(c)
