@@ -30,7 +30,7 @@ COMM_ID_BYTES = 128
 MODE_NATIVE = 0
 MODE_REFERENCE = 1
 FLAG_NO_END_CHUNK = 1
-FLAG_ZLIB9 = 2          # id 5 = zlib.compress(data, 9)'s bytes (chunk_size <= 8192)
+FLAG_ZLIB9 = 2          # id 5 = zlib.compress(data, 9)'s bytes (chunk_size <= 65536)
 MAX_CHUNK = 65536
 
 EXPORTS = (

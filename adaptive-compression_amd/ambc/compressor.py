@@ -101,10 +101,10 @@ class AdaptiveCompressor:
             raise ValueError("mode must be 'native' or 'reference'")
         self.mode = mode
         # id 5's GPU encoder: "zlib9" (zlib.compress(data, 9)'s own bytes -- the
-        # reference's DeflateCompression, advanced_compression.py:76-81 -- chunks
-        # <= 8192) or "v1" ("ambc-deflate v1": valid zlib streams of this
-        # engine's own parse, chunks <= 65536, faster).  None: "zlib9" in
-        # reference mode when every chunk size allows it, else "v1".
+        # reference's DeflateCompression, advanced_compression.py:76-81) or "v1"
+        # ("ambc-deflate v1": valid zlib streams of this engine's own parse,
+        # faster); both take chunks up to the reference's 65536 prefs maximum.
+        # None: "zlib9" in reference mode, else "v1".
         if deflate not in (None, "v1", "zlib9"):
             raise ValueError("deflate must be None, 'v1' or 'zlib9'")
         self._deflate = deflate
@@ -130,8 +130,9 @@ class AdaptiveCompressor:
         """The closest GPU configuration to the reference's ``AdaptiveCompressor()``
         (adaptive_compressor.py:61-62,64-178): its 8-candidate walk, reference mode,
         and its stdlib codecs that have GPU encoders -- RLE, Dictionary, Huffman,
-        Delta, DEFLATE (ids 6/7, bz2/lzma, have no GPU encoder: files where the
-        reference would pick them differ; every package stays decodable by it)."""
+        Delta and DEFLATE as zlib.compress(data, 9)'s own bytes at every size (ids
+        6/7, bz2/lzma, have no GPU encoder: files where the reference would pick
+        them differ; every package stays decodable by it)."""
         comp = cls(mode="reference", methods=(1, 2, 3, 4, 5), **kw)
         comp.CHUNK_SIZE_CANDIDATES = list(REFERENCE_CHUNK_SIZE_CANDIDATES)
         return comp
@@ -148,7 +149,7 @@ class AdaptiveCompressor:
     def deflate(self):
         if self._deflate is not None:
             return self._deflate
-        if self.mode == "reference" and max(int(c) for c in self.CHUNK_SIZE_CANDIDATES) <= 8192:
+        if self.mode == "reference":
             return "zlib9"
         return "v1"
 
@@ -265,8 +266,8 @@ class AdaptiveCompressor:
         return out[:olen.value].tobytes()
 
     def _adaptive_compress(self, file_data):
-        self._note_defaults()
         """One C-ABI call: input bytes -> .ambc body (packages + end chunk)."""
+        self._note_defaults()
         if len(self.CHUNK_SIZE_CANDIDATES) != 1:
             return self._adaptive_compress_multisize(file_data)
         n = len(file_data)

@@ -21,7 +21,7 @@ METHOD_CHUNK_PREFS = {
 REFERENCE_CHUNK_SIZE_CANDIDATES = [131072, 65536, 32768, 16384, 8192, 4096, 2048, 1024]
 
 # selector candidates with a gfx950 encoder; id 5 is "ambc-deflate v1" (a valid
-# zlib stream, not zlib level-9 bytes), chunk_size <= 65536 (or zlib-9 bytes, <= 4096); id 2 (the reference's
+# zlib stream, not zlib level-9 bytes) or zlib-9's own bytes, chunk_size <= 65536; id 2 (the reference's
 # own Dictionary bytes) takes chunks <= 8192, its preferred maximum
 GPU_ENCODE_IDS = (1, 2, 3, 4, 5, 9)
 DEVICE_DECODE_IDS = (1, 2, 3, 4, 9, 255)

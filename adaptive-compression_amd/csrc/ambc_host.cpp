@@ -97,7 +97,7 @@ void ambc_destroy(ambc_ctx* ctx) {
         (void)hipStreamSynchronize(d.stream);
         for (Buf* b : {&d.in, &d.out, &d.slots, &d.plen, &d.ids, &d.sizes, &d.off, &d.scan_tmp,
                        &d.acc, &d.ent_full, &d.ent_tail, &d.body, &d.jobs, &d.produced, &d.dout,
-                       &d.scratch, &d.seg, &d.list, &d.bestpre, &d.gdseq, &d.pending, &d.z9rec, &d.segbase, &d.coll,
+                       &d.scratch, &d.seg, &d.list, &d.bestpre, &d.gdseq, &d.pending, &d.z9rec, &d.z9scr, &d.segbase, &d.coll,
                        &d.inffix})
             b->release();
         for (auto& b : d.msb) b.release();
@@ -140,7 +140,7 @@ int ambc::check_params(const ambc_params* p) {
     if (p->method_mask & ~allowed)
         return fail(AMBC_E_INVAL, "method_mask holds ids without a GPU encoder (allowed: 1, 2, 3, 4, 5, 9)");
     if (((p->method_mask >> AMBC_M_DEFLATE) & 1) && (p->flags & AMBC_FLAG_ZLIB9) && z9_cmax(C) == 0)
-        return fail(AMBC_E_INVAL, "the GPU zlib-9 encoder (AMBC_FLAG_ZLIB9) supports chunk_size <= 8192");
+        return fail(AMBC_E_INVAL, "the GPU zlib-9 encoder (AMBC_FLAG_ZLIB9) supports chunk_size <= 65536");
     if (((p->method_mask >> AMBC_M_DICT) & 1) && p->pref_min[AMBC_M_DICT] <= dict_cmax(p) &&
         dict_cmax(p) > 8192)
         return fail(AMBC_E_INVAL, "the GPU Dictionary encoder takes chunks <= 8192 bytes "
@@ -298,6 +298,10 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
         if (z9) {
             HIPCHK(d.z9rec.ensure((size_t)std::max<uint32_t>(M, 1) * z9_rec_words(z9_cmax(C)) * 4));
             ea.z9rec = d.z9rec.as<uint32_t>();
+            if (z9_cmax(C) > 8192) {   // the big parse's scratch: per resident workgroup, reused by segments
+                HIPCHK(d.z9scr.ensure(z9_scratch_bytes(z9_cmax(C), std::max<uint32_t>(M, 1))));
+                ea.z9scr = d.z9scr.as<uint8_t>();
+            }
         }
     }
     const bool dict = (p->method_mask >> AMBC_M_DICT) & 1;

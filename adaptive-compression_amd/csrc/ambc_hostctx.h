@@ -70,7 +70,7 @@ struct Buf {
 
 // device buffers of one multi-size walk batch (ambc_multisize.cpp)
 struct Batch {
-    Buf coff, clen, slots, plen, ids, sizes, bestpre, gdseq, pending, ent, off, z9rec;
+    Buf coff, clen, slots, plen, ids, sizes, bestpre, gdseq, pending, ent, off, z9rec, z9scr;
     uint32_t* hplen = nullptr;  // pinned copies of plen / ids for the host walk
     uint8_t* hids = nullptr;
     size_t hcap = 0;
@@ -85,7 +85,7 @@ struct Batch {
         return e;
     }
     void release() {
-        for (Buf* b : {&coff, &clen, &slots, &plen, &ids, &sizes, &bestpre, &gdseq, &pending, &ent, &off, &z9rec})
+        for (Buf* b : {&coff, &clen, &slots, &plen, &ids, &sizes, &bestpre, &gdseq, &pending, &ent, &off, &z9rec, &z9scr})
             b->release();
         if (hplen) (void)hipHostFree(hplen);
         if (hids) (void)hipHostFree(hids);
@@ -102,6 +102,7 @@ struct Dev {
     Buf in, out, slots, plen, ids, sizes, off, scan_tmp, acc, ent_full, ent_tail;
     Buf body, jobs, produced, dout, scratch, seg, list, bestpre, gdseq, pending;
     Buf z9rec;                  // zlib-9 id 5: the parse's segments per chunk
+    Buf z9scr;                  // zlib-9 id 5 above 8 KiB: the parse's scratch per resident workgroup
     Buf coll;                   // small device buffers of the collectives (sizes, stats, flags)
     Buf inffix;                 // fixed-Huffman inflate tables (built on the first decode)
     bool inffix_ok = false;

@@ -37,6 +37,7 @@ struct EncArgs {
     uint32_t* bestpre;       // optional: best (len + 18) before LZ4 (k_deflate's threshold)
     uint8_t* gdseq;          // k_deflate: n_chunks x chunk-size scratch for the parse's matches
     uint32_t* z9rec;         // k_z9_parse -> k_z9_code: per-chunk match starts + matches (ambc_zlib9.hip)
+    uint8_t* z9scr;          // chunks > 8192: k_z9_parse_big's scratch, z9_scratch_bytes(cmax, n_chunks)
     uint8_t* pending;        // with k_deflate: 1 = the RLE/Huffman payload was not emitted (id 5 may win)
     uint32_t pref_min[16];
     uint32_t pref_max[16];
@@ -106,6 +107,10 @@ hipError_t launch_dict(const EncArgs& a, uint32_t cmax, hipStream_t s);   // amb
 // record scratch is n_chunks x z9_rec_words(z9_cmax(chunk_size)) u32 words
 uint32_t z9_cmax(uint32_t chunk);   // 0: no zlib-9 encoder for this chunk size
 size_t z9_rec_words(uint32_t cmax);
+// chunks above 8192 (ambc_zlib9_big.hip) also need EncArgs::z9scr
+size_t z9_scratch_bytes(uint32_t cmax, uint32_t n_chunks);
+size_t z9_rec_words_big(uint32_t cmax);
+hipError_t launch_zlib9_big(const EncArgs& a, hipStream_t s);
 hipError_t launch_zlib9(const EncArgs& a, hipStream_t s);
 hipError_t launch_compact(const CompactArgs& a, hipStream_t s);
 hipError_t launch_end_chunk(uint8_t* dst, hipStream_t s);

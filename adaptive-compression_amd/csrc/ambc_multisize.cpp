@@ -54,7 +54,7 @@ int check_size(const ambc_params* p, uint32_t s) {
                                       " bytes with eligible methods: the GPU encoders take chunks up to 65536 bytes");
     if (eligible(p, s, AMBC_M_DEFLATE) && (p->flags & AMBC_FLAG_ZLIB9) && z9_cmax(s) == 0)
         return fail(AMBC_E_INVAL, "a candidate chunk of " + std::to_string(s) +
-                                      " bytes with DEFLATE eligible: the GPU zlib-9 encoder takes chunks up to 8192 bytes");
+                                      " bytes with DEFLATE eligible: the GPU zlib-9 encoder takes chunks up to 65536 bytes");
     if (eligible(p, s, AMBC_M_DICT) && s > 8192)
         return fail(AMBC_E_INVAL, "a candidate chunk of " + std::to_string(s) +
                                       " bytes with Dictionary eligible: the GPU Dictionary encoder takes chunks up to 8192 bytes");
@@ -115,6 +115,10 @@ int launch_batch(Batch& b, hipStream_t st, const uint8_t* d_in, uint64_t n, cons
         if (p->flags & AMBC_FLAG_ZLIB9) {
             HIPCHK(b.z9rec.ensure((size_t)cnt * z9_rec_words(z9_cmax(C)) * 4));
             ea.z9rec = b.z9rec.as<uint32_t>();
+            if (z9_cmax(C) > 8192) {
+                HIPCHK(b.z9scr.ensure(z9_scratch_bytes(z9_cmax(C), cnt)));
+                ea.z9scr = b.z9scr.as<uint8_t>();
+            }
         }
     }
     HIPCHK(launch_encode(ea, st));

@@ -1,0 +1,833 @@
+// ambc_zlib9_big.hip -- zlib.compress(data, 9)'s bytes for chunks of 8193..65536 bytes.
+//
+// The reference's id 5 (advanced_compression.py:76-81) is eligible up to 65536
+// bytes (adaptive_compressor.py:119), and its default walk tries 16 / 32 / 64 KiB
+// candidates (:61-62).  ambc_zlib9.hip keeps the walkers' tables in LDS, which
+// holds them up to 8 KiB; here the same algorithm (oracle/zlib9_model.c, zlib
+// 1.2.11 deflate_slow + _tr_flush_block) runs with the tables in device scratch
+// and adds what only long inputs reach:
+//   - several blocks: zlib flushes a block with its 16383rd symbol (except the
+//     final literal), so a chunk holds up to five blocks, each with its own
+//     trees and stored / static / dynamic choice;
+//   - distances past the window: a chain entry more than MAX_DIST = 32506 back
+//     ends the search;
+//   - the window slide past 65274 bytes (the NIL head at the slide step, no
+//     stored block begun before 32768 once the window slid).
+//
+// k_z9_parse_big<CMAX>: a resident grid of 16-wave workgroups striding over the
+// chunks, each with its own device scratch (Z9Big<CMAX>::BYTES):
+//   1. stable counting sort of positions 1..n-3 by an 11-bit bucket of zlib's
+//      15-bit hash: per-wave counters in LDS (one range of CMAX / 16 positions
+//      per wave, ranks among peers by ballots), the sorted list and every
+//      position's slot in scratch;
+//   2. the chunk in LDS (zeros past n) and the lazy parse by 128 walkers
+//      (8-lane groups, 8 candidates a step, the next step's list entries loaded
+//      one step ahead); segments in scratch;
+//   3. the path from 0: per 64-position window pointer doubling (exits + match
+//      counts to scratch), one thread chains the windows, every window's path
+//      walked on the scalar unit; the matches to the record, symbol starts and
+//      coverage as LDS bitmasks;
+//   4. the blocks: the 16383k-th symbols by a prefix count over the symbol-start
+//      bitmask, each block's range, match rank and stored flag; per-block symbol
+//      counts.
+// k_z9_heap<CMAX> (ambc_z9.h): zlib's heap per (chunk, block), one per lane.
+// k_z9_code_big<CMAX>: one wave per chunk.  Pass 1 builds every block's trees
+// and knows the exact length; a chunk whose id 5 loses stops there.  Pass 2
+// writes the package as one LSB-first bit stream (zlib header, blocks, Adler-32)
+// through a 2 KB LDS ring whose finished words go to the chunk's slot after
+// every 64-position round.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "ambc_internal.h"
+#include "ambc_wave.h"
+#include "ambc_z9.h"
+
+namespace ambc {
+namespace {
+
+constexpr int ZB_NW = 16;                 // waves per chunk in k_z9_parse_big (128 walkers)
+constexpr uint32_t ZB_GRID = 512;         // resident workgroups (2 per CU)
+constexpr uint32_t Z_WSZ = 32768;         // w_size
+constexpr uint32_t Z_SLIDE = 32768 + Z_MAXD;   // strstart that slides the window (65274)
+
+template <int CMAX>
+struct Z9Big {
+    static constexpr uint32_t RANGE = (uint32_t)CMAX / ZB_NW;   // sort positions per wave
+    static constexpr uint32_t NBLK = Z9Rec<CMAX>::NBLK;
+    // device scratch per resident workgroup (bytes)
+    static constexpr size_t LST = 0;                        // u16 [CMAX] positions by bucket (then u32 exits)
+    static constexpr size_t SLOT = LST + 2ull * CMAX;       // u16 [CMAX] position -> index in LST
+    static constexpr size_t SEG = SLOT + 2ull * CMAX;       // u32 [CMAX] the sort's ranks, then segments
+    static constexpr size_t SD = SEG + 4ull * CMAX;         // u16 [CMAX] segment distances
+    static constexpr size_t BYTES = SD + 2ull * CMAX;
+};
+
+template <int CMAX>
+struct Z9BSmem {
+    static constexpr uint32_t NBLK = Z9Rec<CMAX>::NBLK;
+    union {
+        uint16_t cnt[ZB_NW][ZNB];                      // the sort: per-wave bucket cursors
+        alignas(16) uint8_t ch[CMAX + 320];            // the walkers: the chunk, zeros past n
+        struct {                                       // the path
+            uint32_t mask[CMAX / 32];                  // match starts
+            uint32_t cov[CMAX / 32];                   // positions the matches cover
+            uint16_t entry[CMAX / 64], rbase[CMAX / 64];
+            uint32_t lf[NBLK][316];                    // per-block symbol counts
+        } p;
+    };
+    uint32_t bend32[ZNB / 2];                          // bucket ends (u16 pairs)
+    uint32_t bnd[8];                                   // block ends (boundary positions)
+    uint32_t btop[8];                                  // the step top that flushed block b
+    uint32_t nbnd, nmatch;
+    __device__ __forceinline__ uint16_t* bend() { return reinterpret_cast<uint16_t*>(bend32); }
+    __device__ __forceinline__ uint32_t bstart(uint32_t h) { return h ? bend()[h - 1] : 0u; }
+};
+
+__device__ __forceinline__ uint32_t ld_wg(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void st_wg(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// 3-gram at i of the chunk in global memory (i + 2 < n)
+__device__ __forceinline__ uint32_t g_gram(const uint8_t* src, uint32_t i) {
+    return (uint32_t)src[i] | (uint32_t)src[i + 1] << 8 | (uint32_t)src[i + 2] << 16;
+}
+
+// Stable counting sort of positions [1, m) by z_bucket(z_h15): wave w ranks
+// the positions of its range [w RANGE, (w+1) RANGE) in order (ballots over the
+// 11 bucket bits, per-wave LDS cursors); the per-bucket prefix over the waves
+// and the bucket ends; then every position goes to lst[] and its index to slot[].
+template <int CMAX>
+__device__ void z9b_sort(Z9BSmem<CMAX>& S, const uint8_t* src, uint32_t m, uint16_t* lst, uint16_t* slot,
+                         uint32_t* loc, uint32_t wave, uint32_t lane) {
+    constexpr uint32_t T = 64u * ZB_NW, RANGE = Z9Big<CMAX>::RANGE, GR = RANGE / 64;
+    const uint32_t tid = wave * 64u + lane;
+    uint32_t* c32 = reinterpret_cast<uint32_t*>(&S.cnt[0][0]);
+    for (uint32_t b = tid; b < ZB_NW * ZNB / 2; b += T) c32[b] = 0;
+    __syncthreads();
+    const uint64_t below = (1ull << lane) - 1ull;
+    {
+        uint16_t* c = S.cnt[wave];
+#pragma unroll 2
+        for (uint32_t g = 0; g < GR; g++) {
+            const uint32_t i = wave * RANGE + g * 64 + lane;
+            const bool v = i >= 1 && i < m;
+            const uint32_t h = v ? z_bucket(z_h15(g_gram(src, i))) : 0u;
+            uint64_t peers = __ballot(v);
+#pragma unroll
+            for (int b = 0; b < 11; b++) {
+                const uint64_t mb = __ballot(v && ((h >> b) & 1u));
+                peers &= ((h >> b) & 1u) ? mb : ~mb;
+            }
+            const uint32_t base = v ? (uint32_t)c[h] : 0u;
+            if (i < (uint32_t)CMAX) loc[i] = v ? (base + (uint32_t)__popcll(peers & below)) | h << 16 : ~0u;
+            if (v && (peers >> lane) == 1ull) c[h] = (uint16_t)(base + (uint32_t)__popcll(peers));
+        }
+    }
+    __syncthreads();
+    for (uint32_t h = tid; h < ZNB; h += T) {
+        uint32_t run = 0;
+#pragma unroll
+        for (uint32_t r = 0; r < (uint32_t)ZB_NW; r++) {
+            const uint32_t x = S.cnt[r][h];
+            S.cnt[r][h] = (uint16_t)run;
+            run += x;
+        }
+        S.bend()[h] = (uint16_t)run;
+    }
+    __syncthreads();
+    if (wave == 0) {
+        uint32_t c[16], t = 0;
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            c[j] = S.bend32[lane * 16 + j];
+            t += (c[j] & 0xFFFFu) + (c[j] >> 16);
+        }
+        uint32_t run = wave_incl_sum(t) - t;
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const uint32_t r0 = run + (c[j] & 0xFFFFu), r1 = r0 + (c[j] >> 16);
+            S.bend32[lane * 16 + j] = r0 | r1 << 16;
+            run = r1;
+        }
+    }
+    __syncthreads();
+#pragma unroll 2
+    for (uint32_t g = 0; g < GR; g++) {
+        const uint32_t i = wave * RANGE + g * 64 + lane;
+        const uint32_t x = i < (uint32_t)CMAX ? loc[i] : ~0u;   // (this lane's own store)
+        if (x != ~0u) {
+            const uint32_t h = x >> 16;
+            const uint32_t idx = S.bstart(h) + S.cnt[wave][h] + (x & 0xFFFFu);
+            lst[idx] = (uint16_t)i;
+            slot[i] = (uint16_t)idx;
+        }
+    }
+    __syncthreads();
+}
+
+// The lazy parse's walkers (ambc_zlib9.hip z9_walkers, with the list, slots and
+// segments in scratch, the window's MAX_DIST, the slide step's NIL head, and
+// the search stopped at the chain length the step needs).
+template <int CMAX>
+__device__ __forceinline__ void z9b_walkers(Z9BSmem<CMAX>& S, uint32_t n, const uint16_t* lst, const uint16_t* slot,
+                                            uint32_t* seg, uint16_t* sd, uint32_t wave, uint32_t lane) {
+    constexpr uint32_t NWK = (uint32_t)ZB_NW * 8u;
+    const uint32_t* c32 = reinterpret_cast<const uint32_t*>(S.ch);
+    const uint32_t g = lane >> 3, r = lane & 7;
+    const uint32_t wid = wave * 8u + g;
+    // the step at which fill_window slides: the first top s >= 65274 with
+    // lookahead < 262 (65275 for a 65536-byte input); at s = 65274 a hash head of
+    // 32768 reads as NIL (inputs < 65536 only: later heads that far are past MAX_DIST)
+    const uint32_t nil_at = n < 65536u ? Z_SLIDE : 0xFFFFFFFFu;
+    uint32_t q = (uint32_t)(((uint64_t)n * wid) / NWK);
+    uint32_t s = q, P = 2, Pd = 0, c = 0;
+    bool clean = true, done = false;
+#pragma unroll 1
+    for (;;) {
+        if (clean && !done && (q >= n || ld_wg(seg + q) != 0u)) done = true;
+        if (__all(done)) break;
+        const bool act = !done && s >= 1 && s + 3 <= n && P < 258;   // position 0 is zlib's NIL
+        // ---- longest_match(s) over the first `lim` chain entries (4096, or
+        // 1024 when the pending match is >= good_match); key = min(len, nice)
+        // << 16 | candidate: the longest, then the most recent ----
+        uint32_t k0 = 0;
+        {
+            uint32_t tg[4] = {0, 0, 0, 0}, h = 0, lo = 0, j = 0, nice = 0;
+            const uint32_t ss = s & 3u;
+            const uint32_t lim = P >= Z_GOOD ? Z_CHAIN / 4 : Z_CHAIN;
+            if (act) {
+                const uint32_t a = s >> 2;
+                uint32_t w[5];
+#pragma unroll
+                for (int t = 0; t < 5; t++) w[t] = c32[a + t];
+#pragma unroll
+                for (int t = 0; t < 4; t++) tg[t] = __builtin_amdgcn_alignbyte(w[t + 1], w[t], ss);
+                h = z_h15(tg[0] & 0xFFFFFFu);
+                lo = S.bstart(z_bucket(h));
+                j = slot[s];
+                nice = min(Z_MAXM, n - s);
+            }
+            bool gd = !act || j <= lo;
+            uint32_t cnt = 0;
+            int idx = (int)j - 1 - (int)r;
+            uint32_t cpre = !gd && idx >= (int)lo ? (uint32_t)lst[idx] : 0u;
+#pragma unroll 1
+            while (__any(!gd)) {
+                const bool v = !gd && idx >= (int)lo;
+                const uint32_t c = v ? cpre : 0u;
+                idx -= 8;
+                cpre = !gd && idx >= (int)lo ? (uint32_t)lst[idx] : 0u;   // the next step's, issued now
+                const uint32_t a = c >> 2, sh = c & 3u;
+                uint32_t w[5];
+#pragma unroll
+                for (int t = 0; t < 5; t++) w[t] = c32[a + t];
+                uint32_t x[4];
+#pragma unroll
+                for (int t = 0; t < 4; t++) x[t] = __builtin_amdgcn_alignbyte(w[t + 1], w[t], sh);
+                const bool same = v && z_h15(x[0] & 0xFFFFFFu) == h;
+                const uint32_t sm = grp8(__ballot(same), g);
+                const uint32_t kidx = cnt + (uint32_t)__popc(sm & ((1u << r) - 1u)) + 1u;
+                // the hash head may lie MAX_DIST back (deflate_slow's test is <=);
+                // later chain entries must lie above limit = s - MAX_DIST
+                const bool inwin = s - c < Z_MAXD || (s - c == Z_MAXD && kidx == 1u);
+                const bool ok = same && inwin && kidx <= lim;
+                // the slide step: a head of 32768 is NIL, no search at all
+                const bool nilh = grp8(__ballot(same && kidx == 1u && c == Z_WSZ && s == nil_at), g) != 0;
+                uint32_t fm = ~0u;
+#pragma unroll
+                for (int t = 0; t < 4; t++) fm = min(fm, ffbl_raw(x[t] ^ tg[t]) | (uint32_t)t << 5);
+                uint32_t len = fm == ~0u ? 16u : fm >> 3;
+                const uint32_t best = k0 >> 16;
+                const bool can = best < 16 || S.ch[c + best] == S.ch[s + best];
+                bool ext = ok && fm == ~0u && can && !nilh;
+#pragma unroll 1
+                while (__any(ext)) {
+                    if (ext) {
+                        const uint32_t ac = (c + len) >> 2, as = (s + len) >> 2;
+                        uint32_t wc[5], ws[5];
+#pragma unroll
+                        for (int t = 0; t < 5; t++) { wc[t] = c32[ac + t]; ws[t] = c32[as + t]; }
+                        uint32_t f = ~0u;
+#pragma unroll
+                        for (int t = 0; t < 4; t++)
+                            f = min(f, ffbl_raw(__builtin_amdgcn_alignbyte(wc[t + 1], wc[t], sh) ^
+                                                __builtin_amdgcn_alignbyte(ws[t + 1], ws[t], ss)) |
+                                           (uint32_t)t << 5);
+                        if (f != ~0u) { len += f >> 3; ext = false; }
+                        else { len += 16; if (len >= Z_MAXM) ext = false; }
+                    }
+                }
+                const uint32_t Lp = min(min(len, Z_MAXM), nice);
+                const uint32_t key = ok && can && !nilh ? (Lp << 16 | c) : 0u;
+                k0 = nilh ? 0u : max(k0, grp_max8(key));
+                cnt += (uint32_t)__popc(sm);
+                const uint32_t far = grp8(__ballot(v && s - c >= Z_MAXD), g);
+                j = j > lo + 8 ? j - 8 : lo;
+                gd = gd || nilh || j <= lo || far != 0 || cnt >= lim || (k0 >> 16) >= nice;
+            }
+        }
+        if (!done) {
+            uint32_t ML = 2, MD = 0;
+            if (act) {
+                const uint32_t L = k0 >> 16, d = s - (k0 & 0xFFFFu);
+                if (L >= 3 && !(L == 3 && d > Z_TOOFAR)) { ML = L; MD = d; }
+            }
+            if (clean) {
+                if (ML < 3) {
+                    if (r == 0) st_wg(seg + q, 0x80000000u | 1u);
+                    q++;
+                    s = q;
+                } else {
+                    P = ML;
+                    Pd = MD;
+                    c = 0;
+                    s = q + 1;
+                    clean = false;
+                }
+            } else if (ML <= P) {
+                if (r == 0) {
+                    sd[q] = (uint16_t)Pd;
+                    st_wg(seg + q, 0x80000000u | P << 16 | c);
+                }
+                q = s - 1 + P;
+                s = q;
+                P = 2;
+                clean = true;
+            } else {
+                c++;
+                P = ML;
+                Pd = MD;
+                s++;
+            }
+        }
+    }
+}
+
+template <int CMAX>
+__global__ __launch_bounds__(64 * ZB_NW) void k_z9_parse_big(EncArgs A) {
+    constexpr uint32_t NW = ZB_NW, TT = 64u * NW;
+    constexpr uint32_t NBLK = Z9Rec<CMAX>::NBLK;
+    __shared__ Z9BSmem<CMAX> S;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint64_t below = (1ull << lane) - 1ull;
+    uint8_t* scr = A.z9scr + (uint64_t)blockIdx.x * Z9Big<CMAX>::BYTES;
+    uint16_t* lst = reinterpret_cast<uint16_t*>(scr + Z9Big<CMAX>::LST);
+    uint16_t* slot = reinterpret_cast<uint16_t*>(scr + Z9Big<CMAX>::SLOT);
+    uint32_t* seg = reinterpret_cast<uint32_t*>(scr + Z9Big<CMAX>::SEG);
+    uint16_t* sd = reinterpret_cast<uint16_t*>(scr + Z9Big<CMAX>::SD);
+    uint32_t* xit = reinterpret_cast<uint32_t*>(scr + Z9Big<CMAX>::LST);   // after the walkers
+#pragma unroll 1
+    for (uint32_t k = blockIdx.x; k < A.n_chunks; k += gridDim.x) {
+        __syncthreads();   // (the previous chunk's last LDS reads)
+        const uint64_t pos0 = A.coff ? A.coff[k] : (uint64_t)k * A.chunk_size;
+        const uint32_t n = A.coff ? A.clen[k] : (uint32_t)min((uint64_t)A.chunk_size, A.n_total - pos0);
+        uint32_t T = 0;
+        if (n > (uint32_t)CMAX || !z9_gate(A, k, n, T)) continue;
+        const uint8_t* src = A.in + pos0;
+        // ---- 1. the sort (the ranks go through seg[]) ----
+        z9b_sort(S, src, n - 2, lst, slot, seg, wave, lane);
+        // ---- 2. the chunk in LDS, cleared segments, the walkers ----
+        if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+            const uint32_t nv = n >> 4;
+            for (uint32_t q = threadIdx.x; q < nv; q += TT)
+                reinterpret_cast<uint4*>(S.ch)[q] = reinterpret_cast<const uint4*>(src)[q];
+            for (uint32_t i = (nv << 4) + threadIdx.x; i < n; i += TT) S.ch[i] = src[i];
+        } else {
+            for (uint32_t i = threadIdx.x; i < n; i += TT) S.ch[i] = src[i];
+        }
+        for (uint32_t i = n + threadIdx.x; i < (uint32_t)CMAX + 320; i += TT) S.ch[i] = 0;
+        for (uint32_t i = threadIdx.x; i < n; i += TT) seg[i] = 0;
+        __syncthreads();
+        z9b_walkers(S, n, lst, slot, seg, sd, wave, lane);
+        __syncthreads();
+        // ---- 3. the path from 0 (as ambc_zlib9.hip, the exits in scratch) ----
+        const uint32_t nwin = (n + 63) / 64;
+        for (uint32_t w = wave; w < nwin; w += NW) {
+            const uint32_t p = w * 64 + lane;
+            const uint32_t t = p < n ? seg[p] : 0u;
+            uint32_t J = t ? lane + (t & 0xFFFFu) + ((t >> 16) & 0x1FFu) : lane + 1;
+            uint32_t M = (t >> 16) & 0x1FFu ? 1u : 0u;
+#pragma unroll
+            for (int it = 0; it < 6; it++) {
+                const int srcl = (int)(min(J, 63u) << 2);
+                const uint32_t Jj = (uint32_t)__builtin_amdgcn_ds_bpermute(srcl, (int)J);
+                const uint32_t Mj = (uint32_t)__builtin_amdgcn_ds_bpermute(srcl, (int)M);
+                M = J < 64 ? M + Mj : M;
+                J = J < 64 ? Jj : J;
+            }
+            xit[p] = (w * 64 + J) | M << 24;
+        }
+        // (the chunk bytes are dead: the path arrays take their LDS)
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < (uint32_t)CMAX / 64; i += TT) S.p.entry[i] = 0xFFFFu;
+        for (uint32_t i = threadIdx.x; i < (uint32_t)CMAX / 32; i += TT) { S.p.mask[i] = 0; S.p.cov[i] = 0; }
+        for (uint32_t i = threadIdx.x; i < NBLK * 316; i += TT) (&S.p.lf[0][0])[i] = 0;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t cur = 0, mr = 0;
+            while (cur < n) {
+                S.p.entry[cur >> 6] = (uint16_t)(cur & 63u);
+                S.p.rbase[cur >> 6] = (uint16_t)mr;
+                const uint32_t x = xit[cur];
+                mr += x >> 24;
+                cur = x & 0xFFFFFFu;
+            }
+            S.nmatch = mr;
+        }
+        __syncthreads();
+        uint32_t* R = A.z9rec + (uint64_t)k * Z9Rec<CMAX>::STRIDE;
+        for (uint32_t w = wave; w < nwin; w += NW) {
+            const uint32_t e = S.p.entry[w];
+            if (e == 0xFFFFu) continue;
+            const uint32_t p = w * 64 + lane;
+            const uint32_t t = p < n ? seg[p] : 0u;
+            const uint32_t c = t & 0xFFFFu, L = (t >> 16) & 0x1FFu;
+            const uint32_t J1 = lane + max(1u, c + L);
+            uint64_t on = 0;
+            for (uint32_t q = e; q < 64;) {
+                on |= 1ull << q;
+                q = readlane(J1, q);
+            }
+            const bool mt = ((on >> lane) & 1u) && L != 0;
+            const uint64_t mm = __ballot(mt);
+            if (mt) {
+                const uint32_t ms = p + c, d = sd[p];
+                atomicOr(&S.p.mask[ms >> 5], 1u << (ms & 31));
+                R[Z9Rec<CMAX>::MATCH + S.p.rbase[w] + (uint32_t)__popcll(mm & below)] = L | d << 16;
+                for (uint32_t b = ms, e2 = ms + L; b < e2;) {
+                    const uint32_t wd = b >> 5, hi = min(e2, (wd + 1) * 32);
+                    const uint32_t bits = (hi - b == 32 ? ~0u : ((1u << (hi - b)) - 1u)) << (b & 31);
+                    atomicOr(&S.p.cov[wd], bits);
+                    b = hi;
+                }
+            }
+        }
+        __syncthreads();
+        // ---- 4. the blocks: a block ends with its 16383rd symbol (a literal
+        // or a match start: every position no match covers, and every match
+        // start), except the final literal at n - 1 (tallied without the flush
+        // check).  Wave 0 counts symbol starts 64 words at a time. ----
+        if (wave == 0) {
+            const uint32_t nwd = (n + 31) / 32;
+            uint32_t base = 0, want = Z_BLKSYM, nb = 0, mbase = 0;
+            for (uint32_t w0 = 0; w0 < nwd && nb < NBLK - 1; w0 += 64) {
+                const uint32_t w = w0 + lane;
+                uint32_t sym = 0, mk = 0;
+                if (w < nwd) {
+                    const uint32_t valid = (w + 1) * 32 <= n ? ~0u : ((1u << (n & 31)) - 1u);
+                    mk = S.p.mask[w];
+                    sym = (~S.p.cov[w] | mk) & valid;
+                }
+                const uint32_t cs = (uint32_t)__popc(sym), cm = (uint32_t)__popc(mk);
+                const uint32_t incl = wave_incl_sum(cs), minc = wave_incl_sum(cm);
+                while (nb < NBLK - 1) {
+                    const uint64_t hit = __ballot(base + incl >= want && base + incl - cs < want);
+                    if (!hit) break;
+                    const uint32_t hl = (uint32_t)__builtin_ctzll(hit);
+                    // the (want - before)-th set bit of that word
+                    uint32_t x = readlane(sym, hl), need = want - (base + readlane(incl, hl) - readlane(cs, hl));
+                    while (--need) x &= x - 1u;
+                    const uint32_t bit = (uint32_t)__builtin_ctz(x);
+                    const uint32_t p = (w0 + hl) * 32 + bit;
+                    const uint32_t mw = readlane(mk, hl);
+                    if ((mw >> bit) & 1u) {
+                        const uint32_t rank = mbase + readlane(minc, hl) - readlane(cm, hl) +
+                                              (uint32_t)__popc(mw & ((1u << bit) - 1u));
+                        const uint32_t L = R[Z9Rec<CMAX>::MATCH + rank] & 0xFFFFu;
+                        if (lane == 0) { S.bnd[nb] = p + L; S.btop[nb] = p + 1; }
+                    } else {
+                        if (p + 1 == n) break;   // the final literal: no flush
+                        if (lane == 0) { S.bnd[nb] = p + 1; S.btop[nb] = p + 1; }
+                    }
+                    nb++;
+                    want += Z_BLKSYM;
+                }
+                base += readlane(incl, 63);
+                mbase += readlane(minc, 63);
+            }
+            if (lane == 0) S.nbnd = nb;
+        }
+        __syncthreads();
+        const uint32_t nbnd = S.nbnd;
+        // per-block symbol counts: literals (positions no match covers) by position
+        for (uint32_t i = threadIdx.x; i < n; i += TT) {
+            if ((S.p.cov[i >> 5] >> (i & 31)) & 1u) continue;
+            uint32_t b = 0;
+            for (uint32_t q = 0; q < nbnd; q++) b += i >= S.bnd[q] ? 1u : 0u;
+            atomicAdd(&S.p.lf[b][src[i]], 1u);
+        }
+        {
+            // matches by their start: each wave takes 64 mask words at a time,
+            // ranks from the popcounts of the words below
+            for (uint32_t w0 = wave * 64; w0 < (n + 31) / 32; w0 += NW * 64) {
+                const uint32_t w = w0 + lane;
+                const uint32_t mk = w < (n + 31) / 32 ? S.p.mask[w] : 0u;
+                // matches before word w0: sum of the popcounts of the words below
+                uint32_t pre = 0;
+                for (uint32_t q = lane; q < w0; q += 64) pre += (uint32_t)__popc(S.p.mask[q]);
+                pre = wave_sum_u32(pre);
+                const uint32_t cm = (uint32_t)__popc(mk);
+                uint32_t rank = pre + wave_incl_sum(cm) - cm;
+                uint32_t x = mk;
+                while (x) {
+                    const uint32_t bit = (uint32_t)__builtin_ctz(x);
+                    x &= x - 1u;
+                    const uint32_t ms = w * 32 + bit;
+                    const uint32_t rc = R[Z9Rec<CMAX>::MATCH + rank++];
+                    const uint32_t L = rc & 0xFFFFu, d = rc >> 16;
+                    uint32_t b = 0;
+                    for (uint32_t q = 0; q < nbnd; q++) b += ms >= S.bnd[q] ? 1u : 0u;
+                    atomicAdd(&S.p.lf[b][257 + z_lcode(L)], 1u);
+                    atomicAdd(&S.p.lf[b][286 + z_dcode(d)], 1u);
+                }
+            }
+        }
+        for (uint32_t i = threadIdx.x; i < (uint32_t)CMAX / 32; i += TT) R[Z9Rec<CMAX>::MASK + i] = S.p.mask[i];
+        if (threadIdx.x == 0) {
+            R[0] = S.nmatch;
+            R[1] = nbnd + 1;
+        }
+        if (threadIdx.x <= nbnd) {
+            // block b = threadIdx.x: [bs, be), matches before it, the stored flag
+            const uint32_t b = threadIdx.x;
+            const uint32_t bs = b ? S.bnd[b - 1] : 0u, be = b < nbnd ? S.bnd[b] : n;
+            const uint32_t top = b < nbnd ? S.btop[b] : n;
+            const uint32_t thr = n == 65536u ? Z_SLIDE + 1 : Z_SLIDE;
+            uint32_t mb = 0;   // match starts below bs
+            for (uint32_t q = 0; q < (bs >> 5); q++) mb += (uint32_t)__popc(S.p.mask[q]);
+            if (bs & 31) mb += (uint32_t)__popc(S.p.mask[bs >> 5] & ((1u << (bs & 31)) - 1u));
+            uint32_t* B = R + Z9Rec<CMAX>::BLK + 4 * b;
+            B[0] = bs;
+            B[1] = be;
+            B[2] = mb;
+            B[3] = (top >= thr && bs < Z_WSZ) ? Z9B_NOSTORE : 0u;
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < 158 * (nbnd + 1); i += TT) {
+            const uint32_t b = i / 158, o = i % 158;
+            R[Z9Rec<CMAX>::FREQ + i] = S.p.lf[b][2 * o] | S.p.lf[b][2 * o + 1] << 16;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_z9_code_big: trees per block, the exact length, then the bits through a ring
+constexpr uint32_t ZR_W = 512;   // ring words (2 KB): a round writes <= 96, a header <= 150
+
+template <int CMAX>
+struct Z9BCSmem {
+    static constexpr uint32_t NB = Z9Rec<CMAX>::NBLK;
+    alignas(16) uint32_t ring[ZR_W];
+    uint32_t mstart[CMAX / 32 + 2];
+    uint32_t ecl[288], ecd[32];
+    uint32_t heapL[LT_N + 1], heapD[DT_N + 1];
+    uint16_t lfreq[LT_N + 1], ldad[LT_N + 1];
+    uint16_t dfreq[DT_N + 1], ddad[DT_N + 1];
+    uint16_t bfreq[BT_N + 1], bdad[BT_N + 1];
+    uint16_t blcL[16], blcD[16], blcB[16];
+    uint16_t pjd[LT_N + 3], pja[LT_N + 3];
+    uint32_t blc32[16], cnt32[20];
+    uint32_t misc[16];
+    // per block: code lengths and codes of the three trees, the header numbers
+    uint8_t llen[NB][LT_N + 1], dlen[NB][DT_N + 1], blen[NB][BT_N + 1];
+    uint16_t lcode[NB][288], dcode[NB][32], bcode[NB][20];
+    uint32_t kind[NB], lmax[NB], dmax[NB], maxbl[NB];
+};
+
+template <int CMAX>
+__global__ __launch_bounds__(64) void k_z9_code_big(EncArgs A) {
+    constexpr uint32_t RM = ZR_W - 1;
+    __shared__ Z9BCSmem<CMAX> S;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t k = blockIdx.x;
+    const uint64_t pos0 = A.coff ? A.coff[k] : (uint64_t)k * A.chunk_size;
+    const uint32_t n = A.coff ? A.clen[k] : (uint32_t)min((uint64_t)A.chunk_size, A.n_total - pos0);
+    uint32_t T = 0;
+    if (n > (uint32_t)CMAX || !z9_gate(A, k, n, T)) return;
+    const uint8_t* src = A.in + pos0;
+    const uint32_t* R = A.z9rec + (uint64_t)k * Z9Rec<CMAX>::STRIDE;
+    const uint32_t* rec = R + Z9Rec<CMAX>::MATCH;
+    const uint32_t nblk = uniform_u32(R[1]);
+    const uint64_t below = (1ull << lane) - 1ull;
+    l32* W = (l32*)S.ring;
+    for (uint32_t i = lane; i < (uint32_t)CMAX / 32 + 2; i += 64)
+        S.mstart[i] = i < (uint32_t)CMAX / 32 ? R[Z9Rec<CMAX>::MASK + i] : 0u;
+    for (uint32_t i = lane; i < ZR_W; i += 64) S.ring[i] = 0;
+    wave_sync();
+
+    // ---- pass 1: every block's trees, kind and bits ----
+    uint32_t bp = 16;   // after the zlib header
+    for (uint32_t b = 0; b < nblk; b++) {
+        const uint32_t* B = R + Z9Rec<CMAX>::BLK + 4 * b;
+        const uint32_t bs = uniform_u32(B[0]), be = uniform_u32(B[1]), fl = uniform_u32(B[3]);
+        const Z9Tree LT{(l16*)S.lfreq, (l16*)S.ldad, (l8*)S.llen[b], (l16*)S.lcode[b], (l32*)S.heapL, (l16*)S.blcL};
+        const Z9Tree DT{(l16*)S.dfreq, (l16*)S.ddad, (l8*)S.dlen[b], (l16*)S.dcode[b], (l32*)S.heapD, (l16*)S.blcD};
+        const Z9Tree BT{(l16*)S.bfreq, (l16*)S.bdad, (l8*)S.blen[b], (l16*)S.bcode[b], (l32*)S.heapD, (l16*)S.blcB};
+        const uint16_t* F = reinterpret_cast<const uint16_t*>(R + Z9Rec<CMAX>::FREQ + 158 * b);
+        const uint32_t* MG = R + Z9Rec<CMAX>::MERGE + 316 * b;
+        if (lane < 20) S.cnt32[lane] = 0;
+        for (uint32_t i = lane; i < 286; i += 64) S.lfreq[i] = (uint16_t)(F[i] + (i == 256 ? 1u : 0u));
+        if (lane < 30) S.dfreq[lane] = F[286 + lane];
+        wave_sync();
+        l16* PJD = (l16*)S.pjd;
+        l16* PJA = (l16*)S.pja;
+        l32* BLC = (l32*)S.blc32;
+        l32* MISC = (l32*)(S.misc + 12);
+        uint32_t optL = 0, statL = 0, optD = 0, statD = 0, optB = 0, statB = 0;
+        const int lmax = z9_build_w<5, true>(LT, PJD, PJA, BLC, MISC, 286, 15, 0, optL, statL, lane, MG);
+        const int dmax = z9_build_w<1, true>(DT, PJD, PJA, BLC, MISC, 30, 15, 1, optD, statD, lane, MG + 285);
+        VHeap<5> LL;
+        VHeap<1> DL;
+#pragma unroll
+        for (int j = 0; j < 5; j++) {
+            const uint32_t x = 64u * j + lane;
+            LL.h[j] = (int)x <= lmax ? (uint32_t)S.llen[b][x] : 0u;
+        }
+        DL.h[0] = (int)lane <= dmax ? (uint32_t)S.dlen[b][lane] : 0u;
+        (void)z9_rle_par(LL, lmax, false, (l32*)S.cnt32, 0u, S.ring, 0u, lane);
+        (void)z9_rle_par(DL, dmax, false, (l32*)S.cnt32, 0u, S.ring, 0u, lane);
+        wave_sync();
+        if (lane < 19) S.bfreq[lane] = (uint16_t)S.cnt32[lane];
+        wave_sync();
+        (void)z9_build_w<1, false>(BT, PJD, PJA, BLC, MISC, 19, 7, 2, optB, statB, lane);
+        int maxbl;
+        for (maxbl = 18; maxbl >= 3; maxbl--) if (S.blen[b][z_blord[maxbl]] != 0) break;
+        const uint32_t opt = optL + optD + optB + 3u * (uint32_t)(maxbl + 1) + 5 + 5 + 4;
+        const uint32_t stl = statL + statD;
+        uint32_t opt_lenb = (opt + 3 + 7) >> 3;
+        const uint32_t static_lenb = (stl + 3 + 7) >> 3;
+        if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
+        const uint32_t kind = (be - bs + 4 <= opt_lenb && !(fl & Z9B_NOSTORE)) ? 0u : (static_lenb == opt_lenb ? 1u : 2u);
+        if (lane == 0) {
+            S.kind[b] = kind;
+            S.lmax[b] = (uint32_t)lmax;
+            S.dmax[b] = (uint32_t)dmax;
+            S.maxbl[b] = (uint32_t)maxbl;
+        }
+        if (kind == 0) bp = ((bp + 3 + 7) & ~7u) + 32 + 8 * (be - bs);
+        else bp += 3 + (kind == 2 ? opt : stl);
+        wave_sync();
+    }
+    const uint32_t total = (bp + 7) / 8 + 4;
+    if (total + 18 >= T) return;
+
+    // ---- pass 2: the bits ----
+    uint32_t* out32 = reinterpret_cast<uint32_t*>(A.slots + (uint64_t)k * A.slot_stride);
+    uint32_t flushed = 0;   // words [0, flushed) are in the slot
+    auto flush = [&](uint32_t upto) {
+        wave_sync();
+        for (uint32_t w = flushed + lane; w < upto; w += 64) {
+            out32[w] = S.ring[w & RM];
+            S.ring[w & RM] = 0;
+        }
+        wave_sync();
+        flushed = upto;
+    };
+    if (lane == 0) z_put(W, 0, 0xDA78u, 16, RM);   // 78 DA
+    bp = 16;
+    for (uint32_t b = 0; b < nblk; b++) {
+        const uint32_t* B = R + Z9Rec<CMAX>::BLK + 4 * b;
+        const uint32_t bs = uniform_u32(B[0]), be = uniform_u32(B[1]), rank0 = uniform_u32(B[2]);
+        const uint32_t last = b + 1 == nblk ? 1u : 0u;
+        const uint32_t kind = uniform_u32(S.kind[b]);
+        wave_sync();
+        if (kind == 0) {
+            // stored: 3 bits, byte alignment, LEN / NLEN, the bytes
+            const uint32_t len = be - bs;
+            if (lane == 0) z_put(W, bp, last, 3, RM);
+            bp = (bp + 3 + 7) & ~7u;
+            if (lane == 0) z_put(W, bp, len | (~len & 0xFFFFu) << 16, 32, RM);
+            bp += 32;
+            for (uint32_t r0 = 0; r0 < len; r0 += 64) {
+                wave_sync();
+                const uint32_t i = r0 + lane;
+                if (i < len) z_put_atomic(S.ring, bp + 8 * i, src[bs + i], 8, RM);
+                flush((bp + 8 * min(len, r0 + 64)) >> 5);
+            }
+            bp += 8 * len;
+            flush(bp >> 5);
+            continue;
+        }
+        if (kind == 1) {
+            for (uint32_t i = lane; i < 288; i += 64) {
+                uint32_t c, l;
+                if (i < 144) { c = 0x30 + i; l = 8; }
+                else if (i < 256) { c = 0x190 + (i - 144); l = 9; }
+                else if (i < 280) { c = i - 256; l = 7; }
+                else { c = 0xC0 + (i - 280); l = 8; }
+                S.ecl[i] = (__builtin_bitreverse32(c) >> (32 - l)) | l << 16;
+            }
+            if (lane < 30) S.ecd[lane] = (__builtin_bitreverse32(lane) >> 27) | 5u << 16;
+        } else {
+            for (uint32_t i = lane; i < 286; i += 64) S.ecl[i] = S.lcode[b][i] | (uint32_t)S.llen[b][i] << 16;
+            if (lane < 30) S.ecd[lane] = S.dcode[b][lane] | (uint32_t)S.dlen[b][lane] << 16;
+        }
+        wave_sync();
+        {
+            // the block header on the scalar unit
+            SBits sb{0ull, bp & 31u, bp >> 5};
+            sb.acc = sb.n ? (uint64_t)(S.ring[sb.w & RM] & ((1u << sb.n) - 1u)) : 0ull;
+            sb_put(sb, W, kind << 1 | last, 3, lane, RM);
+            if (kind == 2) {
+                const int lmax = (int)uniform_u32(S.lmax[b]), dmax = (int)uniform_u32(S.dmax[b]);
+                const int maxbl = (int)uniform_u32(S.maxbl[b]);
+                sb_put(sb, W, (uint32_t)lmax + 1 - 257, 5, lane, RM);
+                sb_put(sb, W, (uint32_t)dmax, 5, lane, RM);
+                sb_put(sb, W, (uint32_t)maxbl + 1 - 4, 4, lane, RM);
+                for (int r = 0; r <= maxbl; r++) sb_put(sb, W, S.blen[b][z_blord[r]], 3, lane, RM);
+                const uint32_t bcl = lane < 19 ? (uint32_t)S.bcode[b][lane] | (uint32_t)S.blen[b][lane] << 16 : 0u;
+                if (sb.n && lane == 0) W[sb.w & RM] = (uint32_t)sb.acc;
+                wave_sync();
+                VHeap<5> LL;
+                VHeap<1> DL;
+#pragma unroll
+                for (int j = 0; j < 5; j++) {
+                    const uint32_t x = 64u * j + lane;
+                    LL.h[j] = (int)x <= lmax ? (uint32_t)S.llen[b][x] : 0u;
+                }
+                DL.h[0] = (int)lane <= dmax ? (uint32_t)S.dlen[b][lane] : 0u;
+                uint32_t p = sb.w * 32 + sb.n;
+                p += z9_rle_par(LL, lmax, true, (l32*)S.cnt32, bcl, S.ring, p, lane, RM);
+                wave_sync();
+                p += z9_rle_par(DL, dmax, true, (l32*)S.cnt32, bcl, S.ring, p, lane, RM);
+                bp = p;
+            } else {
+                if (sb.n && lane == 0) W[sb.w & RM] = (uint32_t)sb.acc;
+                bp = sb.w * 32 + sb.n;
+            }
+        }
+        flush(bp >> 5);
+        // the block's symbols over [bs, be), position-major, 64 positions a round
+        {
+            uint32_t rank = rank0;
+            int carry = (int)bs;
+            auto fetch = [&](uint32_t q0, uint32_t rk, uint64_t& bmo, uint32_t& xo, uint32_t& co) {
+                const uint32_t pos = q0 + lane;
+                const bool in = pos >= bs && pos < be;
+                const bool m = in && ((S.mstart[pos >> 5] >> (pos & 31)) & 1u);
+                bmo = __ballot(m);
+                xo = m ? rec[rk + (uint32_t)__popcll(bmo & below)] : 0u;
+                co = in ? (uint32_t)src[pos] : 0u;
+            };
+            uint64_t bmn = 0;
+            uint32_t xn = 0, cn = 0;
+            fetch(bs & ~63u, rank, bmn, xn, cn);
+#pragma unroll 1
+            for (uint32_t p0 = bs & ~63u; p0 < be; p0 += 64) {
+                const uint64_t bm = bmn;
+                const uint32_t x = xn, cb = cn;
+                const uint32_t rank2 = rank + (uint32_t)__popcll(bm);
+                if (p0 + 64 < be) fetch(p0 + 64, rank2, bmn, xn, cn);
+                const uint32_t pos = p0 + lane;
+                const bool in = pos >= bs && pos < be;
+                const bool ms = (bm >> lane) & 1u;
+                const uint32_t L = ms ? x & 0xFFFFu : 0u, d = x >> 16;
+                const int e = ms ? (int)(pos + L) : 0;
+                const int E = max(carry, wave_incl_max_i32(e));
+                carry = max(carry, wave_max_i32(e));
+                rank = rank2;
+                const bool lit = in && !ms && E <= (int)pos;
+                const uint32_t c = lit ? cb : 0u;
+                const uint32_t lc = ms ? z_lcode(L) : 0u, dc = ms ? z_dcode(d) : 0u;
+                uint32_t e1 = 0, e2 = 0, v1 = 0, v2 = 0;
+                if (lit) {
+                    e1 = S.ecl[c] >> 16;
+                    v1 = S.ecl[c] & 0xFFFFu;
+                } else if (ms) {
+                    const uint32_t a = S.ecl[257 + lc], bb = S.ecd[dc];
+                    const uint32_t la = a >> 16, lb = bb >> 16;
+                    const uint32_t xl = z_xlb(lc), xd = z_xdb(dc);
+                    e1 = la + xl;
+                    v1 = (a & 0xFFFFu) | ((L - 3) & ((1u << xl) - 1u)) << la;
+                    e2 = lb + xd;
+                    v2 = (bb & 0xFFFFu) | ((d - 1) & ((1u << xd) - 1u)) << lb;
+                }
+                const uint32_t cost = e1 + e2;
+                const uint32_t incl = wave_incl_sum(cost);
+                const uint32_t q = bp + incl - cost;
+                z_put_atomic(S.ring, q, v1, e1, RM);
+                z_put_atomic(S.ring, q + e1, v2, e2, RM);
+                bp += readlane(incl, 63);
+                flush(bp >> 5);
+            }
+        }
+        wave_sync();
+        if (lane == 0) z_put(W, bp, S.ecl[256] & 0xFFFFu, S.ecl[256] >> 16, RM);
+        bp += S.ecl[256] >> 16;
+    }
+    // ---- Adler-32 of the chunk, big-endian after the byte boundary ----
+    uint32_t adler;
+    {
+        uint64_t asum = 0, bsum = 0;
+        for (uint32_t i = lane; i < n; i += 64) {
+            const uint32_t c = src[i];
+            asum += c;
+            bsum += (uint64_t)(n - i) * c;
+        }
+        asum = wave_sum<uint64_t>(asum);
+        bsum = wave_sum<uint64_t>(bsum);
+        adler = (uint32_t)(((n + bsum) % 65521) << 16 | ((1 + asum) % 65521));
+    }
+    bp = (bp + 7) & ~7u;
+    wave_sync();
+    if (lane == 0)
+        for (int i = 0; i < 4; i++) z_put(W, bp + 8 * i, (adler >> (24 - 8 * i)) & 0xFFu, 8, RM);
+    bp += 32;
+    flush((bp + 31) >> 5);
+    if (lane == 0) {
+        A.ids[k] = 5;
+        A.plen[k] = total;
+        A.sizes[k] = 18ull + total;
+    }
+}
+
+template <int CMAX>
+hipError_t launch_z9b_t(const EncArgs& a, hipStream_t s) {
+    const uint32_t g = min(a.n_chunks, ZB_GRID);
+    constexpr uint32_t NB = Z9Rec<CMAX>::NBLK;
+    hipLaunchKernelGGL(k_z9_parse_big<CMAX>, dim3(g), dim3(64 * ZB_NW), 0, s, a);
+    hipLaunchKernelGGL(k_z9_heap<CMAX>, dim3((a.n_chunks * NB + 63) / 64), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_z9_code_big<CMAX>, dim3(a.n_chunks), dim3(64), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+size_t z9_scratch_bytes(uint32_t cmax, uint32_t n_chunks) {
+    const size_t g = std::min<size_t>(n_chunks, ZB_GRID);
+    switch (cmax) {
+        case 16384: return g * Z9Big<16384>::BYTES;
+        case 32768: return g * Z9Big<32768>::BYTES;
+        case 65536: return g * Z9Big<65536>::BYTES;
+        default: return 0;
+    }
+}
+
+size_t z9_rec_words_big(uint32_t cmax) {
+    switch (cmax) {
+        case 16384: return Z9Rec<16384>::STRIDE;
+        case 32768: return Z9Rec<32768>::STRIDE;
+        case 65536: return Z9Rec<65536>::STRIDE;
+        default: return 0;
+    }
+}
+
+hipError_t launch_zlib9_big(const EncArgs& a, hipStream_t s) {
+    if (a.n_chunks == 0) return hipSuccess;
+    if (!a.z9scr) return hipErrorInvalidValue;
+    switch (z9_cmax(a.chunk_size)) {
+        case 16384: return launch_z9b_t<16384>(a, s);
+        case 32768: return launch_z9b_t<32768>(a, s);
+        case 65536: return launch_z9b_t<65536>(a, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace ambc

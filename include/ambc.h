@@ -56,7 +56,7 @@ extern "C" {
 
 #define AMBC_FLAG_NO_END_CHUNK 1u /* shard bodies for multi-GPU reassembly */
 #define AMBC_FLAG_ZLIB9 2u        /* id 5 = zlib.compress(data, 9)'s own bytes (the reference's,
-                                     advanced_compression.py:76-81; chunk_size <= 4096) instead
+                                     advanced_compression.py:76-81; chunk_size <= 65536) instead
                                      of "ambc-deflate v1" */
 
 /* GPU-routable method ids (bit i of method_mask = method id i) */
@@ -65,7 +65,7 @@ extern "C" {
 #define AMBC_M_HUFFMAN 3
 #define AMBC_M_DELTA 4 /* never selected: payload length == n (compression_methods.py:598-608) */
 #define AMBC_M_DEFLATE 5 /* GPU encoder "ambc-deflate v1" (chunk_size <= 65536) or zlib-9 (AMBC_FLAG_ZLIB9,
-                           <= 8192); decode: GPU inflate (packages <= 65536) */
+                           <= 65536); decode: GPU inflate (packages <= 65536) */
 #define AMBC_M_LZ4 9
 #define AMBC_M_RAW 255
 
@@ -129,8 +129,8 @@ int ambc_compress_batch(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const ambc
  * ignored).  ent_sizes/ent_tabs: optional numpy-exact p*log2(p) tables for the
  * chunk sizes Huffman may take (see ambc_params.ent_full).  Writes the .ambc
  * body (packages + end chunk); AMBC_E_INVAL when a size the walk needs has an
- * eligible method the GPU encoders do not take at that size (zlib-9 DEFLATE > 4096,
- * Dictionary > 8192, any > 65536), AMBC_E_RANGE for a raw remainder > 4 GiB. */
+ * eligible method the GPU encoders do not take at that size (Dictionary > 8192,
+ * any > 65536), AMBC_E_RANGE for a raw remainder > 4 GiB. */
 int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const ambc_params* p,
                             const uint32_t* cands, uint32_t n_cands, const uint32_t* ent_sizes,
                             const double* const* ent_tabs, uint32_t n_ent, uint8_t* out,

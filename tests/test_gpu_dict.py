@@ -118,8 +118,8 @@ def test_dict_bodies_match_oracle(ctx, n, seed, chunk, methods, mode):
     data = _text_heavy(n, seed) if seed % 2 else synth.generate(n, seed)
     comp = AdaptiveCompressor(chunk_size=chunk, mode=mode, methods=methods)
     body = comp._adaptive_compress(data)
-    # id 5: reference mode at chunks <= 4096 writes zlib-9's own bytes (deflate=None)
-    gd = 5 in methods and not (mode == "reference" and chunk <= 4096)
+    # id 5: reference mode writes zlib-9's own bytes (deflate=None)
+    gd = 5 in methods and mode != "reference"
     ref, st = orc.compress_body(data, orc.make_params(chunk, mode, methods, n_total=n,
                                                       deflate="gd" if gd else "zlib"))
     assert len(body) == len(ref)

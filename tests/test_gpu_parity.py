@@ -464,8 +464,8 @@ def test_gdeflate_bodies_match_oracle(ctx, n, seed, chunk, methods):
     for mode in ("native", "reference"):
         comp = _compressor(chunk_size=chunk, mode=mode, methods=methods)
         body = comp._adaptive_compress(data)
-        # reference mode at chunks <= 8192 defaults to zlib-9's own bytes
-        z9 = mode == "reference" and chunk <= 8192
+        # reference mode defaults to zlib-9's own bytes (every chunk size)
+        z9 = mode == "reference"
         assert comp.deflate == ("zlib9" if z9 else "v1")
         p = orc.make_params(chunk, mode, methods, n_total=n, deflate="zlib" if z9 else "gd")
         ref, st = orc.compress_body(data, p, nthreads=0)
@@ -745,8 +745,9 @@ def test_like_reference_and_defaults_warning(ctx):
     data = synth.generate(150000, 31)
     comp = AdaptiveCompressor.like_reference()
     assert comp.CHUNK_SIZE_CANDIDATES == REF_CANDS and comp.mode == "reference"
+    assert comp.deflate == "zlib9"
     body = comp._adaptive_compress(data)
-    ref, _ = orc.compress_body_multisize(data, REF_CANDS, (1, 2, 3, 4, 5, 255))
+    ref, _ = orc.compress_body_multisize(data, REF_CANDS, (1, 2, 3, 4, 5, 255), deflate="zlib")
     assert body == ref
     assert comp._adaptive_decompress(body, len(data)) == data
     plain = AdaptiveCompressor()
@@ -758,12 +759,50 @@ def test_like_reference_and_defaults_warning(ctx):
         AdaptiveCompressor(chunk_size=4096)._adaptive_compress(data[:8192])
 
 
-def test_multisize_rejects_oversize_gpu_chunks(ctx):
-    # the zlib-9 encoder's walkers keep their tables in LDS: chunks <= 4096
-    comp = _compressor(methods=(1, 3, 4, 5), deflate="zlib9")
-    comp.CHUNK_SIZE_CANDIDATES = list(REF_CANDS)
-    with pytest.raises(NotImplementedError):
-        comp._adaptive_compress(synth.generate(100000, 5))
+def test_like_reference_reproduces_default_golden(ctx):
+    """The reference's own default-candidates container (tests/golden,
+    default_s3_n12288: AdaptiveCompressor() with its eight CHUNK_SIZE_CANDIDATES
+    and stdlib codecs; one 12 KiB id-5 package, zlib-9's bytes) reproduced by
+    the GPU walk: AdaptiveCompressor.like_reference(), methods {1,2,3,4,5} (the
+    reference's ids 6/7 lose on this input), id 5 through the zlib-9 encoder
+    at every size up to 65536."""
+    from ambc import AdaptiveCompressor
+    rec = [r for r in load_golden("files.json") if r["name"] == "default_s3_n12288"][0]
+    data = synth.generate(rec["size"], rec["seed"])
+    with open(os.path.join(GOLDEN, rec["file"]), "rb") as f:
+        blob = f.read()
+    comp = AdaptiveCompressor.like_reference()
+    assert comp._adaptive_compress(data) == blob[47:]
+    out, stats = comp.compress_bytes(data)
+    assert out == blob
+    assert comp.decompress_bytes(out) == data
+
+
+@pytest.mark.parametrize("methods", [(1, 3, 4, 5), (1, 2, 3, 4, 5)])
+def test_multisize_zlib9_walk_matches_oracle(ctx, methods):
+    """The reference's eight candidates with id 5 as zlib-9's bytes at every size
+    (16 / 32 / 64 KiB included): bodies and stats equal the oracle's walk with the
+    system zlib, every id-5 package equals zlib.compress(chunk, 9)."""
+    import zlib
+    inputs = [synth.generate(12288, 3), synth.generate(200000, 51), _zero_then_random(),
+              bytes(70000), synth.random_bytes(30000, 52) + bytes(100000)]
+    for data in inputs:
+        comp = _compressor(methods=methods, mode="reference", deflate="zlib9")
+        comp.CHUNK_SIZE_CANDIDATES = list(REF_CANDS)
+        body = comp._adaptive_compress(data)
+        ref, st = orc.compress_body_multisize(data, REF_CANDS, tuple(methods) + (255,), deflate="zlib")
+        assert body == ref, (methods, len(data))
+        for k in ("total_chunks", "compressed_chunks", "raw_chunks", "bytes_saved",
+                  "compressed_size_without_overhead", "overhead_bytes"):
+            assert comp.chunk_stats[k] == st[k], k
+        pos = off = 0
+        while pos + 18 <= len(body) and body[pos + 4] != 0:
+            t, orig = body[pos + 4], int.from_bytes(body[pos + 10:pos + 14], "little")
+            clen = int.from_bytes(body[pos + 14:pos + 18], "little")
+            if t == 5:
+                assert body[pos + 18:pos + 18 + clen] == zlib.compress(data[off:off + orig], 9)
+            pos, off = pos + 18 + clen, off + orig
+        assert comp._adaptive_decompress(body, len(data)) == data
 
 
 def test_gdeflate_large_chunks_edge(ctx):

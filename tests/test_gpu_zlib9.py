@@ -130,7 +130,53 @@ def test_zlib9_random_small_chunks(ctx):
         assert _check(data, chunk, (5,), modes=("native",)) > 0
 
 
-def test_zlib9_rejects_large_chunks(ctx):
-    from ambc import _lib
-    with pytest.raises(_lib.AmbcError):
-        _comp(chunk_size=16384, methods=(5,))._adaptive_compress(synth.generate(100000, 1))
+# chunks above 8 KiB (ambc_zlib9_big.hip): several blocks (a block per 16383
+# symbols), distances up to MAX_DIST, the window slide past 65274 bytes
+Z9_BIG_CASES = [((1 << 20) + 333, 31, 16384, (1, 3, 4, 5, 9)), ((1 << 20) + 5, 32, 32768, (5,)),
+                ((1 << 20) + 17, 33, 65536, (1, 3, 4, 5)), (700001, 34, 65536, (5,)),
+                (300000, 35, 12288, (1, 3, 5)), (400000, 36, 40000, (1, 2, 3, 4, 5))]
+
+
+@pytest.mark.parametrize("n,seed,chunk,methods", Z9_BIG_CASES)
+def test_zlib9_big_bodies_match_zlib(ctx, n, seed, chunk, methods):
+    assert _check(synth.generate(n, seed), chunk, methods) > 0
+
+
+def test_zlib9_big_edge_chunks(ctx):
+    """64 KiB zero runs (258-splits over several windows), period-2 data, random
+    bytes followed by zeros (stored blocks, then a Huffman block: the block split
+    at 16383 symbols), small-vocabulary words and biased binary data (chains of
+    4096 entries, MAX_DIST cuts), short alphabets (length-3 matches past
+    TOO_FAR), and the window-slide inputs of tests/test_zlib9_model.py (a hash
+    head of 32768 at step 65274 is NIL)."""
+    from test_zlib9_model import slide_head_case
+    edge = [bytes(65536), b"xy" * 32768, synth.random_bytes(40000, 41) + bytes(25536),
+            synth.random_bytes(20000, 42) + _words(45536, 43), _words(65536, 44, vocab=12),
+            _biased(65536, 0.93, 45), _alphabet(65536, 24, 46), _alphabet(50000, 90, 47),
+            bytes(range(256)) * 256, synth.random_bytes(3000, 48) * 21 + b"!" * 1000]
+    edge += [slide_head_case(n, n) for n in (65317, 65400, 65535)]
+    seen = 0
+    for d in edge:
+        for chunk in (16384, 32768, 65536):
+            seen += _check(d, chunk, (1, 3, 5), modes=("native",))
+    assert seen > 20
+
+
+def test_zlib9_big_random_chunk_contents(ctx):
+    """chunk contents of every kind at 8193..65536 bytes (tails of odd length)"""
+    rng = random.Random(78)
+    parts = []
+    for i in range(40):
+        kind = rng.randrange(4)
+        m = rng.randint(2000, 40000)
+        if kind == 0:
+            parts.append(_words(m, i, vocab=rng.randint(3, 200)))
+        elif kind == 1:
+            parts.append(_biased(m, rng.choice((0.6, 0.9, 0.99)), i))
+        elif kind == 2:
+            parts.append(synth.generate(m, i))
+        else:
+            parts.append(bytes([rng.randrange(4)]) * rng.randint(1, 3000) + _alphabet(m, rng.randint(3, 120), i))
+    data = b"".join(parts)
+    for chunk in (9008, 16384, 24576, 32768, 65536):
+        assert _check(data, chunk, (5,), modes=("native",)) > 0
