@@ -53,45 +53,77 @@ constexpr uint32_t ZB_GRID = 512;         // resident workgroups (2 per CU)
 constexpr uint32_t Z_WSZ = 32768;         // w_size
 constexpr uint32_t Z_SLIDE = 32768 + Z_MAXD;   // strstart that slides the window (65274)
 
+#ifdef AMBC_STAMPS
+// diagnostic build only: thread 0's phase cycles per parsed chunk in
+// A.stamps[(2 M + k) * 8 + phase] (k_dict's slots; phase 7 = 1 marks a parse)
+#define BSTAMP_DECL uint64_t _pt = __builtin_amdgcn_s_memtime(); uint64_t _pa[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define BSTAMP(ph)                                                 \
+    do {                                                           \
+        __builtin_amdgcn_s_waitcnt(0xC07F);                        \
+        const uint64_t _t = __builtin_amdgcn_s_memtime();          \
+        _pa[ph] += _t - _pt;                                       \
+        _pt = _t;                                                  \
+    } while (0)
+#define BSTAMP_FLUSH                                                                  \
+    if (threadIdx.x == 0 && A.stamps) {                                               \
+        _pa[7] = 1;                                                                   \
+        for (int _p = 0; _p < 8; _p++) A.stamps[(2ull * A.n_chunks + k) * 8 + _p] = _pa[_p]; \
+    }
+#else
+#define BSTAMP_DECL
+#define BSTAMP(ph) do {} while (0)
+#define BSTAMP_FLUSH
+#endif
+
 template <int CMAX>
 struct Z9Big {
+    // 64 KiB: the sorted list takes the LDS, the chunk bytes stay in scratch
+    // (zero-padded; 32 workgroups x 64 KB per XCD sit in its L2); smaller
+    // chunks keep both in LDS
+    static constexpr bool CHG = CMAX > 32768;
     static constexpr uint32_t RANGE = (uint32_t)CMAX / ZB_NW;   // sort positions per wave
     static constexpr uint32_t NBLK = Z9Rec<CMAX>::NBLK;
     // device scratch per resident workgroup (bytes)
-    static constexpr size_t LST = 0;                        // u16 [CMAX] positions by bucket (then u32 exits)
-    static constexpr size_t SLOT = LST + 2ull * CMAX;       // u16 [CMAX] position -> index in LST
+    static constexpr size_t LST = 0;                        // u16 [CMAX] positions by bucket (the sort's output)
+    static constexpr size_t SLOT = LST + 2ull * CMAX;       // u16 [CMAX] position -> index in the list
     static constexpr size_t SEG = SLOT + 2ull * CMAX;       // u32 [CMAX] the sort's ranks, then segments
     static constexpr size_t SD = SEG + 4ull * CMAX;         // u16 [CMAX] segment distances
-    static constexpr size_t BYTES = SD + 2ull * CMAX;
+    static constexpr size_t CH = SD + 2ull * CMAX;          // CHG: the chunk, zeros past n
+    static constexpr size_t BYTES = CH + (CHG ? (size_t)CMAX + 320 : 0);
 };
 
 template <int CMAX>
 struct Z9BSmem {
+    static constexpr bool CHG = Z9Big<CMAX>::CHG;
     static constexpr uint32_t NBLK = Z9Rec<CMAX>::NBLK;
+    struct Walk {                                      // the walkers
+        uint16_t lst[CMAX];                            // positions by bucket, ascending inside one
+        alignas(16) uint8_t ch[CHG ? 16 : CMAX + 320]; // the chunk, zeros past n
+    };
+    struct Path {                                      // the path from 0
+        union {
+            uint16_t xit[CMAX];                        // exit offset from the window (10 bits) | matches << 10
+            struct {
+                uint32_t mask[CMAX / 32];              // match starts
+                uint32_t cov[CMAX / 32];               // positions the matches cover
+                uint32_t lf[NBLK][316];                // per-block symbol counts
+            } b;
+        };
+        uint16_t entry[CMAX / 64], rbase[CMAX / 64];
+    };
     union {
         uint16_t cnt[ZB_NW][ZNB];                      // the sort: per-wave bucket cursors
-        alignas(16) uint8_t ch[CMAX + 320];            // the walkers: the chunk, zeros past n
-        struct {                                       // the path
-            uint32_t mask[CMAX / 32];                  // match starts
-            uint32_t cov[CMAX / 32];                   // positions the matches cover
-            uint16_t entry[CMAX / 64], rbase[CMAX / 64];
-            uint32_t lf[NBLK][316];                    // per-block symbol counts
-        } p;
+        Walk w;
+        Path p;
     };
     uint32_t bend32[ZNB / 2];                          // bucket ends (u16 pairs)
+    uint32_t vis[CMAX / 32];                           // clean positions some walker recorded
     uint32_t bnd[8];                                   // block ends (boundary positions)
     uint32_t btop[8];                                  // the step top that flushed block b
     uint32_t nbnd, nmatch;
     __device__ __forceinline__ uint16_t* bend() { return reinterpret_cast<uint16_t*>(bend32); }
     __device__ __forceinline__ uint32_t bstart(uint32_t h) { return h ? bend()[h - 1] : 0u; }
 };
-
-__device__ __forceinline__ uint32_t ld_wg(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void st_wg(uint32_t* p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
 
 // 3-gram at i of the chunk in global memory (i + 2 < n)
 __device__ __forceinline__ uint32_t g_gram(const uint8_t* src, uint32_t i) {
@@ -101,7 +133,8 @@ __device__ __forceinline__ uint32_t g_gram(const uint8_t* src, uint32_t i) {
 // Stable counting sort of positions [1, m) by z_bucket(z_h15): wave w ranks
 // the positions of its range [w RANGE, (w+1) RANGE) in order (ballots over the
 // 11 bucket bits, per-wave LDS cursors); the per-bucket prefix over the waves
-// and the bucket ends; then every position goes to lst[] and its index to slot[].
+// and the bucket ends; then every position goes to lst[] and its index to
+// slot[] (scratch; the list is copied into LDS once the cursors are dead).
 template <int CMAX>
 __device__ void z9b_sort(Z9BSmem<CMAX>& S, const uint8_t* src, uint32_t m, uint16_t* lst, uint16_t* slot,
                          uint32_t* loc, uint32_t wave, uint32_t lane) {
@@ -125,7 +158,7 @@ __device__ void z9b_sort(Z9BSmem<CMAX>& S, const uint8_t* src, uint32_t m, uint1
                 peers &= ((h >> b) & 1u) ? mb : ~mb;
             }
             const uint32_t base = v ? (uint32_t)c[h] : 0u;
-            if (i < (uint32_t)CMAX) loc[i] = v ? (base + (uint32_t)__popcll(peers & below)) | h << 16 : ~0u;
+            loc[i] = v ? (base + (uint32_t)__popcll(peers & below)) | h << 16 : ~0u;
             if (v && (peers >> lane) == 1ull) c[h] = (uint16_t)(base + (uint32_t)__popcll(peers));
         }
     }
@@ -160,7 +193,7 @@ __device__ void z9b_sort(Z9BSmem<CMAX>& S, const uint8_t* src, uint32_t m, uint1
 #pragma unroll 2
     for (uint32_t g = 0; g < GR; g++) {
         const uint32_t i = wave * RANGE + g * 64 + lane;
-        const uint32_t x = i < (uint32_t)CMAX ? loc[i] : ~0u;   // (this lane's own store)
+        const uint32_t x = loc[i];   // (this lane's own store)
         if (x != ~0u) {
             const uint32_t h = x >> 16;
             const uint32_t idx = S.bstart(h) + S.cnt[wave][h] + (x & 0xFFFFu);
@@ -171,14 +204,26 @@ __device__ void z9b_sort(Z9BSmem<CMAX>& S, const uint8_t* src, uint32_t m, uint1
     __syncthreads();
 }
 
-// The lazy parse's walkers (ambc_zlib9.hip z9_walkers, with the list, slots and
-// segments in scratch, the window's MAX_DIST, the slide step's NIL head, and
-// the search stopped at the chain length the step needs).
+// The lazy parse's walkers (ambc_zlib9.hip z9_walkers with the list in LDS,
+// slots and segments in scratch, the chunk bytes in LDS or scratch, the
+// candidates' words loaded one step ahead, the window's MAX_DIST, the slide
+// step's NIL head, and the search stopped at the chain length the step needs).
 template <int CMAX>
-__device__ __forceinline__ void z9b_walkers(Z9BSmem<CMAX>& S, uint32_t n, const uint16_t* lst, const uint16_t* slot,
-                                            uint32_t* seg, uint16_t* sd, uint32_t wave, uint32_t lane) {
+__device__ __forceinline__ void z9b_walkers(Z9BSmem<CMAX>& S, uint32_t n, const uint16_t* slot, uint32_t* seg,
+                                            uint16_t* sd, const uint8_t* gch, uint32_t wave, uint32_t lane) {
+    constexpr bool CHG = Z9Big<CMAX>::CHG;
     constexpr uint32_t NWK = (uint32_t)ZB_NW * 8u;
-    const uint32_t* c32 = reinterpret_cast<const uint32_t*>(S.ch);
+    const uint32_t* c32 = reinterpret_cast<const uint32_t*>(S.w.ch);
+    const uint32_t* g32 = reinterpret_cast<const uint32_t*>(gch);
+    auto W32 = [&](uint32_t i) -> uint32_t {
+        if constexpr (CHG) return g32[i];
+        else return c32[i];
+    };
+    auto B8 = [&](uint32_t i) -> uint32_t {
+        if constexpr (CHG) return gch[i];
+        else return S.w.ch[i];
+    };
+    const uint16_t* lst = S.w.lst;
     const uint32_t g = lane >> 3, r = lane & 7;
     const uint32_t wid = wave * 8u + g;
     // the step at which fill_window slides: the first top s >= 65274 with
@@ -190,7 +235,7 @@ __device__ __forceinline__ void z9b_walkers(Z9BSmem<CMAX>& S, uint32_t n, const 
     bool clean = true, done = false;
 #pragma unroll 1
     for (;;) {
-        if (clean && !done && (q >= n || ld_wg(seg + q) != 0u)) done = true;
+        if (clean && !done && (q >= n || ((S.vis[q >> 5] >> (q & 31)) & 1u))) done = true;
         if (__all(done)) break;
         const bool act = !done && s >= 1 && s + 3 <= n && P < 258;   // position 0 is zlib's NIL
         // ---- longest_match(s) over the first `lim` chain entries (4096, or
@@ -202,34 +247,40 @@ __device__ __forceinline__ void z9b_walkers(Z9BSmem<CMAX>& S, uint32_t n, const 
             const uint32_t ss = s & 3u;
             const uint32_t lim = P >= Z_GOOD ? Z_CHAIN / 4 : Z_CHAIN;
             if (act) {
+                j = slot[s];
                 const uint32_t a = s >> 2;
                 uint32_t w[5];
 #pragma unroll
-                for (int t = 0; t < 5; t++) w[t] = c32[a + t];
+                for (int t = 0; t < 5; t++) w[t] = W32(a + t);
 #pragma unroll
                 for (int t = 0; t < 4; t++) tg[t] = __builtin_amdgcn_alignbyte(w[t + 1], w[t], ss);
                 h = z_h15(tg[0] & 0xFFFFFFu);
                 lo = S.bstart(z_bucket(h));
-                j = slot[s];
                 nice = min(Z_MAXM, n - s);
             }
             bool gd = !act || j <= lo;
             uint32_t cnt = 0;
             int idx = (int)j - 1 - (int)r;
-            uint32_t cpre = !gd && idx >= (int)lo ? (uint32_t)lst[idx] : 0u;
+            uint32_t cn = !gd && idx >= (int)lo ? (uint32_t)lst[idx] : 0u;
+            uint32_t wn[5];
+#pragma unroll
+            for (int t = 0; t < 5; t++) wn[t] = W32((cn >> 2) + t);
 #pragma unroll 1
             while (__any(!gd)) {
                 const bool v = !gd && idx >= (int)lo;
-                const uint32_t c = v ? cpre : 0u;
-                idx -= 8;
-                cpre = !gd && idx >= (int)lo ? (uint32_t)lst[idx] : 0u;   // the next step's, issued now
-                const uint32_t a = c >> 2, sh = c & 3u;
+                const uint32_t c = v ? cn : 0u;
                 uint32_t w[5];
 #pragma unroll
-                for (int t = 0; t < 5; t++) w[t] = c32[a + t];
+                for (int t = 0; t < 5; t++) w[t] = wn[t];
+                // the next step's candidate and its words, issued now
+                idx -= 8;
+                cn = !gd && idx >= (int)lo ? (uint32_t)lst[idx] : 0u;
+#pragma unroll
+                for (int t = 0; t < 5; t++) wn[t] = W32((cn >> 2) + t);
+                const uint32_t sh = c & 3u;
                 uint32_t x[4];
 #pragma unroll
-                for (int t = 0; t < 4; t++) x[t] = __builtin_amdgcn_alignbyte(w[t + 1], w[t], sh);
+                for (int t = 0; t < 4; t++) x[t] = __builtin_amdgcn_alignbyte(w[t + 1], w[t], v ? sh : 0u);
                 const bool same = v && z_h15(x[0] & 0xFFFFFFu) == h;
                 const uint32_t sm = grp8(__ballot(same), g);
                 const uint32_t kidx = cnt + (uint32_t)__popc(sm & ((1u << r) - 1u)) + 1u;
@@ -243,16 +294,19 @@ __device__ __forceinline__ void z9b_walkers(Z9BSmem<CMAX>& S, uint32_t n, const 
 #pragma unroll
                 for (int t = 0; t < 4; t++) fm = min(fm, ffbl_raw(x[t] ^ tg[t]) | (uint32_t)t << 5);
                 uint32_t len = fm == ~0u ? 16u : fm >> 3;
+                // zlib's scan_end test: only a candidate equal in its first 16
+                // bytes can pass a best >= 16; it must also agree at byte best
                 const uint32_t best = k0 >> 16;
-                const bool can = best < 16 || S.ch[c + best] == S.ch[s + best];
-                bool ext = ok && fm == ~0u && can && !nilh;
+                bool ext = ok && fm == ~0u && !nilh;
+                if (ext && best >= 16) ext = B8(c + best) == B8(s + best);
+                const bool can = fm != ~0u || best < 16 || ext;
 #pragma unroll 1
                 while (__any(ext)) {
                     if (ext) {
                         const uint32_t ac = (c + len) >> 2, as = (s + len) >> 2;
                         uint32_t wc[5], ws[5];
 #pragma unroll
-                        for (int t = 0; t < 5; t++) { wc[t] = c32[ac + t]; ws[t] = c32[as + t]; }
+                        for (int t = 0; t < 5; t++) { wc[t] = W32(ac + t); ws[t] = W32(as + t); }
                         uint32_t f = ~0u;
 #pragma unroll
                         for (int t = 0; t < 4; t++)
@@ -280,7 +334,10 @@ __device__ __forceinline__ void z9b_walkers(Z9BSmem<CMAX>& S, uint32_t n, const 
             }
             if (clean) {
                 if (ML < 3) {
-                    if (r == 0) st_wg(seg + q, 0x80000000u | 1u);
+                    if (r == 0) {
+                        seg[q] = 0x80000000u | 1u;
+                        atomicOr(&S.vis[q >> 5], 1u << (q & 31));
+                    }
                     q++;
                     s = q;
                 } else {
@@ -293,7 +350,8 @@ __device__ __forceinline__ void z9b_walkers(Z9BSmem<CMAX>& S, uint32_t n, const 
             } else if (ML <= P) {
                 if (r == 0) {
                     sd[q] = (uint16_t)Pd;
-                    st_wg(seg + q, 0x80000000u | P << 16 | c);
+                    seg[q] = 0x80000000u | P << 16 | c;
+                    atomicOr(&S.vis[q >> 5], 1u << (q & 31));
                 }
                 q = s - 1 + P;
                 s = q;
@@ -313,16 +371,17 @@ template <int CMAX>
 __global__ __launch_bounds__(64 * ZB_NW) void k_z9_parse_big(EncArgs A) {
     constexpr uint32_t NW = ZB_NW, TT = 64u * NW;
     constexpr uint32_t NBLK = Z9Rec<CMAX>::NBLK;
+    constexpr bool CHG = Z9Big<CMAX>::CHG;
     __shared__ Z9BSmem<CMAX> S;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = threadIdx.x >> 6;
     const uint64_t below = (1ull << lane) - 1ull;
     uint8_t* scr = A.z9scr + (uint64_t)blockIdx.x * Z9Big<CMAX>::BYTES;
-    uint16_t* lst = reinterpret_cast<uint16_t*>(scr + Z9Big<CMAX>::LST);
+    uint16_t* glst = reinterpret_cast<uint16_t*>(scr + Z9Big<CMAX>::LST);
     uint16_t* slot = reinterpret_cast<uint16_t*>(scr + Z9Big<CMAX>::SLOT);
     uint32_t* seg = reinterpret_cast<uint32_t*>(scr + Z9Big<CMAX>::SEG);
     uint16_t* sd = reinterpret_cast<uint16_t*>(scr + Z9Big<CMAX>::SD);
-    uint32_t* xit = reinterpret_cast<uint32_t*>(scr + Z9Big<CMAX>::LST);   // after the walkers
+    uint8_t* gch = scr + Z9Big<CMAX>::CH;
 #pragma unroll 1
     for (uint32_t k = blockIdx.x; k < A.n_chunks; k += gridDim.x) {
         __syncthreads();   // (the previous chunk's last LDS reads)
@@ -331,27 +390,40 @@ __global__ __launch_bounds__(64 * ZB_NW) void k_z9_parse_big(EncArgs A) {
         uint32_t T = 0;
         if (n > (uint32_t)CMAX || !z9_gate(A, k, n, T)) continue;
         const uint8_t* src = A.in + pos0;
+        BSTAMP_DECL
         // ---- 1. the sort (the ranks go through seg[]) ----
-        z9b_sort(S, src, n - 2, lst, slot, seg, wave, lane);
-        // ---- 2. the chunk in LDS, cleared segments, the walkers ----
-        if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
-            const uint32_t nv = n >> 4;
-            for (uint32_t q = threadIdx.x; q < nv; q += TT)
-                reinterpret_cast<uint4*>(S.ch)[q] = reinterpret_cast<const uint4*>(src)[q];
-            for (uint32_t i = (nv << 4) + threadIdx.x; i < n; i += TT) S.ch[i] = src[i];
-        } else {
-            for (uint32_t i = threadIdx.x; i < n; i += TT) S.ch[i] = src[i];
+        z9b_sort(S, src, n - 2, glst, slot, seg, wave, lane);
+        BSTAMP(0);
+        // ---- 2. the list (and the chunk) in LDS, cleared segments, the walkers ----
+        {
+            const uint32_t m = n - 2;
+            uint32_t* l32 = reinterpret_cast<uint32_t*>(S.w.lst);
+            const uint32_t* g32 = reinterpret_cast<const uint32_t*>(glst);
+            for (uint32_t i = threadIdx.x; i < (m + 1) / 2; i += TT) l32[i] = g32[i];
+            uint8_t* dst = CHG ? gch : S.w.ch;
+            if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+                const uint32_t nv = n >> 4;
+                for (uint32_t q = threadIdx.x; q < nv; q += TT)
+                    reinterpret_cast<uint4*>(dst)[q] = reinterpret_cast<const uint4*>(src)[q];
+                for (uint32_t i = (nv << 4) + threadIdx.x; i < n; i += TT) dst[i] = src[i];
+            } else {
+                for (uint32_t i = threadIdx.x; i < n; i += TT) dst[i] = src[i];
+            }
+            for (uint32_t i = n + threadIdx.x; i < (uint32_t)CMAX + 320; i += TT) dst[i] = 0;
+            for (uint32_t i = threadIdx.x; i < (uint32_t)CMAX / 32; i += TT) S.vis[i] = 0;
         }
-        for (uint32_t i = n + threadIdx.x; i < (uint32_t)CMAX + 320; i += TT) S.ch[i] = 0;
-        for (uint32_t i = threadIdx.x; i < n; i += TT) seg[i] = 0;
         __syncthreads();
-        z9b_walkers(S, n, lst, slot, seg, sd, wave, lane);
+        BSTAMP(1);
+        z9b_walkers(S, n, slot, seg, sd, gch, wave, lane);
+        BSTAMP(2);
         __syncthreads();
-        // ---- 3. the path from 0 (as ambc_zlib9.hip, the exits in scratch) ----
+        BSTAMP(3);
+        // ---- 3. the path from 0 (as ambc_zlib9.hip): per window the exit offset
+        // and the matches on the way by pointer doubling (the list is dead: LDS) ----
         const uint32_t nwin = (n + 63) / 64;
         for (uint32_t w = wave; w < nwin; w += NW) {
             const uint32_t p = w * 64 + lane;
-            const uint32_t t = p < n ? seg[p] : 0u;
+            const uint32_t t = p < n && ((S.vis[p >> 5] >> (p & 31)) & 1u) ? seg[p] : 0u;
             uint32_t J = t ? lane + (t & 0xFFFFu) + ((t >> 16) & 0x1FFu) : lane + 1;
             uint32_t M = (t >> 16) & 0x1FFu ? 1u : 0u;
 #pragma unroll
@@ -362,32 +434,32 @@ __global__ __launch_bounds__(64 * ZB_NW) void k_z9_parse_big(EncArgs A) {
                 M = J < 64 ? M + Mj : M;
                 J = J < 64 ? Jj : J;
             }
-            xit[p] = (w * 64 + J) | M << 24;
+            S.p.xit[p] = (uint16_t)(J | M << 10);
         }
-        // (the chunk bytes are dead: the path arrays take their LDS)
-        __syncthreads();
         for (uint32_t i = threadIdx.x; i < (uint32_t)CMAX / 64; i += TT) S.p.entry[i] = 0xFFFFu;
-        for (uint32_t i = threadIdx.x; i < (uint32_t)CMAX / 32; i += TT) { S.p.mask[i] = 0; S.p.cov[i] = 0; }
-        for (uint32_t i = threadIdx.x; i < NBLK * 316; i += TT) (&S.p.lf[0][0])[i] = 0;
         __syncthreads();
         if (threadIdx.x == 0) {
             uint32_t cur = 0, mr = 0;
             while (cur < n) {
                 S.p.entry[cur >> 6] = (uint16_t)(cur & 63u);
                 S.p.rbase[cur >> 6] = (uint16_t)mr;
-                const uint32_t x = xit[cur];
-                mr += x >> 24;
-                cur = x & 0xFFFFFFu;
+                const uint32_t x = S.p.xit[cur];
+                mr += x >> 10;
+                cur = (cur & ~63u) + (x & 1023u);
             }
             S.nmatch = mr;
         }
+        __syncthreads();
+        BSTAMP(4);
+        for (uint32_t i = threadIdx.x; i < (uint32_t)CMAX / 32; i += TT) { S.p.b.mask[i] = 0; S.p.b.cov[i] = 0; }
+        for (uint32_t i = threadIdx.x; i < NBLK * 316; i += TT) (&S.p.b.lf[0][0])[i] = 0;
         __syncthreads();
         uint32_t* R = A.z9rec + (uint64_t)k * Z9Rec<CMAX>::STRIDE;
         for (uint32_t w = wave; w < nwin; w += NW) {
             const uint32_t e = S.p.entry[w];
             if (e == 0xFFFFu) continue;
             const uint32_t p = w * 64 + lane;
-            const uint32_t t = p < n ? seg[p] : 0u;
+            const uint32_t t = p < n && ((S.vis[p >> 5] >> (p & 31)) & 1u) ? seg[p] : 0u;
             const uint32_t c = t & 0xFFFFu, L = (t >> 16) & 0x1FFu;
             const uint32_t J1 = lane + max(1u, c + L);
             uint64_t on = 0;
@@ -399,12 +471,12 @@ __global__ __launch_bounds__(64 * ZB_NW) void k_z9_parse_big(EncArgs A) {
             const uint64_t mm = __ballot(mt);
             if (mt) {
                 const uint32_t ms = p + c, d = sd[p];
-                atomicOr(&S.p.mask[ms >> 5], 1u << (ms & 31));
+                atomicOr(&S.p.b.mask[ms >> 5], 1u << (ms & 31));
                 R[Z9Rec<CMAX>::MATCH + S.p.rbase[w] + (uint32_t)__popcll(mm & below)] = L | d << 16;
                 for (uint32_t b = ms, e2 = ms + L; b < e2;) {
                     const uint32_t wd = b >> 5, hi = min(e2, (wd + 1) * 32);
                     const uint32_t bits = (hi - b == 32 ? ~0u : ((1u << (hi - b)) - 1u)) << (b & 31);
-                    atomicOr(&S.p.cov[wd], bits);
+                    atomicOr(&S.p.b.cov[wd], bits);
                     b = hi;
                 }
             }
@@ -422,8 +494,8 @@ __global__ __launch_bounds__(64 * ZB_NW) void k_z9_parse_big(EncArgs A) {
                 uint32_t sym = 0, mk = 0;
                 if (w < nwd) {
                     const uint32_t valid = (w + 1) * 32 <= n ? ~0u : ((1u << (n & 31)) - 1u);
-                    mk = S.p.mask[w];
-                    sym = (~S.p.cov[w] | mk) & valid;
+                    mk = S.p.b.mask[w];
+                    sym = (~S.p.b.cov[w] | mk) & valid;
                 }
                 const uint32_t cs = (uint32_t)__popc(sym), cm = (uint32_t)__popc(mk);
                 const uint32_t incl = wave_incl_sum(cs), minc = wave_incl_sum(cm);
@@ -458,38 +530,35 @@ __global__ __launch_bounds__(64 * ZB_NW) void k_z9_parse_big(EncArgs A) {
         const uint32_t nbnd = S.nbnd;
         // per-block symbol counts: literals (positions no match covers) by position
         for (uint32_t i = threadIdx.x; i < n; i += TT) {
-            if ((S.p.cov[i >> 5] >> (i & 31)) & 1u) continue;
+            if ((S.p.b.cov[i >> 5] >> (i & 31)) & 1u) continue;
             uint32_t b = 0;
             for (uint32_t q = 0; q < nbnd; q++) b += i >= S.bnd[q] ? 1u : 0u;
-            atomicAdd(&S.p.lf[b][src[i]], 1u);
+            atomicAdd(&S.p.b.lf[b][src[i]], 1u);
         }
-        {
-            // matches by their start: each wave takes 64 mask words at a time,
-            // ranks from the popcounts of the words below
-            for (uint32_t w0 = wave * 64; w0 < (n + 31) / 32; w0 += NW * 64) {
-                const uint32_t w = w0 + lane;
-                const uint32_t mk = w < (n + 31) / 32 ? S.p.mask[w] : 0u;
-                // matches before word w0: sum of the popcounts of the words below
-                uint32_t pre = 0;
-                for (uint32_t q = lane; q < w0; q += 64) pre += (uint32_t)__popc(S.p.mask[q]);
-                pre = wave_sum_u32(pre);
-                const uint32_t cm = (uint32_t)__popc(mk);
-                uint32_t rank = pre + wave_incl_sum(cm) - cm;
-                uint32_t x = mk;
-                while (x) {
-                    const uint32_t bit = (uint32_t)__builtin_ctz(x);
-                    x &= x - 1u;
-                    const uint32_t ms = w * 32 + bit;
-                    const uint32_t rc = R[Z9Rec<CMAX>::MATCH + rank++];
-                    const uint32_t L = rc & 0xFFFFu, d = rc >> 16;
-                    uint32_t b = 0;
-                    for (uint32_t q = 0; q < nbnd; q++) b += ms >= S.bnd[q] ? 1u : 0u;
-                    atomicAdd(&S.p.lf[b][257 + z_lcode(L)], 1u);
-                    atomicAdd(&S.p.lf[b][286 + z_dcode(d)], 1u);
-                }
+        // matches by their start: each wave takes 64 mask words at a time, ranks
+        // from the popcounts of the words below
+        for (uint32_t w0 = wave * 64; w0 < (n + 31) / 32; w0 += NW * 64) {
+            const uint32_t w = w0 + lane;
+            const uint32_t mk = w < (n + 31) / 32 ? S.p.b.mask[w] : 0u;
+            uint32_t pre = 0;
+            for (uint32_t q = lane; q < w0; q += 64) pre += (uint32_t)__popc(S.p.b.mask[q]);
+            pre = wave_sum_u32(pre);
+            const uint32_t cm = (uint32_t)__popc(mk);
+            uint32_t rank = pre + wave_incl_sum(cm) - cm;
+            uint32_t x = mk;
+            while (x) {
+                const uint32_t bit = (uint32_t)__builtin_ctz(x);
+                x &= x - 1u;
+                const uint32_t ms = w * 32 + bit;
+                const uint32_t rc = R[Z9Rec<CMAX>::MATCH + rank++];
+                const uint32_t L = rc & 0xFFFFu, d = rc >> 16;
+                uint32_t b = 0;
+                for (uint32_t q = 0; q < nbnd; q++) b += ms >= S.bnd[q] ? 1u : 0u;
+                atomicAdd(&S.p.b.lf[b][257 + z_lcode(L)], 1u);
+                atomicAdd(&S.p.b.lf[b][286 + z_dcode(d)], 1u);
             }
         }
-        for (uint32_t i = threadIdx.x; i < (uint32_t)CMAX / 32; i += TT) R[Z9Rec<CMAX>::MASK + i] = S.p.mask[i];
+        for (uint32_t i = threadIdx.x; i < (uint32_t)CMAX / 32; i += TT) R[Z9Rec<CMAX>::MASK + i] = S.p.b.mask[i];
         if (threadIdx.x == 0) {
             R[0] = S.nmatch;
             R[1] = nbnd + 1;
@@ -501,8 +570,8 @@ __global__ __launch_bounds__(64 * ZB_NW) void k_z9_parse_big(EncArgs A) {
             const uint32_t top = b < nbnd ? S.btop[b] : n;
             const uint32_t thr = n == 65536u ? Z_SLIDE + 1 : Z_SLIDE;
             uint32_t mb = 0;   // match starts below bs
-            for (uint32_t q = 0; q < (bs >> 5); q++) mb += (uint32_t)__popc(S.p.mask[q]);
-            if (bs & 31) mb += (uint32_t)__popc(S.p.mask[bs >> 5] & ((1u << (bs & 31)) - 1u));
+            for (uint32_t q = 0; q < (bs >> 5); q++) mb += (uint32_t)__popc(S.p.b.mask[q]);
+            if (bs & 31) mb += (uint32_t)__popc(S.p.b.mask[bs >> 5] & ((1u << (bs & 31)) - 1u));
             uint32_t* B = R + Z9Rec<CMAX>::BLK + 4 * b;
             B[0] = bs;
             B[1] = be;
@@ -512,8 +581,10 @@ __global__ __launch_bounds__(64 * ZB_NW) void k_z9_parse_big(EncArgs A) {
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < 158 * (nbnd + 1); i += TT) {
             const uint32_t b = i / 158, o = i % 158;
-            R[Z9Rec<CMAX>::FREQ + i] = S.p.lf[b][2 * o] | S.p.lf[b][2 * o + 1] << 16;
+            R[Z9Rec<CMAX>::FREQ + i] = S.p.b.lf[b][2 * o] | S.p.b.lf[b][2 * o + 1] << 16;
         }
+        BSTAMP(5);
+        BSTAMP_FLUSH
     }
 }
 

@@ -3,6 +3,7 @@ GPU (ambc_compress_multisize) and check the body against the oracle's walk.
 
     python scripts/multisize_bench.py [MiB ...]      (default: 32 256)
     MS_SETS="mixed:1,3,4,5;mixed:1,2,3,4,5,9" python scripts/multisize_bench.py 32
+    MS_MODE=reference ...   (id 5 as zlib-9's bytes: AdaptiveCompressor.like_reference()'s walk)
 
 Input: runs, text-like bytes and skewed random bytes in 8-64 KiB segments, so
 every position compresses and the walk never ends in the remainder-raw rule."""
@@ -51,7 +52,7 @@ def main():
     for kind, methods in sets:
         for mib in sizes:
             data = (mixed if kind == "mixed" else text)(int(mib * (1 << 20)), 7)
-            comp = ambc.AdaptiveCompressor(methods=methods)
+            comp = ambc.AdaptiveCompressor(methods=methods, mode=os.environ.get("MS_MODE", "native"))
             comp.CHUNK_SIZE_CANDIDATES = list(comp.REFERENCE_CHUNK_SIZE_CANDIDATES)
             comp._adaptive_compress(data[:1 << 20])            # warm
             t = time.perf_counter()
@@ -61,7 +62,8 @@ def main():
             lib = ambc._lib.load()
             lib.ambc_last_multisize_info(ambc._lib.default_context().h, C.byref(steps), C.byref(ev), C.byref(wns),
                                          C.byref(ens))
-            rec = {"input": kind, "MiB": mib, "methods": list(methods), "seconds": round(dt, 4),
+            rec = {"input": kind, "MiB": mib, "methods": list(methods), "deflate": comp.deflate,
+                   "seconds": round(dt, 4),
                    "GBps": round(len(data) / dt / 1e9, 3), "ratio": round(len(body) / len(data), 5),
                    "chunks": comp.chunk_stats["total_chunks"], "walk_steps": steps.value,
                    "chunk_encodes": ev.value, "walk_ms": round(wns.value / 1e6, 2),
@@ -69,7 +71,8 @@ def main():
             if mib <= 32:
                 from oracle import oracle as orc
                 t = time.perf_counter()
-                ref, _ = orc.compress_body_multisize(data, comp.CHUNK_SIZE_CANDIDATES, tuple(methods) + (255,))
+                ref, _ = orc.compress_body_multisize(data, comp.CHUNK_SIZE_CANDIDATES, tuple(methods) + (255,),
+                                                     deflate="zlib" if comp.deflate == "zlib9" else "gd")
                 rec["oracle_seconds"] = round(time.perf_counter() - t, 2)
                 rec["body_equals_oracle"] = ref == body
             rec["round_trip"] = comp._adaptive_decompress(body, len(data)) == data
