@@ -396,7 +396,13 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
         return finish_compress(d, p, M, Remainder(), d_out, body_len, acc, d_in, end, out_len, st, t0);
     }
     rc = encode_range(ea);
-    if (rc) return rc;
+    if (rc) {
+        if (si && p->mode == AMBC_MODE_REFERENCE) {   // the peers wait in the remainder exchange
+            uint64_t g = UINT64_MAX;
+            (void)shard_allreduce_min(si->t, &g, rc);
+        }
+        return rc;
+    }
     HIPCHK(hipEventRecord(d.ev[1], s));
     if (ea.stamps) {
         stamps.resize((size_t)M * 8);
@@ -458,7 +464,7 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
             k0 = si->k0;
             n_total = si->n_total;
             if (g != UINT64_MAX) g += k0;
-            int rc2 = shard_allreduce_min(si->t, &g);  // AllReduce(MIN) across the ranks
+            int rc2 = shard_allreduce_min(si->t, &g, AMBC_OK);  // AllReduce(MIN) across the ranks
             if (rc2) return rc2;
         }
         if (g != UINT64_MAX) {
@@ -521,7 +527,7 @@ extern "C" int ambc_compress_device(ambc_ctx* ctx, int dev, const void* d_in, ui
     return compress_on(ctx->devs[dev], (const uint8_t*)d_in, n, p, (uint8_t*)d_out, out_cap, out_len, st);
 }
 
-static void add_stats(ambc_stats* a, const ambc_stats& b) {
+void ambc::add_stats(ambc_stats* a, const ambc_stats& b) {
     for (int i = 0; i < 256; i++) a->method_usage[i] += b.method_usage[i];
     a->total_chunks += b.total_chunks;
     a->compressed_chunks += b.compressed_chunks;
@@ -540,11 +546,17 @@ static void add_stats(ambc_stats* a, const ambc_stats& b) {
 // The overlap needs page-locked host buffers (ambc_host_alloc).
 static constexpr uint64_t kSlabBytes = 256ull << 20;
 
+// slab size of the host-fed pipelines (AMBC_SLAB_BYTES overrides, for tests)
+uint64_t ambc::slab_bytes() {
+    const char* e = getenv("AMBC_SLAB_BYTES");
+    return e && strtoull(e, nullptr, 10) > 0 ? strtoull(e, nullptr, 10) : kSlabBytes;
+}
+
 static int compress_slabs(Dev& d, const uint8_t* in, uint64_t n, const ambc_params* p, uint8_t* out,
                           uint64_t out_cap, uint64_t* out_len, ambc_stats* st) {
     const uint64_t t0 = now_ns();
     const uint32_t C = p->chunk_size;
-    const uint64_t SLAB = std::max<uint64_t>(C, kSlabBytes / C * C);
+    const uint64_t SLAB = std::max<uint64_t>(C, slab_bytes() / C * C);
     const uint64_t ns = (n + SLAB - 1) / SLAB;
     const uint64_t sb = ambc_compress_bound(SLAB, C) + 64;
     HIPCHK(hipSetDevice(d.id));
@@ -608,7 +620,7 @@ extern "C" int ambc_compress_batch(ambc_ctx* ctx, const uint8_t* in, uint64_t n,
     if (ctx->devs.size() > 1 && M >= ctx->devs.size())
         return compress_batch_multi(ctx, in, n, p, out, out_cap, out_len, st);
     Dev& d = ctx->devs[0];
-    if (p->mode == AMBC_MODE_NATIVE && n > kSlabBytes)
+    if (p->mode == AMBC_MODE_NATIVE && n > slab_bytes())
         return compress_slabs(d, in, n, p, out, out_cap, out_len, st);
     const uint64_t bound = ambc_compress_bound(n, C);
     HIPCHK(hipSetDevice(d.id));

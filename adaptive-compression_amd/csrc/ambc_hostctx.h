@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -143,6 +144,7 @@ struct ambc_ctx {
     // in-process multi-device communicators (ncclCommInitAll over distinct devices),
     // created on the first sharded call
     std::vector<ncclComm_t> dev_comms;
+    std::mutex comm_mu;          // guards dev_comms against a concurrent abort
 };
 
 namespace ambc {
@@ -155,9 +157,11 @@ int decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t orig_size
                   uint8_t* out, std::vector<ambc_host_chunk>& host, ambc_stats* st,
                   uint8_t* d_out_ext = nullptr);
 void default_registered(const uint64_t* registered, uint64_t reg[4]);
+void add_stats(ambc_stats* a, const ambc_stats& b);   // sums (kernel_ns: max)
+uint64_t slab_bytes();                                 // host-fed pipelines' slab size
 
 // collective of the sharded calls (ambc_shard.cpp)
-int shard_allreduce_min(Transport* t, uint64_t* v);
+int shard_allreduce_min(Transport* t, uint64_t* v, int rc_local);
 int compress_batch_multi(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const ambc_params* p, uint8_t* out,
                          uint64_t out_cap, uint64_t* out_len, ambc_stats* st);
 

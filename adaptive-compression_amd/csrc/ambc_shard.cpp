@@ -57,9 +57,22 @@ struct Transport {
 struct RcclTransport : Transport {
     ncclComm_t comm;
     Dev& d;
+    // in-process ranks: every rank's communicator lives in the ctx, and a failed
+    // rank aborts all of them (ncclCommAbort releases peers blocked in a
+    // collective); the ctx builds fresh ones on its next sharded call
+    std::vector<ncclComm_t>* group = nullptr;
+    std::mutex* group_mu = nullptr;
     RcclTransport(ncclComm_t c, Dev& dev, int nranks, int rank) : comm(c), d(dev) { W = nranks; r = rank; }
+    // this rank's communicator, or null once a failed peer aborted the group
+    ncclComm_t live() {
+        if (!group) return comm;
+        std::lock_guard<std::mutex> lk(*group_mu);
+        return (*group)[r];
+    }
 
     int allgather_u64(const uint64_t* mine, uint32_t k, uint64_t* all) override {
+        ncclComm_t comm = live();
+        if (!comm) return fail(AMBC_E_COMM, "communicator aborted by a failed rank");
         HIPCHK(hipSetDevice(d.id));
         HIPCHK(d.coll.ensure((size_t)(W + 1) * k * 8));
         uint64_t* buf = d.coll.as<uint64_t>();
@@ -70,6 +83,8 @@ struct RcclTransport : Transport {
         return AMBC_OK;
     }
     int allreduce_u64(uint64_t* v, uint32_t k, int op) override {
+        ncclComm_t comm = live();
+        if (!comm) return fail(AMBC_E_COMM, "communicator aborted by a failed rank");
         HIPCHK(hipSetDevice(d.id));
         HIPCHK(d.coll.ensure((size_t)k * 8));
         uint64_t* buf = d.coll.as<uint64_t>();
@@ -81,6 +96,8 @@ struct RcclTransport : Transport {
         return AMBC_OK;
     }
     int gather(const uint8_t* src, uint8_t* dst, const uint64_t* offs, const uint64_t* lens, int root) override {
+        ncclComm_t comm = live();
+        if (!comm) return fail(AMBC_E_COMM, "communicator aborted by a failed rank");
         HIPCHK(hipSetDevice(d.id));
         // pieces of at most 1 GiB per send/recv (both sides cut the same way)
         constexpr uint64_t PIECE = 1ull << 30;
@@ -101,7 +118,12 @@ struct RcclTransport : Transport {
         HIPCHK(hipStreamSynchronize(d.stream));
         return AMBC_OK;
     }
-    void abort() override {}
+    void abort() override {
+        if (!group) return;   // a process per GPU: the status exchanges keep the ranks in step
+        std::lock_guard<std::mutex> lk(*group_mu);
+        for (ncclComm_t& c : *group)
+            if (c) { (void)ncclCommAbort(c); c = nullptr; }
+    }
 };
 
 // ---------------------------------------------------------------------------
@@ -199,7 +221,30 @@ struct SelfTransport : Transport {
     }
 };
 
-int shard_allreduce_min(Transport* t, uint64_t* v) { return t->allreduce_u64(v, 1, AMBC_OP_MIN); }
+// the reference-mode remainder exchange: MIN of the first no-winner chunk, and
+// of an ok flag, so that a rank that failed before the exchange still joins it
+// and every rank leaves together
+int shard_allreduce_min(Transport* t, uint64_t* v, int rc_local) {
+    uint64_t x[2] = {*v, rc_local ? 0ull : 1ull};
+    int rc = t->allreduce_u64(x, 2, AMBC_OP_MIN);
+    if (rc) return rc;
+    if (rc_local) return rc_local;
+    if (!x[1]) return fail(AMBC_E_COMM, "another rank failed before the remainder exchange");
+    *v = x[0];
+    return AMBC_OK;
+}
+
+// every rank's status (MIN of 64 + rc): the ranks continue together or fail
+// together, so that none waits in a collective for a rank that already left
+static int all_ok(Transport& t, int rc_local) {
+    const std::string mine = g_err;
+    uint64_t v = (uint64_t)(64 + rc_local);
+    int rc = t.allreduce_u64(&v, 1, AMBC_OP_MIN);
+    if (rc) return rc;
+    const int code = (int)v - 64;
+    if (code == AMBC_OK) return AMBC_OK;
+    return fail(code, rc_local ? mine : "another rank failed (" + std::to_string(code) + ")");
+}
 
 static void shard_bounds(uint64_t n_total, uint32_t C, int W, int r, uint64_t* k0, uint64_t* k1) {
     const uint64_t M = (n_total + C - 1) / C;
@@ -244,10 +289,22 @@ static int shard_compress(Dev& d, Transport& t, const uint8_t* d_shard, uint64_t
     const uint64_t b0 = std::min(k0 * C, n_total), b1 = std::min(k1 * C, n_total);
     ambc_params q = *p;
     if (t.r != t.W - 1) q.flags |= AMBC_FLAG_NO_END_CHUNK;   // the last rank ends the body
+    // pre-flight: what would make a rank leave before the collectives
+    {
+        const uint64_t bound = ambc_compress_bound(b1 - b0, C) - (t.r != t.W - 1 ? END_CHUNK : 0);
+        const int pre = out_cap < bound ? fail(AMBC_E_CAPACITY, "device output capacity < ambc_compress_bound")
+                                        : AMBC_OK;
+        if (t.W > 1 && (rc = all_ok(t, pre))) return rc;
+        if (pre) return pre;
+    }
     ShardInfo si{&t, k0, n_total};
     uint64_t len = 0;
     ambc_stats lst{};
     rc = compress_on(d, d_shard, b1 - b0, &q, d_out, out_cap, &len, &lst, t.W > 1 ? &si : nullptr);
+    if (t.W > 1) {
+        const int rc2 = all_ok(t, rc);
+        if (rc2) return rc2;
+    }
     if (rc) return rc;
     const uint64_t t0 = now_ns();
     // 1. sizes (and the root's capacity) -> file offsets
@@ -302,6 +359,9 @@ static int shard_decompress(Dev& d, Transport& t, const uint8_t* body, uint64_t 
     std::string derr;
     if (o1 - o0 > out_cap) {
         drc = fail(AMBC_E_CAPACITY, "device output capacity < this rank's decoded range");
+    } else if (root == 0 && t.r == 0 && out_cap < orig_size) {
+        // the root gathers (or, lenient bodies, decodes) the whole output
+        drc = fail(AMBC_E_CAPACITY, "root's capacity < orig_size");
     } else if (b1 > b0) {
         std::vector<ambc_host_chunk> host;
         drc = decompress_on(d, body + b0, b1 - b0, o1 - o0, reg, nullptr, host, &lst, d_out);
@@ -322,12 +382,11 @@ static int shard_decompress(Dev& d, Transport& t, const uint8_t* body, uint64_t 
         if (root == 0) {
             std::vector<uint64_t> lens(t.W);
             for (int q = 0; q < t.W; q++) lens[q] = oo[q + 1] - oo[q];
-            if (t.r == 0 && out_cap < orig_size) return fail(AMBC_E_CAPACITY, "root's capacity < orig_size");
             if ((rc = t.gather(d_out, d_out, oo.data(), lens.data(), 0))) return rc;
         }
     } else {
         if (root != 0) return SHARD_WHOLE;
-        if (t.r == 0) {
+        if (t.r == 0) {   // (out_cap >= orig_size: checked with the status above)
             std::vector<ambc_host_chunk> host;
             if ((rc = decompress_on(d, body, blen, orig_size, reg, nullptr, host, &lst, d_out))) return rc;
         }
@@ -350,13 +409,21 @@ static int make_transports(ambc_ctx* ctx, std::unique_ptr<Hub>& hub, std::vector
     std::set<int> ids;
     for (auto& d : ctx->devs) ids.insert(d.id);
     if ((int)ids.size() == G && !getenv("AMBC_LOCAL_TRANSPORT")) {
-        if (ctx->dev_comms.empty()) {
+        bool fresh = ctx->dev_comms.empty();
+        for (ncclComm_t c : ctx->dev_comms) fresh = fresh || !c;   // aborted by a failed call
+        if (fresh) {
+            for (ncclComm_t c : ctx->dev_comms) if (c) (void)ncclCommDestroy(c);
             std::vector<int> dl;
             for (auto& d : ctx->devs) dl.push_back(d.id);
             ctx->dev_comms.assign(G, nullptr);
             NCCLCHK(ncclCommInitAll(ctx->dev_comms.data(), G, dl.data()));
         }
-        for (int g = 0; g < G; g++) ts.emplace_back(new RcclTransport(ctx->dev_comms[g], ctx->devs[g], G, g));
+        for (int g = 0; g < G; g++) {
+            RcclTransport* rt = new RcclTransport(ctx->dev_comms[g], ctx->devs[g], G, g);
+            rt->group = &ctx->dev_comms;
+            rt->group_mu = &ctx->comm_mu;
+            ts.emplace_back(rt);
+        }
     } else {
         hub.reset(new Hub(G));
         for (int g = 0; g < G; g++) ts.emplace_back(new LocalTransport(*hub, ctx->devs[g], g));
@@ -387,6 +454,111 @@ static int run_ranks(std::vector<std::unique_ptr<Transport>>& ts, F fn) {
     return AMBC_OK;
 }
 
+// Host buffers over several devices.  Native mode: the input streams through
+// the devices in chunk-aligned slabs dealt round-robin (slab s on device s % G);
+// every device overlaps the H2D of its next slab, the compression of this one and
+// the D2H of the previous one (compress_slabs' pipeline, ambc_host.cpp), and after
+// every round an AllGather of the slabs' body sizes gives each slab its file
+// offset, so every body goes straight to its place in the host output.  The
+// AllGather carries each rank's status: a failed rank still joins it and all
+// leave together.  Reference mode (the remainder-raw rule is global): contiguous
+// shards, one compress each (shard_compress), whole-shard copies.
+static int compress_multi_slabs(ambc_ctx* ctx, std::vector<std::unique_ptr<Transport>>& ts, const uint8_t* in,
+                                uint64_t n, const ambc_params* p, uint8_t* out, uint64_t out_cap, uint64_t* out_len,
+                                ambc_stats* st) {
+    const uint64_t t0 = now_ns();
+    const int G = (int)ts.size();
+    const uint32_t C = p->chunk_size;
+    const uint64_t SLAB = std::max<uint64_t>(C, slab_bytes() / C * C);
+    const uint64_t ns = (n + SLAB - 1) / SLAB;
+    const uint64_t rounds = (ns + G - 1) / G;
+    const uint64_t sb = ambc_compress_bound(SLAB, C) + 64;
+    std::vector<ambc_stats> sst(G);
+    std::vector<uint64_t> kern(G, 0), total(G, 0);
+    auto slab_len = [&](uint64_t s) { return s < ns ? std::min(SLAB, n - s * SLAB) : 0ull; };
+    int rc = run_ranks(ts, [&](int g) -> int {
+        Dev& d = ctx->devs[g];
+        Transport& t = *ts[g];
+        HIPCHK(hipSetDevice(d.id));
+        HIPCHK(d.in.ensure(2 * (SLAB + 64)));
+        HIPCHK(d.out.ensure(2 * sb));
+        uint8_t* din[2] = {d.in.as<uint8_t>(), d.in.as<uint8_t>() + SLAB + 64};
+        uint8_t* dout[2] = {d.out.as<uint8_t>(), d.out.as<uint8_t>() + sb};
+        hipEvent_t* h2d_done = d.xev;
+        hipEvent_t* comp_done = d.xev + 2;
+        hipEvent_t* d2h_done = d.xev + 4;
+        auto up = [&](uint64_t j) -> int {
+            const uint64_t s = j * G + g;
+            if (s >= ns) return AMBC_OK;
+            if (j >= 2) HIPCHK(hipStreamWaitEvent(d.xs[0], comp_done[j & 1], 0));  // din[j&1] free
+            HIPCHK(hipMemcpyAsync(din[j & 1], in + s * SLAB, slab_len(s), hipMemcpyHostToDevice, d.xs[0]));
+            HIPCHK(hipEventRecord(h2d_done[j & 1], d.xs[0]));
+            return AMBC_OK;
+        };
+        ambc_stats tot{};
+        uint64_t base = 0;
+        int rl = up(0);
+        std::vector<uint64_t> all((size_t)2 * G);
+        for (uint64_t j = 0; j < rounds; j++) {
+            const uint64_t s = j * G + g;
+            uint64_t len = 0;
+            ambc_stats s1{};
+            if (rl == AMBC_OK && j + 1 < rounds) rl = up(j + 1);
+            if (rl == AMBC_OK && s < ns) {
+                auto run = [&]() -> int {
+                    HIPCHK(hipStreamWaitEvent(d.stream, h2d_done[j & 1], 0));
+                    if (j >= 2) HIPCHK(hipStreamWaitEvent(d.stream, d2h_done[j & 1], 0));  // dout[j&1] free
+                    ambc_params q = *p;
+                    if (s + 1 != ns) { q.flags |= AMBC_FLAG_NO_END_CHUNK; q.ent_tail = nullptr; }
+                    int r2 = compress_on(d, din[j & 1], slab_len(s), &q, dout[j & 1], sb, &len, &s1);
+                    if (r2) return r2;
+                    HIPCHK(hipEventRecord(comp_done[j & 1], d.stream));
+                    return AMBC_OK;
+                };
+                rl = run();
+            }
+            // this round's body sizes and statuses -> the slabs' file offsets
+            const std::string err = g_err;
+            const uint64_t mine[2] = {len, (uint64_t)(64 + rl)};
+            int rc2 = t.allgather_u64(mine, 2, all.data());
+            if (rc2) return rc2;
+            uint64_t off = base, round_total = 0;
+            int peer = AMBC_OK;
+            for (int q = 0; q < G; q++) {
+                if (q < g) off += all[2 * q];
+                round_total += all[2 * q];
+                if ((int)all[2 * q + 1] - 64 != AMBC_OK && peer == AMBC_OK) peer = (int)all[2 * q + 1] - 64;
+            }
+            if (rl) return fail(rl, err);
+            if (peer) return fail(peer, "another device failed its slab (" + std::to_string(peer) + ")");
+            if (base + round_total > out_cap) return fail(AMBC_E_CAPACITY, "output buffer too small for the body");
+            if (len) {
+                HIPCHK(hipStreamWaitEvent(d.xs[1], comp_done[j & 1], 0));
+                HIPCHK(hipMemcpyAsync(out + off, dout[j & 1], len, hipMemcpyDeviceToHost, d.xs[1]));
+                HIPCHK(hipEventRecord(d2h_done[j & 1], d.xs[1]));
+            }
+            base += round_total;
+            kern[g] += s1.kernel_ns;
+            add_stats(&tot, s1);
+        }
+        HIPCHK(hipStreamSynchronize(d.xs[0]));
+        HIPCHK(hipStreamSynchronize(d.xs[1]));
+        int rc3 = reduce_stats(t, &tot);
+        if (rc3) return rc3;
+        sst[g] = tot;
+        total[g] = base;
+        return AMBC_OK;
+    });
+    if (rc) return rc;
+    *out_len = total[0];
+    if (st) {
+        *st = sst[0];
+        st->kernel_ns = *std::max_element(kern.begin(), kern.end());
+        st->total_ns = now_ns() - t0;
+    }
+    return AMBC_OK;
+}
+
 int compress_batch_multi(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const ambc_params* p, uint8_t* out,
                          uint64_t out_cap, uint64_t* out_len, ambc_stats* st) {
     const uint64_t t0 = now_ns();
@@ -394,6 +566,7 @@ int compress_batch_multi(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const amb
     std::vector<std::unique_ptr<Transport>> ts;
     int rc = make_transports(ctx, hub, ts);
     if (rc) return rc;
+    if (p->mode == AMBC_MODE_NATIVE) return compress_multi_slabs(ctx, ts, in, n, p, out, out_cap, out_len, st);
     const int G = (int)ts.size();
     std::vector<ambc_stats> sst(G);
     std::vector<ambc_shard_info> inf(G);

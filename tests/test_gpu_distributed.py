@@ -31,7 +31,9 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _body(n, chunk, methods, seed, mode="native"):
     data = orc.synth(n, seed)
-    body, _ = orc.compress_body(data, orc.make_params(chunk, mode, methods, n_total=n))
+    # id 5 in native mode: the GPU's "ambc-deflate v1" (reference mode: zlib-9's bytes)
+    body, _ = orc.compress_body(data, orc.make_params(chunk, mode, methods, n_total=n,
+                                                      deflate="gd" if mode == "native" else "zlib"))
     return data, body
 
 
@@ -101,6 +103,46 @@ def test_sharded_reference_mode_remainder(hip_lib, shards, raw_at):
     assert st.total_chunks == expect_total
     assert st.raw_chunks == (1 if raw_at is not None else 0)
     multi.close()
+
+
+@pytest.mark.parametrize("shards,n,chunk,methods,slab", [
+    (3, (5 << 20) + 333, 4096, (1, 3, 4, 9), 1 << 20),      # 6 slabs over 3 devices, ragged tail
+    (2, (3 << 20) + 8192 * 5, 8192, (1, 3, 4, 9), 1 << 19),  # C4's chunk
+    (4, (1 << 20) + 77, 4096, (1, 3, 4, 5), 300000),         # a slab that is not a chunk multiple, id 5
+    (3, 700000, 1024, (1, 2, 3, 4), 1 << 18),                # the last round leaves a device idle
+])
+def test_multi_device_slab_pipeline_equals_single_device(hip_lib, shards, n, chunk, methods, slab):
+    """Host-fed native compress over several devices: chunk-aligned slabs dealt
+    round-robin, H2D / compress / D2H overlapped per device, every slab's body
+    written at the file offset of a per-round AllGather of sizes -- the body and
+    stats equal the single-device call and the oracle."""
+    data, ref = _body(n, chunk, methods + (255,), 57)
+    one = _ctx([0])
+    single, st1 = _compress(one, data, chunk, methods)
+    os.environ["AMBC_SLAB_BYTES"] = str(slab)
+    try:
+        multi = _ctx([0] * shards)
+        got, st = _compress(multi, data, chunk, methods)
+    finally:
+        del os.environ["AMBC_SLAB_BYTES"]
+    assert (single == ref) is True and (got == ref) is True   # (no byte diff of megabytes on failure)
+    assert st.total_chunks == st1.total_chunks and st.compressed_chunks == st1.compressed_chunks
+    assert list(st.method_usage) == list(st1.method_usage)
+    assert st.payload_bytes == st1.payload_bytes and st.bytes_saved == st1.bytes_saved
+    # a buffer too small for the body: every device fails at the same round, none hangs
+    from ambc import _lib
+    os.environ["AMBC_SLAB_BYTES"] = str(slab)
+    try:
+        p, keep = __import__("ambc").AdaptiveCompressor(chunk_size=chunk, methods=methods)._params(n)
+        small = bytearray(len(ref) // 2)
+        olen = C.c_uint64()
+        rc = multi.lib.ambc_compress_batch(multi.h, _lib.addr(data), n, C.byref(p), _lib.addr(small),
+                                           len(small), C.byref(olen), None)
+    finally:
+        del os.environ["AMBC_SLAB_BYTES"]
+    assert rc == _lib.AMBC_E_CAPACITY
+    multi.close()
+    one.close()
 
 
 def test_sharded_compress_reports_capacity_consistently(hip_lib):
@@ -264,3 +306,68 @@ def test_two_rank_rccl_bench(hip_lib):
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == 2 and line["config"]["round_trip_bit_exact"] is True
     assert line["config"]["reassembly_to_rank0"]["rank0_prefix_equal"] is True
+
+
+def test_inprocess_rccl_devices(hip_lib):
+    """A ctx over every GPU of the box: ncclCommInitAll communicators (no host
+    transport), the slab pipeline in native mode, contiguous shards with the
+    remainder exchange in reference mode, and the split decode -- all equal to
+    the single-device results.  Skips on a one-GPU box."""
+    ng = _ngpus(hip_lib)
+    if ng < 2:
+        pytest.skip("one GPU on this box")
+    from ambc.distributed import decompress_multi
+    assert "AMBC_LOCAL_TRANSPORT" not in os.environ
+    devs = list(range(min(ng, 8)))
+    n, chunk = (24 << 20) + 999, 4096
+    data, ref = _body(n, chunk, (1, 3, 4, 9, 255), 61)
+    multi = _ctx(devs)
+    os.environ["AMBC_SLAB_BYTES"] = str(2 << 20)
+    try:
+        got, st = _compress(multi, data, chunk, (1, 3, 4, 9))
+    finally:
+        del os.environ["AMBC_SLAB_BYTES"]
+    assert got == ref
+    rdata = _ref_mode_input(1024, 24 * len(devs), 29)
+    rref, _ = orc.compress_body(rdata, orc.make_params(1024, "reference", (1, 3, 4, 255), n_total=len(rdata)))
+    rgot, _ = _compress(multi, rdata, 1024, (1, 3, 4), mode="reference")
+    assert rgot == rref
+    assert decompress_multi(multi, ref, n) == data
+    multi.close()
+
+
+def test_rccl_multi_rank_shards(hip_lib):
+    """One process per GPU over RCCL (ambc_comm_init_rank; AMBC_LOCAL_TRANSPORT
+    unset): compress_shard / decompress_shard / the xGMI gather in native mode
+    (chunks 4096 and 8192) and reference mode, rank 0's body equal to the oracle
+    and its decode equal to the input (tests/rccl_shard_worker.py).  Skips on a
+    one-GPU box."""
+    ng = _ngpus(hip_lib)
+    if ng < 2:
+        pytest.skip("one GPU on this box: RCCL admits one rank per device")
+    import json
+    world = min(ng, 8)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = {k: v for k, v in os.environ.items() if k != "AMBC_LOCAL_TRANSPORT"}
+    env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world))
+    procs = []
+    for r in range(world):
+        e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(REPO, "tests", "rccl_shard_worker.py")],
+                                      env=e, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = []
+    try:
+        for pr in procs:
+            o, e = pr.communicate(timeout=240)
+            outs.append((pr.returncode, o, e))
+    finally:
+        for pr in procs:
+            if pr.poll() is None:
+                pr.kill()
+    for rc, o, e in outs:
+        assert rc == 0, e[-2000:]
+        line = json.loads(o.strip().splitlines()[-1])
+        assert line["ok"] is True
