@@ -289,38 +289,39 @@ static int shard_compress(Dev& d, Transport& t, const uint8_t* d_shard, uint64_t
     const uint64_t b0 = std::min(k0 * C, n_total), b1 = std::min(k1 * C, n_total);
     ambc_params q = *p;
     if (t.r != t.W - 1) q.flags |= AMBC_FLAG_NO_END_CHUNK;   // the last rank ends the body
-    // pre-flight: what would make a rank leave before the collectives
-    {
+    // reference mode exchanges inside compress_on (the remainder): first agree
+    // that no rank leaves before it (its own check of the output capacity)
+    if (t.W > 1 && p->mode == AMBC_MODE_REFERENCE) {
         const uint64_t bound = ambc_compress_bound(b1 - b0, C) - (t.r != t.W - 1 ? END_CHUNK : 0);
         const int pre = out_cap < bound ? fail(AMBC_E_CAPACITY, "device output capacity < ambc_compress_bound")
                                         : AMBC_OK;
-        if (t.W > 1 && (rc = all_ok(t, pre))) return rc;
-        if (pre) return pre;
+        if ((rc = all_ok(t, pre))) return rc;
     }
     ShardInfo si{&t, k0, n_total};
     uint64_t len = 0;
     ambc_stats lst{};
     rc = compress_on(d, d_shard, b1 - b0, &q, d_out, out_cap, &len, &lst, t.W > 1 ? &si : nullptr);
-    if (t.W > 1) {
-        const int rc2 = all_ok(t, rc);
-        if (rc2) return rc2;
-    }
-    if (rc) return rc;
+    const std::string err = g_err;
     const uint64_t t0 = now_ns();
-    // 1. sizes (and the root's capacity) -> file offsets
-    std::vector<uint64_t> all((size_t)2 * t.W);
-    const uint64_t mine[2] = {len, out_cap};
-    if ((rc = t.allgather_u64(mine, 2, all.data()))) return rc;
+    // 1. sizes, the root's capacity and every rank's status -> file offsets (a
+    //    rank whose compress failed still joins, and all leave together)
+    std::vector<uint64_t> all((size_t)3 * t.W);
+    const uint64_t mine[3] = {len, out_cap, (uint64_t)(64 + rc)};
+    int rc2 = t.allgather_u64(mine, 3, all.data());
+    if (rc) return fail(rc, err);
+    if (rc2) return rc2;
     std::vector<uint64_t> offs(t.W + 1, 0), lens(t.W);
     for (int i = 0; i < t.W; i++) {
-        lens[i] = all[2 * i];
+        const int code = (int)all[3 * i + 2] - 64;
+        if (code != AMBC_OK) return fail(code, "another rank failed to compress its shard (" + std::to_string(code) + ")");
+        lens[i] = all[3 * i];
         offs[i + 1] = offs[i] + lens[i];
     }
     // 2. statistics
     if ((rc = reduce_stats(t, &lst))) return rc;
     // 4. optional gather onto rank 0
     if (root == 0) {
-        if (offs[t.W] > all[1]) return fail(AMBC_E_CAPACITY, "root's output capacity < the whole body");
+        if (offs[t.W] > all[1]) return fail(AMBC_E_CAPACITY, "root's output capacity < the whole body");   // (rank 0's cap)
         if ((rc = t.gather(d_out, d_out, offs.data(), lens.data(), 0))) return rc;
     }
     lst.total_ns += now_ns() - t0;
