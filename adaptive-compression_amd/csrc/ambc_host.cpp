@@ -8,12 +8,15 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -101,10 +104,14 @@ void ambc_destroy(ambc_ctx* ctx) {
                        &d.inffix})
             b->release();
         for (auto& b : d.msb) b.release();
+        d.dw.release();
         for (auto& x : d.mss) if (x) { (void)hipStreamSynchronize(x); (void)hipStreamDestroy(x); }
         for (void* b : d.stage) (void)hipHostFree(b);
         for (auto& ev : d.stage_ev) (void)hipEventDestroy(ev);
         for (auto& x : d.stage_st) (void)hipStreamDestroy(x);
+        for (void* b : d.stage1) (void)hipHostFree(b);
+        for (auto& ev : d.stage1_ev) (void)hipEventDestroy(ev);
+        for (auto& x : d.stage1_st) (void)hipStreamDestroy(x);
         for (auto& ev : d.ev) (void)hipEventDestroy(ev);
         for (auto& ev : d.xev) (void)hipEventDestroy(ev);
         for (auto& x : d.xs) { (void)hipStreamSynchronize(x); (void)hipStreamDestroy(x); }
@@ -960,9 +967,12 @@ int follow_chain(const uint8_t* body, uint64_t blen, uint64_t start, uint64_t li
 // the chain is the thread's (the walk is deterministic), else it is walked there.
 // Jobs are built in parallel; offsets by one serial prefix pass.
 void walk_body(const uint8_t* body, uint64_t blen, uint64_t orig_size, const uint64_t reg[4],
-               const std::map<uint32_t, uint64_t>& known, Walk& w) {
-    const unsigned T = std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+               const std::map<uint32_t, uint64_t>& known, Walk& w, unsigned tmax = 16) {
+    const unsigned T = std::min(tmax, std::max(1u, std::thread::hardware_concurrency()));
     if (blen < (32ull << 20) || T < 2) { walk_body_serial(body, blen, orig_size, reg, known, w); return; }
+    const bool tr = getenv("AMBC_WALK_TRACE") != nullptr;
+    uint64_t tm[8], tn = 0;
+    tm[tn++] = now_ns();
     std::vector<std::vector<uint64_t>> seg(T);
     std::vector<uint64_t> sexit(T, UINT64_MAX);
     std::vector<int> sstat(T, 0);
@@ -991,6 +1001,7 @@ void walk_body(const uint8_t* body, uint64_t blen, uint64_t orig_size, const uin
         discover(0);
         for (auto& x : th) x.join();
     }
+    tm[tn++] = now_ns();
     // stitch the true chain
     std::vector<uint64_t> H(seg[0]);
     uint64_t q = sexit[0];
@@ -1005,6 +1016,7 @@ void walk_body(const uint8_t* body, uint64_t blen, uint64_t orig_size, const uin
             status = follow_chain(body, blen, q, s0[t + 1], H, &q);
         }
     }
+    tm[tn++] = now_ns();
     // jobs in parallel, then offsets and the out >= orig_size stop in order
     const size_t K = H.size();
     std::vector<DecJob> J(K);
@@ -1021,6 +1033,7 @@ void walk_body(const uint8_t* body, uint64_t blen, uint64_t orig_size, const uin
         build(0);
         for (auto& x : th) x.join();
     }
+    tm[tn++] = now_ns();
     // offsets: per-block sums, a prefix over the blocks, then each block finds its
     // own stop (a header that ends the walk, or out reaching orig_size) and fills
     // in its offsets; the walk stops at the first block's stop
@@ -1051,6 +1064,7 @@ void walk_body(const uint8_t* body, uint64_t blen, uint64_t orig_size, const uin
     par(bsum);
     for (unsigned t = 0; t < T; t++) { bo[t + 1] += bo[t]; bs[t + 1] += bs[t]; }
     par(fill);
+    tm[tn++] = now_ns();
     size_t nj = K;
     bool stopped = false;
     for (unsigned t = 0; t < T; t++)
@@ -1076,6 +1090,12 @@ void walk_body(const uint8_t* body, uint64_t blen, uint64_t orig_size, const uin
     }
     w.scratch = scr;
     w.total = total;
+    tm[tn++] = now_ns();
+    if (tr) {
+        fprintf(stderr, "[ambc walk] T=%u K=%zu:", T, K);
+        for (uint64_t i = 1; i < tn; i++) fprintf(stderr, " %.2f", (tm[i] - tm[i - 1]) / 1e6);
+        fprintf(stderr, " ms (discover, stitch, jobs, offsets, finish)\n");
+    }
 }
 
 }  // namespace
@@ -1148,10 +1168,20 @@ static void inflate_all(const uint8_t* body, const std::vector<ambc_host_chunk>&
 constexpr size_t kStagePiece = 8u << 20;
 constexpr uint64_t kStageMin = 64ull << 20;   // below this the runtime's own path
 
-static int ensure_stage(Dev& d, unsigned T) {
-    if (d.stage_st.size() >= T) return AMBC_OK;
+struct StageSet {
+    std::vector<void*>* buf;
+    std::vector<hipStream_t>* st;
+    std::vector<hipEvent_t>* ev;
+};
+static StageSet stage_set(Dev& d, int set) {
+    return set ? StageSet{&d.stage1, &d.stage1_st, &d.stage1_ev} : StageSet{&d.stage, &d.stage_st, &d.stage_ev};
+}
+
+static int ensure_stage(Dev& d, unsigned T, int set = 0) {
+    StageSet S = stage_set(d, set);
+    if (S.st->size() >= T) return AMBC_OK;
     HIPCHK(hipSetDevice(d.id));
-    while (d.stage_st.size() < T) {
+    while (S.st->size() < T) {
         void* b[2] = {nullptr, nullptr};
         hipStream_t st;
         hipEvent_t ev[2];
@@ -1160,38 +1190,41 @@ static int ensure_stage(Dev& d, unsigned T) {
         HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
         HIPCHK(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
-        d.stage.push_back(b[0]); d.stage.push_back(b[1]);
-        d.stage_st.push_back(st);
-        d.stage_ev.push_back(ev[0]); d.stage_ev.push_back(ev[1]);
+        S.buf->push_back(b[0]); S.buf->push_back(b[1]);
+        S.st->push_back(st);
+        S.ev->push_back(ev[0]); S.ev->push_back(ev[1]);
     }
     return AMBC_OK;
 }
 
-static unsigned stage_threads(uint64_t n) {
+static unsigned stage_threads(uint64_t n, unsigned cap = 16) {
     const char* e = getenv("AMBC_HOST_THREADS");
-    unsigned t = e ? (unsigned)std::max(1, atoi(e)) : std::min(16u, std::thread::hardware_concurrency());
+    unsigned t = e ? (unsigned)std::max(1, atoi(e)) : std::min(cap, std::thread::hardware_concurrency());
     return std::max(1u, std::min<unsigned>(t, (unsigned)(n / kStagePiece) + 1));
 }
 
+static void hugepage_advice(void* dst, uint64_t n) {
+    // a fresh output (calloc'd bytes) is faulted in on first touch: ask for 2 MiB
+    // pages so that 4 GiB is 2048 faults, not a million (advice only)
+    const uintptr_t lo = ((uintptr_t)dst + (2u << 20) - 1) & ~(uintptr_t)((2u << 20) - 1);
+    const uintptr_t hi = ((uintptr_t)dst + n) & ~(uintptr_t)((2u << 20) - 1);
+    if (hi > lo) (void)madvise((void*)lo, hi - lo, MADV_HUGEPAGE);
+}
+
 // to_dev: host src -> device dst; else device src -> host dst
-static int copy_staged(Dev& d, void* dst, const void* src, uint64_t n, bool to_dev) {
-    const unsigned T = stage_threads(n);
-    int rc = ensure_stage(d, T);
+static int copy_staged(Dev& d, void* dst, const void* src, uint64_t n, bool to_dev, int set = 0, unsigned cap = 16) {
+    const unsigned T = stage_threads(n, cap);
+    int rc = ensure_stage(d, T, set);
     if (rc) return rc;
-    if (!to_dev) {
-        // a fresh output (calloc'd bytes) is faulted in on first touch: ask for 2 MiB
-        // pages so that 4 GiB is 2048 faults, not a million (advice only)
-        const uintptr_t lo = ((uintptr_t)dst + (2u << 20) - 1) & ~(uintptr_t)((2u << 20) - 1);
-        const uintptr_t hi = ((uintptr_t)dst + n) & ~(uintptr_t)((2u << 20) - 1);
-        if (hi > lo) (void)madvise((void*)lo, hi - lo, MADV_HUGEPAGE);
-    }
+    StageSet S = stage_set(d, set);
+    if (!to_dev) hugepage_advice(dst, n);
     std::vector<int> err(T, 0);
     auto run = [&](unsigned t) {
         if (hipSetDevice(d.id) != hipSuccess) { err[t] = 1; return; }
         const uint64_t a = n * t / T, b = n * (t + 1) / T;
-        uint8_t* pb[2] = {static_cast<uint8_t*>(d.stage[2 * t]), static_cast<uint8_t*>(d.stage[2 * t + 1])};
-        hipEvent_t* ev = &d.stage_ev[2 * t];
-        hipStream_t st = d.stage_st[t];
+        uint8_t* pb[2] = {static_cast<uint8_t*>((*S.buf)[2 * t]), static_cast<uint8_t*>((*S.buf)[2 * t + 1])};
+        hipEvent_t* ev = &(*S.ev)[2 * t];
+        hipStream_t st = (*S.st)[t];
         const uint8_t* s8 = static_cast<const uint8_t*>(src);
         uint8_t* d8 = static_cast<uint8_t*>(dst);
         if (to_dev) {
@@ -1234,9 +1267,651 @@ static int copy_staged(Dev& d, void* dst, const void* src, uint64_t n, bool to_d
     return AMBC_OK;
 }
 
+// An upload in pieces taken in file order (piece q by thread q % T), each
+// marked done once its DMA has completed, so that a consumer can start on the
+// prefix [0, x) as soon as it has arrived (wait_prefix).
+struct OrderedUpload {
+    std::mutex m;
+    std::condition_variable cv;
+    std::vector<uint8_t> done;
+    uint64_t n = 0, ready = 0;     // ready: the leading pieces all done
+    bool failed = false;
+    std::vector<std::thread> th;
+    // registered mode: the caller's pages pinned piece by piece and copied by
+    // DMA (no staging copy); pieces [a, b) of the host range, their events
+    struct RegPiece { uintptr_t a, b; hipEvent_t ev; bool reg; };
+    std::vector<RegPiece> rp;
+    std::unique_ptr<std::atomic<int>[]> issued;   // piece j's DMA and event record are queued
+    Dev* dev = nullptr;
+    void mark(uint64_t q) {
+        std::lock_guard<std::mutex> lk(m);
+        done[q] = 1;
+        while (ready < done.size() && done[ready]) ready++;
+        cv.notify_all();
+    }
+    void fail_all() {
+        std::lock_guard<std::mutex> lk(m);
+        failed = true;
+        cv.notify_all();
+    }
+    // false when the upload failed
+    bool wait_prefix(uint64_t bytes) {
+        const uint64_t need = std::min<uint64_t>(done.size(), (bytes + kStagePiece - 1) / kStagePiece);
+        std::unique_lock<std::mutex> lk(m);
+        cv.wait(lk, [&] { return failed || ready >= need; });
+        return !failed;
+    }
+    void join() { for (auto& x : th) if (x.joinable()) x.join(); th.clear(); }
+    // registered mode: after join(), wait for the DMAs and unpin
+    void release() {
+        join();
+        for (auto& p : rp) {
+            if (p.ev) { (void)hipEventSynchronize(p.ev); (void)hipEventDestroy(p.ev); p.ev = nullptr; }
+            if (p.reg) { (void)hipHostUnregister(reinterpret_cast<void*>(p.a)); p.reg = false; }
+        }
+    }
+    ~OrderedUpload() { release(); }
+};
+
+// The registered upload: one helper thread pins the body piece by piece (4 KiB
+// aligned interior; the unaligned head and tail bytes are copied first) and
+// queues each piece's DMA on its own stream; a piece counts as done once its
+// DMA's event has fired (a waiter thread marks them in order).  A piece the
+// runtime refuses to pin goes through a staging buffer copy instead.
+static int start_registered_upload(Dev& d, uint8_t* dst, const uint8_t* src, uint64_t n, OrderedUpload& u) {
+    constexpr uint64_t PIECE = 64ull << 20;
+    const uintptr_t PG = 4096, sb = (uintptr_t)src, se = sb + n;
+    const uintptr_t ra = (sb + PG - 1) & ~(PG - 1), rb = se & ~(PG - 1);
+    if (rb <= ra + PG) return AMBC_E_INVAL;   // (too small: the staged upload)
+    HIPCHK(hipSetDevice(d.id));
+    // the edges first, synchronously (a few KiB)
+    if (ra > sb) HIPCHK(hipMemcpy(dst, src, ra - sb, hipMemcpyHostToDevice));
+    if (se > rb) HIPCHK(hipMemcpy(dst + (rb - sb), src + (rb - sb), se - rb, hipMemcpyHostToDevice));
+    for (uintptr_t x = ra; x < rb; x += PIECE)
+        u.rp.push_back(OrderedUpload::RegPiece{x, std::min<uintptr_t>(rb, x + PIECE), nullptr, false});
+    for (auto& p : u.rp) HIPCHK(hipEventCreateWithFlags(&p.ev, hipEventDisableTiming));
+    u.issued.reset(new std::atomic<int>[u.rp.size()]);
+    for (size_t j = 0; j < u.rp.size(); j++) u.issued[j].store(0);
+    // piece j covers body bytes [a - sb, b - sb); done[] is kept per kStagePiece as
+    // in the staged mode: the waiter marks the staged-size pieces a DMA covers
+    const uint64_t np = (n + kStagePiece - 1) / kStagePiece;
+    u.n = n;
+    u.done.assign(np, 0);
+    u.dev = &d;
+    if (!d.xs[0]) HIPCHK(hipStreamCreateWithFlags(&d.xs[0], hipStreamNonBlocking));
+    u.th.emplace_back([&d, &u, dst, src, sb] {
+        if (hipSetDevice(d.id) != hipSuccess) { u.fail_all(); return; }
+        for (auto& p : u.rp) {
+            const uint64_t off = p.a - sb, len = p.b - p.a;
+            p.reg = hipHostRegister(reinterpret_cast<void*>(p.a), len, hipHostRegisterDefault) == hipSuccess;
+            const hipError_t e = p.reg ? hipMemcpyAsync(dst + off, src + off, len, hipMemcpyHostToDevice, d.xs[0])
+                                       : hipMemcpy(dst + off, src + off, len, hipMemcpyHostToDevice);
+            if (e != hipSuccess || hipEventRecord(p.ev, d.xs[0]) != hipSuccess) { u.fail_all(); return; }
+            u.issued[&p - u.rp.data()].store(1, std::memory_order_release);
+        }
+    });
+    u.th.emplace_back([&u, sb, n, np] {
+        // mark the staged-size pieces whose bytes are all on the device
+        uint64_t q = 0;
+        for (auto& p : u.rp) {
+            // (an event not yet recorded reads as complete: wait for the record first)
+            while (!u.issued[&p - u.rp.data()].load(std::memory_order_acquire)) {
+                { std::lock_guard<std::mutex> lk(u.m); if (u.failed) return; }
+                std::this_thread::sleep_for(std::chrono::microseconds(20));
+            }
+            hipError_t e;
+            while ((e = hipEventQuery(p.ev)) == hipErrorNotReady) std::this_thread::sleep_for(std::chrono::microseconds(50));
+            if (e != hipSuccess) { u.fail_all(); return; }
+            const uint64_t upto = (&p == &u.rp.back()) ? n : p.b - sb;
+            while (q < np && std::min<uint64_t>(n, (q + 1) * kStagePiece) <= upto) u.mark(q++);
+        }
+        while (q < np) u.mark(q++);
+    });
+    return AMBC_OK;
+}
+
+static int start_ordered_upload(Dev& d, uint8_t* dst, const uint8_t* src, uint64_t n, unsigned T, OrderedUpload& u) {
+    int rc = ensure_stage(d, T, 0);
+    if (rc) return rc;
+    const uint64_t np = (n + kStagePiece - 1) / kStagePiece;
+    u.n = n;
+    u.done.assign(np, 0);
+    for (unsigned t = 0; t < T; t++) {
+        u.th.emplace_back([&d, &u, dst, src, n, np, t, T] {
+            if (hipSetDevice(d.id) != hipSuccess) { u.fail_all(); return; }
+            uint8_t* pb[2] = {static_cast<uint8_t*>(d.stage[2 * t]), static_cast<uint8_t*>(d.stage[2 * t + 1])};
+            hipEvent_t* ev = &d.stage_ev[2 * t];
+            hipStream_t st = d.stage_st[t];
+            uint64_t pend[2] = {UINT64_MAX, UINT64_MAX};   // piece in flight per buffer
+            int cur = 0;
+            for (uint64_t q = t; q < np; q += T, cur ^= 1) {
+                if (pend[cur] != UINT64_MAX) {
+                    if (hipEventSynchronize(ev[cur]) != hipSuccess) { u.fail_all(); return; }
+                    u.mark(pend[cur]);
+                }
+                const uint64_t off = q * kStagePiece;
+                const size_t len = (size_t)std::min<uint64_t>(kStagePiece, n - off);
+                std::memcpy(pb[cur], src + off, len);
+                if (hipMemcpyAsync(dst + off, pb[cur], len, hipMemcpyHostToDevice, st) != hipSuccess ||
+                    hipEventRecord(ev[cur], st) != hipSuccess) { u.fail_all(); return; }
+                pend[cur] = q;
+            }
+            for (int b = 0; b < 2; b++) {
+                const int c = cur ^ b;
+                if (pend[c] == UINT64_MAX) continue;
+                if (hipEventSynchronize(ev[c]) != hipSuccess) { u.fail_all(); return; }
+                u.mark(pend[c]);
+            }
+        });
+    }
+    return AMBC_OK;
+}
+
+// The copy back of a decode goes straight from the device into the caller's
+// output: its pages are faulted in (2 MiB pages where the kernel grants them)
+// and registered with the runtime piece by piece, ahead of the decode, on a
+// helper thread; each decoded range is then one DMA on the copy stream after the
+// kernels that wrote it -- no staging copy on the host.  The page-unaligned head
+// and tail bytes (and any piece the runtime refuses to register) go through the
+// staged copy at the end.
+struct OutDMA {
+    static constexpr uintptr_t PG = 4096, HP = 2u << 20, PIECE = 128u << 20;
+    struct Piece { uintptr_t a, b; bool reg; };
+    Dev& d;
+    uint8_t* out;
+    uint64_t n;
+    const uint8_t* src;                 // device bytes
+    uintptr_t ob, oe, ra, rb;           // registrable [ra, rb)
+    std::vector<Piece> pcs;
+    std::mutex m;
+    std::condition_variable cv;
+    size_t prepped = 0;                 // pieces [0, prepped) faulted in and (if reg) registered
+    bool stop_prep = false;
+    size_t pnext = 0;                   // first piece not yet copied
+    std::vector<std::pair<uint64_t, uint64_t>> staged;   // ranges the DMA does not cover
+    std::thread prep;
+
+    OutDMA(Dev& dv, uint8_t* o, uint64_t len, const uint8_t* s) : d(dv), out(o), n(len), src(s) {
+        ob = (uintptr_t)out;
+        oe = ob + n;
+        ra = (ob + PG - 1) & ~(PG - 1);
+        rb = oe & ~(PG - 1);
+        if (rb > ra) {
+            for (uintptr_t x = ra; x < rb;) {
+                const uintptr_t y = std::min<uintptr_t>(rb, ((x + PIECE) & ~(HP - 1)) > x ? ((x + PIECE) & ~(HP - 1)) : rb);
+                pcs.push_back(Piece{x, y, false});
+                x = y;
+            }
+        }
+        hugepage_advice(out, n);
+        prep = std::thread([this] { run_prep(); });
+    }
+    ~OutDMA() { unreg_all(); }
+
+    void run_prep() {
+        if (hipSetDevice(d.id) != hipSuccess) { std::lock_guard<std::mutex> lk(m); prepped = pcs.size(); cv.notify_all(); return; }
+        const unsigned TP = std::max(1u, std::min(8u, stage_threads(n, 8)));
+        for (size_t j = 0; j < pcs.size(); j++) {
+            { std::lock_guard<std::mutex> lk(m); if (stop_prep) break; }
+            Piece& pc = pcs[j];
+            std::vector<std::thread> th;
+            for (unsigned t = 0; t < TP; t++)
+                th.emplace_back([&pc, t, TP] {
+                    const uintptr_t a = pc.a + (pc.b - pc.a) * t / TP, b = pc.a + (pc.b - pc.a) * (t + 1) / TP;
+                    for (uintptr_t x = a & ~(PG - 1); x < b; x += PG)
+                        if (x >= pc.a) *reinterpret_cast<volatile uint8_t*>(x) = 0;   // (fresh output: zeros)
+                });
+            for (auto& x : th) x.join();
+            pc.reg = hipHostRegister(reinterpret_cast<void*>(pc.a), pc.b - pc.a, hipHostRegisterDefault) == hipSuccess;
+            { std::lock_guard<std::mutex> lk(m); prepped = j + 1; }
+            cv.notify_all();
+        }
+        std::lock_guard<std::mutex> lk(m);
+        prepped = pcs.size();
+        cv.notify_all();
+    }
+    void unreg_all() {
+        { std::lock_guard<std::mutex> lk(m); stop_prep = true; }
+        if (prep.joinable()) prep.join();
+        (void)hipStreamSynchronize(d.xs[1]);
+        for (auto& pc : pcs) if (pc.reg) { (void)hipHostUnregister(reinterpret_cast<void*>(pc.a)); pc.reg = false; }
+    }
+    // DMA of the pieces entirely below output offset upto, after event `after`
+    int copy_ready(uint64_t upto, hipEvent_t after) {
+        std::unique_lock<std::mutex> lk(m);
+        while (pnext < pcs.size() && pcs[pnext].b <= ob + upto) {
+            cv.wait(lk, [&] { return prepped > pnext; });
+            const Piece& pc = pcs[pnext];
+            const uint64_t lo = pc.a - ob, hi = pc.b - ob;
+            if (pc.reg) {
+                if (after) HIPCHK(hipStreamWaitEvent(d.xs[1], after, 0));
+                HIPCHK(hipMemcpyAsync(out + lo, src + lo, hi - lo, hipMemcpyDeviceToHost, d.xs[1]));
+            } else {
+                staged.emplace_back(lo, hi);
+            }
+            pnext++;
+        }
+        return AMBC_OK;
+    }
+    // the rest after `after`, then the unaligned edges and the unregistered pieces
+    int finish(hipEvent_t after) {
+        int rc = copy_ready(n, after);
+        if (rc) { unreg_all(); return rc; }
+        HIPCHK(hipStreamSynchronize(d.xs[1]));
+        unreg_all();
+        if (ra > ob || rb <= ra) staged.emplace_back(0, std::min<uint64_t>(n, rb > ra ? ra - ob : n));
+        if (rb > ra && oe > rb) staged.emplace_back(rb - ob, n);
+        for (auto& r : staged) {
+            if (r.second <= r.first) continue;
+            if (r.second - r.first >= kStageMin) {
+                rc = copy_staged(d, out + r.first, src + r.first, r.second - r.first, false, 1);
+                if (rc) return rc;
+            } else {
+                HIPCHK(hipMemcpy(out + r.first, src + r.first, r.second - r.first, hipMemcpyDeviceToHost));
+            }
+        }
+        return AMBC_OK;
+    }
+};
+
+// Large host-to-host decodes as a pipeline (SURVEY 8(d) T_api): the body goes
+// up in ordered pieces while the host walks its headers; the jobs are cut into
+// slabs of about kSlabOut output bytes, slab s is decoded as soon as the body
+// pieces its packages read have arrived, and copied back (pinned staging on its
+// own threads) while slab s+1 decodes and the upload goes on -- PCIe carries the
+// body up and the output down at once.  PIPE_FALLBACK: some package decoded to
+// another length than its header announced (the reference's lenient paths need
+// the re-walk of the sequential path below, which redoes the whole call).
+constexpr int PIPE_FALLBACK = 1;
+constexpr uint64_t kSlabOut = 256ull << 20;
+
+static int decompress_pipelined(Dev& d, const uint8_t* body, uint64_t blen, uint64_t orig_size,
+                                const uint64_t reg[4], uint8_t* out, std::vector<ambc_host_chunk>& host,
+                                ambc_stats* st) {
+    const uint64_t t0 = now_ns();
+    HIPCHK(hipSetDevice(d.id));
+    hipStream_t s = d.stream;
+    HIPCHK(d.body.ensure(blen + 64));
+    std::unique_ptr<OrderedUpload> upp(new OrderedUpload());
+    // the body by DMA from its own (pinned) pages, else through the staging buffers
+    int rc = getenv("AMBC_STAGED_UPLOAD") ? AMBC_E_INVAL
+                                          : start_registered_upload(d, d.body.as<uint8_t>(), body, blen, *upp);
+    if (rc) {
+        upp.reset(new OrderedUpload());
+        rc = start_ordered_upload(d, d.body.as<uint8_t>(), body, blen, stage_threads(blen, 8), *upp);
+        if (rc) return rc;
+    }
+    OrderedUpload& up = *upp;
+    // the header walk meanwhile, on the host body
+    std::map<uint32_t, uint64_t> known;
+    Walk w;
+    uint64_t t = now_ns();
+    walk_body(body, blen, orig_size, reg, known, w, 12);
+    const uint64_t walk_ns = now_ns() - t;
+    if (w.marker_error) {
+        up.release();
+        return fail(AMBC_E_MARKER, "Marker mismatch in chunk header.");
+    }
+    const uint32_t nj = (uint32_t)w.jobs.size();
+    const uint64_t cap = std::max(w.total, orig_size) + 64;
+    HIPCHK(d.dout.ensure(cap));
+    HIPCHK(d.jobs.ensure((size_t)std::max<uint32_t>(nj, 1) * sizeof(DecJob)));
+    HIPCHK(d.produced.ensure((size_t)std::max<uint32_t>(nj, 1) * 4));
+    HIPCHK(d.scratch.ensure(w.scratch + 64));
+    HIPCHK(d.list.ensure((size_t)std::max<uint32_t>(nj, 1) * 4));
+    // slabs of jobs (by output offset), per slab one list per decode kernel
+    const char* es = getenv("AMBC_DECODE_SLAB");   // (tests: many slabs on small bodies)
+    const uint64_t slab_out = es && strtoull(es, nullptr, 10) ? strtoull(es, nullptr, 10) : kSlabOut;
+    std::vector<uint32_t> sj{0};
+    for (uint32_t i = 1; i < nj; i++)
+        if (w.jobs[i].out_off >= (uint64_t)sj.size() * slab_out) sj.push_back(i);
+    sj.push_back(nj);
+    const size_t S = sj.size() - 1;
+    std::vector<uint32_t> lists(nj), lcnt(S * DEC_KINDS, 0), lbase(S * DEC_KINDS, 0);
+    std::vector<uint64_t> bneed(S, 0), o0(S + 1, 0);
+    {
+        uint32_t at = 0;
+        for (size_t q = 0; q < S; q++) {
+            for (uint32_t i = sj[q]; i < sj[q + 1]; i++) {
+                lcnt[q * DEC_KINDS + w.kind[i]]++;
+                bneed[q] = std::max<uint64_t>(bneed[q], w.jobs[i].body_off + w.jobs[i].clen);
+            }
+            for (int k = 0; k < DEC_KINDS; k++) { lbase[q * DEC_KINDS + k] = at; at += lcnt[q * DEC_KINDS + k]; }
+            std::vector<uint32_t> fill(lbase.begin() + q * DEC_KINDS, lbase.begin() + (q + 1) * DEC_KINDS);
+            for (uint32_t i = sj[q]; i < sj[q + 1]; i++) lists[fill[w.kind[i]]++] = i;
+            o0[q] = q == 0 ? 0 : std::min<uint64_t>(w.jobs[sj[q]].out_off, orig_size);
+        }
+        o0[S] = orig_size;
+        if (S) bneed[S - 1] = blen;   // (the last slab waits for the whole body)
+    }
+    if (nj) HIPCHK(hipMemcpyAsync(d.jobs.p, w.jobs.data(), nj * sizeof(DecJob), hipMemcpyHostToDevice, s));
+    if (nj) HIPCHK(hipMemcpyAsync(d.list.p, lists.data(), nj * 4, hipMemcpyHostToDevice, s));
+    if (w.total < orig_size) HIPCHK(hipMemsetAsync(d.dout.as<uint8_t>() + w.total, 0, orig_size - w.total, s));
+    if (!d.inffix_ok) {
+        HIPCHK(d.inffix.ensure(INF_FIXED_U16 * 2));
+        HIPCHK(launch_inflate_fixed_tables(d.inffix.as<uint16_t>(), s));
+        d.inffix_ok = true;
+    }
+    DecArgs a{};
+    a.body = d.body.as<uint8_t>();
+    a.out = d.dout.as<uint8_t>();
+    a.out_cap = cap;
+    a.jobs = d.jobs.as<DecJob>();
+    a.n_jobs = nj;
+    a.scratch = d.scratch.as<uint8_t>();
+    a.produced = d.produced.as<uint32_t>();
+    a.inf_fixed = d.inffix.as<uint16_t>();
+    std::vector<hipEvent_t> evb(S), eve(S);
+    struct EvFree {
+        std::vector<hipEvent_t>& a; std::vector<hipEvent_t>& b;
+        ~EvFree() { for (auto e : a) if (e) (void)hipEventDestroy(e); for (auto e : b) if (e) (void)hipEventDestroy(e); }
+    } evfree{evb, eve};
+    for (size_t q = 0; q < S; q++) {
+        HIPCHK(hipEventCreate(&evb[q]));
+        HIPCHK(hipEventCreate(&eve[q]));
+    }
+    OutDMA od(d, out, orig_size, d.dout.as<uint8_t>());
+    const uint64_t tk = now_ns();
+    for (size_t q = 0; q < S; q++) {
+        if (!up.wait_prefix(bneed[q])) { od.unreg_all(); up.release(); return fail(AMBC_E_DEVICE, "staged body upload failed"); }
+        HIPCHK(hipEventRecord(evb[q], s));
+        for (int k = 0; k < DEC_KINDS; k++) {
+            a.list = d.list.as<uint32_t>() + lbase[q * DEC_KINDS + k];
+            a.n_list = lcnt[q * DEC_KINDS + k];
+            const hipError_t e = launch_decode(k, a, s);
+            if (e != hipSuccess) { od.unreg_all(); up.release(); return fail(AMBC_E_DEVICE, hipGetErrorString(e)); }
+        }
+        HIPCHK(hipEventRecord(eve[q], s));
+        const int rc2 = od.copy_ready(o0[q + 1], eve[q]);
+        if (rc2) { od.unreg_all(); up.release(); return rc2; }
+    }
+    up.release();
+    const uint64_t h2d_ns = now_ns() - t0;
+    std::vector<uint32_t> prod(nj);
+    if (nj) HIPCHK(hipMemcpyAsync(prod.data(), d.produced.p, nj * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    rc = od.finish(S ? eve[S - 1] : nullptr);
+    if (rc) return rc;
+    const uint64_t d2h_busy = now_ns() - tk;
+    uint64_t kern_ns = 0;
+    for (size_t q = 0; q < S; q++) {
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, evb[q], eve[q]));
+        kern_ns += (uint64_t)(ms * 1e6);
+    }
+    std::vector<ambc_host_chunk> hostinf;
+    for (uint32_t i = 0; i < nj; i++) {
+        if (prod[i] == DEC_PRODUCED_HOST) {
+            const DecJob& jb = w.jobs[i];
+            hostinf.push_back(ambc_host_chunk{jb.body_off, jb.out_off, jb.clen, jb.orig, 5, 0});
+            continue;
+        }
+        if (prod[i] == 0xFFFFFFFFu) return fail(AMBC_E_DEVICE, "decode job failed");
+        if (prod[i] != w.jobs[i].expect) return PIPE_FALLBACK;
+    }
+    const uint64_t t_inf = now_ns();
+    inflate_all(body, w.zlib, out, orig_size);
+    inflate_all(body, hostinf, out, orig_size);
+    const uint64_t inflate_ns = now_ns() - t_inf;
+    host = w.host;
+    if (st) {
+        std::memset(st, 0, sizeof *st);
+        st->total_chunks = w.jobs.size();
+        st->payload_bytes = w.total;
+        st->h2d_ns = h2d_ns;            // the upload's span (overlapped with the walk and the decode)
+        st->d2h_ns = d2h_busy;          // from the first decode launch to the last output byte
+        st->walk_ns = walk_ns;
+        st->kernel_ns = kern_ns;
+        st->host_codec_ns = inflate_ns;
+        st->total_ns = now_ns() - t0;
+    }
+    return AMBC_OK;
+}
+
+// ---- the decode pipeline with the header walk on the device (ambc_walk.hip) ----
+constexpr uint64_t kWalkPiece = 64ull << 20;     // body bytes of header positions per walked piece
+constexpr uint32_t kWalkHostCap = 1u << 20;      // packages for host codecs the device lists hold
+constexpr uint64_t kOutSlack = 1ull << 20;       // output room past orig_size (a last package's overshoot)
+static_assert(sizeof(HostChunk) == sizeof(ambc_host_chunk), "HostChunk mirrors ambc_host_chunk");
+
+static uint64_t env_u64(const char* name, uint64_t dflt) {
+    const char* e = getenv(name);
+    return e && *e ? strtoull(e, nullptr, 10) : dflt;
+}
+
+static int walk_buffers(Dev& d, uint64_t piece) {
+    DevWalk& w = d.dw;
+    if (!w.ws) HIPCHK(hipStreamCreateWithFlags(&w.ws, hipStreamNonBlocking));
+    for (auto& e : w.ev) if (!e) HIPCHK(hipEventCreate(&e));
+    if (!w.hst) HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&w.hst), sizeof(WalkState), hipHostMallocDefault));
+    if (w.sized >= piece) return AMBC_OK;
+    const uint64_t nc = piece / 4 + 2;     // a marker takes 4 bytes: candidates of a piece
+    const uint64_t nn = piece / 18 + 2;    // headers are >= 18 bytes apart: chain nodes of a piece
+    HIPCHK(w.state.ensure(sizeof(WalkState)));
+    HIPCHK(w.tcnt.ensure((piece / 65536 + 4) * 4));
+    HIPCHK(w.cand.ensure(nc * 8));
+    HIPCHK(w.ja.ensure((nc + 1) * 4));
+    HIPCHK(w.jb.ensure((nc + 1) * 4));
+    HIPCHK(w.flg.ensure(nc));
+    HIPCHK(w.mark.ensure(nc));
+    HIPCHK(w.bc.ensure((nc / 1024 + 2) * 4));
+    HIPCHK(w.chain.ensure(nn * 4));
+    HIPCHK(w.olen.ensure(nn * 8));
+    HIPCHK(w.slen.ensure(nn * 8));
+    HIPCHK(w.bo.ensure((nn / 1024 + 2) * 8));
+    HIPCHK(w.bs.ensure((nn / 1024 + 2) * 8));
+    HIPCHK(w.kind.ensure(nn));
+    HIPCHK(w.host.ensure((size_t)kWalkHostCap * sizeof(HostChunk)));
+    HIPCHK(w.hinf.ensure((size_t)kWalkHostCap * sizeof(HostChunk)));
+    for (int q = 0; q < 2; q++) {
+        HIPCHK(w.jobs[q].ensure(nn * sizeof(DecJob)));
+        HIPCHK(w.list[q].ensure(nn * 4));
+        HIPCHK(w.produced[q].ensure(nn * 4));
+    }
+    w.sized = piece;
+    return AMBC_OK;
+}
+
+// Large host-to-host decodes with the header walk on the device: the body goes
+// up in order; each piece of kWalkPiece bytes of header positions is walked on
+// the walk stream as soon as it (plus the 17 bytes after it) has arrived, its
+// jobs are decoded on the decode stream once the payloads they read are up, and
+// the decoded range goes back by DMA into the caller's registered output -- the
+// walk of piece k + 1, the decode of piece k, the upload and the copy back all
+// overlap.  The host sees a few counters per piece (kernel grids) and, at the
+// end, the packages left to host codecs.  PIPE_FALLBACK as decompress_pipelined.
+static int decompress_devwalk(Dev& d, const uint8_t* body, uint64_t blen, uint64_t orig_size,
+                              const uint64_t reg[4], uint8_t* out, std::vector<ambc_host_chunk>& host,
+                              ambc_stats* st) {
+    const uint64_t t0 = now_ns();
+    HIPCHK(hipSetDevice(d.id));
+    hipStream_t s = d.stream;
+    DevWalk& w = d.dw;
+    const uint64_t piece = std::max<uint64_t>(64, env_u64("AMBC_WALK_PIECE", kWalkPiece));
+    int rc = walk_buffers(d, piece);
+    if (rc) return rc;
+    HIPCHK(d.body.ensure(blen + 64));
+    const uint64_t cap = orig_size + kOutSlack;
+    HIPCHK(d.dout.ensure(cap + 64));
+    if (!d.inffix_ok) {
+        HIPCHK(d.inffix.ensure(INF_FIXED_U16 * 2));
+        HIPCHK(launch_inflate_fixed_tables(d.inffix.as<uint16_t>(), s));
+        d.inffix_ok = true;
+    }
+    HIPCHK(hipMemsetAsync(w.state.p, 0, sizeof(WalkState), w.ws));
+    std::unique_ptr<OrderedUpload> upp(new OrderedUpload());
+    rc = getenv("AMBC_STAGED_UPLOAD") ? AMBC_E_INVAL
+                                      : start_registered_upload(d, d.body.as<uint8_t>(), body, blen, *upp);
+    if (rc) {
+        upp.reset(new OrderedUpload());
+        rc = start_ordered_upload(d, d.body.as<uint8_t>(), body, blen, stage_threads(blen, 8), *upp);
+        if (rc) return rc;
+    }
+    OrderedUpload& up = *upp;
+    OutDMA od(d, out, orig_size, d.dout.as<uint8_t>());
+    std::vector<hipEvent_t> evs;   // per piece: decode start, decode end, after the check
+    struct EvFree {
+        std::vector<hipEvent_t>& v;
+        ~EvFree() { for (auto e : v) if (e) (void)hipEventDestroy(e); }
+    } evfree{evs};
+    auto abort_all = [&](int code) {
+        od.unreg_all();
+        up.release();
+        (void)hipStreamSynchronize(w.ws);
+        (void)hipStreamSynchronize(s);
+        return code;
+    };
+    WalkArgs wa{};
+    wa.body = d.body.as<uint8_t>();
+    wa.blen = blen;
+    wa.orig_size = orig_size;
+    std::memcpy(wa.reg, reg, sizeof wa.reg);
+    wa.st = w.state.as<WalkState>();
+    wa.tcnt = w.tcnt.as<uint32_t>();
+    wa.cand = w.cand.as<uint64_t>();
+    wa.ja = w.ja.as<uint32_t>();
+    wa.jb = w.jb.as<uint32_t>();
+    wa.flg = w.flg.as<uint8_t>();
+    wa.mark = w.mark.as<uint8_t>();
+    wa.bc = w.bc.as<uint32_t>();
+    wa.chain = w.chain.as<uint32_t>();
+    wa.olen = w.olen.as<uint64_t>();
+    wa.slen = w.slen.as<uint64_t>();
+    wa.bo = w.bo.as<uint64_t>();
+    wa.bs = w.bs.as<uint64_t>();
+    wa.kind = w.kind.as<uint8_t>();
+    wa.host = w.host.as<HostChunk>();
+    wa.host_cap = kWalkHostCap;
+    wa.hinf = w.hinf.as<HostChunk>();
+    wa.hinf_cap = kWalkHostCap;
+    DecArgs a{};
+    a.body = d.body.as<uint8_t>();
+    a.out = d.dout.as<uint8_t>();
+    a.out_cap = cap;
+    a.inf_fixed = d.inffix.as<uint16_t>();
+    const uint64_t emax = blen >= HDR ? blen - (HDR - 1) : 0;   // header positions [0, emax)
+    uint64_t walk_ns = 0, njobs = 0, total = 0;
+    const uint64_t tk = now_ns();
+    for (uint64_t pa = 0, k = 0;; pa += piece, k++) {
+        const uint64_t e = std::min(emax, pa + piece);
+        const bool last = e >= emax;
+        if (!up.wait_prefix(last ? blen : e + HDR - 1)) return abort_all(fail(AMBC_E_DEVICE, "body upload failed"));
+        const int q = (int)(k & 1);
+        if (k >= 2) HIPCHK(hipStreamWaitEvent(w.ws, evs[3 * (k - 2) + 2], 0));   // piece k-2's buffers are free
+        wa.a = pa;
+        wa.e = std::max(pa, e);
+        wa.last = last ? 1u : 0u;
+        wa.jobs = w.jobs[q].as<DecJob>();
+        wa.list = w.list[q].as<uint32_t>();
+        wa.produced = w.produced[q].as<uint32_t>();
+        uint32_t rounds = 2;
+        for (uint64_t m = (wa.e - wa.a) / HDR + 2; m > 1; m >>= 1) rounds++;
+        HIPCHK(hipEventRecord(w.ev[0], w.ws));
+        const hipError_t he = launch_walk_piece(wa, rounds, w.ws);
+        if (he != hipSuccess) return abort_all(fail(AMBC_E_DEVICE, hipGetErrorString(he)));
+        HIPCHK(hipEventRecord(w.ev[1], w.ws));
+        HIPCHK(hipMemcpyAsync(w.hst, w.state.p, sizeof(WalkState), hipMemcpyDeviceToHost, w.ws));
+        HIPCHK(hipStreamSynchronize(w.ws));
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, w.ev[0], w.ev[1]));
+        walk_ns += (uint64_t)(ms * 1e6);
+        const WalkState hs = *w.hst;
+        if (getenv("AMBC_WALK_TRACE"))
+            fprintf(stderr, "[ambc devwalk] piece %llu [%llu, %llu) nc %u root %u nchain %u nj %u stop %u entry %lld "
+                    "err %u out %llu chg %u%u%u%u\n", (unsigned long long)k, (unsigned long long)wa.a,
+                    (unsigned long long)wa.e, hs.nc, hs.root, hs.nchain, hs.nj, hs.stop, (long long)hs.entry, hs.err,
+                    (unsigned long long)hs.out, hs.chg[0], hs.chg[1], hs.chg[2], hs.chg[3]);
+        if (hs.err) return abort_all(fail(AMBC_E_MARKER, "Marker mismatch in chunk header."));
+        if (hs.nhost > kWalkHostCap || hs.out > cap) return abort_all(PIPE_FALLBACK);
+        const uint32_t nj = hs.nj;
+        njobs += nj;
+        total = hs.out;
+        if (hs.scr) {
+            // (a reallocation waits for the device: the pieces before are done with it)
+            HIPCHK(w.scratch[q].ensure(hs.scr + 64));
+        }
+        if (!up.wait_prefix(hs.bneed)) return abort_all(fail(AMBC_E_DEVICE, "body upload failed"));
+        for (int x = 0; x < 3; x++) {
+            evs.push_back(nullptr);
+            HIPCHK(hipEventCreate(&evs.back()));
+        }
+        a.jobs = wa.jobs;
+        a.n_jobs = nj;
+        a.scratch = w.scratch[q].as<uint8_t>();
+        a.produced = w.produced[q].as<uint32_t>();
+        HIPCHK(hipEventRecord(evs[3 * k], s));
+        for (int kk = 0; kk < DEC_KINDS; kk++) {
+            a.list = wa.list + hs.kbase[kk];
+            a.n_list = hs.kcount[kk];
+            const hipError_t e2 = launch_decode(kk, a, s);
+            if (e2 != hipSuccess) return abort_all(fail(AMBC_E_DEVICE, hipGetErrorString(e2)));
+        }
+        HIPCHK(hipEventRecord(evs[3 * k + 1], s));
+        wa.nj = nj;
+        const hipError_t e3 = launch_walk_check(wa, s);
+        if (e3 != hipSuccess) return abort_all(fail(AMBC_E_DEVICE, hipGetErrorString(e3)));
+        HIPCHK(hipEventRecord(evs[3 * k + 2], s));
+        rc = od.copy_ready(std::min(total, orig_size), evs[3 * k + 1]);
+        if (rc) return abort_all(rc);
+        if (hs.entry == WALK_ENDED) break;
+    }
+    if (total < orig_size) HIPCHK(hipMemsetAsync(d.dout.as<uint8_t>() + total, 0, orig_size - total, s));
+    hipEvent_t evz = nullptr;
+    HIPCHK(hipEventCreate(&evz));
+    evs.push_back(evz);
+    HIPCHK(hipEventRecord(evz, s));
+    up.release();
+    const uint64_t h2d_ns = now_ns() - t0;
+    HIPCHK(hipMemcpyAsync(w.hst, w.state.p, sizeof(WalkState), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const WalkState hs = *w.hst;
+    if (hs.failed) return abort_all(fail(AMBC_E_DEVICE, "decode job failed"));
+    if (hs.mismatch || hs.nhinf > kWalkHostCap) return abort_all(PIPE_FALLBACK);
+    rc = od.finish(evz);
+    if (rc) return rc;
+    const uint64_t d2h_busy = now_ns() - tk;
+    uint64_t kern_ns = 0;
+    for (size_t k = 0; k + 2 < evs.size(); k += 3) {
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, evs[k], evs[k + 1]));
+        kern_ns += (uint64_t)(ms * 1e6);
+    }
+    // the packages left to host codecs, in body order
+    std::vector<ambc_host_chunk> hl(hs.nhost), hinf(hs.nhinf), zl;
+    if (hs.nhost) HIPCHK(hipMemcpy(hl.data(), w.host.p, hs.nhost * sizeof(HostChunk), hipMemcpyDeviceToHost));
+    if (hs.nhinf) HIPCHK(hipMemcpy(hinf.data(), w.hinf.p, hs.nhinf * sizeof(HostChunk), hipMemcpyDeviceToHost));
+    auto by_body = [](const ambc_host_chunk& x, const ambc_host_chunk& y) { return x.body_off < y.body_off; };
+    std::sort(hl.begin(), hl.end(), by_body);
+    std::sort(hinf.begin(), hinf.end(), by_body);
+    host.clear();
+    for (const auto& h : hl) (h.type == 5 ? zl : host).push_back(h);
+    const uint64_t t_inf = now_ns();
+    inflate_all(body, zl, out, orig_size);
+    inflate_all(body, hinf, out, orig_size);
+    const uint64_t inflate_ns = now_ns() - t_inf;
+    if (st) {
+        std::memset(st, 0, sizeof *st);
+        st->total_chunks = njobs;
+        st->payload_bytes = total;
+        st->h2d_ns = h2d_ns;            // the upload's span (overlapped with the walk and the decode)
+        st->d2h_ns = d2h_busy;          // from the first walk to the last output byte
+        st->walk_ns = walk_ns;          // device time of the walk kernels (overlapped with the decode)
+        st->kernel_ns = kern_ns;
+        st->host_codec_ns = inflate_ns;
+        st->total_ns = now_ns() - t0;
+    }
+    return AMBC_OK;
+}
+
 int ambc::decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t orig_size,
                         const uint64_t reg[4], uint8_t* out, std::vector<ambc_host_chunk>& host,
                         ambc_stats* st, uint8_t* d_out_ext) {
+    if (!d_out_ext && out && blen >= env_u64("AMBC_DEVWALK_MIN", kStageMin) && !getenv("AMBC_DECODE_SEQUENTIAL")) {
+        const int prc = getenv("AMBC_HOST_WALK") ? decompress_pipelined(d, body, blen, orig_size, reg, out, host, st)
+                                                 : decompress_devwalk(d, body, blen, orig_size, reg, out, host, st);
+        if (prc != PIPE_FALLBACK) return prc;   // (lenient package lengths: the sequential path below)
+        if (getenv("AMBC_DECODE_STRICT")) return fail(AMBC_E_DEVICE, "decode pipeline fell back (AMBC_DECODE_STRICT)");
+    }
     const uint64_t t0 = now_ns();
     HIPCHK(hipSetDevice(d.id));
     hipStream_t s = d.stream;
@@ -1452,6 +2127,22 @@ extern "C" int ambc_decompress_device(ambc_ctx* ctx, int dev, const uint8_t* bod
     std::vector<ambc_host_chunk> host;
     return decompress_on(ctx->devs[dev], body, body_len, orig_size, reg, nullptr, host, st,
                          static_cast<uint8_t*>(d_out));
+}
+
+// host code only (diagnostics): the threaded header walk of the decode path on
+// a host body -> packages, output bytes, wall ns (threads: 0 = default)
+extern "C" int ambc_debug_walk(const uint8_t* body, uint64_t blen, uint64_t orig_size, uint32_t threads,
+                               uint64_t* n_pkgs, uint64_t* total, uint64_t* ns) {
+    uint64_t reg[4];
+    default_registered(nullptr, reg);
+    std::map<uint32_t, uint64_t> known;
+    Walk w;
+    const uint64_t t = now_ns();
+    walk_body(body, blen, orig_size, reg, known, w, threads ? threads : 16);
+    if (ns) *ns = now_ns() - t;
+    if (n_pkgs) *n_pkgs = w.jobs.size();
+    if (total) *total = w.total;
+    return w.marker_error ? AMBC_E_MARKER : AMBC_OK;
 }
 
 // Multi-GPU decode split: the reference's header walk with the

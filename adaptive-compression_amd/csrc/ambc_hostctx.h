@@ -94,8 +94,32 @@ struct Batch {
     }
 };
 
+// buffers of the device header walk (ambc_walk.hip) in the decode pipeline:
+// the walk's per-piece arrays, and the jobs / lists / produced / scratch of two
+// pieces in flight (piece k decodes while piece k + 1 is walked)
+struct DevWalk {
+    Buf state, tcnt, cand, ja, jb, flg, mark, bc, chain, olen, slen, bo, bs, kind, host, hinf;
+    Buf jobs[2], list[2], produced[2], scratch[2];
+    hipStream_t ws = nullptr;      // the walk's stream
+    WalkState* hst = nullptr;      // pinned copy of the state
+    hipEvent_t ev[2] = {};         // around a piece's walk (timing)
+    uint64_t sized = 0;            // piece bytes the buffers are sized for
+    void release() {
+        for (Buf* b : {&state, &tcnt, &cand, &ja, &jb, &flg, &mark, &bc, &chain, &olen, &slen, &bo, &bs, &kind,
+                       &host, &hinf, &jobs[0], &jobs[1], &list[0], &list[1], &produced[0], &produced[1],
+                       &scratch[0], &scratch[1]})
+            b->release();
+        if (ws) { (void)hipStreamSynchronize(ws); (void)hipStreamDestroy(ws); ws = nullptr; }
+        if (hst) (void)hipHostFree(hst);
+        hst = nullptr;
+        for (auto& e : ev) if (e) { (void)hipEventDestroy(e); e = nullptr; }
+        sized = 0;
+    }
+};
+
 struct Dev {
     int id = 0;
+    DevWalk dw;
     hipStream_t stream = nullptr;
     hipEvent_t ev[6] = {};
     hipStream_t xs[2] = {};     // copy streams of the slab pipeline: H2D, D2H
@@ -117,10 +141,11 @@ struct Dev {
     hipStream_t cs = nullptr;   // scan + compaction of pipelined segments
     hipEvent_t pev[8] = {};     // segment i encoded
     Buf segbase;                // body offset of every segment (device)
-    // pinned staging for large pageable copies: 2 buffers + 2 events per copy thread
-    std::vector<void*> stage;
-    std::vector<hipStream_t> stage_st;
-    std::vector<hipEvent_t> stage_ev;
+    // pinned staging for large pageable copies: 2 buffers + 2 events per copy
+    // thread; set 0 uploads, set 1 downloads (the decode pipeline runs both at once)
+    std::vector<void*> stage, stage1;
+    std::vector<hipStream_t> stage_st, stage1_st;
+    std::vector<hipEvent_t> stage_ev, stage1_ev;
 };
 
 // One shard of a sharded compress (ambc_shard.cpp): in reference mode the

@@ -99,6 +99,71 @@ constexpr uint32_t DEC_PRODUCED_HOST = 0xFFFFFFFEu;  // k_decode_inflate: output
 constexpr uint32_t DEC_VERBATIM = 256;
 constexpr uint32_t DEC_SKIP = 257;
 
+// ---- the device header walk (ambc_walk.hip), one body piece at a time ----
+constexpr uint64_t WALK_ENDED = ~0ull;   // WalkState::entry once the walk has stopped
+constexpr uint32_t WALK_ROUNDS = 48;     // bound of the pointer-doubling rounds
+constexpr uint32_t WALK_GRID = 1024;     // workgroups of the grid-stride walk kernels
+
+// ambc_host_chunk's layout (a package left to a host codec)
+struct HostChunk {
+    uint64_t body_off, out_off;
+    uint32_t clen, orig, type, reserved;
+};
+
+struct WalkState {
+    uint64_t entry;     // the chain's next header position (WALK_ENDED: stopped)
+    uint64_t out;       // output bytes of all jobs so far
+    uint64_t scr;       // this piece's scratch bytes
+    uint64_t bneed;     // body bytes this piece's jobs read
+    uint64_t tot_o, tot_s;
+    uint32_t err;       // 1: a header without the marker where the walk reads one
+    uint32_t nc, nchain, nj, stop, root;
+    uint32_t nhost;     // packages for host codecs so far (all pieces)
+    uint32_t pad;
+    uint32_t kcount[16], kbase[16], kfill[16];
+    uint32_t chg[WALK_ROUNDS + 1];   // round k marked a new node
+    // decode checks (all pieces): a package decoded to another length than its
+    // header announced, a job failed, packages the GPU handed back to host zlib
+    uint32_t mismatch, failed, nhinf;
+};
+
+struct WalkArgs {
+    const uint8_t* body;
+    uint64_t blen;
+    uint64_t a, e;            // candidate header positions [a, e) (bytes up to e + 17 uploaded)
+    uint64_t orig_size;
+    uint64_t reg[4];          // registered ids
+    uint32_t last;            // the body's last piece
+    uint32_t ntiles;
+    uint32_t round;
+    WalkState* st;
+    uint32_t* tcnt;           // per 64 KiB tile: candidates -> offsets
+    uint64_t* cand;           // candidate positions, ascending
+    uint32_t* ja;             // links, then doubled links (ja / jb alternate)
+    uint32_t* jb;
+    uint8_t* flg;
+    uint8_t* mark;
+    uint32_t* bc;             // per 1024 candidates: chain nodes -> offsets
+    uint32_t* chain;          // the chain's candidates, in order
+    uint64_t* olen;           // per chain node: output / scratch bytes
+    uint64_t* slen;
+    uint64_t* bo;             // per 1024 chain nodes: sums -> offsets
+    uint64_t* bs;
+    uint8_t* kind;
+    DecJob* jobs;             // this piece's jobs, lists (by kind) and produced[]
+    uint32_t* list;
+    const uint32_t* produced;
+    HostChunk* host;          // packages for host codecs (ids 6/7, zlib outside the GPU's domain)
+    uint32_t host_cap;
+    HostChunk* hinf;          // id-5 packages the GPU inflate handed back
+    uint32_t hinf_cap;
+    uint32_t nj;              // k_walk_check: the piece's jobs
+};
+// the walk of one piece on stream s (rounds: pointer-doubling rounds to launch)
+hipError_t launch_walk_piece(WalkArgs a, uint32_t rounds, hipStream_t s);
+// after the piece's decode: produced[] against the jobs' expected lengths
+hipError_t launch_walk_check(const WalkArgs& a, hipStream_t s);
+
 // launchers (ambc_kernels.hip)
 hipError_t launch_encode(const EncArgs& a, hipStream_t s);
 hipError_t launch_deflate(const EncArgs& a, hipStream_t s);   // ambc_deflate.hip

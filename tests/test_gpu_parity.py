@@ -832,15 +832,28 @@ def _pkg(t, orig, payload):
     return b"\xff\xff\x00\x00" + bytes((t, 0)) + struct.pack("<III", orig, orig, len(payload)) + payload
 
 
-def test_parallel_header_walk_large_bodies(ctx):
-    """Bodies above 32 MiB take the threaded header walk: payloads full of fake
-    headers (the speculative segment chains must not be trusted), unregistered
-    ids, a short Huffman package (re-walk with known lengths), a marker mismatch
-    after the out >= orig_size stop (ignored) and one before it (raises)."""
+@pytest.mark.parametrize("npk,slab", [(700, None), (1100, None), (1100, 8 << 20)])
+def test_parallel_header_walk_large_bodies(ctx, npk, slab):
+    """Bodies above 32 MiB take the threaded header walk, above 64 MiB the
+    pipelined decode (ordered upload, slabs decoded as their body pieces
+    arrive, copied back while the next decodes; AMBC_DECODE_SLAB = 8 MiB: many
+    slabs): payloads full of fake headers (the speculative segment chains must
+    not be trusted), unregistered ids, a short Huffman package (re-walk with
+    known lengths: the pipeline falls back), a marker mismatch after the out >=
+    orig_size stop (ignored) and one before it (raises)."""
+    if slab:
+        os.environ["AMBC_DECODE_SLAB"] = str(slab)
+    try:
+        _large_body_walks(npk)
+    finally:
+        os.environ.pop("AMBC_DECODE_SLAB", None)
+
+
+def _large_body_walks(npk):
     rng = np.random.default_rng(5)
     fake = _pkg(1, 4096, b"\x00\x10" * 8)[:18]
     pieces, orig = [], 0
-    for k in range(700):
+    for k in range(npk):
         raw = bytearray(rng.integers(0, 256, 65536, dtype=np.uint8).tobytes())
         for q in range(0, 65536 - 64, 4099):
             raw[q:q + 18] = fake                       # markers inside payloads
@@ -856,7 +869,11 @@ def test_parallel_header_walk_large_bodies(ctx):
     assert len(body) > (40 << 20)
     comp = _compressor()
     for osz in (orig, orig - 12345, orig // 3):
-        assert comp._adaptive_decompress(body, osz) == orc.decompress_body(body, osz), osz
+        assert (comp._adaptive_decompress(body, osz) == orc.decompress_body(body, osz)) is True, osz
+    # the same body without the short Huffman package: no fallback
+    clean = b"".join(p_ for i, p_ in enumerate(pieces) if p_[4] != 3) + _pkg(0, 0, b"")[:16]
+    corig = orig - 50
+    assert (comp._adaptive_decompress(clean, corig) == orc.decompress_body(clean, corig)) is True
     # a corrupted marker: after the stop it is never reached, before it it raises
     bad = bytearray(body)
     p = len(pieces[0]) + len(pieces[1])
