@@ -1669,7 +1669,7 @@ static int decompress_pipelined(Dev& d, const uint8_t* body, uint64_t blen, uint
 }
 
 // ---- the decode pipeline with the header walk on the device (ambc_walk.hip) ----
-constexpr uint64_t kWalkPiece = 64ull << 20;     // body bytes of header positions per walked piece
+constexpr uint64_t kWalkPiece = 128ull << 20;    // body bytes of header positions per walked piece
 constexpr uint32_t kWalkHostCap = 1u << 20;      // packages for host codecs the device lists hold
 constexpr uint64_t kOutSlack = 1ull << 20;       // output room past orig_size (a last package's overshoot)
 static_assert(sizeof(HostChunk) == sizeof(ambc_host_chunk), "HostChunk mirrors ambc_host_chunk");
@@ -1681,7 +1681,13 @@ static uint64_t env_u64(const char* name, uint64_t dflt) {
 
 static int walk_buffers(Dev& d, uint64_t piece) {
     DevWalk& w = d.dw;
-    if (!w.ws) HIPCHK(hipStreamCreateWithFlags(&w.ws, hipStreamNonBlocking));
+    if (!w.ws) {
+        // the walk's launches are short and gate the next piece's decode: ahead of
+        // the decode kernels' workgroups in the dispatch queue
+        int lo = 0, hi = 0;
+        HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIPCHK(hipStreamCreateWithPriority(&w.ws, hipStreamNonBlocking, hi));
+    }
     for (auto& e : w.ev) if (!e) HIPCHK(hipEventCreate(&e));
     if (!w.hst) HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&w.hst), sizeof(WalkState), hipHostMallocDefault));
     if (w.sized >= piece) return AMBC_OK;
@@ -1727,7 +1733,11 @@ static int decompress_devwalk(Dev& d, const uint8_t* body, uint64_t blen, uint64
     HIPCHK(hipSetDevice(d.id));
     hipStream_t s = d.stream;
     DevWalk& w = d.dw;
-    const uint64_t piece = std::max<uint64_t>(64, env_u64("AMBC_WALK_PIECE", kWalkPiece));
+    // pieces of kWalkPiece bytes, the first ones smaller (8 MiB, doubling) so that
+    // the decode and the copy back start early; AMBC_WALK_PIECE: one fixed size
+    const uint64_t fixed = env_u64("AMBC_WALK_PIECE", 0);
+    const uint64_t piece = fixed ? std::max<uint64_t>(64, fixed) : kWalkPiece;
+    uint64_t plen = fixed ? piece : std::min<uint64_t>(piece, 8ull << 20);
     int rc = walk_buffers(d, piece);
     if (rc) return rc;
     HIPCHK(d.body.ensure(blen + 64));
@@ -1792,8 +1802,8 @@ static int decompress_devwalk(Dev& d, const uint8_t* body, uint64_t blen, uint64
     const uint64_t emax = blen >= HDR ? blen - (HDR - 1) : 0;   // header positions [0, emax)
     uint64_t walk_ns = 0, njobs = 0, total = 0;
     const uint64_t tk = now_ns();
-    for (uint64_t pa = 0, k = 0;; pa += piece, k++) {
-        const uint64_t e = std::min(emax, pa + piece);
+    for (uint64_t pa = 0, k = 0;; pa += plen, plen = std::min(piece, 2 * plen), k++) {
+        const uint64_t e = std::min(emax, pa + plen);
         const bool last = e >= emax;
         if (!up.wait_prefix(last ? blen : e + HDR - 1)) return abort_all(fail(AMBC_E_DEVICE, "body upload failed"));
         const int q = (int)(k & 1);
@@ -1804,10 +1814,8 @@ static int decompress_devwalk(Dev& d, const uint8_t* body, uint64_t blen, uint64
         wa.jobs = w.jobs[q].as<DecJob>();
         wa.list = w.list[q].as<uint32_t>();
         wa.produced = w.produced[q].as<uint32_t>();
-        uint32_t rounds = 2;
-        for (uint64_t m = (wa.e - wa.a) / HDR + 2; m > 1; m >>= 1) rounds++;
         HIPCHK(hipEventRecord(w.ev[0], w.ws));
-        const hipError_t he = launch_walk_piece(wa, rounds, w.ws);
+        const hipError_t he = launch_walk_piece(wa, w.ws);
         if (he != hipSuccess) return abort_all(fail(AMBC_E_DEVICE, hipGetErrorString(he)));
         HIPCHK(hipEventRecord(w.ev[1], w.ws));
         HIPCHK(hipMemcpyAsync(w.hst, w.state.p, sizeof(WalkState), hipMemcpyDeviceToHost, w.ws));
@@ -1818,9 +1826,9 @@ static int decompress_devwalk(Dev& d, const uint8_t* body, uint64_t blen, uint64
         const WalkState hs = *w.hst;
         if (getenv("AMBC_WALK_TRACE"))
             fprintf(stderr, "[ambc devwalk] piece %llu [%llu, %llu) nc %u root %u nchain %u nj %u stop %u entry %lld "
-                    "err %u out %llu chg %u%u%u%u\n", (unsigned long long)k, (unsigned long long)wa.a,
+                    "err %u out %llu\n", (unsigned long long)k, (unsigned long long)wa.a,
                     (unsigned long long)wa.e, hs.nc, hs.root, hs.nchain, hs.nj, hs.stop, (long long)hs.entry, hs.err,
-                    (unsigned long long)hs.out, hs.chg[0], hs.chg[1], hs.chg[2], hs.chg[3]);
+                    (unsigned long long)hs.out);
         if (hs.err) return abort_all(fail(AMBC_E_MARKER, "Marker mismatch in chunk header."));
         if (hs.nhost > kWalkHostCap || hs.out > cap) return abort_all(PIPE_FALLBACK);
         const uint32_t nj = hs.nj;
@@ -1840,8 +1848,8 @@ static int decompress_devwalk(Dev& d, const uint8_t* body, uint64_t blen, uint64
         a.scratch = w.scratch[q].as<uint8_t>();
         a.produced = w.produced[q].as<uint32_t>();
         HIPCHK(hipEventRecord(evs[3 * k], s));
-        for (int kk = 0; kk < DEC_KINDS; kk++) {
-            a.list = wa.list + hs.kbase[kk];
+        for (int kk = 0, kb = 0; kk < DEC_KINDS; kb += hs.kcount[kk++]) {
+            a.list = wa.list + kb;
             a.n_list = hs.kcount[kk];
             const hipError_t e2 = launch_decode(kk, a, s);
             if (e2 != hipSuccess) return abort_all(fail(AMBC_E_DEVICE, hipGetErrorString(e2)));

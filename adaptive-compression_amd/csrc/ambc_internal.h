@@ -101,8 +101,8 @@ constexpr uint32_t DEC_SKIP = 257;
 
 // ---- the device header walk (ambc_walk.hip), one body piece at a time ----
 constexpr uint64_t WALK_ENDED = ~0ull;   // WalkState::entry once the walk has stopped
-constexpr uint32_t WALK_ROUNDS = 48;     // bound of the pointer-doubling rounds
-constexpr uint32_t WALK_GRID = 1024;     // workgroups of the grid-stride walk kernels
+constexpr uint32_t WALK_GRID = 128;      // workgroups of the grid-stride walk kernels (small: they
+                                         // share the chip with the decode of the piece before)
 
 // ambc_host_chunk's layout (a package left to a host codec)
 struct HostChunk {
@@ -120,8 +120,7 @@ struct WalkState {
     uint32_t nc, nchain, nj, stop, root;
     uint32_t nhost;     // packages for host codecs so far (all pieces)
     uint32_t pad;
-    uint32_t kcount[16], kbase[16], kfill[16];
-    uint32_t chg[WALK_ROUNDS + 1];   // round k marked a new node
+    uint32_t kcount[16], kfill[16];   // jobs per decode kernel (lists in kind order)
     // decode checks (all pieces): a package decoded to another length than its
     // header announced, a job failed, packages the GPU handed back to host zlib
     uint32_t mismatch, failed, nhinf;
@@ -135,15 +134,14 @@ struct WalkArgs {
     uint64_t reg[4];          // registered ids
     uint32_t last;            // the body's last piece
     uint32_t ntiles;
-    uint32_t round;
     WalkState* st;
     uint32_t* tcnt;           // per 64 KiB tile: candidates -> offsets
     uint64_t* cand;           // candidate positions, ascending
-    uint32_t* ja;             // links, then doubled links (ja / jb alternate)
-    uint32_t* jb;
+    uint32_t* ja;             // links (successor candidate, or nc: none)
+    uint32_t* jb;             // where the path from a node leaves its block
     uint8_t* flg;
     uint8_t* mark;
-    uint32_t* bc;             // per 1024 candidates: chain nodes -> offsets
+    uint32_t* bc;             // per block of candidates: entry node, chain nodes -> offsets
     uint32_t* chain;          // the chain's candidates, in order
     uint64_t* olen;           // per chain node: output / scratch bytes
     uint64_t* slen;
@@ -159,8 +157,8 @@ struct WalkArgs {
     uint32_t hinf_cap;
     uint32_t nj;              // k_walk_check: the piece's jobs
 };
-// the walk of one piece on stream s (rounds: pointer-doubling rounds to launch)
-hipError_t launch_walk_piece(WalkArgs a, uint32_t rounds, hipStream_t s);
+// the walk of one piece on stream s
+hipError_t launch_walk_piece(WalkArgs a, hipStream_t s);
 // after the piece's decode: produced[] against the jobs' expected lengths
 hipError_t launch_walk_check(const WalkArgs& a, hipStream_t s);
 

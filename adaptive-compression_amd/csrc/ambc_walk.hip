@@ -14,9 +14,9 @@
 //      (binary search), or to a sink with the reason: the walk stops at it
 //      (type 0, overrun), ends after it (< 18 bytes left), leaves the piece, or
 //      its successor holds no marker (a mismatch if the walk gets there);
-//   3. the chain from the entry candidate is marked by pointer doubling (round
-//      k marks the 2^k-th successors of the marked nodes; a round that marks
-//      nothing new ends it) -- marker bytes inside payloads are candidates too,
+//   3. the chain from the entry candidate is marked block by block (pointer
+//      doubling in LDS within blocks of 4096 candidates, one serial step per
+//      block between them) -- marker bytes inside payloads are candidates too,
 //      but nothing on the chain links to them;
 //   4. the marked candidates, compacted in order, are the packages: each one's
 //      decode job (ambc_host.cpp make_job restated), scans of the output and
@@ -51,14 +51,10 @@ __device__ __forceinline__ uint32_t rd32u(const uint8_t* p) {
 __device__ __forceinline__ uint32_t gtid() { return blockIdx.x * blockDim.x + threadIdx.x; }
 __device__ __forceinline__ uint32_t gsize() { return gridDim.x * blockDim.x; }
 
-// candidate bits of the 16 positions at the 16-aligned base: the marker at
-// base + t, for the positions in [a, e)
-__device__ __forceinline__ uint32_t tile_bits(const uint8_t* body, uint64_t base, uint64_t a, uint64_t e) {
+// candidate bits of the 16 positions at the 16-aligned base (w: the 16 bytes
+// there and the next 4): the marker at base + t, for the positions in [a, e)
+__device__ __forceinline__ uint32_t tile_bits(const uint32_t w[5], uint64_t base, uint64_t a, uint64_t e) {
     if (base >= e) return 0;
-    const uint32_t* b32 = reinterpret_cast<const uint32_t*>(body + base);
-    uint32_t w[5];
-#pragma unroll
-    for (int q = 0; q < 5; q++) w[q] = b32[q];     // (base + 20 <= e + 19 <= blen + 2: the buffer's slack)
     uint32_t m = 0;
 #pragma unroll
     for (int t = 0; t < 16; t++) {
@@ -68,6 +64,19 @@ __device__ __forceinline__ uint32_t tile_bits(const uint8_t* body, uint64_t base
     const uint32_t lo = a > base ? (uint32_t)(a - base) : 0u;
     const uint32_t hi = e - base >= 16 ? 16u : (uint32_t)(e - base);
     return m & ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+}
+
+// one 16-byte load per lane (coalesced), the 4 bytes after it from the next lane
+// (the last lane loads them); every lane of the wave must call this
+__device__ __forceinline__ void load_group(const uint8_t* body, uint64_t base, uint64_t e, uint32_t w[5]) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    // (the group after the last one in [a, e) too: its first bytes end the markers at e - 3 .. e - 1;
+    // base + 16 <= e + 31 < blen + 64, the buffer's slack)
+    if (base < e + 16) v = *reinterpret_cast<const uint4*>(body + base);
+    w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+    uint32_t nx = (uint32_t)__shfl_down((int)v.x, 1);
+    if ((threadIdx.x & 63) == 63 && base < e) nx = *reinterpret_cast<const uint32_t*>(body + base + 16);
+    w[4] = nx;
 }
 
 // exclusive scan over a 256-thread workgroup (LDS, off the hot loops)
@@ -108,8 +117,12 @@ __device__ void serial_block_scan(T* v, uint32_t n, T* s, T* total) {
 __global__ __launch_bounds__(256) void k_walk_count(WalkArgs A) {
     const uint64_t t0 = (A.a & ~15ull) + (uint64_t)blockIdx.x * WT_TILE;
     uint32_t c = 0;
-    for (uint32_t g = threadIdx.x; g < WT_TILE / 16; g += 256)
-        c += (uint32_t)__popc(tile_bits(A.body, t0 + 16ull * g, A.a, A.e));
+    for (uint32_t g = threadIdx.x; g < WT_TILE / 16; g += 256) {
+        const uint64_t base = t0 + 16ull * g;
+        uint32_t w[5];
+        load_group(A.body, base, A.e, w);
+        c += (uint32_t)__popc(tile_bits(w, base, A.a, A.e));
+    }
     __shared__ uint32_t red[4];
     c = wave_sum_u32(c);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
@@ -123,8 +136,7 @@ __global__ __launch_bounds__(256) void k_walk_tscan(WalkArgs A) {
     WalkState* st = A.st;
     serial_block_scan<uint32_t>(A.tcnt, A.ntiles, s, &st->nc);
     const uint32_t t = threadIdx.x;
-    if (t < 16) { st->kcount[t] = 0; st->kbase[t] = 0; st->kfill[t] = 0; }
-    for (uint32_t k = t; k <= WALK_ROUNDS; k += 256) st->chg[k] = 0;
+    if (t < 16) { st->kcount[t] = 0; st->kfill[t] = 0; }
     if (t == 0) {
         st->nchain = 0; st->nj = 0; st->stop = ~0u; st->root = ~0u;
         st->scr = 0; st->bneed = 0; st->tot_o = 0; st->tot_s = 0;
@@ -138,7 +150,9 @@ __global__ __launch_bounds__(256) void k_walk_list(WalkArgs A) {
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (uint32_t g0 = 0; g0 < WT_TILE / 16; g0 += 256) {
         const uint64_t base = t0 + 16ull * (g0 + threadIdx.x);
-        uint32_t m = tile_bits(A.body, base, A.a, A.e);
+        uint32_t w[5];
+        load_group(A.body, base, A.e, w);
+        uint32_t m = tile_bits(w, base, A.a, A.e);
         const uint32_t c = (uint32_t)__popc(m);
         const uint32_t incl = wave_incl_sum(c);
         if (lane == 63) wsum[wave] = incl;
@@ -192,92 +206,145 @@ __global__ __launch_bounds__(256) void k_walk_link(WalkArgs A) {
         }
         A.ja[i] = link;
         A.flg[i] = f;
-        const bool root = p == entry;
-        A.mark[i] = root ? 1 : 0;
-        if (root) { st->root = i; st->chg[0] = 1; }
-    }
-}
-
-// the entry must be a candidate when it lies in the piece
-__global__ void k_walk_root(WalkArgs A) {
-    WalkState* st = A.st;
-    if (st->entry != WALK_ENDED && st->entry < A.e && st->root == ~0u) {
-        st->err = 1;
-        st->entry = WALK_ENDED;
+        if (p == entry) st->root = i;
     }
 }
 
 // ---- 3. the chain --------------------------------------------------------
+// Candidates in blocks of BN (links only go forward).  bexit: per block, by
+// pointer doubling in LDS, where the path from each node leaves the block.
+// bentry: one thread follows the chain from the entry block to block -- one
+// step per block the chain visits.  bmark: per visited block, the nodes on the
+// path from its entry node (pointer doubling in LDS), and their count.
 
-__global__ __launch_bounds__(256) void k_walk_mark(WalkArgs A) {
-    WalkState* st = A.st;
-    const uint32_t k = A.round;
-    if (!st->chg[k]) return;
-    const uint32_t* J = (k & 1) ? A.jb : A.ja;
-    const uint32_t nc = st->nc;
-    bool any = false;
-    for (uint32_t i = gtid(); i < nc; i += gsize()) {
-        if (!A.mark[i]) continue;
-        const uint32_t j = J[i];
-        if (j < nc && !A.mark[j]) { A.mark[j] = 1; any = true; }
-    }
-    if (any) st->chg[k + 1] = 1;
-}
+constexpr uint32_t BN = 4096;           // candidates per block (1024 threads x 4)
+constexpr uint32_t BT = 1024;
+constexpr uint16_t LNONE = 0xFFFF;
 
-__global__ __launch_bounds__(256) void k_walk_jump(WalkArgs A) {
-    WalkState* st = A.st;
-    const uint32_t k = A.round;
-    if (!st->chg[k + 1]) return;
-    const uint32_t* src = (k & 1) ? A.jb : A.ja;
-    uint32_t* dst = (k & 1) ? A.ja : A.jb;
-    const uint32_t nc = st->nc;
-    for (uint32_t i = gtid(); i <= nc; i += gsize()) dst[i] = src[src[i]];
-}
-
-__global__ __launch_bounds__(256) void k_walk_mcount(WalkArgs A) {
-    const uint32_t nc = A.st->nc, nb = (nc + 1023) / 1024;
-    __shared__ uint32_t red[4];
+__global__ __launch_bounds__(1024) void k_walk_bexit(WalkArgs A) {
+    const uint32_t nc = A.st->nc, nb = (nc + BN - 1) / BN;
+    __shared__ uint16_t v[BN];
     for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
+        const uint32_t base = b * BN, n = min(BN, nc - base);
+        for (uint32_t l = threadIdx.x; l < n; l += BT) {
+            const uint32_t j = A.ja[base + l];
+            v[l] = (uint16_t)(j < base + n ? j - base : l);   // the last node in the block points to itself
+        }
+        __syncthreads();
+        for (uint32_t o = 1; o < n; o <<= 1) {
+            uint16_t t[BN / BT];
+#pragma unroll
+            for (uint32_t q = 0; q < BN / BT; q++) {
+                const uint32_t l = threadIdx.x + BT * q;
+                t[q] = l < n ? v[v[l]] : (uint16_t)0;
+            }
+            __syncthreads();
+#pragma unroll
+            for (uint32_t q = 0; q < BN / BT; q++) {
+                const uint32_t l = threadIdx.x + BT * q;
+                if (l < n) v[l] = t[q];
+            }
+            __syncthreads();
+        }
+        for (uint32_t l = threadIdx.x; l < n; l += BT) A.jb[base + l] = A.ja[base + v[l]];
+        if (threadIdx.x == 0) A.bc[b] = ~0u;             // (bentry: the block's entry node)
+        __syncthreads();
+    }
+}
+
+__global__ void k_walk_bentry(WalkArgs A) {
+    WalkState* st = A.st;
+    if (threadIdx.x) return;
+    if (st->entry != WALK_ENDED && st->entry < A.e && st->root == ~0u) {
+        st->err = 1;                                     // the entry lies in the piece but holds no marker
+        st->entry = WALK_ENDED;
+        return;
+    }
+    const uint32_t nc = st->nc;
+    for (uint32_t x = st->root; x < nc; x = A.jb[x]) A.bc[x / BN] = x;
+}
+
+__global__ __launch_bounds__(1024) void k_walk_bmark(WalkArgs A) {
+    const uint32_t nc = A.st->nc, nb = (nc + BN - 1) / BN;
+    __shared__ uint16_t v[BN];
+    __shared__ uint8_t m[BN];
+    __shared__ uint32_t red[BT / 64];
+    for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
+        const uint32_t base = b * BN, n = min(BN, nc - base);
+        if (threadIdx.x == 0) red[0] = A.bc[b];
+        __syncthreads();
+        const uint32_t e0 = red[0];
+        __syncthreads();
+        if (e0 == ~0u) {                                 // (uniform over the workgroup)
+            for (uint32_t l = threadIdx.x; l < n; l += BT) A.mark[base + l] = 0;
+            if (threadIdx.x == 0) A.bc[b] = 0;
+            continue;
+        }
+        for (uint32_t l = threadIdx.x; l < n; l += BT) {
+            const uint32_t j = A.ja[base + l];
+            v[l] = j < base + n ? (uint16_t)(j - base) : LNONE;
+            m[l] = base + l == e0 ? 1 : 0;
+        }
+        __syncthreads();
+        // round k: the 2^k-th successors of the marked nodes, then the links doubled
+        for (uint32_t o = 1; o < 2 * n; o <<= 1) {
+#pragma unroll
+            for (uint32_t q = 0; q < BN / BT; q++) {
+                const uint32_t l = threadIdx.x + BT * q;
+                if (l < n && m[l] && v[l] != LNONE) m[v[l]] = 1;
+            }
+            __syncthreads();
+            uint16_t t[BN / BT];
+#pragma unroll
+            for (uint32_t q = 0; q < BN / BT; q++) {
+                const uint32_t l = threadIdx.x + BT * q;
+                t[q] = l < n && v[l] != LNONE ? v[v[l]] : LNONE;
+            }
+            __syncthreads();
+#pragma unroll
+            for (uint32_t q = 0; q < BN / BT; q++) {
+                const uint32_t l = threadIdx.x + BT * q;
+                if (l < n) v[l] = t[q];
+            }
+            __syncthreads();
+        }
         uint32_t c = 0;
-        for (uint32_t q = 0; q < 4; q++) {
-            const uint32_t i = b * 1024 + q * 256 + threadIdx.x;
-            c += i < nc && A.mark[i] ? 1u : 0u;
+        for (uint32_t l = threadIdx.x; l < n; l += BT) {
+            A.mark[base + l] = m[l];
+            c += m[l];
         }
         c = wave_sum_u32(c);
         if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
         __syncthreads();
-        if (threadIdx.x == 0) A.bc[b] = red[0] + red[1] + red[2] + red[3];
+        if (threadIdx.x == 0) {
+            uint32_t tot = 0;
+            for (uint32_t w = 0; w < BT / 64; w++) tot += red[w];
+            A.bc[b] = tot;
+        }
         __syncthreads();
     }
 }
 
 __global__ __launch_bounds__(256) void k_walk_bscan(WalkArgs A) {
     __shared__ uint32_t s[256];
-    serial_block_scan<uint32_t>(A.bc, (A.st->nc + 1023) / 1024, s, &A.st->nchain);
+    serial_block_scan<uint32_t>(A.bc, (A.st->nc + BN - 1) / BN, s, &A.st->nchain);
 }
 
+// the marked candidates in order: 16 consecutive nodes per thread
 __global__ __launch_bounds__(256) void k_walk_chain(WalkArgs A) {
-    const uint32_t nc = A.st->nc, nb = (nc + 1023) / 1024;
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    __shared__ uint32_t ws[4];
+    const uint32_t nc = A.st->nc, nb = (nc + BN - 1) / BN;
+    __shared__ uint32_t s[256];
     for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
-        uint32_t at = A.bc[b];
-        for (uint32_t q = 0; q < 4; q++) {
-            const uint32_t i = b * 1024 + q * 256 + threadIdx.x;
-            const bool m = i < nc && A.mark[i];
-            const uint64_t bal = __ballot(m);
-            const uint32_t r = (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
-            if (lane == 0) ws[wave] = (uint32_t)__popcll(bal);
-            __syncthreads();
-            uint32_t before = 0, tot = 0;
+        const uint32_t i0 = b * BN + 16 * threadIdx.x;
+        uint32_t bits = 0;
 #pragma unroll
-            for (int w = 0; w < 4; w++) {
-                before += (uint32_t)w < wave ? ws[w] : 0u;
-                tot += ws[w];
-            }
-            if (m) A.chain[at + before + r] = i;
-            at += tot;
-            __syncthreads();
+        for (int q = 0; q < 16; q++) bits |= (i0 + q < nc && A.mark[i0 + q] ? 1u : 0u) << q;
+        uint32_t tot;
+        uint32_t at = A.bc[b] + block_excl<uint32_t>((uint32_t)__popc(bits), s, tot);
+        while (bits) {
+            const uint32_t q = (uint32_t)__builtin_ctz(bits);
+            bits &= bits - 1u;
+            A.chain[at++] = i0 + q;
         }
     }
 }
@@ -316,9 +383,8 @@ __device__ uint64_t lz4_bound_d(const uint8_t* p, uint32_t plen) {
 
 // chain node r's decode job (ambc_host.cpp make_job / expect_len), its output
 // bytes and scratch reservation; a stop node gets an empty placeholder
-__global__ __launch_bounds__(256) void k_walk_jobs(WalkArgs A) {
-    const uint32_t nchain = A.st->nchain;
-    for (uint32_t r = gtid(); r < nchain; r += gsize()) {
+__device__ __forceinline__ void walk_job(const WalkArgs& A, uint32_t r, uint64_t& expect, uint64_t& sneed) {
+    {
         const uint32_t i = A.chain[r];
         const uint64_t hp = A.cand[i];
         const uint8_t* h = A.body + hp;
@@ -327,7 +393,8 @@ __global__ __launch_bounds__(256) void k_walk_jobs(WalkArgs A) {
         const bool stop = A.flg[i] & F_STOP;
         DecJob j{};
         uint32_t kind = DEC_KIND_HEAVY;
-        uint64_t sneed = 0, expect = 0;
+        sneed = 0;
+        expect = 0;
         j.body_off = hp + 18;
         j.clen = clen;
         j.orig = orig;
@@ -390,14 +457,20 @@ __global__ __launch_bounds__(256) void k_walk_jobs(WalkArgs A) {
     }
 }
 
-__global__ __launch_bounds__(256) void k_walk_bsum(WalkArgs A) {
+// the jobs, and per 1024 chain nodes the sums of their output / scratch bytes
+__global__ __launch_bounds__(256) void k_walk_jobs(WalkArgs A) {
     const uint32_t n = A.st->nchain, nb = (n + 1023) / 1024;
     __shared__ uint64_t so[256], ss[256];
     for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
         uint64_t o = 0, s = 0;
         for (uint32_t q = 0; q < 4; q++) {
             const uint32_t r = b * 1024 + q * 256 + threadIdx.x;
-            if (r < n) { o += A.olen[r]; s += A.slen[r]; }
+            if (r < n) {
+                uint64_t ex, sn;
+                walk_job(A, r, ex, sn);
+                o += ex;
+                s += sn;
+            }
         }
         uint64_t to, ts;
         (void)block_excl<uint64_t>(o, so, to);
@@ -473,27 +546,36 @@ __global__ __launch_bounds__(256) void k_walk_kcount(WalkArgs A) {
     if (threadIdx.x < DEC_KINDS && hist[threadIdx.x]) atomicAdd(&A.st->kcount[threadIdx.x], hist[threadIdx.x]);
 }
 
-__global__ void k_walk_kbase(WalkArgs A) {
-    WalkState* st = A.st;
-    uint32_t at = 0;
-    for (int k = 0; k < DEC_KINDS; k++) {
-        st->kbase[k] = at;
-        st->kfill[k] = at;
-        at += st->kcount[k];
-    }
-}
-
 __global__ __launch_bounds__(256) void k_walk_lists(WalkArgs A) {
     WalkState* st = A.st;
     const uint32_t nj = st->nj;
-    for (uint32_t r = gtid(); r < nj; r += gsize()) {
-        A.list[atomicAdd(&st->kfill[A.kind[r]], 1u)] = r;
-        const DecJob j = A.jobs[r];
-        if (j.type != DEC_SKIP) continue;
-        const uint32_t t = A.body[j.body_off - 18 + 4];
-        if (t == 5 && !j.clen) continue;              // an empty zlib payload decodes to nothing
-        const uint32_t q = atomicAdd(&st->nhost, 1u);
-        if (q < A.host_cap) A.host[q] = HostChunk{j.body_off, j.out_off, j.clen, j.orig, t, 0};
+    __shared__ uint32_t cnt[16], base[16];
+    for (uint32_t r0 = blockIdx.x * 256; r0 < nj; r0 += gridDim.x * 256) {
+        // ranks within the workgroup by LDS atomics, one global atomic per kind
+        if (threadIdx.x < 16) cnt[threadIdx.x] = 0;
+        __syncthreads();
+        const uint32_t r = r0 + threadIdx.x;
+        const uint32_t k = r < nj ? A.kind[r] : 0u;
+        const uint32_t loc = r < nj ? atomicAdd(&cnt[k], 1u) : 0u;
+        __syncthreads();
+        if (threadIdx.x < DEC_KINDS && cnt[threadIdx.x]) {
+            uint32_t kb = 0;                              // the kind's list starts after the lists before it
+            for (uint32_t q = 0; q < threadIdx.x; q++) kb += st->kcount[q];
+            base[threadIdx.x] = kb + atomicAdd(&st->kfill[threadIdx.x], cnt[threadIdx.x]);
+        }
+        __syncthreads();
+        if (r < nj) {
+            A.list[base[k] + loc] = r;
+            const DecJob j = A.jobs[r];
+            if (j.type == DEC_SKIP) {
+                const uint32_t t = A.body[j.body_off - 18 + 4];
+                if (!(t == 5 && !j.clen)) {                   // (an empty zlib payload decodes to nothing)
+                    const uint32_t q = atomicAdd(&st->nhost, 1u);
+                    if (q < A.host_cap) A.host[q] = HostChunk{j.body_off, j.out_off, j.clen, j.orig, t, 0};
+                }
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -516,7 +598,7 @@ __global__ __launch_bounds__(256) void k_walk_check(WalkArgs A) {
 
 }  // namespace
 
-hipError_t launch_walk_piece(WalkArgs a, uint32_t rounds, hipStream_t s) {
+hipError_t launch_walk_piece(WalkArgs a, hipStream_t s) {
     const uint64_t a0 = a.a & ~15ull;
     a.ntiles = a.e > a.a ? (uint32_t)((a.e - a0 + WT_TILE - 1) / WT_TILE) : 0u;
     const dim3 B(256), G(WALK_GRID);
@@ -524,22 +606,16 @@ hipError_t launch_walk_piece(WalkArgs a, uint32_t rounds, hipStream_t s) {
     hipLaunchKernelGGL(k_walk_tscan, dim3(1), B, 0, s, a);
     if (a.ntiles) hipLaunchKernelGGL(k_walk_list, dim3(a.ntiles), B, 0, s, a);
     hipLaunchKernelGGL(k_walk_link, G, B, 0, s, a);
-    hipLaunchKernelGGL(k_walk_root, dim3(1), dim3(1), 0, s, a);
-    for (uint32_t k = 0; k < rounds && k < WALK_ROUNDS; k++) {
-        a.round = k;
-        hipLaunchKernelGGL(k_walk_mark, G, B, 0, s, a);
-        hipLaunchKernelGGL(k_walk_jump, G, B, 0, s, a);
-    }
-    hipLaunchKernelGGL(k_walk_mcount, G, B, 0, s, a);
+    hipLaunchKernelGGL(k_walk_bexit, G, dim3(BT), 0, s, a);
+    hipLaunchKernelGGL(k_walk_bentry, dim3(1), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_walk_bmark, G, dim3(BT), 0, s, a);
     hipLaunchKernelGGL(k_walk_bscan, dim3(1), B, 0, s, a);
     hipLaunchKernelGGL(k_walk_chain, G, B, 0, s, a);
     hipLaunchKernelGGL(k_walk_jobs, G, B, 0, s, a);
-    hipLaunchKernelGGL(k_walk_bsum, G, B, 0, s, a);
     hipLaunchKernelGGL(k_walk_bscan64, dim3(1), B, 0, s, a);
     hipLaunchKernelGGL(k_walk_fill, G, B, 0, s, a);
     hipLaunchKernelGGL(k_walk_fin, dim3(1), dim3(1), 0, s, a);
     hipLaunchKernelGGL(k_walk_kcount, G, B, 0, s, a);
-    hipLaunchKernelGGL(k_walk_kbase, dim3(1), dim3(1), 0, s, a);
     hipLaunchKernelGGL(k_walk_lists, G, B, 0, s, a);
     return hipGetLastError();
 }
