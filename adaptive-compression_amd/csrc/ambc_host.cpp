@@ -443,6 +443,24 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
             fprintf(stderr, "[ambc stamps] z9 parsed=%.0f wave-0 cycles/chunk: load %.0f sort %.0f walk %.0f "
                     "wait %.0f path %.0f out %.0f\n", gs[7], gs[0] / c, gs[1] / c, gs[2] / c, gs[3] / c,
                     gs[4] / c, gs[5] / c);
+            // the spread over chunks: percentiles of a parsed chunk's cycles, and the
+            // share of all cycles in the slowest 10 %
+            std::vector<double> tot;
+            for (uint32_t q = 0; q < M; q++)
+                if (g[(size_t)q * 8 + 7]) {
+                    double t = 0;
+                    for (int ph = 0; ph < 6; ph++) t += (double)g[(size_t)q * 8 + ph];
+                    tot.push_back(t);
+                }
+            if (!tot.empty()) {
+                std::sort(tot.begin(), tot.end());
+                auto pct = [&](double f) { return tot[std::min(tot.size() - 1, (size_t)(f * tot.size()))]; };
+                double all = 0, top = 0;
+                for (size_t q = 0; q < tot.size(); q++) { all += tot[q]; if (q >= tot.size() * 9 / 10) top += tot[q]; }
+                fprintf(stderr, "[ambc stamps] z9 chunk cycles p10 %.0f p50 %.0f p90 %.0f p99 %.0f max %.0f; "
+                        "slowest 10%% hold %.1f%%\n", pct(0.1), pct(0.5), pct(0.9), pct(0.99), tot.back(),
+                        100.0 * top / all);
+            }
         }
         if (deflate) {
             std::vector<unsigned long long> g((size_t)M * 8);

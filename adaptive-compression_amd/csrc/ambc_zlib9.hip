@@ -162,6 +162,33 @@ __device__ void z9_sort(Z9Smem<CMAX>& S, uint32_t m, uint32_t wave, uint32_t lan
 }
 
 
+// Positions where zlib finds no match at all: no earlier position with the same
+// 15-bit hash (hash_head is NIL), position 0 (zlib's NIL) and the last two
+// (fewer than MIN_MATCH bytes of lookahead).  From a clean position on such a
+// run is all literals, each position clean again, so a walker takes it in one
+// step (seg[q] = c literals, no match).  Bit s of S.mask (free until the path).
+// A bucket whose entries below s are more than 4 is taken as "maybe a match".
+template <int CMAX>
+__device__ __forceinline__ void z9_literal_mask(Z9Smem<CMAX>& S, uint32_t n, uint32_t wave, uint32_t lane) {
+    constexpr uint32_t NW = Z9Smem<CMAX>::NW;
+    for (uint32_t b = wave * 64u; b < (uint32_t)CMAX; b += 64u * NW) {
+        const uint32_t s = b + lane;
+        bool lit = true;
+        if (s >= 1 && s + 3 <= n) {
+            const uint32_t h = z_h15(z_gram(S, s));
+            const uint32_t lo = S.bstart(z_bucket(h)), j = S.slot[s];
+            if (j > lo + 4) {
+                lit = false;
+            } else {
+                for (uint32_t t = lo; t < j; t++)
+                    if (z_h15(z_gram(S, S.lst[t])) == h) { lit = false; break; }
+            }
+        }
+        const uint64_t m = __ballot(lit);
+        if (lane == 0) { S.mask[b >> 5] = (uint32_t)m; S.mask[(b >> 5) + 1] = (uint32_t)(m >> 32); }
+    }
+}
+
 // The lazy parse's walkers (deflate_slow).  A position is CLEAN when the
 // parser stands there with no pending match (prev_length < 3): right after a
 // match, or with a pending literal and no match at the previous position.
@@ -187,7 +214,27 @@ __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t
     for (;;) {
         if (clean && !done && (q >= n || vs[q] != 0u)) done = true;
         if (__all(done)) break;
-        const bool act = !done && s >= 1 && s + 3 <= n && P < 258;   // position 0 is zlib's NIL
+        // a run of literal positions from a clean q: one step
+        bool skip = false;
+#ifndef AMBC_Z9_NOSKIP
+        if (clean && !done && ((S.mask[q >> 5] >> (q & 31)) & 1u)) {
+            uint32_t e = q;
+            for (;;) {
+                const uint32_t sh = e & 31u;
+                const uint32_t w = ~(S.mask[e >> 5] >> sh);   // bit t: e + t takes a match (t < 32 - sh)
+                const uint32_t t = w ? (uint32_t)__builtin_ctz(w) : 32u;
+                if (t < 32u - sh) { e += t; break; }
+                e += 32u - sh;
+                if (e >= n) break;
+            }
+            e = min(e, n);
+            if (r == 0) vs[q] = 0x80000000u | (e - q);
+            q = e;
+            s = q;
+            skip = true;
+        }
+#endif
+        const bool act = !done && !skip && s >= 1 && s + 3 <= n && P < 258;   // position 0 is zlib's NIL
         // ---- longest_match(s): k0 over the first 4096 chain entries, k1 over
         // the first 1024; key = min(len, nice) << 16 | candidate (the longest,
         // then the most recent) ----
@@ -234,6 +281,7 @@ __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t
                 // length differs cannot be longer -- no full compare for it
                 const uint32_t best = k0 >> 16;
                 const bool can = best < 16 || S.ch[c + best] == S.ch[s + best];
+#ifdef AMBC_Z9_SOLOEXT
                 bool ext = ok && fm == ~0u && can;
 #pragma unroll 1
                 while (__any(ext)) {
@@ -252,6 +300,45 @@ __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t
                         else { len += 16; if (len >= Z_MAXM) ext = false; }
                     }
                 }
+#else
+                // the first 16 bytes equal: the group extends its candidates together,
+                // the most recent first, 128 bytes a step (lane r compares bytes
+                // [16 r, 16 r + 16) past the known length); once one reaches nice the
+                // older ones cannot win (longest_match stops there)
+                uint32_t em = grp8(__ballot(ok && fm == ~0u && can), g);
+#pragma unroll 1
+                while (__any(em != 0u)) {
+                    const bool gact = em != 0u;
+                    const uint32_t rr = gact ? (uint32_t)__builtin_ctz(em) : 0u;
+                    const uint32_t src = g * 8u + rr;
+                    const uint32_t cc = (uint32_t)__shfl((int)c, (int)src);
+                    const uint32_t ll = (uint32_t)__shfl((int)len, (int)src);
+                    const uint32_t off = ll + 16u * r;
+                    uint32_t f = ~0u;
+                    if (gact && off < Z_MAXM) {
+                        const uint32_t ac = (cc + off) >> 2, as = (s + off) >> 2, csh = cc & 3u;
+                        uint32_t wc[5], ws[5];
+#pragma unroll
+                        for (int t = 0; t < 5; t++) { wc[t] = c32[ac + t]; ws[t] = c32[as + t]; }
+#pragma unroll
+                        for (int t = 0; t < 4; t++)
+                            f = min(f, ffbl_raw(__builtin_amdgcn_alignbyte(wc[t + 1], wc[t], csh) ^
+                                                __builtin_amdgcn_alignbyte(ws[t + 1], ws[t], ss)) |
+                                           (uint32_t)t << 5);
+                    } else if (gact) {
+                        f = 0;          // past the longest match zlib takes: the length is capped there
+                    }
+                    const uint32_t mm = grp8(__ballot(gact && f != ~0u), g);
+                    const uint32_t r0 = mm ? (uint32_t)__builtin_ctz(mm) : 0u;
+                    const uint32_t f0 = (uint32_t)__shfl((int)f, (int)(g * 8u + r0));
+                    const uint32_t L2 = mm ? ll + 16u * r0 + (f0 >> 3) : ll + 128u;
+                    if (gact && r == rr) len = L2;
+                    if (gact && (mm || L2 >= Z_MAXM)) {
+                        em &= em - 1u;                                       // this candidate is done
+                        if (min(L2, Z_MAXM) >= nice) em = 0;                 // reached nice
+                    }
+                }
+#endif
                 const uint32_t Lp = min(min(len, Z_MAXM), nice);
                 const uint32_t key = ok && can ? (Lp << 16 | c) : 0u;
                 k0 = max(k0, grp_max8(key));
@@ -262,7 +349,7 @@ __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t
                 gd = gd || j <= lo || far != 0 || cnt >= Z_CHAIN || (k0 >> 16) >= nice;
             }
         }
-        if (!done) {
+        if (!done && !skip) {
             uint32_t ML = 2, MD = 0;
             if (act) {
                 const uint32_t key = P >= Z_GOOD ? k1 : k0;
@@ -354,6 +441,7 @@ __global__ __launch_bounds__(64 * Z9Cfg<CMAX>::NW) void k_z9_parse(EncArgs A) {
     PSTAMP(0);
     z9_sort(S, n - 2, wave, lane);
     for (uint32_t i = threadIdx.x; i < (uint32_t)CMAX; i += 64u * NW) S.seg[i] = 0;
+    z9_literal_mask(S, n, wave, lane);
     __syncthreads();
     PSTAMP(1);
     z9_walkers(S, n, wave, lane);
