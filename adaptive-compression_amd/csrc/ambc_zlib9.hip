@@ -74,6 +74,7 @@ struct Z9Smem {
     alignas(16) uint32_t seg[CMAX];
     alignas(16) uint16_t sd[CMAX];           // the segment's match distance
     uint16_t entry[CMAX / 64], rbase[CMAX / 64];   // the path: entry lane / match rank per window
+    uint16_t wrs[CMAX / 32];                 // the walk: the byte run holding position 32 w starts here
     uint32_t mask[CMAX / 32];                // the path's match starts
     uint32_t cov[CMAX / 32];                 // positions the path's matches cover
     uint32_t nmatch;
@@ -185,7 +186,36 @@ __device__ __forceinline__ void z9_literal_mask(Z9Smem<CMAX>& S, uint32_t n, uin
             }
         }
         const uint64_t m = __ballot(lit);
-        if (lane == 0) { S.mask[b >> 5] = (uint32_t)m; S.mask[(b >> 5) + 1] = (uint32_t)(m >> 32); }
+        // byte runs: bit p of S.cov (free until the path) = a run starts at p (and
+        // every p >= n, which bounds the walks' forward scans)
+        const bool rb = s == 0 || s >= n || S.ch[s] != S.ch[s - 1];
+        const uint64_t rm = __ballot(rb);
+        if (lane == 0) {
+            S.mask[b >> 5] = (uint32_t)m; S.mask[(b >> 5) + 1] = (uint32_t)(m >> 32);
+            S.cov[b >> 5] = (uint32_t)rm; S.cov[(b >> 5) + 1] = (uint32_t)(rm >> 32);
+        }
+    }
+    __syncthreads();
+    // per 32-position word: the start of the run holding its first position (the
+    // last run start before it, by an exclusive max-scan over the words)
+    if (wave == 0) {
+        constexpr uint32_t NWD = (uint32_t)CMAX / 32, K = (NWD + 63) / 64;
+        int last = -1;
+        int lb[K];
+#pragma unroll
+        for (uint32_t t = 0; t < K; t++) {
+            const uint32_t w = lane * K + t;
+            const uint32_t x = w < NWD ? S.cov[w] : 0u;
+            lb[t] = x ? (int)(w * 32 + 31 - __builtin_clz(x)) : -1;
+            last = max(last, lb[t]);
+        }
+        int run = wave_excl_max(last, -1);
+#pragma unroll
+        for (uint32_t t = 0; t < K; t++) {
+            const uint32_t w = lane * K + t;
+            if (w < NWD) S.wrs[w] = (uint16_t)((S.cov[w] & 1u) ? w * 32 : (uint32_t)max(run, 0));
+            run = max(run, lb[t]);
+        }
     }
 }
 
@@ -207,7 +237,13 @@ __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t
     const uint32_t* c32 = reinterpret_cast<const uint32_t*>(S.ch);
     const uint32_t g = lane >> 3, r = lane & 7;
     const uint32_t wid = wave * 8u + g;
+#ifdef AMBC_Z9_UNIFORM
     uint32_t q = (uint32_t)(((uint64_t)n * wid) / NWK);
+#else
+    // a position's chain grows with the positions before it (text: about
+    // linearly), so equal work per walker puts the starts at n * sqrt(w / NWK)
+    uint32_t q = min(n, (uint32_t)((float)n * sqrtf((float)wid / (float)NWK)));
+#endif
     uint32_t s = q, P = 2, Pd = 0, c = 0;
     bool clean = true, done = false;
 #pragma unroll 1
@@ -254,8 +290,35 @@ __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t
                 j = S.slot[s];
                 nice = min(Z_MAXM, n - s);
             }
-            bool gd = !act || j <= lo;
             uint32_t cnt = 0;
+#ifndef AMBC_Z9_NORUN
+            // Inside a byte run [rs, re) with s + 3 <= re, every earlier position of
+            // the run is a chain entry (same 3 bytes, one bucket, contiguous in lst
+            // just below s) and matches exactly re - s bytes (then s sees the run's
+            // end and the candidate the run): the most recent, s - 1, stands for them
+            // all; the chain goes on below the run (zlib counts those entries).
+            if (act && s >= 2 && (tg[0] & 0xFFFFFFu) == (tg[0] & 0xFFu) * 0x010101u && S.ch[s - 1] == (tg[0] & 0xFFu)) {
+                const uint32_t w = s >> 5, b = s & 31u;
+                const uint32_t xb = S.cov[w] & (b == 31u ? ~0u : ((2u << b) - 1u));
+                const uint32_t rs = max(1u, xb ? w * 32 + 31 - (uint32_t)__builtin_clz(xb) : (uint32_t)S.wrs[w]);
+                uint32_t wf = w, xf = S.cov[w] & (b == 31u ? 0u : ~((2u << b) - 1u)), re = s + Z_MAXM + 3;
+#pragma unroll 1
+                for (int t = 0; t < 10; t++) {
+                    if (xf) { re = wf * 32 + (uint32_t)__builtin_ctz(xf); break; }
+                    if (++wf >= (uint32_t)CMAX / 32) { re = CMAX; break; }
+                    xf = S.cov[wf];
+                }
+                const uint32_t B = s - rs;
+                if (re >= s + 3 && B >= 8 && B <= j - lo) {
+                    const uint32_t key = min(min(re - s, Z_MAXM), nice) << 16 | (s - 1);
+                    k0 = key;
+                    k1 = key;
+                    cnt = B;
+                    j -= B;
+                }
+            }
+#endif
+            bool gd = !act || j <= lo || cnt >= Z_CHAIN || (k0 >> 16) >= nice;
 #pragma unroll 1
             while (__any(!gd)) {
                 const int idx = (int)j - 1 - (int)r;
