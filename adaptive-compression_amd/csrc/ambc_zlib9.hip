@@ -237,13 +237,10 @@ __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t
     const uint32_t* c32 = reinterpret_cast<const uint32_t*>(S.ch);
     const uint32_t g = lane >> 3, r = lane & 7;
     const uint32_t wid = wave * 8u + g;
-#ifdef AMBC_Z9_UNIFORM
+    // (measured and not kept: starts at n * sqrt(w / NWK), for chains that grow
+    // along the chunk -- ASCII 17.3 -> 23.7 ms per 256 MiB: the walkers' overrun
+    // until they meet another walker's path, not the chain lengths, sets the time)
     uint32_t q = (uint32_t)(((uint64_t)n * wid) / NWK);
-#else
-    // a position's chain grows with the positions before it (text: about
-    // linearly), so equal work per walker puts the starts at n * sqrt(w / NWK)
-    uint32_t q = min(n, (uint32_t)((float)n * sqrtf((float)wid / (float)NWK)));
-#endif
     uint32_t s = q, P = 2, Pd = 0, c = 0;
     bool clean = true, done = false;
 #pragma unroll 1
