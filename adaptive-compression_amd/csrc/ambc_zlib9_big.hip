@@ -89,7 +89,11 @@ struct Z9Big {
     static constexpr size_t SEG = SLOT + 2ull * CMAX;       // u32 [CMAX] the sort's ranks, then segments
     static constexpr size_t SD = SEG + 4ull * CMAX;         // u16 [CMAX] segment distances
     static constexpr size_t CH = SD + 2ull * CMAX;          // CHG: the chunk, zeros past n
-    static constexpr size_t BYTES = CH + (CHG ? (size_t)CMAX + 320 : 0);
+    // CHG: the walk's byte-run starts (bitmask) and per-word run starts (u16),
+    // which do not fit the LDS beside the list
+    static constexpr size_t RUNB = (CH + (CHG ? (size_t)CMAX + 320 : 0) + 15) & ~(size_t)15;
+    static constexpr size_t WRS = RUNB + (CHG ? (size_t)CMAX / 8 : 0);
+    static constexpr size_t BYTES = WRS + (CHG ? (size_t)CMAX / 16 : 0);
 };
 
 template <int CMAX>
@@ -118,6 +122,9 @@ struct Z9BSmem {
     };
     uint32_t bend32[ZNB / 2];                          // bucket ends (u16 pairs)
     uint32_t vis[CMAX / 32];                           // clean positions some walker recorded
+    uint32_t litm[CMAX / 32];                          // the walk: positions that take no match (z9b_literal_mask)
+    uint32_t runb[CHG ? 1 : CMAX / 32];                //   byte-run starts, and every position >= n (CHG: scratch)
+    uint16_t wrs[CHG ? 1 : CMAX / 32];                 //   the run holding position 32 w starts here (CHG: scratch)
     uint32_t bnd[8];                                   // block ends (boundary positions)
     uint32_t btop[8];                                  // the step top that flushed block b
     uint32_t nbnd, nmatch;
@@ -208,9 +215,69 @@ __device__ void z9b_sort(Z9BSmem<CMAX>& S, const uint8_t* src, uint32_t m, uint1
 // slots and segments in scratch, the chunk bytes in LDS or scratch, the
 // candidates' words loaded one step ahead, the window's MAX_DIST, the slide
 // step's NIL head, and the search stopped at the chain length the step needs).
+// As ambc_zlib9.hip's z9_literal_mask: positions without any earlier same-hash
+// position (and 0, and the last two) take no match; byte-run starts for the
+// walkers' run shortcut, and per 32-position word the start of its first run.
+template <int CMAX>
+__device__ void z9b_literal_mask(Z9BSmem<CMAX>& S, uint32_t n, const uint16_t* slot, const uint8_t* gch,
+                                 uint32_t* runb, uint16_t* wrs, uint32_t wave, uint32_t lane) {
+    constexpr bool CHG = Z9Big<CMAX>::CHG;
+    const uint32_t* c32 = reinterpret_cast<const uint32_t*>(S.w.ch);
+    const uint32_t* g32 = reinterpret_cast<const uint32_t*>(gch);
+    auto W32 = [&](uint32_t i) -> uint32_t {
+        if constexpr (CHG) return g32[i];
+        else return c32[i];
+    };
+    auto B8 = [&](uint32_t i) -> uint32_t {
+        if constexpr (CHG) return gch[i];
+        else return S.w.ch[i];
+    };
+    auto gram = [&](uint32_t i) -> uint32_t {
+        return __builtin_amdgcn_alignbyte(W32((i >> 2) + 1), W32(i >> 2), i & 3) & 0xFFFFFFu;
+    };
+    for (uint32_t b = wave * 64u; b < (uint32_t)CMAX; b += 64u * ZB_NW) {
+        const uint32_t p = b + lane;
+        bool lit = true;
+        if (p >= 1 && p + 3 <= n) {
+            const uint32_t h = z_h15(gram(p));
+            const uint32_t lo = S.bstart(z_bucket(h)), j = slot[p];
+            if (j > lo + 4) {
+                lit = false;
+            } else {
+                for (uint32_t t = lo; t < j; t++)
+                    if (z_h15(gram(S.w.lst[t])) == h) { lit = false; break; }
+            }
+        }
+        const uint64_t m = __ballot(lit);
+        const uint64_t rm = __ballot(p == 0 || p >= n || B8(p) != B8(p - 1));
+        if (lane == 0) {
+            S.litm[b >> 5] = (uint32_t)m; S.litm[(b >> 5) + 1] = (uint32_t)(m >> 32);
+            runb[b >> 5] = (uint32_t)rm; runb[(b >> 5) + 1] = (uint32_t)(rm >> 32);
+        }
+    }
+    __syncthreads();
+    if (wave == 0) {
+        constexpr uint32_t NWD = (uint32_t)CMAX / 32, K = (NWD + 63) / 64;
+        int last = -1;
+#pragma unroll 1
+        for (uint32_t t = 0; t < K; t++) {
+            const uint32_t x = runb[lane * K + t];
+            if (x) last = (int)((lane * K + t) * 32 + 31 - __builtin_clz(x));
+        }
+        int run = wave_excl_max(last, -1);
+#pragma unroll 1
+        for (uint32_t t = 0; t < K; t++) {
+            const uint32_t w = lane * K + t, x = runb[w];
+            wrs[w] = (uint16_t)((x & 1u) ? w * 32 : (uint32_t)max(run, 0));
+            if (x) run = (int)(w * 32 + 31 - __builtin_clz(x));
+        }
+    }
+}
+
 template <int CMAX>
 __device__ __forceinline__ void z9b_walkers(Z9BSmem<CMAX>& S, uint32_t n, const uint16_t* slot, uint32_t* seg,
-                                            uint16_t* sd, const uint8_t* gch, uint32_t wave, uint32_t lane) {
+                                            uint16_t* sd, const uint8_t* gch, const uint32_t* runb,
+                                            const uint16_t* wrs, uint32_t wave, uint32_t lane) {
     constexpr bool CHG = Z9Big<CMAX>::CHG;
     constexpr uint32_t NWK = (uint32_t)ZB_NW * 8u;
     const uint32_t* c32 = reinterpret_cast<const uint32_t*>(S.w.ch);
@@ -237,7 +304,30 @@ __device__ __forceinline__ void z9b_walkers(Z9BSmem<CMAX>& S, uint32_t n, const 
     for (;;) {
         if (clean && !done && (q >= n || ((S.vis[q >> 5] >> (q & 31)) & 1u))) done = true;
         if (__all(done)) break;
-        const bool act = !done && s >= 1 && s + 3 <= n && P < 258;   // position 0 is zlib's NIL
+        // a run of match-less positions from a clean q in one step (at most 512:
+        // the path's exit offsets hold 10 bits)
+        bool skip = false;
+        if (clean && !done && ((S.litm[q >> 5] >> (q & 31)) & 1u)) {
+            uint32_t e = q;
+            const uint32_t emax = min(n, q + 512u);
+            for (;;) {
+                const uint32_t sh = e & 31u;
+                const uint32_t w = ~(S.litm[e >> 5] >> sh);
+                const uint32_t t = w ? (uint32_t)__builtin_ctz(w) : 32u;
+                if (t < 32u - sh) { e += t; break; }
+                e += 32u - sh;
+                if (e >= emax) break;
+            }
+            e = min(e, emax);
+            if (r == 0) {
+                seg[q] = 0x80000000u | (e - q);
+                atomicOr(&S.vis[q >> 5], 1u << (q & 31));
+            }
+            q = e;
+            s = q;
+            skip = true;
+        }
+        const bool act = !done && !skip && s >= 1 && s + 3 <= n && P < 258;   // position 0 is zlib's NIL
         // ---- longest_match(s) over the first `lim` chain entries (4096, or
         // 1024 when the pending match is >= good_match); key = min(len, nice)
         // << 16 | candidate: the longest, then the most recent ----
@@ -258,8 +348,31 @@ __device__ __forceinline__ void z9b_walkers(Z9BSmem<CMAX>& S, uint32_t n, const 
                 lo = S.bstart(z_bucket(h));
                 nice = min(Z_MAXM, n - s);
             }
-            bool gd = !act || j <= lo;
             uint32_t cnt = 0;
+            bool rgd = false;
+            // inside a byte run (ambc_zlib9.hip): the run's earlier positions all
+            // match exactly to its end, the most recent stands for them; a run
+            // reaching MAX_DIST back ends the chain inside it
+            if (act && s >= 2 && (tg[0] & 0xFFFFFFu) == (tg[0] & 0xFFu) * 0x010101u && B8(s - 1) == (tg[0] & 0xFFu)) {
+                const uint32_t w = s >> 5, b = s & 31u;
+                const uint32_t xb = runb[w] & (b == 31u ? ~0u : ((2u << b) - 1u));
+                const uint32_t rs = max(1u, xb ? w * 32 + 31 - (uint32_t)__builtin_clz(xb) : (uint32_t)wrs[w]);
+                uint32_t wf = w, xf = runb[w] & (b == 31u ? 0u : ~((2u << b) - 1u)), re = s + Z_MAXM + 3;
+#pragma unroll 1
+                for (int t = 0; t < 10; t++) {
+                    if (xf) { re = wf * 32 + (uint32_t)__builtin_ctz(xf); break; }
+                    if (++wf >= (uint32_t)CMAX / 32) { re = CMAX; break; }
+                    xf = runb[wf];
+                }
+                const uint32_t B = s - rs;
+                if (re >= s + 3 && B >= 8 && B <= j - lo && !(s == nil_at && s - 1 == Z_WSZ)) {
+                    k0 = min(min(re - s, Z_MAXM), nice) << 16 | (s - 1);
+                    cnt = B;
+                    j -= B;
+                    rgd = s - rs >= Z_MAXD;      // the chain's next entries lie past MAX_DIST
+                }
+            }
+            bool gd = !act || rgd || j <= lo || cnt >= lim || (k0 >> 16) >= nice;
             int idx = (int)j - 1 - (int)r;
             uint32_t cn = !gd && idx >= (int)lo ? (uint32_t)lst[idx] : 0u;
             uint32_t wn[5];
@@ -300,21 +413,39 @@ __device__ __forceinline__ void z9b_walkers(Z9BSmem<CMAX>& S, uint32_t n, const 
                 bool ext = ok && fm == ~0u && !nilh;
                 if (ext && best >= 16) ext = B8(c + best) == B8(s + best);
                 const bool can = fm != ~0u || best < 16 || ext;
+                // the group extends its first-16-equal candidates together, most
+                // recent first, 128 bytes a step, until one reaches nice
+                uint32_t em = grp8(__ballot(ext), g);
 #pragma unroll 1
-                while (__any(ext)) {
-                    if (ext) {
-                        const uint32_t ac = (c + len) >> 2, as = (s + len) >> 2;
+                while (__any(em != 0u)) {
+                    const bool gact = em != 0u;
+                    const uint32_t rr = gact ? (uint32_t)__builtin_ctz(em) : 0u;
+                    const uint32_t src = g * 8u + rr;
+                    const uint32_t cc = (uint32_t)__shfl((int)c, (int)src);
+                    const uint32_t ll = (uint32_t)__shfl((int)len, (int)src);
+                    const uint32_t off = ll + 16u * r;
+                    uint32_t f = ~0u;
+                    if (gact && off < Z_MAXM) {
+                        const uint32_t ac = (cc + off) >> 2, as = (s + off) >> 2, csh = cc & 3u;
                         uint32_t wc[5], ws[5];
 #pragma unroll
                         for (int t = 0; t < 5; t++) { wc[t] = W32(ac + t); ws[t] = W32(as + t); }
-                        uint32_t f = ~0u;
 #pragma unroll
                         for (int t = 0; t < 4; t++)
-                            f = min(f, ffbl_raw(__builtin_amdgcn_alignbyte(wc[t + 1], wc[t], sh) ^
+                            f = min(f, ffbl_raw(__builtin_amdgcn_alignbyte(wc[t + 1], wc[t], csh) ^
                                                 __builtin_amdgcn_alignbyte(ws[t + 1], ws[t], ss)) |
                                            (uint32_t)t << 5);
-                        if (f != ~0u) { len += f >> 3; ext = false; }
-                        else { len += 16; if (len >= Z_MAXM) ext = false; }
+                    } else if (gact) {
+                        f = 0;
+                    }
+                    const uint32_t mm = grp8(__ballot(gact && f != ~0u), g);
+                    const uint32_t r0 = mm ? (uint32_t)__builtin_ctz(mm) : 0u;
+                    const uint32_t f0 = (uint32_t)__shfl((int)f, (int)(g * 8u + r0));
+                    const uint32_t L2 = mm ? ll + 16u * r0 + (f0 >> 3) : ll + 128u;
+                    if (gact && r == rr) len = L2;
+                    if (gact && (mm || L2 >= Z_MAXM)) {
+                        em &= em - 1u;
+                        if (min(L2, Z_MAXM) >= nice) em = 0;
                     }
                 }
                 const uint32_t Lp = min(min(len, Z_MAXM), nice);
@@ -326,7 +457,7 @@ __device__ __forceinline__ void z9b_walkers(Z9BSmem<CMAX>& S, uint32_t n, const 
                 gd = gd || nilh || j <= lo || far != 0 || cnt >= lim || (k0 >> 16) >= nice;
             }
         }
-        if (!done) {
+        if (!done && !skip) {
             uint32_t ML = 2, MD = 0;
             if (act) {
                 const uint32_t L = k0 >> 16, d = s - (k0 & 0xFFFFu);
@@ -382,6 +513,8 @@ __global__ __launch_bounds__(64 * ZB_NW) void k_z9_parse_big(EncArgs A) {
     uint32_t* seg = reinterpret_cast<uint32_t*>(scr + Z9Big<CMAX>::SEG);
     uint16_t* sd = reinterpret_cast<uint16_t*>(scr + Z9Big<CMAX>::SD);
     uint8_t* gch = scr + Z9Big<CMAX>::CH;
+    uint32_t* runb = CHG ? reinterpret_cast<uint32_t*>(scr + Z9Big<CMAX>::RUNB) : S.runb;
+    uint16_t* wrs = CHG ? reinterpret_cast<uint16_t*>(scr + Z9Big<CMAX>::WRS) : S.wrs;
 #pragma unroll 1
     for (uint32_t k = blockIdx.x; k < A.n_chunks; k += gridDim.x) {
         __syncthreads();   // (the previous chunk's last LDS reads)
@@ -413,8 +546,10 @@ __global__ __launch_bounds__(64 * ZB_NW) void k_z9_parse_big(EncArgs A) {
             for (uint32_t i = threadIdx.x; i < (uint32_t)CMAX / 32; i += TT) S.vis[i] = 0;
         }
         __syncthreads();
+        z9b_literal_mask(S, n, slot, gch, runb, wrs, wave, lane);
+        __syncthreads();
         BSTAMP(1);
-        z9b_walkers(S, n, slot, seg, sd, gch, wave, lane);
+        z9b_walkers(S, n, slot, seg, sd, gch, runb, wrs, wave, lane);
         BSTAMP(2);
         __syncthreads();
         BSTAMP(3);
