@@ -286,6 +286,13 @@ int ambc_last_kernel_times(ambc_ctx* ctx, int dev, uint64_t* encode_ns, uint64_t
                            uint64_t* compact_ns);
 int ambc_last_encode_launches(ambc_ctx* ctx, int dev, uint32_t* n_launch);
 
+/* diagnostics, host code only: the threaded host header walk of the decode path
+ * (used for bodies below the device walk's size and for the lenient re-walk) over
+ * a host body -> packages, output bytes, wall ns (threads 0 = default);
+ * AMBC_E_MARKER where _adaptive_decompress would raise */
+int ambc_debug_walk(const uint8_t* body, uint64_t body_len, uint64_t orig_size, uint32_t threads,
+                    uint64_t* n_pkgs, uint64_t* total, uint64_t* ns);
+
 #ifdef __cplusplus
 }
 #endif
