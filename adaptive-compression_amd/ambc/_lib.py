@@ -31,6 +31,7 @@ MODE_NATIVE = 0
 MODE_REFERENCE = 1
 FLAG_NO_END_CHUNK = 1
 FLAG_ZLIB9 = 2          # id 5 = zlib.compress(data, 9)'s bytes (chunk_size <= 65536)
+FLAG_INPUT_PADDED = 4   # device inputs: 64 readable bytes after n (large chunks read in place)
 MAX_CHUNK = 65536
 
 EXPORTS = (

@@ -31,7 +31,7 @@
 
 namespace ambc {
 
-template <int CMAX>
+template <int CMAX, bool GL = false>
 struct EncSmem {
     // work = union, by lifetime.  Selection: hist | code | clen | Huffman tree
     // (parent/pbit), whose space the first occurrences (first/order) reuse once
@@ -44,7 +44,7 @@ struct EncSmem {
     // zero padded up to CMAX; reads past CMAX (the LZ4 loads of lanes beyond n,
     // match lengths capped below n) land in work[], which follows: in bounds,
     // and never part of a result
-    alignas(16) uint8_t chunk[CMAX];
+    alignas(16) uint8_t chunk[GL ? 16 : CMAX];   // GL: the chunk is read in place from the input
     alignas(16) uint32_t work[WORK / 4];
     __device__ __forceinline__ uint8_t* wb() { return reinterpret_cast<uint8_t*>(work); }
     __device__ __forceinline__ uint32_t* hist() { return work; }
@@ -139,11 +139,18 @@ __device__ __forceinline__ uint8_t lz4_hdr_byte(uint32_t q, uint32_t n, uint32_t
 #define STAMP_FLUSH
 #endif
 
-template <int CMAX>
+// GL (chunks of 16 KiB and more, no forced / analysed encode, 16-byte aligned
+// chunk starts): the chunk is read in place from the input through the caches
+// instead of a CMAX-byte LDS copy -- only LZ4 (and id 5's gates) take such
+// chunks, and a 64 KiB chunk in LDS held the CU to 2 workgroups, one wave
+// each, through 1024 latency-bound LZ4 rounds; in place, the work area alone
+// (4 KB) lets 20 workgroups share the CU.  Reads past n stay inside the input's
+// 64 bytes of slack or the next chunk and never reach a result.
+template <int CMAX, bool GL = false>
 __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
     constexpr int BS = CMAX >= 4096 ? 64 : CMAX / 64;  // bytes per lane per round
     constexpr int ROUNDS = CMAX / (64 * BS);
-    __shared__ EncSmem<CMAX> S;
+    __shared__ EncSmem<CMAX, GL> S;
 
     const uint32_t lane = threadIdx.x;
     const uint32_t k = blockIdx.x;
@@ -156,7 +163,10 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
     STAMP_DECL
 
     // ---- stage the chunk in LDS (16 B per lane per load, coalesced) ----
-    {
+    const uint8_t* ch = GL ? src : S.chunk;
+    if constexpr (GL) {
+        for (uint32_t i = lane; i < 256; i += 64) S.hist()[i] = 0;
+    } else {
         const uint32_t nv = n >> 4;
         if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
             for (uint32_t v = lane; v < nv; v += 64)
@@ -194,17 +204,20 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
     const bool fast_samples = step == 4;
     uint32_t pairs = 0, samp = 0, dsamp = 0;
     int rs_carry = -1;
-    const uint32_t* c32 = reinterpret_cast<const uint32_t*>(S.chunk);
+    const uint32_t* c32 = reinterpret_cast<const uint32_t*>(ch);
 #pragma unroll 1
     for (int r = 0; r < (need_a ? ROUNDS : 0); r++) {
         const uint32_t b0 = (uint32_t)(r * 64 + lane) * BS;
+        // (GL: a lane block starting at or past n reads nothing -- its bytes are all
+        // masked, and past n + 64 the input may end)
+        const bool rd = !GL || b0 < n;
         // previous byte; position 0 always starts a run (the reference's prev = None)
-        uint32_t pw = b0 ? c32[(b0 >> 2) - 1] : ~((uint32_t)S.chunk[0] << 24);
+        uint32_t pw = b0 ? (rd ? c32[(b0 >> 2) - 1] : 0u) : ~((uint32_t)ch[0] << 24);
         int lb = -1, fc = -1;
-        uint32_t starts = 0, cur = S.chunk[b0], rc = 0;
+        uint32_t starts = 0, cur = rd ? ch[b0] : 0u, rc = 0;
 #pragma unroll 1
         for (int q = 0; q < BS / 16; q++) {
-            const uint4 v4 = *reinterpret_cast<const uint4*>(S.chunk + b0 + 16 * q);
+            const uint4 v4 = rd ? *reinterpret_cast<const uint4*>(ch + b0 + 16 * q) : make_uint4(0, 0, 0, 0);
             const uint32_t wv[4] = {v4.x, v4.y, v4.z, v4.w};
 #pragma unroll
             for (int e = 0; e < 4; e++) {
@@ -255,7 +268,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
             // other steps: positions p = step * i in the lane's block
 #pragma unroll 1
             for (uint32_t p = (b0 + step - 1) / step * step; p < b0 + BS && p + 1 < n; p += step) {
-                const uint32_t c = S.chunk[p], nx = S.chunk[p + 1];
+                const uint32_t c = ch[p], nx = ch[p + 1];
                 samp += c == nx;
                 dsamp += (c > nx ? c - nx : nx - c) < 32u;
             }
@@ -288,8 +301,8 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
 #pragma unroll 1
         for (int r = 0; r < ROUNDS; r++) {
             const uint32_t b0 = (uint32_t)(r * 64 + lane) * BS;
-            uint32_t prev = b0 ? S.chunk[b0 - 1] : 0x100u;
-            for_block_bytes<BS>(S.chunk, b0, [&](uint32_t p, uint32_t c, uint32_t) {
+            uint32_t prev = b0 ? ch[b0 - 1] : 0x100u;
+            for_block_bytes<BS>(ch, b0, [&](uint32_t p, uint32_t c, uint32_t) {
                 if (p < n && c != prev) atomicMin(&first[c], p);
                 prev = c;
             });
@@ -501,7 +514,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
             const int i = base + (int)lane;
             const bool act = i <= mlim;
             // loads run for every lane (past n: padding / work[] bytes of inactive lanes)
-            const uint32_t v = lds_rd32(S.chunk, (uint32_t)i);
+            const uint32_t v = lds_rd32(ch, (uint32_t)i);
             const uint32_t h = (v * 2654435761u) >> (32 - LZ4_HASH_BITS);
             // candidate: the last earlier 64-position window's position with my hash
             int cand = (int)last[h] - 1;
@@ -518,7 +531,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
             }
             // the window's highest position per hash (the reads above see earlier windows only)
             atomicMax(&last[h], (uint32_t)i + 1u);
-            const uint32_t cv = lds_rd32(S.chunk, (uint32_t)max(cand, 0));
+            const uint32_t cv = lds_rd32(ch, (uint32_t)max(cand, 0));
             const bool valid = act && cand >= 0 && cv == v;
             const uint64_t vm = __ballot(valid);
             wave_sync();
@@ -533,7 +546,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
             const uint32_t lim = run_l ? n - 5 - (uint32_t)i : 0u;
             uint32_t L = 0;
             if (run_l) {   // only possible match starts read their 12 bytes (fewer LDS bank conflicts)
-                const uint32_t* c32 = reinterpret_cast<const uint32_t*>(S.chunk);
+                const uint32_t* c32 = reinterpret_cast<const uint32_t*>(ch);
                 const uint32_t cs = (uint32_t)cand;
                 const uint32_t si = (uint32_t)i & 3u, sc = cs & 3u;
                 const uint32_t ai = ((uint32_t)i + 4) >> 2, ac = (cs + 4) >> 2;
@@ -602,7 +615,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                         uint32_t fd = 0;
                         bool eq = false;
                         if (q < lj) {
-                            const uint32_t xx = lds_rd32(S.chunk, j + q) ^ lds_rd32(S.chunk, c + q);
+                            const uint32_t xx = lds_rd32(ch, j + q) ^ lds_rd32(ch, c + q);
                             eq = xx == 0;
                             fd = xx ? (uint32_t)__builtin_ctz(xx) >> 3 : 4;
                         }
@@ -672,7 +685,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                     if (anchor < (uint32_t)base) {
                         const uint32_t dst = readlane(ql, (uint32_t)__builtin_ctzll(sel));
                         const uint32_t len = (uint32_t)base - anchor;
-                        for (uint32_t t = lane; t < len; t += 64) blk[dst + t] = S.chunk[anchor + t];
+                        for (uint32_t t = lane; t < len; t += 64) blk[dst + t] = ch[anchor + t];
                     }
                 }
                 emitted = __builtin_amdgcn_readfirstlane(emitted + tot);
@@ -696,7 +709,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                 uint32_t b;
                 if (t == 0) b = (flit >= 15 ? 15 : flit) << 4;
                 else if (t < 1 + fxl) b = ext_byte(flit, fxl, t - 1);
-                else if (t < fin) b = S.chunk[anchor + t - 1 - fxl];
+                else if (t < fin) b = ch[anchor + t - 1 - fxl];
                 else b = 0;   // end mark
                 o[t] = (uint8_t)b;
             }
@@ -706,7 +719,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
             best = blen + 41;
         } else if (force) {
             // stored block: 15 B header, size | 0x80000000, raw bytes, end mark
-            for (uint32_t t = lane; t < n + 4; t += 64) blk[t] = t < n ? S.chunk[t] : 0;
+            for (uint32_t t = lane; t < n + 4; t += 64) blk[t] = t < n ? ch[t] : 0;
             if (lane < 19) slot[lane] = lz4_hdr_byte(lane, n, n | 0x80000000u);
             win = 9;
             wlen = n + 23;
@@ -736,16 +749,16 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
     if (defer) {
     } else if (win == 4) {
         for (uint32_t i = lane; i < n; i += 64)
-            slot[i] = i ? (uint8_t)(S.chunk[i] - S.chunk[i - 1]) : S.chunk[0];
+            slot[i] = i ? (uint8_t)(ch[i] - ch[i - 1]) : ch[0];
     } else if (win == 255) {
         // in place: k_compact copies the chunk from the input (saves writing and
         // re-reading a third of a mixed input's bytes through the slots)
         const uint32_t nv = (A.flags & ENC_RAW_IN_PLACE) ? 0u : (n + 15) >> 4;
         for (uint32_t v = lane; v < nv; v += 64)
-            reinterpret_cast<uint4*>(slot)[v] = reinterpret_cast<const uint4*>(S.chunk)[v];
-    } else if (win == 1 && S.hist()[S.chunk[0]] == n) {
+            reinterpret_cast<uint4*>(slot)[v] = reinterpret_cast<const uint4*>(ch)[v];
+    } else if (win == 1 && S.hist()[ch[0]] == n) {
         // one byte value: (c, 255) pairs and the remainder (compression_methods.py:95-109)
-        const uint32_t c = S.chunk[0];
+        const uint32_t c = ch[0];
         for (uint32_t j = lane; j < pairs; j += 64) {
             slot[2 * j] = (uint8_t)c;
             slot[2 * j + 1] = (uint8_t)(j + 1 < pairs ? 255u : n - 255u * (pairs - 1));
@@ -754,7 +767,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         // pair starts -> region (u16) in windows of CAPP entries (a forced RLE on
         // incompressible data has up to n pairs), then (byte, count) pairs
         uint16_t* ps = reinterpret_cast<uint16_t*>(S.work);
-        constexpr uint32_t CAPP = EncSmem<CMAX>::WORK / 2;
+        constexpr uint32_t CAPP = EncSmem<CMAX, GL>::WORK / 2;
 #pragma unroll 1
         for (uint32_t wb = 0; wb < pairs; wb += CAPP - 1) {
             uint32_t base_idx = 0;
@@ -762,12 +775,12 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
 #pragma unroll 1
             for (int r = 0; r < ROUNDS; r++) {
                 const uint32_t b0 = (uint32_t)(r * 64 + lane) * BS;
-                const uint32_t prevb = b0 ? S.chunk[b0 - 1] : 0x100u;
+                const uint32_t prevb = b0 ? ch[b0 - 1] : 0x100u;
                 int lb = -1;
                 uint32_t cnt = 0;
                 {
                     uint32_t prev = prevb;
-                    for_block_bytes<BS>(S.chunk, b0, [&](uint32_t p, uint32_t c, uint32_t) {
+                    for_block_bytes<BS>(ch, b0, [&](uint32_t p, uint32_t c, uint32_t) {
                         if (p < n && c != prev) lb = (int)p;
                         prev = c;
                     });
@@ -776,7 +789,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                 rs_c = max(rs_c, wave_max_i32(lb));
                 const uint32_t off0 = b0 == 0 ? 254u : (uint32_t)((int)(b0 - 1) - rs) % 255u;
                 uint32_t off = off0, prev = prevb;
-                for_block_bytes<BS>(S.chunk, b0, [&](uint32_t p, uint32_t c, uint32_t) {
+                for_block_bytes<BS>(ch, b0, [&](uint32_t p, uint32_t c, uint32_t) {
                     off = c != prev ? 0u : (off == 254u ? 0u : off + 1u);
                     if (p < n && off == 0) cnt++;
                     prev = c;
@@ -784,7 +797,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                 const uint32_t incl = wave_incl_sum(cnt);
                 uint32_t idx = base_idx + incl - cnt;
                 off = off0; prev = prevb;
-                for_block_bytes<BS>(S.chunk, b0, [&](uint32_t p, uint32_t c, uint32_t) {
+                for_block_bytes<BS>(ch, b0, [&](uint32_t p, uint32_t c, uint32_t) {
                     off = c != prev ? 0u : (off == 254u ? 0u : off + 1u);
                     if (p < n && off == 0) {
                         if (idx >= wb && idx < wb + CAPP) ps[idx - wb] = (uint16_t)p;
@@ -799,7 +812,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
             for (uint32_t j = wb + lane; j < we; j += 64) {
                 const uint32_t st = ps[j - wb];
                 const uint32_t en = j + 1 < pairs ? ps[j + 1 - wb] : n;
-                slot[2 * j] = S.chunk[st];
+                slot[2 * j] = ch[st];
                 slot[2 * j + 1] = (uint8_t)(en - st);
             }
             wave_sync();
@@ -825,7 +838,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         const uint32_t nwords = (nbytes + 3) >> 2;
         // forced encodes of high-entropy data can outgrow the LDS region: stage the
         // bit words in the slot behind the payload instead (slot holds 3C + 1344 B)
-        const bool gstage = (nwords + 1) * 4 > (uint32_t)EncSmem<CMAX>::STAGE;
+        const bool gstage = (nwords + 1) * 4 > (uint32_t)EncSmem<CMAX, GL>::STAGE;
         if (gstage) bits = reinterpret_cast<uint32_t*>(slot + ((wlen + 15) & ~15u));
         for (uint32_t w = lane; w < nwords + 1; w += 64) bits[w] = 0;
         if (gstage) __threadfence();
@@ -835,13 +848,13 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         for (int r = 0; r < ROUNDS; r++) {
             const uint32_t b0 = (uint32_t)(r * 64 + lane) * BS;
             uint32_t my = 0;
-            for_block_bytes<BS>(S.chunk, b0, [&](uint32_t p, uint32_t c, uint32_t) {
+            for_block_bytes<BS>(ch, b0, [&](uint32_t p, uint32_t c, uint32_t) {
                 if (p < n) my += S.clen()[c];
             });
             const uint32_t incl = wave_incl_sum(my);
             uint32_t bp = bitbase + incl - my;
             uint32_t cw = bp >> 5, acc = 0;
-            for_block_bytes<BS>(S.chunk, b0, [&](uint32_t p, uint32_t s, uint32_t) {
+            for_block_bytes<BS>(ch, b0, [&](uint32_t p, uint32_t s, uint32_t) {
                 if (p < n) {
                     const uint32_t L = S.clen()[s], cd = S.code()[s];
                     const uint32_t o = bp & 31, w = bp >> 5;
@@ -1111,7 +1124,16 @@ __global__ __launch_bounds__(256) void k_equal(const uint8_t* a, const uint8_t* 
 // ---------------------------------------------------------------------------
 template <int CMAX>
 static hipError_t launch_encode_t(const EncArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_encode<CMAX>, dim3(a.n_chunks), dim3(64), 0, s, a);
+    // 16 KiB and more: the chunk in place (see k_encode) unless a forced / analysed
+    // encode may take the other methods' LDS-bound paths
+    static const uint32_t gl_min = getenv("AMBC_ENC_GL_MIN") ? (uint32_t)atoi(getenv("AMBC_ENC_GL_MIN")) : 16384u;
+    if constexpr (CMAX >= 4096) {
+        if (CMAX >= gl_min && (a.flags & ENC_IN_ALIGNED) && !(a.flags & (ENC_FORCE | ENC_ANALYZE))) {
+            hipLaunchKernelGGL((k_encode<CMAX, true>), dim3(a.n_chunks), dim3(64), 0, s, a);
+            return hipGetLastError();
+        }
+    }
+    hipLaunchKernelGGL((k_encode<CMAX, false>), dim3(a.n_chunks), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 

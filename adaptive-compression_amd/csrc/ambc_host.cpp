@@ -283,6 +283,11 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
     // raw packages go from the input straight to the body (aligned inputs: k_compact's dword loads)
     const bool raw_in_place = ((uintptr_t)d_in & 3) == 0 && !getenv("AMBC_RAW_VIA_SLOT");
     if (raw_in_place) ea.flags |= ENC_RAW_IN_PLACE;
+    // chunks read in place (k_encode, >= 16 KiB): 16-byte aligned chunk starts and
+    // 64 readable bytes after the input (the library's own input buffers have them)
+    const bool padded = (p->flags & AMBC_FLAG_INPUT_PADDED) ||
+                        (d.in.p && d_in >= d.in.as<uint8_t>() && d_in + n + 64 <= d.in.as<uint8_t>() + d.in.cap);
+    if (((uintptr_t)d_in & 15) == 0 && (C & 15) == 0 && padded && !getenv("AMBC_ENC_LDS")) ea.flags |= ENC_IN_ALIGNED;
 
     TRACE("compress_on n=%llu M=%u C=%u", (unsigned long long)n, M, C);
     std::vector<unsigned long long> stamps;

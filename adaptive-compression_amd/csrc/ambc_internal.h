@@ -12,6 +12,7 @@ constexpr uint32_t ENC_FORCE = 1;    // CompressionMethod.compress(chunk) semant
 constexpr uint32_t ENC_ANALYZE = 2;  // also evaluate every should_use
 constexpr uint32_t ENC_EMIT_PENDING = 4;  // emit only the chunks the first pass deferred and id 5 did not take
 constexpr uint32_t ENC_RAW_IN_PLACE = 8;  // raw (255) payloads are not copied to the slot: k_compact reads the input
+constexpr uint32_t ENC_IN_ALIGNED = 16;   // every chunk starts 16-byte aligned in the input (k_encode may read it in place)
 
 // k_deflate's per-chunk device scratch: the parse's matches (2 cmax bytes), then
 // for chunks above 16 KiB the match-start masks (cmax / 8 bytes)

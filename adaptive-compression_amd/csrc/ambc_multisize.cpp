@@ -95,6 +95,10 @@ int launch_batch(Batch& b, hipStream_t st, const uint8_t* d_in, uint64_t n, cons
     ea.coff = b.coff.as<uint64_t>();
     ea.clen = b.clen.as<uint32_t>();
     for (int i = 0; i < 16; i++) { ea.pref_min[i] = p->pref_min[i]; ea.pref_max[i] = p->pref_max[i]; }
+    // chunks on the 16-byte grid of the library's padded input copy: read in place
+    bool aligned = ((uintptr_t)d_in & 15) == 0 && !getenv("AMBC_ENC_LDS");
+    for (uint64_t q : pos) aligned = aligned && (q & 15) == 0;
+    if (aligned) ea.flags |= ENC_IN_ALIGNED;
     if (ent) {   // numpy's p*log2(p) terms for an s-byte chunk (Huffman should_use near 7.0)
         HIPCHK(b.ent.ensure((size_t)(s + 1) * 8));
         HIPCHK(hipMemcpyAsync(b.ent.p, ent, (size_t)(s + 1) * 8, hipMemcpyHostToDevice, st));
@@ -188,6 +192,7 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
     // MiB of mixed data, reference candidates: best of 1-8 ahead x 256-2048
     // walks; AMBC_MS_WALKS / AMBC_MS_SPEC override them for such sweeps)
     static const uint64_t KMAX_ = getenv("AMBC_MS_WALKS") ? strtoull(getenv("AMBC_MS_WALKS"), nullptr, 10) : 512;
+    static const uint64_t SPAN_ = getenv("AMBC_MS_SPAN") ? strtoull(getenv("AMBC_MS_SPAN"), nullptr, 10) : 512 << 10;
     uint32_t max_cand = 0;
     for (uint32_t i = 0; i < n_cands; i++)
         if (any_eligible(p, cands[i])) max_cand = std::max(max_cand, cands[i]);
@@ -196,7 +201,7 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
         // wins everywhere (homogeneous data) every walk runs on the same lattice
         // and joins the next one at once; elsewhere the mixed choices shift their
         // phases until they meet
-        const uint64_t K = std::max<uint64_t>(1, std::min<uint64_t>(KMAX_, n / (512 << 10)));
+        const uint64_t K = std::max<uint64_t>(1, std::min<uint64_t>(KMAX_, n / std::max<uint64_t>(SPAN_, 1)));
         const uint64_t lat = max_cand ? max_cand : g;
         std::set<uint64_t> starts;
         for (uint64_t k = 0; k < K; k++) starts.insert((k * n / K) / lat * lat);
@@ -258,7 +263,9 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
     // right one saves a round, whose latency -- the slowest 64 KiB encode -- is
     // the walk's cost; a wrong one costs idle device time only)
     static const int SPEC = getenv("AMBC_MS_SPEC") ? atoi(getenv("AMBC_MS_SPEC")) : 2;
+    uint64_t t_dec = 0, t_req = 0, t_launch = 0, t_wait = 0, t_fill = 0;   // (AMBC_TRACE breakdown)
     while (!active.empty()) {
+        uint64_t tq = now_ns();
         std::vector<Walk> still;
         for (Walk w : active) {
             for (;;) {
@@ -279,6 +286,8 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
         still.erase(std::unique(still.begin(), still.end(), [](const Walk& x, const Walk& y) { return x.pos == y.pos; }),
                     still.end());
         active.swap(still);
+        t_dec += now_ns() - tq;
+        tq = now_ns();
         if (active.empty()) break;
         steps++;
         std::map<uint32_t, std::vector<uint64_t>> req;
@@ -300,6 +309,7 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
             }
         }
         const uint64_t tk = now_ns();
+        t_req += tk - tq;
         std::vector<std::pair<uint32_t, std::vector<uint64_t>>> jobs;
         for (auto& r : req) {
             if (check_size(p, r.first)) {       // speculative only: never decided from
@@ -312,23 +322,31 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
         // (the 64 KiB class runs at 2 workgroups per CU: the small ones fill in)
         for (size_t j0 = 0; j0 < jobs.size(); j0 += 8) {
             const size_t j1 = std::min(jobs.size(), j0 + 8);
+            uint64_t tl = now_ns();
             for (size_t j = j0; j < j1; j++) {
                 int rc = launch_batch(d.msb[j - j0], d.mss[j - j0], d_in, n, p, jobs[j].first, jobs[j].second,
                                       ent_of(jobs[j].first));
                 if (rc) return rc;
             }
+            t_launch += now_ns() - tl;
             for (size_t j = j0; j < j1; j++) {
+                tl = now_ns();
                 HIPCHK(hipStreamSynchronize(d.mss[j - j0]));
+                t_wait += now_ns() - tl;
+                tl = now_ns();
                 const Batch& bb = d.msb[j - j0];
                 for (size_t q = 0; q < jobs[j].second.size(); q++)
                     cache[key(jobs[j].second[q], jobs[j].first)] = Eval{bb.hplen[q], bb.hids[q]};
                 evaluated += jobs[j].second.size();
+                t_fill += now_ns() - tl;
             }
         }
         kernel_ns += now_ns() - tk;
     }
 
     const uint64_t t_walk = now_ns() - t0;
+    TRACE("multisize walk ms: decide %.2f requests %.2f launch %.2f wait %.2f fill %.2f (total %.2f)", t_dec / 1e6,
+          t_req / 1e6, t_launch / 1e6, t_wait / 1e6, t_fill / 1e6, t_walk / 1e6);
     // ---- the reference's walk from 0, read off the decisions ----
     struct Pkg { uint64_t pos; uint32_t s, plen; uint8_t id; uint64_t off; };
     std::vector<Pkg> path;

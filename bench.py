@@ -105,6 +105,7 @@ def make_params(args, methods, n):
     p.chunk_size = args.chunk
     p.mode = _lib.MODE_REFERENCE if args.mode == "reference" else _lib.MODE_NATIVE
     p.method_mask = method_mask(methods)
+    p.flags = _lib.FLAG_INPUT_PADDED      # (the device inputs below carry 64 bytes of slack)
     for i in range(16):
         lo, hi = METHOD_CHUNK_PREFS.get(i, (1, 0))
         p.pref_min[i], p.pref_max[i] = lo, min(hi, 0xFFFFFFFF)

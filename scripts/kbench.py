@@ -50,7 +50,7 @@ def main():
     ctx = _lib.Context()
     lib = ctx.lib
     n = args.size
-    d_in = lib.ambc_device_alloc(ctx.h, 0, n)
+    d_in = lib.ambc_device_alloc(ctx.h, 0, n + 64)   # + the slack AMBC_FLAG_INPUT_PADDED promises
     cap = lib.ambc_compress_bound(n, args.chunk)
     d_out = lib.ambc_device_alloc(ctx.h, 0, cap)
     tab = entropy_terms(args.chunk)
@@ -64,7 +64,7 @@ def main():
         for mset in msets:
             p = _lib.Params()
             p.chunk_size = args.chunk
-            p.flags = args.flags
+            p.flags = args.flags | _lib.FLAG_INPUT_PADDED
             p.method_mask = method_mask(mset)
             for i in range(16):
                 lo, hi = METHOD_CHUNK_PREFS.get(i, (1, 0))
