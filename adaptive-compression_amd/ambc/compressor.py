@@ -240,14 +240,14 @@ class AdaptiveCompressor:
         ent_sizes = (C.c_uint32 * max(1, len(tabs)))(*sorted(sizes))
         ent_ptrs = (C.c_void_p * max(1, len(tabs)))(*[t.ctypes.data for t in tabs])
         carr = (C.c_uint32 * len(cands))(*cands)
-        cap = n + 64            # compressed packages are shorter than their chunks; one raw remainder
-        out = np.empty(cap, dtype=np.uint8)     # (no zero fill: the call writes what it returns)
         olen = C.c_uint64()
         st = _lib.Stats()
         src = file_data if isinstance(file_data, (bytes, bytearray)) else bytes(file_data)
+        # out = NULL: the body stays on the device until it is fetched into a
+        # bytes object of exactly its size (see _adaptive_decompress for why
+        # writing into a fresh, private bytes object is sound)
         rc = ctx.lib.ambc_compress_multisize(ctx.h, _lib.addr(src), n, C.byref(p), carr, len(cands), ent_sizes,
-                                             ent_ptrs, len(tabs), out.ctypes.data, cap, C.byref(olen),
-                                             C.byref(st))
+                                             ent_ptrs, len(tabs), None, 0, C.byref(olen), C.byref(st))
         if rc == _lib.AMBC_E_RANGE:
             raise struct.error("argument out of range")
         if rc == _lib.AMBC_E_INVAL:
@@ -263,7 +263,12 @@ class AdaptiveCompressor:
             "compressed_size_without_overhead": int(st.payload_bytes),
             "overhead_bytes": int(st.overhead_bytes)}
         self.method_usage_ids = [m.type_id for m in self.compression_methods]
-        return out[:olen.value].tobytes()
+        out = bytes(olen.value)
+        if sys.getrefcount(out) != 2:
+            raise RuntimeError("body buffer is shared: refusing to write into it")
+        _lib.check(ctx.lib.ambc_fetch_body(ctx.h, C.cast(C.c_char_p(out), C.POINTER(C.c_uint8)), olen.value),
+                   ctx.lib)
+        return out
 
     def _adaptive_compress(self, file_data):
         """One C-ABI call: input bytes -> .ambc body (packages + end chunk)."""

@@ -485,10 +485,20 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         if (lane == 0) A.bestpre[k] = best | (uniform ? 0x80000000u : 0u) | (single ? 0x40000000u : 0u);
     }
     const uint32_t best_pre = best;   // before LZ4 (a deferred Huffman compares against it)
+    const bool eval = A.flags & ENC_EVAL;
+    // prefix sizes to report (ENC_EVAL + lz4sub): sub_c[sj..sj_end) -- ascending,
+    // below n, within id 9's prefs; they end in order as the parse passes b - 12
+    uint32_t sj = 0, sj_end = 0;
+    if (A.lz4sub && ((mm >> 9) & 1u)) {
+        while (sj < A.n_subc && A.sub_c[sj] < max(A.pref_min[9], 13u)) sj++;
+        sj_end = sj;
+        while (sj_end < A.n_subc && A.sub_c[sj_end] < n && A.sub_c[sj_end] <= A.pref_max[9]) sj_end++;
+    }
     // LZ4's frame is at least 23 + 10 + ext(n - 10) bytes: a literal at 0 (no
     // candidate), one match up to n - 5, the last five bytes literal; with the
     // 18-B header it cannot win unless best > 51 + ext(n - 10) (zero runs: RLE 52)
-    if (eligible(9) && (force || (n >= 1024 && best > 51 + ext_len(n - 10)))) {
+    const bool lz4_main = eligible(9) && (force || (n >= 1024 && best > 51 + ext_len(n - 10)));
+    if (lz4_main || sj < sj_end) {
         // the walk's hash table overlays hist[]: keep the counts in registers
         uint32_t hsave[4];
 #pragma unroll
@@ -503,10 +513,18 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         const int mlim = (int)n - 12;       // last position a match may start; <0: none
         uint8_t* blk = slot + 19;
         uint32_t emitted = 0, anchor = 0, nextp = 0;
-        bool alive = true;
+        bool alive = lz4_main;              // the chunk's own LZ4 can still win
         constexpr uint32_t LCAP = 16;       // per-lane precomputed match length cap
+        // prefix sub_c[sj] is done: its block = emitted + add (this round's sequences
+        // that start by b - 12) + the final literals from endp
+        auto sub_done = [&](uint32_t add, uint32_t endp) {
+            const uint32_t b = A.sub_c[sj];
+            const uint32_t fl = b - endp;
+            if (lane == 0) A.lz4sub[(uint64_t)k * LZ4_SUB_MAX + sj] = emitted + add + 1 + ext_len(fl) + fl;
+            sj++;
+        };
 #pragma unroll 1
-        for (int base = 0; base <= mlim && alive; base += 64) {
+        for (int base = 0; base <= mlim && (alive || sj < sj_end); base += 64) {
             // control state is wave-uniform: keep it in SGPRs
             nextp = __builtin_amdgcn_readfirstlane(nextp);
             anchor = __builtin_amdgcn_readfirstlane(anchor);
@@ -538,7 +556,10 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
             STAMP(2);
             if (base + 63 < (int)nextp) continue;   // round lies inside the previous match
             uint32_t p = __builtin_amdgcn_readfirstlane((int)nextp > base ? nextp - (uint32_t)base : 0u);
-            if ((vm & (~0ull << p)) == 0ull) continue;   // no match starts here: all literals
+            if ((vm & (~0ull << p)) == 0ull) {     // no match starts here: all literals
+                while (sj < sj_end && (uint32_t)base + 64 > A.sub_c[sj] - 12) sub_done(0, anchor);
+                continue;
+            }
             // per-lane match length in one step: bytes 4..15 behind the known four
             // (four aligned dwords per side, issued together), so L <= LCAP = 16;
             // the walk extends the selected longer ones with the whole wave
@@ -650,23 +671,42 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                 const uint32_t sz = me ? 3 + xl + lit + xm : 0u;
                 const uint32_t incl = wave_incl_sum(sz);
                 const uint32_t tot = readlane(incl, 63);
+                // prefixes whose last match start b - 12 this round passes: the
+                // round's sequences up to the last one starting by b - 12 (t), whose
+                // match is capped at b - 5; none: the block ends with the anchor
+                while (sj < sj_end && max(np, (uint32_t)base + 64) > A.sub_c[sj] - 12) {
+                    const uint32_t b = A.sub_c[sj];
+                    const uint32_t r = b - 12 - (uint32_t)base;      // lanes 0..r start by b - 12
+                    const uint64_t sb = sel & (r >= 63 ? ~0ull : (2ull << r) - 1ull);
+                    if (!sb) {
+                        sub_done(0, anchor);
+                    } else {
+                        const uint32_t t = 63u - (uint32_t)__builtin_clzll(sb);
+                        const uint32_t it = (uint32_t)base + t;
+                        const uint32_t lb = min(readlane(L, t), b - 5 - it);
+                        const uint32_t szb = 3 + readlane(xl, t) + readlane(lit, t) + ext_len(lb - 4);
+                        sub_done(readlane(incl, t) - readlane(sz, t) + szb, it + lb);
+                    }
+                }
                 // the sequential walk gives up at the first sequence that makes
                 // block + 1 >= budget; the round total decides the same way
-                if (emitted + tot + 1 >= budget) { alive = false; break; }
+                if (alive && emitted + tot + 1 >= budget) alive = false;
+                if (!alive && sj >= sj_end) break;
+                const bool st_on = alive && !eval;           // (decision only: sizes, no bytes)
                 // 32-bit offsets from the (uniform) block pointer: saddr stores
                 const uint32_t q0 = emitted + incl - sz;     // token
                 const uint32_t ql = q0 + 1 + xl;             // first literal
 #ifdef AMBC_EXP_NOSTORE
                 if (0) {
 #else
-                if (me) {
+                if (me && st_on) {
 #endif
                     blk[q0] = (uint8_t)((lit >= 15 ? 15 : lit) << 4 | (ml >= 15 ? 15 : ml));
                     const uint32_t offv = (uint32_t)(i - cand);
                     blk[ql + lit] = (uint8_t)offv;
                     blk[ql + lit + 1] = (uint8_t)(offv >> 8);
                 }
-                if (ext && me) {
+                if (ext && me && st_on) {
                     for (uint32_t t = 0; t < xl; t++) blk[q0 + 1 + t] = (uint8_t)ext_byte(lit, xl, t);
                     for (uint32_t t = 0; t < xm; t++) blk[ql + lit + 2 + t] = (uint8_t)ext_byte(ml, xm, t);
                 }
@@ -675,7 +715,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                 // literal of the next selected lane's sequence, at offset i - pe
                 // of its literals (its pe is that sequence's literal start); the
                 // first sequence's literals from before this round by the whole wave
-                {
+                if (st_on) {
                     const uint64_t rest = sel >> lane;
                     const uint32_t nx = rest ? lane + (uint32_t)__builtin_ctzll(rest) : lane;
                     const uint32_t qn = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(nx << 2), (int)ql);
@@ -694,6 +734,9 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
             nextp = __builtin_amdgcn_readfirstlane(np);
             STAMP(7);
         }
+        // (by construction every prefix ends inside the loop; a leftover reads as lost)
+        for (; sj < sj_end; sj++)
+            if (lane == 0) A.lz4sub[(uint64_t)k * LZ4_SUB_MAX + sj] = 0xFFFFFFFFu;
         uint32_t fin = 0, flit = 0, fxl = 0;
         if (alive) {
             flit = n - anchor;
@@ -705,7 +748,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
             // final literals, frame header, block size, end mark
             const uint32_t blen = emitted + fin;
             uint8_t* o = blk + emitted;
-            for (uint32_t t = lane; t < fin + 4; t += 64) {
+            for (uint32_t t = lane; t < (eval ? 0u : fin + 4); t += 64) {
                 uint32_t b;
                 if (t == 0) b = (flit >= 15 ? 15 : flit) << 4;
                 else if (t < 1 + fxl) b = ext_byte(flit, fxl, t - 1);
@@ -713,7 +756,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                 else b = 0;   // end mark
                 o[t] = (uint8_t)b;
             }
-            if (lane < 19) slot[lane] = lz4_hdr_byte(lane, n, blen);
+            if (lane < 19 && !eval) slot[lane] = lz4_hdr_byte(lane, n, blen);
             win = 9;
             wlen = blen + 23;
             best = blen + 41;
@@ -746,7 +789,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
     // launch (ENC_EMIT_PENDING) that repeats this chunk's selection
     const bool defer = A.pending && !(A.flags & ENC_EMIT_PENDING) && (win == 1 || win == 3);
     if (A.pending && !(A.flags & ENC_EMIT_PENDING) && lane == 0) A.pending[k] = defer ? 1 : 0;
-    if (defer) {
+    if (defer || eval) {
     } else if (win == 4) {
         for (uint32_t i = lane; i < n; i += 64)
             slot[i] = i ? (uint8_t)(ch[i] - ch[i - 1]) : ch[0];

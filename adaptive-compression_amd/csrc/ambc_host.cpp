@@ -1189,7 +1189,6 @@ static void inflate_all(const uint8_t* body, const std::vector<ambc_host_chunk>&
 // the CPU copy of the previous piece; the host side (memcpy, and the first-touch
 // page faults of a freshly allocated output) runs on all T threads at once.
 constexpr size_t kStagePiece = 8u << 20;
-constexpr uint64_t kStageMin = 64ull << 20;   // below this the runtime's own path
 
 struct StageSet {
     std::vector<void*>* buf;
@@ -1235,7 +1234,7 @@ static void hugepage_advice(void* dst, uint64_t n) {
 }
 
 // to_dev: host src -> device dst; else device src -> host dst
-static int copy_staged(Dev& d, void* dst, const void* src, uint64_t n, bool to_dev, int set = 0, unsigned cap = 16) {
+int ambc::copy_staged(Dev& d, void* dst, const void* src, uint64_t n, bool to_dev, int set, unsigned cap) {
     const unsigned T = stage_threads(n, cap);
     int rc = ensure_stage(d, T, set);
     if (rc) return rc;

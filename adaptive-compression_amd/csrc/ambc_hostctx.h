@@ -71,26 +71,35 @@ struct Buf {
 
 // device buffers of one multi-size walk batch (ambc_multisize.cpp)
 struct Batch {
-    Buf coff, clen, slots, plen, ids, sizes, bestpre, gdseq, pending, ent, off, z9rec, z9scr;
-    uint32_t* hplen = nullptr;  // pinned copies of plen / ids for the host walk
+    Buf coff, clen, slots, plen, ids, sizes, bestpre, gdseq, pending, ent, off, z9rec, z9scr, lz4sub;
+    uint32_t* hplen = nullptr;  // pinned copies of plen / ids / LZ4 prefix lengths for the host walk
     uint8_t* hids = nullptr;
+    uint32_t* hlz = nullptr;
+    uint64_t* hpos = nullptr;   // pinned chunk positions (the upload's source)
     size_t hcap = 0;
-    hipError_t host_ensure(size_t n) {
-        if (n <= hcap) return hipSuccess;
+    void host_free() {
         if (hplen) (void)hipHostFree(hplen);
         if (hids) (void)hipHostFree(hids);
-        hplen = nullptr; hids = nullptr; hcap = 0;
+        if (hlz) (void)hipHostFree(hlz);
+        if (hpos) (void)hipHostFree(hpos);
+        hplen = nullptr; hids = nullptr; hlz = nullptr; hpos = nullptr; hcap = 0;
+    }
+    hipError_t host_ensure(size_t n) {
+        if (n <= hcap) return hipSuccess;
+        host_free();
+        n = std::max<size_t>(n, 1024);
         hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&hplen), n * 4);
         if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&hids), n);
+        if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&hlz), n * 4 * LZ4_SUB_MAX);
+        if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&hpos), n * 8);
         if (e == hipSuccess) hcap = n;
         return e;
     }
     void release() {
-        for (Buf* b : {&coff, &clen, &slots, &plen, &ids, &sizes, &bestpre, &gdseq, &pending, &ent, &off, &z9rec, &z9scr})
+        for (Buf* b : {&coff, &clen, &slots, &plen, &ids, &sizes, &bestpre, &gdseq, &pending, &ent, &off, &z9rec, &z9scr,
+                       &lz4sub})
             b->release();
-        if (hplen) (void)hipHostFree(hplen);
-        if (hids) (void)hipHostFree(hids);
-        hplen = nullptr; hids = nullptr; hcap = 0;
+        host_free();
     }
 };
 
@@ -136,6 +145,7 @@ struct Dev {
     uint32_t ms_steps = 0;      // last multi-size walk: batched evaluation rounds,
     uint64_t ms_evaluated = 0;  //   chunk encodes they ran,
     uint64_t ms_walk_ns = 0, ms_emit_ns = 0;  // and the time of the walk / of the final encode
+    uint64_t ms_body = 0;       // a multi-size body kept in `out` for ambc_fetch_body (0: none)
     uint64_t t_encode = 0, t_scan = 0, t_compact = 0;
     uint32_t n_launch = 1;      // k_encode launches of the last compress call (pipelined segments)
     hipStream_t cs = nullptr;   // scan + compaction of pipelined segments
@@ -184,6 +194,9 @@ int decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t orig_size
 void default_registered(const uint64_t* registered, uint64_t reg[4]);
 void add_stats(ambc_stats* a, const ambc_stats& b);   // sums (kernel_ns: max)
 uint64_t slab_bytes();                                 // host-fed pipelines' slab size
+// large pageable <-> device copies through pinned staging buffers on T threads
+constexpr uint64_t kStageMin = 64ull << 20;            // below this the runtime's own path
+int copy_staged(Dev& d, void* dst, const void* src, uint64_t n, bool to_dev, int set = 0, unsigned cap = 16);
 
 // collective of the sharded calls (ambc_shard.cpp)
 int shard_allreduce_min(Transport* t, uint64_t* v, int rc_local);

@@ -13,6 +13,8 @@ constexpr uint32_t ENC_ANALYZE = 2;  // also evaluate every should_use
 constexpr uint32_t ENC_EMIT_PENDING = 4;  // emit only the chunks the first pass deferred and id 5 did not take
 constexpr uint32_t ENC_RAW_IN_PLACE = 8;  // raw (255) payloads are not copied to the slot: k_compact reads the input
 constexpr uint32_t ENC_IN_ALIGNED = 16;   // every chunk starts 16-byte aligned in the input (k_encode may read it in place)
+constexpr uint32_t ENC_EVAL = 32;         // decision only (multi-size walk): plen / ids, no payload written
+constexpr uint32_t LZ4_SUB_MAX = 8;       // EncArgs::sub_c entries
 
 // k_deflate's per-chunk device scratch: the parse's matches (2 cmax bytes), then
 // for chunks above 16 KiB the match-start masks (cmax / 8 bytes)
@@ -44,6 +46,14 @@ struct EncArgs {
     uint32_t pref_max[16];
     const uint64_t* coff;    // optional chunk table (multi-size walk): chunk k = in[coff[k], coff[k] + clen[k])
     const uint32_t* clen;    //   (else chunk k = in[k * chunk_size, ...) clamped to n_total)
+    // ENC_EVAL + lz4sub: the LZ4 block length of every prefix [0, b) of the chunk
+    // for b in sub_c[] (ascending) with b < n and id 9's prefs, from the chunk's
+    // own parse ("ambc-lz4 greedy v2" is prefix-consistent: the prefix's parse is
+    // the chunk's up to the last match start b - 12, that match capped at b - 5);
+    // lz4sub[k * LZ4_SUB_MAX + j] for sub_c[j], others left untouched
+    uint32_t* lz4sub;
+    uint32_t sub_c[LZ4_SUB_MAX];
+    uint32_t n_subc;
 };
 
 // gather the packages into the body at their scanned offsets

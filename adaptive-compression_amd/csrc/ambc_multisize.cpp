@@ -14,36 +14,37 @@
 // them advance in lock step.  One step evaluates every (position, size) the
 // active walks need in ONE batch per size: the chunks are read in place from the
 // uploaded input through a chunk-offset table (k_encode / k_dict / k_deflate,
-// one workgroup per chunk).  A walk stops when its next position has already
-// been decided (it joined the path of another walk: from there on both are the
-// same walk) or at the end.  Every decided position's successor is decided, so
-// the walk from 0 -- the reference's walk -- is then read off the decisions.
-// The chosen chunks are encoded once more (grouped by size) into slots and
+// one workgroup per chunk), decision only (ENC_EVAL: no payload bytes).  With
+// LZ4 (id 9) among the methods one parse per position serves every size: the
+// largest LZ4-eligible size M is encoded with all its methods and reports the
+// LZ4 block of each smaller candidate prefix (k_encode's lz4sub -- the greedy
+// parse of a prefix is the chunk's own up to its last match start); the smaller
+// sizes run only their other methods, and id 9 joins them last in id order on
+// the host.  A walk stops when its next position has already been decided (it
+// joined the path of another walk: from there on both are the same walk) or at
+// the end.  Every decided position's successor is decided, so the walk from 0
+// -- the reference's walk -- is then read off the decisions.  The chosen chunks
+// are encoded once more (grouped by size, all methods, bytes this time) into
+// slots -- the walk's decision must come out again, or the call fails -- and
 // moved into the body at their offsets (k_compact with per-package lengths).
 #include <algorithm>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <numeric>
-#include <set>
-#include <unordered_map>
 
 #include "ambc_hostctx.h"
 
 namespace ambc {
 namespace {
 
-struct Eval {
-    uint32_t plen;   // payload of the size's winner
-    uint8_t id;      // 255: no method beats raw at this size
-};
-
 bool eligible(const ambc_params* p, uint32_t s, uint32_t id) {
     return ((p->method_mask >> id) & 1) && p->pref_min[id] <= s && s <= p->pref_max[id];
 }
 
-bool any_eligible(const ambc_params* p, uint32_t s) {
+bool any_eligible(const ambc_params* p, uint32_t s, uint32_t skip = 0) {
     for (uint32_t id = 1; id < 16; id++)
-        if (eligible(p, s, id)) return true;
+        if (id != skip && eligible(p, s, id)) return true;
     return false;
 }
 
@@ -61,16 +62,16 @@ int check_size(const ambc_params* p, uint32_t s) {
     return AMBC_OK;
 }
 
-// The encoders over the s-byte chunks at pos[] (one workgroup each) on stream
-// st: per chunk the winner of the reference's method loop for that size, its
-// payload left in the batch's slot k, plen / ids copied back into hp / hi (valid
-// after the stream synchronizes).  The launch sequence is compress_on's
-// (k_encode, k_dict against its winner, k_deflate against both, then the
-// deferred emits).
+// The encoders over the s-byte chunks at pos[0..cnt) (one workgroup each) on
+// stream st with the methods of p: per chunk the winner of the reference's
+// method loop for that size, plen / ids copied back into hplen / hids (and, with
+// subs, the LZ4 prefix blocks into hlz) -- valid after the stream synchronizes.
+// The launch sequence is compress_on's (k_encode, k_dict against its winner,
+// k_deflate against both, then -- bytes wanted -- the deferred emits).  eval:
+// decisions only; pos must then be b.hpos (pinned, uploaded asynchronously).
 int launch_batch(Batch& b, hipStream_t st, const uint8_t* d_in, uint64_t n, const ambc_params* p, uint32_t s,
-                 const std::vector<uint64_t>& pos, const double* ent) {
-    const uint32_t cnt = (uint32_t)pos.size();
-    HIPCHK(b.host_ensure(cnt));
+                 const uint64_t* pos, uint32_t cnt, const double* ent, bool eval, const uint32_t* subc = nullptr,
+                 uint32_t nsub = 0) {
     const uint32_t C = (s + 15) & ~15u;
     const uint32_t stride = slot_stride_for(C);
     HIPCHK(b.coff.ensure((size_t)cnt * 8));
@@ -79,7 +80,7 @@ int launch_batch(Batch& b, hipStream_t st, const uint8_t* d_in, uint64_t n, cons
     HIPCHK(b.plen.ensure((size_t)cnt * 4 + 4));
     HIPCHK(b.ids.ensure((size_t)cnt + 16));
     HIPCHK(b.sizes.ensure((size_t)cnt * 8 + 8));
-    HIPCHK(hipMemcpyAsync(b.coff.p, pos.data(), (size_t)cnt * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(b.coff.p, pos, (size_t)cnt * 8, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(b.clen.p), (int)s, cnt, st));
     EncArgs ea{};
     ea.in = d_in;
@@ -94,16 +95,23 @@ int launch_batch(Batch& b, hipStream_t st, const uint8_t* d_in, uint64_t n, cons
     ea.sizes = b.sizes.as<uint64_t>();
     ea.coff = b.coff.as<uint64_t>();
     ea.clen = b.clen.as<uint32_t>();
+    if (eval) ea.flags |= ENC_EVAL;
     for (int i = 0; i < 16; i++) { ea.pref_min[i] = p->pref_min[i]; ea.pref_max[i] = p->pref_max[i]; }
     // chunks on the 16-byte grid of the library's padded input copy: read in place
     bool aligned = ((uintptr_t)d_in & 15) == 0 && !getenv("AMBC_ENC_LDS");
-    for (uint64_t q : pos) aligned = aligned && (q & 15) == 0;
+    for (uint32_t q = 0; q < cnt && aligned; q++) aligned = (pos[q] & 15) == 0;
     if (aligned) ea.flags |= ENC_IN_ALIGNED;
     if (ent) {   // numpy's p*log2(p) terms for an s-byte chunk (Huffman should_use near 7.0)
         HIPCHK(b.ent.ensure((size_t)(s + 1) * 8));
         HIPCHK(hipMemcpyAsync(b.ent.p, ent, (size_t)(s + 1) * 8, hipMemcpyHostToDevice, st));
         if (s == C) ea.ent_full = b.ent.as<double>();
         else ea.ent_tail = b.ent.as<double>();
+    }
+    if (nsub) {
+        HIPCHK(b.lz4sub.ensure((size_t)cnt * LZ4_SUB_MAX * 4));
+        ea.lz4sub = b.lz4sub.as<uint32_t>();
+        ea.n_subc = nsub;
+        for (uint32_t j = 0; j < nsub; j++) ea.sub_c[j] = subc[j];
     }
     const bool dict = eligible(p, s, AMBC_M_DICT);
     const bool deflate = eligible(p, s, AMBC_M_DEFLATE);
@@ -129,13 +137,16 @@ int launch_batch(Batch& b, hipStream_t st, const uint8_t* d_in, uint64_t n, cons
     if (dict) HIPCHK(launch_dict(ea, std::min<uint32_t>(C, p->pref_max[AMBC_M_DICT]), st));
     if (deflate) {
         HIPCHK((p->flags & AMBC_FLAG_ZLIB9) ? launch_zlib9(ea, st) : launch_deflate(ea, st));
-        EncArgs ep = ea;
-        ep.flags |= ENC_EMIT_PENDING;
-        ep.bestpre = nullptr;
-        HIPCHK(launch_encode(ep, st));
+        if (!eval) {
+            EncArgs ep = ea;
+            ep.flags |= ENC_EMIT_PENDING;
+            ep.bestpre = nullptr;
+            HIPCHK(launch_encode(ep, st));
+        }
     }
     HIPCHK(hipMemcpyAsync(b.hplen, b.plen.p, (size_t)cnt * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(b.hids, b.ids.p, cnt, hipMemcpyDeviceToHost, st));
+    if (nsub) HIPCHK(hipMemcpyAsync(b.hlz, b.lz4sub.p, (size_t)cnt * LZ4_SUB_MAX * 4, hipMemcpyDeviceToHost, st));
     return AMBC_OK;
 }
 
@@ -145,7 +156,50 @@ struct Decision {
     uint8_t id;      // 255: the rest of the input as one raw package
 };
 
-inline uint64_t key(uint64_t pos, uint32_t s) { return pos << 18 | s; }
+// Per walk position (pos = idx * g) and candidate index i: the evaluation of
+// size S_i = min(cands[i], n - pos).  Part "O": the winner of the size's methods
+// other than LZ4 -- or, at the position's LZ4 size M, of all of them; part "L":
+// LZ4's block for S_i < M, from M's launch.  Positions live in pages of 256,
+// allocated when a walk first reaches them.
+struct PosTable {
+    static constexpr uint32_t PB = 8;
+    struct Page {
+        std::vector<uint32_t> plen, lz;
+        std::vector<uint8_t> id;
+        std::vector<uint32_t> have, req;            // bit i: part O of candidate i known / asked for
+        std::vector<uint8_t> mhave, mreq, decided;  // M's launch known / asked for; decision taken
+        std::vector<Decision> dec;
+    };
+    uint64_t g = 1;
+    uint32_t nc = 0;
+    std::vector<std::unique_ptr<Page>> pages;
+    void init(uint64_t n, uint64_t g_, uint32_t nc_) {
+        g = g_;
+        nc = nc_;
+        pages.clear();
+        pages.resize((size_t)((n / g >> PB) + 1));
+    }
+    // (page, slot) of position pos, the page created on first use
+    Page& at(uint64_t pos, uint32_t& slot) {
+        const uint64_t x = pos / g;
+        slot = (uint32_t)(x & ((1u << PB) - 1));
+        std::unique_ptr<Page>& pg = pages[(size_t)(x >> PB)];
+        if (!pg) {
+            pg.reset(new Page);
+            const size_t m = (size_t)1 << PB;
+            pg->plen.assign(m * nc, 0);
+            pg->lz.assign(m * nc, 0xFFFFFFFFu);
+            pg->id.assign(m * nc, 255);
+            pg->have.assign(m, 0);
+            pg->req.assign(m, 0);
+            pg->mhave.assign(m, 0);
+            pg->mreq.assign(m, 0);
+            pg->decided.assign(m, 0);
+            pg->dec.assign(m, Decision{0, 0, 0});
+        }
+        return *pg;
+    }
+};
 
 }  // namespace
 }  // namespace ambc
@@ -153,17 +207,23 @@ inline uint64_t key(uint64_t pos, uint32_t s) { return pos << 18 | s; }
 using namespace ambc;
 
 extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const ambc_params* p,
-                                       const uint32_t* cands, uint32_t n_cands, const uint32_t* ent_sizes,
+                                       const uint32_t* cands_in, uint32_t n_cands_in, const uint32_t* ent_sizes,
                                        const double* const* ent_tabs, uint32_t n_ent, uint8_t* out,
                                        uint64_t out_cap, uint64_t* out_len, ambc_stats* st) {
-    if (!ctx || ctx->devs.empty() || !p || !out_len || (n && !in) || !cands || !n_cands)
+    if (!ctx || ctx->devs.empty() || !p || !out_len || (n && !in) || !cands_in || !n_cands_in)
         return fail(AMBC_E_INVAL, "bad arguments");
-    for (uint32_t i = 0; i < n_cands; i++)
-        if (cands[i] == 0 || cands[i] > (1u << 17)) return fail(AMBC_E_INVAL, "candidate sizes must be in [1, 131072]");
+    for (uint32_t i = 0; i < n_cands_in; i++)
+        if (cands_in[i] == 0 || cands_in[i] > (1u << 17)) return fail(AMBC_E_INVAL, "candidate sizes must be in [1, 131072]");
     const uint32_t allowed = (1u << AMBC_M_RLE) | (1u << AMBC_M_DICT) | (1u << AMBC_M_HUFFMAN) |
                              (1u << AMBC_M_DELTA) | (1u << AMBC_M_DEFLATE) | (1u << AMBC_M_LZ4);
     if (p->method_mask & ~allowed)
         return fail(AMBC_E_INVAL, "method_mask holds ids without a GPU encoder (allowed: 1, 2, 3, 4, 5, 9)");
+    // a repeated candidate is the same package with the same ratio: never strictly better
+    std::vector<uint32_t> cands;
+    for (uint32_t i = 0; i < n_cands_in; i++)
+        if (std::find(cands.begin(), cands.end(), cands_in[i]) == cands.end()) cands.push_back(cands_in[i]);
+    const uint32_t nc = (uint32_t)cands.size();
+    if (nc > 32) return fail(AMBC_E_INVAL, "at most 32 distinct candidate sizes");
     const uint64_t t0 = now_ns();
     Dev& d = ctx->devs[0];
     HIPCHK(hipSetDevice(d.id));
@@ -177,15 +237,30 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
     };
     // the input, uploaded once (64 bytes of slack for the encoders' padded loads)
     HIPCHK(d.in.ensure(n + 64));
-    if (n) HIPCHK(hipMemcpyAsync(d.in.p, in, n, hipMemcpyHostToDevice, s));
+    if (n >= kStageMin) {
+        int rc = copy_staged(d, d.in.p, in, n, true);
+        if (rc) return rc;
+    } else if (n) {
+        HIPCHK(hipMemcpyAsync(d.in.p, in, n, hipMemcpyHostToDevice, s));
+    }
     HIPCHK(hipMemsetAsync(d.in.as<uint8_t>() + n, 0, 64, s));
     const uint8_t* d_in = d.in.as<uint8_t>();
 
+    // ---- LZ4 shared across sizes: M (the largest LZ4-eligible size at a position)
+    // reports the smaller LZ4-eligible candidates' prefixes (sorted list subc) ----
+    std::vector<uint32_t> subc(cands);
+    std::sort(subc.begin(), subc.end());
+    const bool lzshare = ((p->method_mask >> AMBC_M_LZ4) & 1) && subc.size() <= LZ4_SUB_MAX &&
+                         !getenv("AMBC_MS_NOSHARE");
+    ambc_params po = *p;                       // the other methods (sizes below M)
+    if (lzshare) po.method_mask &= ~(1u << AMBC_M_LZ4);
+    const uint32_t nsub = (uint32_t)subc.size();
+
     // ---- the walks ----
     uint64_t g = 0;
-    for (uint32_t i = 0; i < n_cands; i++) g = std::gcd(g, (uint64_t)cands[i]);
-    std::unordered_map<uint64_t, Eval> cache;          // (pos, s) -> the size's winner
-    std::unordered_map<uint64_t, Decision> dec;        // pos -> the reference's decision there
+    for (uint32_t c : cands) g = std::gcd(g, (uint64_t)c);
+    PosTable T;
+    T.init(n, g, nc);
     struct Walk { uint64_t pos; uint32_t last; };      // last: the size it took the step before
     std::vector<Walk> active;
     // walks: one per 512 KiB, at most 512; speculation: 2 positions ahead (256
@@ -194,8 +269,8 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
     static const uint64_t KMAX_ = getenv("AMBC_MS_WALKS") ? strtoull(getenv("AMBC_MS_WALKS"), nullptr, 10) : 512;
     static const uint64_t SPAN_ = getenv("AMBC_MS_SPAN") ? strtoull(getenv("AMBC_MS_SPAN"), nullptr, 10) : 512 << 10;
     uint32_t max_cand = 0;
-    for (uint32_t i = 0; i < n_cands; i++)
-        if (any_eligible(p, cands[i])) max_cand = std::max(max_cand, cands[i]);
+    for (uint32_t c : cands)
+        if (any_eligible(p, c)) max_cand = std::max(max_cand, c);
     {
         // walk starts on the lattice of the largest eligible size: where that size
         // wins everywhere (homogeneous data) every walk runs on the same lattice
@@ -203,60 +278,137 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
         // phases until they meet
         const uint64_t K = std::max<uint64_t>(1, std::min<uint64_t>(KMAX_, n / std::max<uint64_t>(SPAN_, 1)));
         const uint64_t lat = max_cand ? max_cand : g;
-        std::set<uint64_t> starts;
-        for (uint64_t k = 0; k < K; k++) starts.insert((k * n / K) / lat * lat);
+        std::vector<uint64_t> starts;
+        for (uint64_t k = 0; k < K; k++) starts.push_back((k * n / K) / lat * lat);
+        starts.erase(std::unique(starts.begin(), starts.end()), starts.end());
         if (n)
             for (uint64_t b0 : starts) active.push_back(Walk{b0, max_cand ? max_cand : cands[0]});
     }
     for (auto& x : d.mss)
         if (!x) HIPCHK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
     HIPCHK(hipStreamSynchronize(s));                   // (the input upload)
-    uint32_t steps = 0;
-    uint64_t evaluated = 0;
-    uint64_t kernel_ns = 0;
-    // the (position, size) pairs a decision at pos needs; false when all are known
-    auto needs = [&](uint64_t pos, std::map<uint32_t, std::vector<uint64_t>>* req) -> bool {
-        bool any = false;
+
+    // the sizes at pos: S[i] = min(cands[i], remain); canonical = the first index
+    // of its size; M = the largest LZ4-eligible one (0: none / no sharing)
+    struct Sizes { uint32_t S[32]; uint32_t canon; uint32_t M; };
+    const uint32_t maxc = *std::max_element(cands.begin(), cands.end());
+    Sizes inner;                                       // every position with remain >= maxc
+    bool have_inner = false;
+    uint32_t jsub[32];                                 // subc index of cands[i]
+    for (uint32_t i = 0; i < nc; i++)
+        jsub[i] = (uint32_t)(std::lower_bound(subc.begin(), subc.end(), cands[i]) - subc.begin());
+    auto sizes_at = [&](uint64_t pos, Sizes& z) {
         const uint64_t remain = n - pos;
-        for (uint32_t i = 0; i < n_cands; i++) {
-            const uint32_t sz = (uint32_t)std::min<uint64_t>(cands[i], remain);
-            if (!any_eligible(p, sz)) continue;
-            const uint64_t kk = key(pos, sz);
-            if (cache.count(kk)) continue;
-            any = true;
-            if (req) {
-                cache[kk] = Eval{0, 0xFE};     // requested (filled by the batch)
-                (*req)[sz].push_back(pos);
-            }
+        if (have_inner && remain >= maxc) { z = inner; return; }
+        z.canon = 0;
+        z.M = 0;
+        for (uint32_t i = 0; i < nc; i++) {
+            z.S[i] = (uint32_t)std::min<uint64_t>(cands[i], remain);
+            bool dup = false;
+            for (uint32_t j = 0; j < i && !dup; j++) dup = z.S[j] == z.S[i];
+            if (!dup) z.canon |= 1u << i;
+            if (lzshare && eligible(p, z.S[i], AMBC_M_LZ4)) z.M = std::max(z.M, z.S[i]);
         }
-        return any;
     };
-    // the reference's decision at pos (adaptive_compressor.py:546-590), all sizes known
+    if (n >= maxc) {
+        sizes_at(0, inner);
+        have_inner = true;
+    }
+    // part O of candidate i at a position: needed (not raw by construction)?
+    auto needs_o = [&](const Sizes& z, uint32_t i) {
+        return z.S[i] == z.M ? false : any_eligible(lzshare ? &po : p, z.S[i]);
+    };
+    auto needs_m = [&](const Sizes& z) { return z.M != 0; };
+    auto ready = [&](uint64_t pos) -> bool {
+        Sizes z;
+        sizes_at(pos, z);
+        uint32_t sl;
+        PosTable::Page& pg = T.at(pos, sl);
+        if (needs_m(z) && !pg.mhave[sl]) return false;
+        for (uint32_t i = 0; i < nc; i++)
+            if (((z.canon >> i) & 1) && needs_o(z, i) && !((pg.have[sl] >> i) & 1)) return false;
+        return true;
+    };
+    // the reference's decision at pos (adaptive_compressor.py:546-590), all parts known
     auto decide = [&](uint64_t pos) -> Decision {
+        Sizes z;
+        sizes_at(pos, z);
+        uint32_t sl;
+        PosTable::Page& pg = T.at(pos, sl);
         const uint64_t remain = n - pos;
         double best_ratio = 1.0;
         uint32_t best_s = 0, best_plen = 0;
         uint8_t best_id = 255;
-        std::vector<uint32_t> seen;
-        for (uint32_t i = 0; i < n_cands; i++) {
-            const uint32_t sz = (uint32_t)std::min<uint64_t>(cands[i], remain);
-            // the same clamped size again: same package, same ratio (never strictly better)
-            if (std::find(seen.begin(), seen.end(), sz) != seen.end()) continue;
-            seen.push_back(sz);
+        for (uint32_t i = 0; i < nc; i++) {
+            // (the same clamped size again: same package, same ratio -- never strictly better)
+            if (!((z.canon >> i) & 1)) continue;
+            const uint32_t sz = z.S[i];
             if (!any_eligible(p, sz)) continue;
-            const Eval& e = cache[key(pos, sz)];
-            if (e.id == 255) continue;
-            const double ratio = (double)(e.plen + HDR) / (double)sz;
+            const size_t e = (size_t)sl * nc + i;
+            uint32_t plen = pg.plen[e];
+            uint8_t id = pg.id[e];
+            if (sz != z.M && !needs_o(z, i)) id = 255;            // no other method: raw so far
+            if (lzshare && sz < z.M && eligible(p, sz, AMBC_M_LZ4)) {
+                // id 9 comes last in id order: it wins only strictly below the others
+                const uint32_t lb = pg.lz[e];
+                const uint32_t other = id == 255 ? sz : plen + HDR;
+                if (lb != 0xFFFFFFFFu && (uint64_t)lb + 41 < other) { plen = lb + 23; id = 9; }
+            }
+            if (id == 255) continue;
+            const double ratio = (double)(plen + HDR) / (double)sz;
             if (ratio < best_ratio) {
                 best_ratio = ratio;
                 best_s = sz;
-                best_plen = e.plen;
-                best_id = e.id;
+                best_plen = plen;
+                best_id = id;
             }
         }
         if (best_id == 255) return Decision{(uint32_t)std::min<uint64_t>(remain, 0xFFFFFFFFull), (uint32_t)remain, 255};
         return Decision{best_s, best_plen, best_id};
     };
+    // requests of one round: (size, kind) -> positions; kind 1 = M's launch
+    std::map<std::pair<uint32_t, int>, std::vector<uint64_t>> req;
+    auto request = [&](uint64_t pos) {
+        Sizes z;
+        sizes_at(pos, z);
+        uint32_t sl;
+        PosTable::Page& pg = T.at(pos, sl);
+        if (needs_m(z) && !pg.mhave[sl] && !pg.mreq[sl]) {
+            pg.mreq[sl] = 1;
+            req[{z.M, 1}].push_back(pos);
+        }
+        for (uint32_t i = 0; i < nc; i++) {
+            if (!((z.canon >> i) & 1) || !needs_o(z, i)) continue;
+            if (((pg.have[sl] | pg.req[sl]) >> i) & 1) continue;
+            pg.req[sl] |= 1u << i;
+            req[{z.S[i], 0}].push_back(pos);
+        }
+    };
+    // a batch's results into the table
+    auto fill = [&](const Batch& bb, uint32_t sz, int kind, const std::vector<uint64_t>& poss) {
+        for (size_t q = 0; q < poss.size(); q++) {
+            const uint64_t pos = poss[q];
+            Sizes z;
+            sizes_at(pos, z);
+            uint32_t sl;
+            PosTable::Page& pg = T.at(pos, sl);
+            for (uint32_t i = 0; i < nc; i++) {
+                if (!((z.canon >> i) & 1)) continue;
+                const size_t e = (size_t)sl * nc + i;
+                if (z.S[i] == sz && (kind == 1 || z.S[i] != z.M)) {
+                    pg.plen[e] = bb.hplen[q];
+                    pg.id[e] = bb.hids[q];
+                    pg.have[sl] |= 1u << i;
+                }
+                if (kind == 1 && z.S[i] < z.M) pg.lz[e] = bb.hlz[q * LZ4_SUB_MAX + jsub[i]];   // (S[i] = cands[i])
+            }
+            if (kind == 1) pg.mhave[sl] = 1;
+        }
+    };
+
+    uint32_t steps = 0;
+    uint64_t evaluated = 0;
+    uint64_t kernel_ns = 0;
     // Rounds: every walk decides as far as the known sizes reach; then ONE batch
     // per size evaluates each walk's next position and SPEC positions further
     // along the path it would take if it kept its last step size (a guess: a
@@ -269,12 +421,13 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
         std::vector<Walk> still;
         for (Walk w : active) {
             for (;;) {
-                if (dec.count(w.pos)) break;               // joined a decided path
-                if (needs(w.pos, nullptr)) { still.push_back(w); break; }
+                uint32_t sl;
+                PosTable::Page& pg = T.at(w.pos, sl);
+                if (pg.decided[sl]) break;                 // joined a decided path
+                if (!ready(w.pos)) { still.push_back(w); break; }
                 const Decision dd = decide(w.pos);
-                if (dd.id == 255 && n - w.pos > 0xFFFFFFFFull)
-                    return fail(AMBC_E_RANGE, "raw remainder exceeds a u32 chunk field");
-                dec[w.pos] = dd;
+                pg.decided[sl] = 1;
+                pg.dec[sl] = dd;
                 if (dd.id == 255) break;                   // the rest is raw: done
                 w.last = dd.s;
                 w.pos += dd.s;
@@ -290,42 +443,56 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
         tq = now_ns();
         if (active.empty()) break;
         steps++;
-        std::map<uint32_t, std::vector<uint64_t>> req;
+        req.clear();
         for (const Walk& w : active) {
             uint64_t q = w.pos;
             for (int k = 0; k <= SPEC && q < n; k++, q += w.last) {
-                if (k && dec.count(q)) break;
-                (void)needs(q, &req);
+                if (k) {
+                    uint32_t sl;
+                    if (T.at(q, sl).decided[sl]) break;
+                }
+                request(q);
             }
         }
+        std::vector<std::pair<std::pair<uint32_t, int>, std::vector<uint64_t>>> jobs;
         for (auto& r : req) {
-            int rc = check_size(p, r.first);
-            if (rc) {
+            const ambc_params* pk = r.first.second == 1 || !lzshare ? p : &po;
+            if (int rc = check_size(pk, r.first.first)) {
                 // only an error if a walk itself needs this size (not a speculative position)
                 for (uint64_t q : r.second)
                     if (std::binary_search(active.begin(), active.end(), Walk{q, 0},
                                            [](const Walk& x, const Walk& y) { return x.pos < y.pos; }))
                         return rc;
-            }
-        }
-        const uint64_t tk = now_ns();
-        t_req += tk - tq;
-        std::vector<std::pair<uint32_t, std::vector<uint64_t>>> jobs;
-        for (auto& r : req) {
-            if (check_size(p, r.first)) {       // speculative only: never decided from
-                for (uint64_t q : r.second) cache.erase(key(q, r.first));
+                // speculative only: never decided from -- forget the requests
+                for (uint64_t q : r.second) {
+                    Sizes z;
+                    sizes_at(q, z);
+                    uint32_t sl;
+                    PosTable::Page& pg = T.at(q, sl);
+                    if (r.first.second == 1) pg.mreq[sl] = 0;
+                    for (uint32_t i = 0; i < nc; i++)
+                        if (z.S[i] == r.first.first) pg.req[sl] &= ~(1u << i);
+                }
                 continue;
             }
             jobs.emplace_back(r.first, std::move(r.second));
         }
-        // up to 8 size classes at once, each on its own stream and batch buffers
-        // (the 64 KiB class runs at 2 workgroups per CU: the small ones fill in)
+        const uint64_t tk = now_ns();
+        t_req += tk - tq;
+        // up to 8 batches at once, each on its own stream and batch buffers
+        // (the 64 KiB class runs at 20 workgroups per CU in place: the small ones fill in)
         for (size_t j0 = 0; j0 < jobs.size(); j0 += 8) {
             const size_t j1 = std::min(jobs.size(), j0 + 8);
             uint64_t tl = now_ns();
             for (size_t j = j0; j < j1; j++) {
-                int rc = launch_batch(d.msb[j - j0], d.mss[j - j0], d_in, n, p, jobs[j].first, jobs[j].second,
-                                      ent_of(jobs[j].first));
+                Batch& bb = d.msb[j - j0];
+                const auto& jb = jobs[j];
+                const uint32_t cnt = (uint32_t)jb.second.size();
+                HIPCHK(bb.host_ensure(cnt));
+                std::memcpy(bb.hpos, jb.second.data(), (size_t)cnt * 8);
+                const bool mk = jb.first.second == 1;
+                int rc = launch_batch(bb, d.mss[j - j0], d_in, n, mk || !lzshare ? p : &po, jb.first.first, bb.hpos,
+                                      cnt, ent_of(jb.first.first), true, mk ? subc.data() : nullptr, mk ? nsub : 0);
                 if (rc) return rc;
             }
             t_launch += now_ns() - tl;
@@ -334,9 +501,7 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
                 HIPCHK(hipStreamSynchronize(d.mss[j - j0]));
                 t_wait += now_ns() - tl;
                 tl = now_ns();
-                const Batch& bb = d.msb[j - j0];
-                for (size_t q = 0; q < jobs[j].second.size(); q++)
-                    cache[key(jobs[j].second[q], jobs[j].first)] = Eval{bb.hplen[q], bb.hids[q]};
+                fill(d.msb[j - j0], jobs[j].first.first, jobs[j].first.second, jobs[j].second);
                 evaluated += jobs[j].second.size();
                 t_fill += now_ns() - tl;
             }
@@ -352,18 +517,23 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
     std::vector<Pkg> path;
     uint64_t body = 0;
     for (uint64_t pos = 0; pos < n;) {
-        auto it = dec.find(pos);
-        if (it == dec.end()) return fail(AMBC_E_DEVICE, "multi-size walk: undecided position on the path");
-        const Decision& dd = it->second;
+        uint32_t sl;
+        PosTable::Page& pg = T.at(pos, sl);
+        if (!pg.decided[sl]) return fail(AMBC_E_DEVICE, "multi-size walk: undecided position on the path");
+        const Decision& dd = pg.dec[sl];
+        if (dd.id == 255 && n - pos > 0xFFFFFFFFull)
+            return fail(AMBC_E_RANGE, "raw remainder exceeds a u32 chunk field");
         path.push_back(Pkg{pos, dd.s, dd.plen, dd.id, body});
         body += HDR + (uint64_t)dd.plen;
         if (dd.id == 255) break;
         pos += dd.s;
     }
     body += END_CHUNK;
-    if (out_cap < body) return fail(AMBC_E_CAPACITY, "output capacity below the body size");
+    T.pages.clear();
+    d.ms_body = 0;
+    if (out && out_cap < body) return fail(AMBC_E_CAPACITY, "output capacity below the body size");
 
-    // ---- the chosen chunks, encoded again per size, into the body ----
+    // ---- the chosen chunks, encoded again per size (all methods, bytes), into the body ----
     HIPCHK(d.out.ensure(body + 64));
     uint8_t* d_body = d.out.as<uint8_t>();
     const uint64_t te = now_ns();
@@ -378,22 +548,23 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
             const uint32_t sz = gl[j].first;
             Batch& bb = d.msb[j - j0];
             hipStream_t xs = d.mss[j - j0];
-            std::vector<uint64_t> pos;
-            for (size_t i : gl[j].second) {
-                pos.push_back(path[i].pos);
-                offs[j - j0].push_back(path[i].off);
+            const uint32_t cnt = (uint32_t)gl[j].second.size();
+            HIPCHK(bb.host_ensure(cnt));
+            for (uint32_t q = 0; q < cnt; q++) {
+                bb.hpos[q] = path[gl[j].second[q]].pos;
+                offs[j - j0].push_back(path[gl[j].second[q]].off);
             }
-            int rc = launch_batch(bb, xs, d_in, n, p, sz, pos, ent_of(sz));
+            int rc = launch_batch(bb, xs, d_in, n, p, sz, bb.hpos, cnt, ent_of(sz), false);
             if (rc) return rc;
-            HIPCHK(bb.off.ensure(pos.size() * 8));
-            HIPCHK(hipMemcpyAsync(bb.off.p, offs[j - j0].data(), pos.size() * 8, hipMemcpyHostToDevice, xs));
+            HIPCHK(bb.off.ensure((size_t)cnt * 8));
+            HIPCHK(hipMemcpyAsync(bb.off.p, offs[j - j0].data(), (size_t)cnt * 8, hipMemcpyHostToDevice, xs));
             CompactArgs ca{};
             ca.slots = bb.slots.as<uint8_t>();
             ca.slot_stride = slot_stride_for((sz + 15) & ~15u);
             ca.plen = bb.plen.as<uint32_t>();
             ca.ids = bb.ids.as<uint8_t>();
             ca.off = bb.off.as<uint64_t>();
-            ca.n_chunks = (uint32_t)pos.size();
+            ca.n_chunks = cnt;
             ca.clen = bb.clen.as<uint32_t>();
             ca.n_total = n;
             ca.chunk_size = (sz + 15) & ~15u;
@@ -422,16 +593,24 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
         HIPCHK(launch_copy(d_body + pk.off + HDR, d_in + pk.pos, pk.s, s));
     }
     HIPCHK(launch_end_chunk(d_body + body - END_CHUNK, s));
-    HIPCHK(hipMemcpyAsync(out, d_body, body, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    kernel_ns += now_ns() - te;
+    const uint64_t tc = now_ns();
+    kernel_ns += tc - te;
+    if (!out) {
+        d.ms_body = body;                       // (ambc_fetch_body)
+    } else if (body >= kStageMin) {
+        int rc = copy_staged(d, out, d_body, body, false);
+        if (rc) return rc;
+    } else {
+        HIPCHK(hipMemcpy(out, d_body, body, hipMemcpyDeviceToHost));
+    }
     *out_len = body;
     d.ms_steps = steps;
     d.ms_evaluated = evaluated;
     d.ms_walk_ns = t_walk;
     d.ms_emit_ns = now_ns() - te;
-    TRACE("multisize n=%llu steps=%u evaluated=%llu path=%zu", (unsigned long long)n, steps,
-          (unsigned long long)evaluated, path.size());
+    TRACE("multisize n=%llu steps=%u evaluated=%llu path=%zu emit %.2f ms (copy back %.2f)", (unsigned long long)n,
+          steps, (unsigned long long)evaluated, path.size(), (now_ns() - te) / 1e6, (now_ns() - tc) / 1e6);
     if (st) {
         std::memset(st, 0, sizeof *st);
         for (const Pkg& pk : path) {
@@ -446,6 +625,19 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
         st->kernel_ns = kernel_ns;
         st->total_ns = now_ns() - t0;
     }
+    return AMBC_OK;
+}
+
+extern "C" int ambc_fetch_body(ambc_ctx* ctx, uint8_t* out, uint64_t cap) {
+    if (!ctx || ctx->devs.empty() || !out) return fail(AMBC_E_INVAL, "bad arguments");
+    Dev& d = ctx->devs[0];
+    if (!d.ms_body) return fail(AMBC_E_INVAL, "no body kept on the device");
+    if (cap < d.ms_body) return fail(AMBC_E_CAPACITY, "output capacity below the body size");
+    HIPCHK(hipSetDevice(d.id));
+    const uint64_t body = d.ms_body;
+    d.ms_body = 0;
+    if (body >= kStageMin) return copy_staged(d, out, d.out.p, body, false);
+    HIPCHK(hipMemcpy(out, d.out.p, body, hipMemcpyDeviceToHost));
     return AMBC_OK;
 }
 

@@ -133,11 +133,16 @@ int ambc_compress_batch(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const ambc
  * chunk sizes Huffman may take (see ambc_params.ent_full).  Writes the .ambc
  * body (packages + end chunk); AMBC_E_INVAL when a size the walk needs has an
  * eligible method the GPU encoders do not take at that size (Dictionary > 8192,
- * any > 65536), AMBC_E_RANGE for a raw remainder > 4 GiB. */
+ * any > 65536), AMBC_E_RANGE for a raw remainder > 4 GiB.  out == NULL: the
+ * body stays on the device, *out_len gives its size, and ambc_fetch_body copies
+ * it out (a caller can then allocate exactly the body's size). */
 int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const ambc_params* p,
                             const uint32_t* cands, uint32_t n_cands, const uint32_t* ent_sizes,
                             const double* const* ent_tabs, uint32_t n_ent, uint8_t* out,
                             uint64_t out_cap, uint64_t* out_len, ambc_stats* st);
+/* the body the last ambc_compress_multisize(out = NULL) left on the device into
+ * out (cap >= its size); AMBC_E_INVAL when there is none */
+int ambc_fetch_body(ambc_ctx* ctx, uint8_t* out, uint64_t cap);
 /* of the last ambc_compress_multisize: batched evaluation rounds, chunk encodes,
  * wall time of the walks and of the final encode + body assembly */
 int ambc_last_multisize_info(ambc_ctx* ctx, uint32_t* steps, uint64_t* evaluated, uint64_t* walk_ns,

@@ -736,6 +736,44 @@ def test_multisize_many_walks_match_oracle(ctx):
         assert comp._adaptive_decompress(body, len(data)) == data
 
 
+def _lz4_prefix_inputs():
+    """Inputs whose LZ4 parses cross the candidate prefixes in every way: long
+    matches over several prefix ends at once (zero runs), short periods (matches
+    everywhere, some ending by b - 5 exactly), incompressible stretches (the
+    chunk's own LZ4 gives up while its prefixes are still open), text."""
+    rnd = random.Random(99)
+    text = synth.generate(90000, 61)
+    per = bytes(rnd.randrange(256) for _ in range(37)) * 2500
+    noise = bytes(rnd.randrange(256) for _ in range(70000))
+    return [bytes(5000) + text[:60000],
+            per[:80000],
+            noise[:40000] + bytes(30000) + text[:20000],
+            text[:1000] + bytes(1019) + text[:70000],
+            b"".join(bytes([rnd.randrange(4)]) * rnd.randrange(1, 2000) for _ in range(200))[:150000],
+            noise[:65536 + 4096 + 11]]
+
+
+@pytest.mark.parametrize("cands", [REF_CANDS, [65536, 3072, 1024], [6144, 2048, 1536, 1024],
+                                   [16384, 1024, 8192, 4096]])
+def test_multisize_lz4_shared_prefixes(ctx, cands, monkeypatch):
+    """One LZ4 parse per position serves every candidate size (k_encode's lz4sub):
+    the bodies equal the oracle's walk and the walk without the sharing
+    (AMBC_MS_NOSHARE) at every input and candidate list."""
+    for data in _lz4_prefix_inputs():
+        for methods in ((1, 3, 4, 9), (9,), (1, 2, 3, 4, 5, 9)):
+            comp = _compressor(methods=methods)
+            comp.CHUNK_SIZE_CANDIDATES = list(cands)
+            monkeypatch.delenv("AMBC_MS_NOSHARE", raising=False)
+            body = comp._adaptive_compress(data)
+            ref, st = orc.compress_body_multisize(data, cands, tuple(methods) + (255,))
+            assert body == ref, (methods, cands, len(data))
+            assert comp.chunk_stats["total_chunks"] == st["total_chunks"]
+            monkeypatch.setenv("AMBC_MS_NOSHARE", "1")
+            assert comp._adaptive_compress(data) == ref
+            monkeypatch.delenv("AMBC_MS_NOSHARE")
+            assert comp._adaptive_decompress(body, len(data)) == data
+
+
 def test_like_reference_and_defaults_warning(ctx):
     """AdaptiveCompressor.like_reference(): the reference's 8-candidate walk with
     its GPU-encodable stdlib codecs, body equal to the oracle's walk; an instance
