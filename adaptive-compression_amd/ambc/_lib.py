@@ -46,7 +46,7 @@ EXPORTS = (
     "ambc_comm_allreduce_u64", "ambc_comm_allgather_u64", "ambc_comm_gather", "ambc_shard_range",
     "ambc_compress_shard", "ambc_decompress_shard", "ambc_decompress_multi",
     "ambc_synth_device_range", "ambc_device_equal", "ambc_compress_multisize",
-    "ambc_last_multisize_info", "ambc_fetch_body", "ambc_debug_walk",
+    "ambc_last_multisize_info", "ambc_fetch_body", "ambc_compress_multisize_ex", "ambc_debug_walk",
 )
 
 
@@ -144,6 +144,9 @@ def _declare(lib):
                                      C.POINTER(Stats)], i32),
         "ambc_last_multisize_info": ([vp, C.POINTER(u32), C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)], i32),
         "ambc_fetch_body": ([vp, u8p, u64], i32),
+        "ambc_compress_multisize_ex": ([vp, u8p, u64, C.POINTER(Params), C.POINTER(u32), u32, C.POINTER(u32),
+                                        C.POINTER(C.c_void_p), u32, vp, u8p, u64, C.POINTER(u64),
+                                        C.POINTER(Stats)], i32),
         "ambc_debug_walk": ([u8p, u64, u64, u32, C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)], i32),
     }
     for name, (args, res) in sig.items():

@@ -49,8 +49,8 @@ from .container import (FORMAT_VERSION, MAGIC_NUMBER, MARKER_BYTES, MARKER_LENGT
                         build_header, marker_bytes_aligned, parse_header,
                         update_compressed_size)
 from .methods import DECODE_METHODS, GPU_METHODS, NoCompression
-from .registry import (DEFAULT_CHUNK_SIZE, DEFAULT_METHODS, HOST_LIBRARY_IDS, METHOD_CHUNK_PREFS,
-                       METHOD_NAMES, REFERENCE_CHUNK_SIZE_CANDIDATES, method_mask)
+from .registry import (DEFAULT_CHUNK_SIZE, DEFAULT_METHODS, HOST_LIBRARY_IDS, HOST_SCORED_IDS,
+                       METHOD_CHUNK_PREFS, METHOD_NAMES, REFERENCE_CHUNK_SIZE_CANDIDATES, method_mask)
 
 _TERMS = {}
 
@@ -113,8 +113,10 @@ class AdaptiveCompressor:
         if chunk_size is not None:
             self.CHUNK_SIZE_CANDIDATES = [int(chunk_size)]
         ids = tuple(DEFAULT_METHODS if methods is None else [m for m in methods if m != 255])
-        method_mask(ids)                    # validates: GPU encoders only
-        self.compression_methods = [GPU_METHODS[i]() for i in sorted(set(ids))] + [NoCompression()]
+        # validates: GPU encoders, plus the host-scored bz2 / lzma (ids 6 / 7)
+        method_mask([i for i in ids if i not in HOST_SCORED_IDS])
+        self.compression_methods = [(GPU_METHODS.get(i) or DECODE_METHODS[i])() for i in sorted(set(ids))]
+        self.compression_methods.append(NoCompression())
         # decode side: every id the reference registers here (+ LZ4, which it
         # registers when python-lz4 is installed)
         self.method_lookup = {i: cls() for i, cls in DECODE_METHODS.items()}
@@ -126,14 +128,18 @@ class AdaptiveCompressor:
         self.chunk_stats = None
 
     @classmethod
-    def like_reference(cls, **kw):
+    def like_reference(cls, full_set=False, **kw):
         """The closest GPU configuration to the reference's ``AdaptiveCompressor()``
         (adaptive_compressor.py:61-62,64-178): its 8-candidate walk, reference mode,
         and its stdlib codecs that have GPU encoders -- RLE, Dictionary, Huffman,
-        Delta and DEFLATE as zlib.compress(data, 9)'s own bytes at every size (ids
-        6/7, bz2/lzma, have no GPU encoder: files where the reference would pick
-        them differ; every package stays decodable by it)."""
-        comp = cls(mode="reference", methods=(1, 2, 3, 4, 5), **kw)
+        Delta and DEFLATE as zlib.compress(data, 9)'s own bytes at every size.
+        full_set=True adds BZIP2 and LZMA (ids 6 / 7, no GPU encoder), scored on
+        host threads beside the device's encoders: the reference's whole default
+        method set, byte for byte (slow where the reference is: bz2 / lzma on
+        every candidate chunk).  Without them, files where the reference would
+        pick 6 / 7 differ; every package stays decodable by it."""
+        ids = (1, 2, 3, 4, 5, 6, 7) if full_set else (1, 2, 3, 4, 5)
+        comp = cls(mode="reference", methods=ids, **kw)
         comp.CHUNK_SIZE_CANDIDATES = list(REFERENCE_CHUNK_SIZE_CANDIDATES)
         return comp
 
@@ -196,7 +202,7 @@ class AdaptiveCompressor:
         p.chunk_size = C_
         p.mode = _lib.MODE_REFERENCE if self.mode == "reference" else _lib.MODE_NATIVE
         p.flags = _lib.FLAG_ZLIB9 if self.deflate == "zlib9" else 0
-        p.method_mask = method_mask([m.type_id for m in self.compression_methods])
+        p.method_mask = method_mask(self._gpu_ids())
         for i in range(16):
             lo, hi = self.method_chunk_prefs.get(i, (1, 0))
             p.pref_min[i], p.pref_max[i] = max(0, lo), min(hi, 0xFFFFFFFF)
@@ -209,6 +215,13 @@ class AdaptiveCompressor:
 
     def _ctx(self):
         return _lib.default_context(self.devices)
+
+    def _gpu_ids(self):
+        return [m.type_id for m in self.compression_methods
+                if m.type_id != 255 and m.type_id not in HOST_SCORED_IDS]
+
+    def _host_methods(self):
+        return [m for m in self.compression_methods if m.type_id in HOST_SCORED_IDS]
 
     def _adaptive_compress_multisize(self, file_data):
         """_adaptive_compress (adaptive_compressor.py:363-394) with several
@@ -223,7 +236,7 @@ class AdaptiveCompressor:
         cands = [int(c) for c in self.CHUNK_SIZE_CANDIDATES]
         p = _lib.Params()
         p.flags = _lib.FLAG_ZLIB9 if self.deflate == "zlib9" else 0
-        p.method_mask = method_mask([m.type_id for m in self.compression_methods])
+        p.method_mask = method_mask(self._gpu_ids())
         for i in range(16):
             lo, hi = self.method_chunk_prefs.get(i, (1, 0))
             p.pref_min[i], p.pref_max[i] = max(0, lo), min(hi, 0xFFFFFFFF)
@@ -231,7 +244,7 @@ class AdaptiveCompressor:
         # the candidates and the remainders n - k*g (g = gcd: every position)
         lo3, hi3 = self.method_chunk_prefs.get(3, (1, 0))
         sizes = set()
-        if 3 in [m.type_id for m in self.compression_methods]:
+        if 3 in self._gpu_ids():
             g = math.gcd(*cands)
             sizes = {c for c in cands if lo3 <= c <= hi3}
             k0, k1 = max(0, -(-(n - hi3) // g)), (n - lo3) // g if n >= lo3 else -1
@@ -243,11 +256,24 @@ class AdaptiveCompressor:
         olen = C.c_uint64()
         st = _lib.Stats()
         src = file_data if isinstance(file_data, (bytes, bytearray)) else bytes(file_data)
+        # ids 6 / 7: host-scored beside the device (hostcodecs.py)
+        host = None
+        if self._host_methods():
+            from .hostcodecs import HostScorer
+            host = HostScorer(src, self._host_methods(), self.method_chunk_prefs)
         # out = NULL: the body stays on the device until it is fetched into a
         # bytes object of exactly its size (see _adaptive_decompress for why
         # writing into a fresh, private bytes object is sound)
-        rc = ctx.lib.ambc_compress_multisize(ctx.h, _lib.addr(src), n, C.byref(p), carr, len(cands), ent_sizes,
-                                             ent_ptrs, len(tabs), None, 0, C.byref(olen), C.byref(st))
+        try:
+            rc = ctx.lib.ambc_compress_multisize_ex(ctx.h, _lib.addr(src), n, C.byref(p), carr, len(cands),
+                                                    ent_sizes, ent_ptrs, len(tabs),
+                                                    C.addressof(host.struct) if host else None, None, 0,
+                                                    C.byref(olen), C.byref(st))
+        finally:
+            if host:
+                host.close()
+        if host and host.error is not None:
+            raise host.error
         if rc == _lib.AMBC_E_RANGE:
             raise struct.error("argument out of range")
         if rc == _lib.AMBC_E_INVAL:
@@ -274,6 +300,12 @@ class AdaptiveCompressor:
         """One C-ABI call: input bytes -> .ambc body (packages + end chunk)."""
         self._note_defaults()
         if len(self.CHUNK_SIZE_CANDIDATES) != 1:
+            return self._adaptive_compress_multisize(file_data)
+        if self._host_methods():
+            # host-scored ids: the reference loop with one candidate (reference mode)
+            if self.mode != "reference":
+                raise NotImplementedError("host-scored ids 6 / 7 (bz2 / lzma) need mode='reference' "
+                                          "or several CHUNK_SIZE_CANDIDATES")
             return self._adaptive_compress_multisize(file_data)
         n = len(file_data)
         p, keep = self._params(n)

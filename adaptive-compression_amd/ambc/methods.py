@@ -25,6 +25,8 @@ import struct
 import zlib
 from abc import ABC, abstractmethod
 
+import numpy as np
+
 from . import _lib
 from .container import MARKER_BYTES
 
@@ -229,9 +231,21 @@ class NoCompression(CompressionMethod):
         return bytes(data[:original_length])
 
 
-# ---- the reference's stdlib library wrappers (decode of ids 5/6/7) -----------
+# ---- the reference's stdlib library wrappers (decode of ids 5/6/7; ids 6/7 --
+# bz2 / lzma, no GPU encoder -- also host-scored in the walk, hostcodecs.py) ----
 def _fit(b, n):
     return b[:n] if len(b) > n else b + bytes(n - len(b))
+
+
+def calculate_entropy(data):
+    """advanced_compression.py:48-57: numpy's Shannon entropy of the byte counts,
+    in the same order of operations (the should_use gates compare it with 7.7 / 8.0)."""
+    if not data:
+        return 0.0
+    counts = np.bincount(np.frombuffer(bytes(data), dtype=np.uint8), minlength=256)
+    probs = counts / len(data)
+    probs = probs[probs > 0]
+    return -np.sum(probs * np.log2(probs))
 
 
 class DeflateCompression(CompressionMethod):
@@ -257,6 +271,10 @@ class Bzip2Compression(CompressionMethod):
     def compress(self, data, level=9):
         return bz2.compress(data, compresslevel=level) if data else b""
 
+    def should_use(self, data, threshold=0.9):
+        # advanced_compression.py:139-150
+        return len(data) >= 1024 and calculate_entropy(data) < 7.7
+
     def decompress(self, data, original_length):
         if not data:
             return b""
@@ -276,6 +294,10 @@ class LZMACompression(CompressionMethod):
         c = lzma.LZMACompressor(format=lzma.FORMAT_XZ, check=lzma.CHECK_CRC64,
                                 filters=[{"id": lzma.FILTER_LZMA2, "dict_size": 1 << 24}])
         return c.compress(data) + c.flush()
+
+    def should_use(self, data, threshold=0.9):
+        # advanced_compression.py:202-213
+        return len(data) >= 8192 and calculate_entropy(data) < 8.0
 
     def decompress(self, data, original_length):
         if not data:

@@ -29,6 +29,10 @@ DEVICE_DECODE_IDS = (1, 2, 3, 4, 9, 255)
 # decode side id 5 is inflated on the GPU (k_decode_inflate), ids 6 / 7 by the
 # reference's stdlib wrappers on the host
 HOST_LIBRARY_IDS = (5, 6, 7)
+# ids the walk scores on the host (the reference's bz2 / lzma wrappers, no GPU
+# encoder): AdaptiveCompressor(methods=(..., 6, 7)) in reference mode or with
+# several CHUNK_SIZE_CANDIDATES -- see hostcodecs.py
+HOST_SCORED_IDS = (6, 7)
 DEFAULT_METHODS = (1, 3, 4, 9)         # + 255 always
 DEFAULT_CHUNK_SIZE = 4096
 

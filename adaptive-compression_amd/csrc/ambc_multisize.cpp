@@ -154,6 +154,7 @@ struct Decision {
     uint32_t s;      // chunk size taken at this position (the remainder when raw)
     uint32_t plen;
     uint8_t id;      // 255: the rest of the input as one raw package
+    uint8_t host;    // the package comes from a host-scored method (ambc_host_codecs)
 };
 
 // Per walk position (pos = idx * g) and candidate index i: the evaluation of
@@ -164,9 +165,10 @@ struct Decision {
 struct PosTable {
     static constexpr uint32_t PB = 8;
     struct Page {
-        std::vector<uint32_t> plen, lz;
-        std::vector<uint8_t> id;
+        std::vector<uint32_t> plen, lz, hlen;
+        std::vector<uint8_t> id, hid;               // (hid / hlen: the host codecs' winner, 0: none)
         std::vector<uint32_t> have, req;            // bit i: part O of candidate i known / asked for
+        std::vector<uint32_t> hhave, hreq;          //   ... the host part of candidate i
         std::vector<uint8_t> mhave, mreq, decided;  // M's launch known / asked for; decision taken
         std::vector<Decision> dec;
     };
@@ -190,12 +192,16 @@ struct PosTable {
             pg->plen.assign(m * nc, 0);
             pg->lz.assign(m * nc, 0xFFFFFFFFu);
             pg->id.assign(m * nc, 255);
+            pg->hlen.assign(m * nc, 0);
+            pg->hid.assign(m * nc, 0);
+            pg->hhave.assign(m, 0);
+            pg->hreq.assign(m, 0);
             pg->have.assign(m, 0);
             pg->req.assign(m, 0);
             pg->mhave.assign(m, 0);
             pg->mreq.assign(m, 0);
             pg->decided.assign(m, 0);
-            pg->dec.assign(m, Decision{0, 0, 0});
+            pg->dec.assign(m, Decision{0, 0, 0, 0});
         }
         return *pg;
     }
@@ -207,9 +213,18 @@ struct PosTable {
 using namespace ambc;
 
 extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const ambc_params* p,
-                                       const uint32_t* cands_in, uint32_t n_cands_in, const uint32_t* ent_sizes,
+                                       const uint32_t* cands, uint32_t n_cands, const uint32_t* ent_sizes,
                                        const double* const* ent_tabs, uint32_t n_ent, uint8_t* out,
                                        uint64_t out_cap, uint64_t* out_len, ambc_stats* st) {
+    return ambc_compress_multisize_ex(ctx, in, n, p, cands, n_cands, ent_sizes, ent_tabs, n_ent, nullptr, out, out_cap,
+                                      out_len, st);
+}
+
+extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const ambc_params* p,
+                                          const uint32_t* cands_in, uint32_t n_cands_in, const uint32_t* ent_sizes,
+                                          const double* const* ent_tabs, uint32_t n_ent, const ambc_host_codecs* hc,
+                                          uint8_t* out, uint64_t out_cap, uint64_t* out_len, ambc_stats* st) {
+    if (hc && (!hc->eval || !hc->emit)) hc = nullptr;
     if (!ctx || ctx->devs.empty() || !p || !out_len || (n && !in) || !cands_in || !n_cands_in)
         return fail(AMBC_E_INVAL, "bad arguments");
     for (uint32_t i = 0; i < n_cands_in; i++)
@@ -270,7 +285,7 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
     static const uint64_t SPAN_ = getenv("AMBC_MS_SPAN") ? strtoull(getenv("AMBC_MS_SPAN"), nullptr, 10) : 512 << 10;
     uint32_t max_cand = 0;
     for (uint32_t c : cands)
-        if (any_eligible(p, c)) max_cand = std::max(max_cand, c);
+        if (hc || any_eligible(p, c)) max_cand = std::max(max_cand, c);
     {
         // walk starts on the lattice of the largest eligible size: where that size
         // wins everywhere (homogeneous data) every walk runs on the same lattice
@@ -327,6 +342,7 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
         if (needs_m(z) && !pg.mhave[sl]) return false;
         for (uint32_t i = 0; i < nc; i++)
             if (((z.canon >> i) & 1) && needs_o(z, i) && !((pg.have[sl] >> i) & 1)) return false;
+        if (hc && (pg.hhave[sl] & z.canon) != z.canon) return false;
         return true;
     };
     // the reference's decision at pos (adaptive_compressor.py:546-590), all parts known
@@ -338,21 +354,28 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
         const uint64_t remain = n - pos;
         double best_ratio = 1.0;
         uint32_t best_s = 0, best_plen = 0;
-        uint8_t best_id = 255;
+        uint8_t best_id = 255, best_host = 0;
         for (uint32_t i = 0; i < nc; i++) {
             // (the same clamped size again: same package, same ratio -- never strictly better)
             if (!((z.canon >> i) & 1)) continue;
             const uint32_t sz = z.S[i];
-            if (!any_eligible(p, sz)) continue;
+            if (!hc && !any_eligible(p, sz)) continue;
             const size_t e = (size_t)sl * nc + i;
             uint32_t plen = pg.plen[e];
             uint8_t id = pg.id[e];
+            uint8_t host = 0;
             if (sz != z.M && !needs_o(z, i)) id = 255;            // no other method: raw so far
             if (lzshare && sz < z.M && eligible(p, sz, AMBC_M_LZ4)) {
                 // id 9 comes last in id order: it wins only strictly below the others
                 const uint32_t lb = pg.lz[e];
                 const uint32_t other = id == 255 ? sz : plen + HDR;
                 if (lb != 0xFFFFFFFFu && (uint64_t)lb + 41 < other) { plen = lb + 23; id = 9; }
+            }
+            if (hc && pg.hid[e] && pg.hlen[e] + HDR < sz) {
+                // the host codecs' winner joins in id order: smaller len, or a tie with a higher id
+                const uint32_t hl = pg.hlen[e];
+                const uint8_t hi = pg.hid[e];
+                if (id == 255 || hl < plen || (hl == plen && hi < id)) { plen = hl; id = hi; host = 1; }
             }
             if (id == 255) continue;
             const double ratio = (double)(plen + HDR) / (double)sz;
@@ -361,11 +384,16 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
                 best_s = sz;
                 best_plen = plen;
                 best_id = id;
+                best_host = host;
             }
         }
-        if (best_id == 255) return Decision{(uint32_t)std::min<uint64_t>(remain, 0xFFFFFFFFull), (uint32_t)remain, 255};
-        return Decision{best_s, best_plen, best_id};
+        if (best_id == 255)
+            return Decision{(uint32_t)std::min<uint64_t>(remain, 0xFFFFFFFFull), (uint32_t)remain, 255, 0};
+        return Decision{best_s, best_plen, best_id, best_host};
     };
+    // host-codec requests of one round: (position, size), and where they go
+    std::vector<uint64_t> hpos;
+    std::vector<uint32_t> hsize;
     // requests of one round: (size, kind) -> positions; kind 1 = M's launch
     std::map<std::pair<uint32_t, int>, std::vector<uint64_t>> req;
     auto request = [&](uint64_t pos) {
@@ -378,11 +406,45 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
             req[{z.M, 1}].push_back(pos);
         }
         for (uint32_t i = 0; i < nc; i++) {
-            if (!((z.canon >> i) & 1) || !needs_o(z, i)) continue;
+            if (!((z.canon >> i) & 1)) continue;
+            if (hc && !(((pg.hhave[sl] | pg.hreq[sl]) >> i) & 1)) {
+                pg.hreq[sl] |= 1u << i;
+                hpos.push_back(pos);
+                hsize.push_back(z.S[i]);
+            }
+            if (!needs_o(z, i)) continue;
             if (((pg.have[sl] | pg.req[sl]) >> i) & 1) continue;
             pg.req[sl] |= 1u << i;
             req[{z.S[i], 0}].push_back(pos);
         }
+    };
+    // the host codecs' answers for the round's pairs into the table
+    std::vector<uint8_t> hid_out;
+    std::vector<uint32_t> hlen_out;
+    uint64_t t_host = 0;
+    auto host_round = [&]() -> int {
+        if (!hc || hpos.empty()) return AMBC_OK;
+        const uint64_t th = now_ns();
+        hid_out.assign(hpos.size(), 0);
+        hlen_out.assign(hpos.size(), 0);
+        if (hc->eval(hc->user, hpos.data(), hsize.data(), (uint32_t)hpos.size(), hid_out.data(), hlen_out.data()))
+            return fail(AMBC_E_CODEC, "host codec evaluation failed");
+        for (size_t q = 0; q < hpos.size(); q++) {
+            Sizes z;
+            sizes_at(hpos[q], z);
+            uint32_t sl;
+            PosTable::Page& pg = T.at(hpos[q], sl);
+            for (uint32_t i = 0; i < nc; i++)
+                if (((z.canon >> i) & 1) && z.S[i] == hsize[q]) {
+                    pg.hid[(size_t)sl * nc + i] = hid_out[q];
+                    pg.hlen[(size_t)sl * nc + i] = hlen_out[q];
+                    pg.hhave[sl] |= 1u << i;
+                }
+        }
+        hpos.clear();
+        hsize.clear();
+        t_host += now_ns() - th;
+        return AMBC_OK;
     };
     // a batch's results into the table
     auto fill = [&](const Batch& bb, uint32_t sz, int kind, const std::vector<uint64_t>& poss) {
@@ -444,6 +506,8 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
         if (active.empty()) break;
         steps++;
         req.clear();
+        hpos.clear();
+        hsize.clear();
         for (const Walk& w : active) {
             uint64_t q = w.pos;
             for (int k = 0; k <= SPEC && q < n; k++, q += w.last) {
@@ -496,6 +560,10 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
                 if (rc) return rc;
             }
             t_launch += now_ns() - tl;
+            if (j0 == 0) {                       // the host codecs while the device works
+                int rc = host_round();
+                if (rc) return rc;
+            }
             for (size_t j = j0; j < j1; j++) {
                 tl = now_ns();
                 HIPCHK(hipStreamSynchronize(d.mss[j - j0]));
@@ -506,14 +574,18 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
                 t_fill += now_ns() - tl;
             }
         }
+        if (jobs.empty()) {
+            int rc = host_round();
+            if (rc) return rc;
+        }
         kernel_ns += now_ns() - tk;
     }
 
     const uint64_t t_walk = now_ns() - t0;
-    TRACE("multisize walk ms: decide %.2f requests %.2f launch %.2f wait %.2f fill %.2f (total %.2f)", t_dec / 1e6,
-          t_req / 1e6, t_launch / 1e6, t_wait / 1e6, t_fill / 1e6, t_walk / 1e6);
+    TRACE("multisize walk ms: decide %.2f requests %.2f launch %.2f wait %.2f fill %.2f host %.2f (total %.2f)",
+          t_dec / 1e6, t_req / 1e6, t_launch / 1e6, t_wait / 1e6, t_fill / 1e6, t_host / 1e6, t_walk / 1e6);
     // ---- the reference's walk from 0, read off the decisions ----
-    struct Pkg { uint64_t pos; uint32_t s, plen; uint8_t id; uint64_t off; };
+    struct Pkg { uint64_t pos; uint32_t s, plen; uint8_t id, host; uint64_t off; };
     std::vector<Pkg> path;
     uint64_t body = 0;
     for (uint64_t pos = 0; pos < n;) {
@@ -523,7 +595,7 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
         const Decision& dd = pg.dec[sl];
         if (dd.id == 255 && n - pos > 0xFFFFFFFFull)
             return fail(AMBC_E_RANGE, "raw remainder exceeds a u32 chunk field");
-        path.push_back(Pkg{pos, dd.s, dd.plen, dd.id, body});
+        path.push_back(Pkg{pos, dd.s, dd.plen, dd.id, dd.host, body});
         body += HDR + (uint64_t)dd.plen;
         if (dd.id == 255) break;
         pos += dd.s;
@@ -539,7 +611,7 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
     const uint64_t te = now_ns();
     std::map<uint32_t, std::vector<size_t>> groups;
     for (size_t i = 0; i < path.size(); i++)
-        if (path[i].id != 255) groups[path[i].s].push_back(i);
+        if (path[i].id != 255 && !path[i].host) groups[path[i].s].push_back(i);
     std::vector<std::pair<uint32_t, std::vector<size_t>>> gl(groups.begin(), groups.end());
     for (size_t j0 = 0; j0 < gl.size(); j0 += 8) {
         const size_t j1 = std::min(gl.size(), j0 + 8);
@@ -579,6 +651,20 @@ extern "C" int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_
                 if (bb.hplen[q] != pk.plen || bb.hids[q] != pk.id)
                     return fail(AMBC_E_DEVICE, "multi-size walk: re-encode differs");
             }
+        }
+    }
+    {   // host-scored packages: header + the caller's payload bytes
+        std::vector<uint8_t> hb;
+        for (const Pkg& pk : path) {
+            if (!pk.host) continue;
+            hb.assign((size_t)HDR + pk.plen, 0);
+            const uint8_t h[6] = {0xFF, 0xFF, 0, 0, pk.id, 0};
+            std::memcpy(hb.data(), h, 6);
+            const uint32_t f[3] = {pk.s, pk.s, pk.plen};
+            std::memcpy(hb.data() + 6, f, 12);
+            if (hc->emit(hc->user, pk.pos, pk.s, pk.id, hb.data() + HDR, pk.plen))
+                return fail(AMBC_E_CODEC, "host codec emit failed");
+            HIPCHK(hipMemcpy(d_body + pk.off, hb.data(), hb.size(), hipMemcpyHostToDevice));
         }
     }
     if (!path.empty() && path.back().id == 255) {   // the raw remainder package

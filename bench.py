@@ -72,6 +72,9 @@ def parse():
                          "1,3,4,5 = every package decodable by the stdlib-only reference; "
                          "a trailing z = id 5 as zlib.compress(data, 9)'s own bytes; "
                          "1,2,3,4 = the reference's own bytes (byte-pinned set)")
+    ap.add_argument("--walk-bytes", type=int, default=256 << 20,
+                    help="multi-size walk leg (the reference's eight candidates) on this prefix; 0: skip")
+    ap.add_argument("--walk-methods", default="1,3,4,9;1,2,3,4,5")
     ap.add_argument("--api-bytes", type=int, default=256 << 20,
                     help="input size of the AdaptiveCompressor.compress(path, path) leg (0: skip)")
     a = ap.parse_args()
@@ -317,6 +320,29 @@ def alt_leg(lib, ctx, d_in, n, args, methods, steps, zlib9=False):
                        "header_walk_ms": round(ds.walk_ns / 1e6, 3), "host_api_GBps": round(n / dwall / 1e9, 3)}}
 
 
+def walk_leg(ctx, d_in, nbytes, methods):
+    """The reference's default API path: _adaptive_compress with its eight
+    CHUNK_SIZE_CANDIDATES (the multi-size walk, ambc_compress_multisize) on the
+    first nbytes of the same input, host bytes in and out (upload, walk, final
+    encode, body copy back); the second call is timed; bit-exact decode."""
+    from ambc import AdaptiveCompressor
+    data = bytes(d_in.download(nbytes))
+    comp = AdaptiveCompressor(methods=methods)
+    comp.CHUNK_SIZE_CANDIDATES = list(comp.REFERENCE_CHUNK_SIZE_CANDIDATES)
+    comp._adaptive_compress(data)
+    t = time.perf_counter()
+    body = comp._adaptive_compress(data)
+    dt = time.perf_counter() - t
+    steps, ev, wns, ens = C.c_uint32(), C.c_uint64(), C.c_uint64(), C.c_uint64()
+    ctx.lib.ambc_last_multisize_info(comp._ctx().h, C.byref(steps), C.byref(ev), C.byref(wns), C.byref(ens))
+    ok = comp._adaptive_decompress(body, nbytes) == data
+    return {"methods": methods, "candidates": comp.CHUNK_SIZE_CANDIDATES, "bytes": nbytes,
+            "GBps": round(nbytes / dt / 1e9, 3), "seconds": round(dt, 4), "ratio": round(len(body) / nbytes, 5),
+            "packages": comp.chunk_stats["total_chunks"], "walk_rounds": steps.value, "chunk_encodes": ev.value,
+            "walk_ms": round(wns.value / 1e6, 2), "final_encode_ms": round(ens.value / 1e6, 2),
+            "round_trip_bit_exact": ok}
+
+
 def percentile(xs, q):
     """Linear-interpolated percentile of a small sample (rank 0's own step times)."""
     v = sorted(xs)
@@ -479,6 +505,13 @@ def main():
                               max(2, args.steps // 2), zlib9=z)
                 log(f"alt: {alt}")
                 alts.append(alt)
+    walks = []
+    if rank == 0 and world == 1 and args.walk_bytes:
+        for ms in args.walk_methods.split(";"):
+            if ms.strip():
+                w = walk_leg(ctx, d_in, min(n, args.walk_bytes), [int(x) for x in ms.split(",")])
+                log(f"walk: {w}")
+                walks.append(w)
     if rank == 0 and world == 1 and args.api_bytes:
         api = api_leg(args.api_bytes, args.chunk, args.mode, methods, args.seed)
         log(f"api: {api}")
@@ -507,7 +540,8 @@ def main():
                        "reassembly_to_rank0": reasm,
                        "step_ms_p50": round(percentile(step_s, 50) * 1e3, 3),
                        "step_ms_p90": round(percentile(step_s, 90) * 1e3, 3),
-                       "e2e_pinned_host": e2e, "api_file": api, "alt_method_sets": alts},
+                       "e2e_pinned_host": e2e, "api_file": api, "alt_method_sets": alts,
+                       "multisize_walk": walks},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,

@@ -140,6 +140,29 @@ int ambc_compress_multisize(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const 
                             const uint32_t* cands, uint32_t n_cands, const uint32_t* ent_sizes,
                             const double* const* ent_tabs, uint32_t n_ent, uint8_t* out,
                             uint64_t out_cap, uint64_t* out_len, ambc_stats* st);
+/* Host-scored methods for the walk: the reference's library codecs without a GPU
+ * encoder (bz2 / lzma, ids 6 / 7: advanced_compression.py:112-213), evaluated by
+ * the caller.  eval: for the (position, size) pairs of one walk round, id[i] =
+ * the host method that wins size[i] bytes at pos[i] among the host codecs (ids
+ * ascending, strict "<" on len + 18, only below len + 18 < size; 0: none) and
+ * len[i] its payload bytes.  emit: a host-won package's payload (len bytes) into
+ * dst.  Both return 0, or nonzero to fail the call (AMBC_E_CODEC). */
+typedef struct {
+    int (*eval)(void* user, const uint64_t* pos, const uint32_t* size, uint32_t count, uint8_t* id,
+                uint32_t* len);
+    int (*emit)(void* user, uint64_t pos, uint32_t size, uint8_t id, uint8_t* dst, uint32_t len);
+    void* user;
+} ambc_host_codecs;
+
+/* ambc_compress_multisize with host-scored methods beside the GPU's (hc may be
+ * NULL): at every size the host winner joins the GPU's in id order (the smaller
+ * len; a tie to the lower id).  CHUNK_SIZE_CANDIDATES = [C] is the reference
+ * loop of reference mode. */
+int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const ambc_params* p,
+                               const uint32_t* cands, uint32_t n_cands, const uint32_t* ent_sizes,
+                               const double* const* ent_tabs, uint32_t n_ent, const ambc_host_codecs* hc,
+                               uint8_t* out, uint64_t out_cap, uint64_t* out_len, ambc_stats* st);
+
 /* the body the last ambc_compress_multisize(out = NULL) left on the device into
  * out (cap >= its size); AMBC_E_INVAL when there is none */
 int ambc_fetch_body(ambc_ctx* ctx, uint8_t* out, uint64_t cap);

@@ -816,6 +816,67 @@ def test_like_reference_reproduces_default_golden(ctx):
     assert comp.decompress_bytes(out) == data
 
 
+def _word_text(n, seed):
+    """word text with a large vocabulary: bz2 / lzma beat zlib-9 on its larger chunks"""
+    rnd = random.Random(seed)
+    vocab = ["".join(chr(97 + rnd.randrange(26)) for _ in range(rnd.randrange(2, 11))) for _ in range(3000)]
+    out, have = [], 0
+    while have < n:
+        w = vocab[min(int(rnd.paretovariate(1.1)) - 1, 2999)] + (". " if rnd.random() < 0.07 else " ")
+        out.append(w)
+        have += len(w)
+    return "".join(out).encode()[:n]
+
+
+@pytest.mark.parametrize("cands", [REF_CANDS, [16384], [65536, 8192]])
+def test_host_scored_bz2_lzma_walk_matches_oracle(ctx, cands):
+    """The reference's whole default method set {1..7}: ids 6 / 7 (bz2-9 / LZMA, no
+    GPU encoder) scored on host threads beside the device's encoders
+    (ambc_compress_multisize_ex + hostcodecs.py), id 5 as zlib-9's bytes: bodies
+    and stats equal the oracle's restatement of the reference loop with the same
+    stdlib calls (orc.select_reference_set), and the host codecs win somewhere."""
+    inputs = [_word_text(120000, 81), synth.generate(60000, 82), _word_text(9000, 83) + bytes(30000),
+              synth.random_bytes(20000, 84) + _word_text(50000, 85),
+              synth.random_bytes(30000, 86) * 3]                  # LZMA's long match wins
+    ids = (1, 2, 3, 4, 5, 6, 7)
+    used = {6: 0, 7: 0}
+    for data in inputs:
+        comp = _compressor(methods=ids, mode="reference", deflate="zlib9")
+        comp.CHUNK_SIZE_CANDIDATES = list(cands)
+        body = comp._adaptive_compress(data)
+        ref, st = orc.compress_body_multisize(data, cands, ids + (255,), deflate="zlib", reference_set=True)
+        assert body == ref, (cands, len(data))
+        for k in ("total_chunks", "compressed_chunks", "raw_chunks", "bytes_saved",
+                  "compressed_size_without_overhead", "overhead_bytes"):
+            assert comp.chunk_stats[k] == st[k], k
+        for k in used:
+            used[k] += comp.chunk_stats["method_usage"][k]
+        assert comp._adaptive_decompress(body, len(data)) == data
+    assert used[6] > 0 and (used[7] > 0 or cands != REF_CANDS), used
+
+
+def test_host_scored_ids_need_reference_mode(ctx):
+    comp = _compressor(methods=(1, 3, 6), chunk_size=4096)
+    with pytest.raises(NotImplementedError):
+        comp._adaptive_compress(bytes(10000))
+
+
+def test_like_reference_full_set_reproduces_default_golden(ctx):
+    """AdaptiveCompressor.like_reference(full_set=True) -- the reference's default
+    walk with its whole stdlib method set {1..7} -- reproduces its own golden
+    default_s3_n12288 container byte for byte (bz2 and LZMA scored and losing)."""
+    from ambc import AdaptiveCompressor
+    rec = [r for r in load_golden("files.json") if r["name"] == "default_s3_n12288"][0]
+    data = synth.generate(rec["size"], rec["seed"])
+    with open(os.path.join(GOLDEN, rec["file"]), "rb") as f:
+        blob = f.read()
+    comp = AdaptiveCompressor.like_reference(full_set=True)
+    assert [m.type_id for m in comp.compression_methods] == [1, 2, 3, 4, 5, 6, 7, 255]
+    out, stats = comp.compress_bytes(data)
+    assert out == blob
+    assert comp.decompress_bytes(out) == data
+
+
 @pytest.mark.parametrize("methods", [(1, 3, 4, 5), (1, 2, 3, 4, 5)])
 def test_multisize_zlib9_walk_matches_oracle(ctx, methods):
     """The reference's eight candidates with id 5 as zlib-9's bytes at every size
