@@ -139,6 +139,84 @@ __device__ __forceinline__ uint8_t lz4_hdr_byte(uint32_t q, uint32_t n, uint32_t
 #define STAMP_FLUSH
 #endif
 
+__device__ __forceinline__ uint32_t hdr_byte(uint32_t q, uint32_t type, uint32_t n, uint32_t clen) {
+    if (q < 4) return q < 2 ? 0xFFu : 0u;       // marker ff ff 00 00
+    if (q == 4) return type;
+    if (q == 5) return 0;                        // k_value
+    if (q < 10) return (n >> (8 * (q - 6))) & 0xFF;      // used_bytes
+    if (q < 14) return (n >> (8 * (q - 10))) & 0xFF;     // original_length
+    return (clen >> (8 * (q - 14))) & 0xFF;              // compressed_length
+}
+
+// ---- direct emission (measured experiment, EncArgs::dstat) ----
+constexpr unsigned long long DE_AGG = 1ull << 62, DE_INCL = 2ull << 62, DE_VAL = (1ull << 62) - 1;
+
+// aligned dword i of src (GLC: a global buffer this workgroup has just written,
+// read past the vector L1)
+template <bool GLC>
+__device__ __forceinline__ uint32_t de_rd(const uint8_t* src, uint32_t i) {
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(src) + i;
+    if constexpr (GLC) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return *p;
+}
+
+// dst[0, len) = src[0, len) by the wave (src 4-byte aligned; dword stores where
+// dst is aligned, the 0-3 edge bytes singly)
+template <bool GLC>
+__device__ void de_copy(uint8_t* dst, const uint8_t* src, uint32_t len, uint32_t lane) {
+    const uint32_t head = min(len, (uint32_t)((4 - ((uintptr_t)dst & 3)) & 3));
+    if (lane < head) dst[lane] = (uint8_t)(de_rd<GLC>(src, lane >> 2) >> (8 * (lane & 3)));
+    uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + head);
+    const uint32_t nw = (len - head) >> 2;
+    for (uint32_t w = lane; w < nw; w += 64) {
+        const uint32_t o = head + 4 * w;
+        const uint32_t lo = de_rd<GLC>(src, o >> 2);
+        const uint32_t hi = (o & 3) ? de_rd<GLC>(src, (o >> 2) + 1) : 0u;
+        d32[w] = __builtin_amdgcn_alignbyte(hi, lo, o & 3);
+    }
+    for (uint32_t t = head + 4 * nw + lane; t < len; t += 64)
+        dst[t] = (uint8_t)(de_rd<GLC>(src, t >> 2) >> (8 * (t & 3)));
+}
+
+// Decoupled look-back without waiting: publish chunk g's package size, then sum
+// the predecessors' published sizes back to one that knows its inclusive prefix.
+// false (the chunk goes through its slot and k_compact) as soon as a predecessor
+// has published nothing yet, or after 1024 of them.
+// waits: polls (s_sleep between them) of a window whose first unpublished
+// predecessor blocks the look-back before it gives up (0: none)
+__device__ bool de_lookback(unsigned long long* st, uint64_t g, uint64_t size, uint64_t& pre, uint32_t lane,
+                            uint32_t waits) {
+    if (lane == 0) __hip_atomic_store(&st[g], DE_AGG | size, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t acc = 0;
+    int64_t j = (int64_t)g - 1;
+    uint32_t w = 0;
+#pragma unroll 1
+    for (int it = 0; it < 16; it++, j -= 64) {
+        const int64_t q = j - (int64_t)lane;
+        const unsigned long long v =
+            q >= 0 ? __hip_atomic_load(&st[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : DE_INCL;
+        const uint32_t f = (uint32_t)(v >> 62);
+        const uint64_t stop = __ballot(f != 1u);
+        const uint32_t a = stop ? (uint32_t)__builtin_ctzll(stop) : 64u;
+        if (a < 64 && readlane(f, a) == 0u && w < waits) {   // wait for it: the same window again
+            w++;
+            __builtin_amdgcn_s_sleep(8);
+            it--;
+            j += 64;
+            continue;
+        }
+        acc += wave_sum<uint64_t>((lane < a || (lane == a && f == 2u)) ? (uint64_t)(v & DE_VAL) : 0ull);
+        if (a < 64) {
+            if (readlane(f, a) != 2u) return false;
+            pre = acc;
+            if (lane == 0)
+                __hip_atomic_store(&st[g], DE_INCL | (acc + size), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return true;
+        }
+    }
+    return false;
+}
+
 // GL (chunks of 16 KiB and more, no forced / analysed encode, 16-byte aligned
 // chunk starts): the chunk is read in place from the input through the caches
 // instead of a CMAX-byte LDS copy -- only LZ4 (and id 5's gates) take such
@@ -157,7 +235,8 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
     const uint64_t pos0 = A.coff ? A.coff[k] : (uint64_t)k * A.chunk_size;
     const uint32_t n = A.coff ? A.clen[k] : (uint32_t)min((uint64_t)A.chunk_size, A.n_total - pos0);
     const uint8_t* src = A.in + pos0;
-    uint8_t* slot = A.slots + (uint64_t)k * A.slot_stride;
+    uint8_t* const slot0 = A.slots + (uint64_t)k * A.slot_stride;   // the chunk's scratch slot
+    uint8_t* slot = slot0;              // where the payload goes (direct emission: the body)
     // second pass after k_deflate: only the deferred chunks id 5 did not take
     if ((A.flags & ENC_EMIT_PENDING) && (!A.pending[k] || A.ids[k] == 5)) return;
     STAMP_DECL
@@ -789,7 +868,30 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
     // launch (ENC_EMIT_PENDING) that repeats this chunk's selection
     const bool defer = A.pending && !(A.flags & ENC_EMIT_PENDING) && (win == 1 || win == 3);
     if (A.pending && !(A.flags & ENC_EMIT_PENDING) && lane == 0) A.pending[k] = defer ? 1 : 0;
-    if (defer || eval) {
+    // direct emission: the package goes to its final offset when every earlier
+    // chunk has published its size (LZ4 payloads move from the slot they were
+    // built in, raw ones from the chunk, the others are emitted there below)
+    bool placed = false;
+    if (A.dstat && !defer && !eval) {
+        uint64_t pre = 0;
+        placed = de_lookback(A.dstat, (uint64_t)A.kbase + k, (uint64_t)HDR + wlen, pre, lane, A.dwait) &&
+                 pre + HDR + wlen <= A.dcap;
+        if (placed) {
+            uint8_t* dst = A.dout + pre;
+            if (lane < HDR) dst[lane] = (uint8_t)hdr_byte(lane, win, n, wlen);
+            if (win == 9) {
+                __threadfence();
+                de_copy<true>(dst + HDR, slot, wlen, lane);
+            } else if (win == 255) {
+                de_copy<false>(dst + HDR, ch, n, lane);
+            }
+            slot = dst + HDR;
+            if (lane == 0) A.placed[k] = 1;
+        } else if (lane == 0) {
+            A.placed[k] = 0;
+        }
+    }
+    if (defer || eval || (placed && (win == 9 || win == 255))) {
     } else if (win == 4) {
         for (uint32_t i = lane; i < n; i += 64)
             slot[i] = i ? (uint8_t)(ch[i] - ch[i - 1]) : ch[0];
@@ -882,7 +984,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         // forced encodes of high-entropy data can outgrow the LDS region: stage the
         // bit words in the slot behind the payload instead (slot holds 3C + 1344 B)
         const bool gstage = (nwords + 1) * 4 > (uint32_t)EncSmem<CMAX, GL>::STAGE;
-        if (gstage) bits = reinterpret_cast<uint32_t*>(slot + ((wlen + 15) & ~15u));
+        if (gstage) bits = reinterpret_cast<uint32_t*>(slot0 + ((wlen + 15) & ~15u));   // (always the slot)
         for (uint32_t w = lane; w < nwords + 1; w += 64) bits[w] = 0;
         if (gstage) __threadfence();
         wave_sync();
@@ -943,14 +1045,6 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
 // aligned slot loads and stored 4-byte aligned; the 1-3 edge bytes shared
 // with the neighbouring packages are written as single bytes.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t hdr_byte(uint32_t q, uint32_t type, uint32_t n, uint32_t clen) {
-    if (q < 4) return q < 2 ? 0xFFu : 0u;       // marker ff ff 00 00
-    if (q == 4) return type;
-    if (q == 5) return 0;                        // k_value
-    if (q < 10) return (n >> (8 * (q - 6))) & 0xFF;      // used_bytes
-    if (q < 14) return (n >> (8 * (q - 10))) & 0xFF;     // original_length
-    return (clen >> (8 * (q - 14))) & 0xFF;              // compressed_length
-}
 
 __device__ __forceinline__ void compact_package(const CompactArgs& A, uint32_t k, uint32_t lane) {
     const uint64_t o = A.off[k] + (A.base ? *A.base : 0ull);
@@ -1011,7 +1105,7 @@ __device__ __forceinline__ void compact_package(const CompactArgs& A, uint32_t k
 __global__ __launch_bounds__(256) void k_compact(CompactArgs A) {
     const uint32_t lane = threadIdx.x & 63;
     for (uint32_t k = blockIdx.x * 4 + (threadIdx.x >> 6); k < A.n_chunks; k += gridDim.x * 4)
-        compact_package(A, k, lane);
+        if (!A.placed || !A.placed[k]) compact_package(A, k, lane);
 }
 
 __global__ void k_seg_base(uint64_t* base, const uint64_t* off_last, const uint64_t* size_last) {

@@ -317,6 +317,20 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
         }
     }
     const bool dict = (p->method_mask >> AMBC_M_DICT) & 1;
+    // direct emission (measured experiment, off by default: DESIGN §4): packages
+    // whose predecessors have all published their sizes go straight to d_out
+    static const bool direct_env = getenv("AMBC_DIRECT_EMIT") != nullptr;
+    const bool direct = direct_env && !deflate && !dict && p->mode != AMBC_MODE_REFERENCE && !si && M > 0;
+    if (direct) {
+        HIPCHK(d.dstat.ensure((size_t)M * 8));
+        HIPCHK(d.placed.ensure((size_t)M));
+        HIPCHK(hipMemsetAsync(d.dstat.p, 0, (size_t)M * 8, s));
+        ea.dstat = d.dstat.as<unsigned long long>();
+        ea.dout = d_out;
+        ea.dcap = out_cap;
+        ea.dwait = (uint32_t)atoi(getenv("AMBC_DIRECT_EMIT"));
+        ea.placed = d.placed.as<uint8_t>();
+    }
     // the kernels of one chunk range [k0, k1): every per-chunk array offset to k0
     auto seg_args = [&](uint32_t k0, uint32_t k1) {
         EncArgs e = ea;
@@ -331,6 +345,8 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
         if (e.pending) e.pending += k0;
         if (e.gdseq) e.gdseq += (uint64_t)k0 * gd_seq_bytes(gd_cmax);
         if (e.z9rec) e.z9rec += (uint64_t)k0 * z9_rec_words(z9_cmax(C));
+        if (e.placed) e.placed += k0;
+        e.kbase = k0;
         return e;
     };
     auto encode_range = [&](const EncArgs& e) -> int {
@@ -389,6 +405,7 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
             ca.chunk_size = C;
             ca.out = d_out;
             ca.in = raw_in_place ? d_in + (uint64_t)k0 * C : nullptr;
+            ca.placed = direct ? d.placed.as<uint8_t>() + k0 : nullptr;
             // beside the next segment's encoder the compaction runs as a resident
             // grid (per-package-group workgroups would wait behind the encoder's
             // queued workgroups for every dispatch); the last one runs alone
@@ -405,6 +422,14 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
         std::vector<uint64_t> acc(260);
         HIPCHK(hipMemcpyAsync(acc.data(), d.acc.p, 260 * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
+        if (direct && getenv("AMBC_TRACE_DE")) {
+            std::vector<uint8_t> pl(M);
+            HIPCHK(hipMemcpy(pl.data(), d.placed.p, M, hipMemcpyDeviceToHost));
+            uint64_t c = 0;
+            for (uint8_t x : pl) c += x;
+            fprintf(stderr, "[ambc] direct emission: %llu of %u packages placed by k_encode\n",
+                    (unsigned long long)c, M);
+        }
         return finish_compress(d, p, M, Remainder(), d_out, body_len, acc, d_in, end, out_len, st, t0);
     }
     rc = encode_range(ea);
@@ -534,6 +559,7 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
     ca.chunk_size = C;
     ca.out = d_out;
     ca.in = raw_in_place ? d_in : nullptr;
+    ca.placed = direct ? d.placed.as<uint8_t>() : nullptr;
     HIPCHK(launch_compact(ca, s));
     HIPCHK(hipEventRecord(d.ev[3], s));
     if (trace_on()) { HIPCHK(hipStreamSynchronize(s)); TRACE("compact done"); }
