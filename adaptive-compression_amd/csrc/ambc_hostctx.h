@@ -140,8 +140,8 @@ struct Dev {
     Buf coll;                   // small device buffers of the collectives (sizes, stats, flags)
     Buf inffix;                 // fixed-Huffman inflate tables (built on the first decode)
     bool inffix_ok = false;
-    Batch msb[8];               // multi-size walk batches, one per concurrent size class
-    hipStream_t mss[8] = {};    //   and their streams (created on the first walk)
+    Batch msb[16];              // multi-size walk batches: 8 concurrent size classes per walk group
+    hipStream_t mss[16] = {};   //   and their streams (created on the first walk)
     uint32_t ms_steps = 0;      // last multi-size walk: batched evaluation rounds,
     uint64_t ms_evaluated = 0;  //   chunk encodes they ran,
     uint64_t ms_walk_ns = 0, ms_emit_ns = 0;  // and the time of the walk / of the final encode

@@ -475,13 +475,56 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
     // per size evaluates each walk's next position and SPEC positions further
     // along the path it would take if it kept its last step size (a guess: a
     // right one saves a round, whose latency -- the slowest 64 KiB encode -- is
-    // the walk's cost; a wrong one costs idle device time only)
+    // the walk's cost; a wrong one costs idle device time only).  The walks run
+    // in GROUPS interleaved groups: while the device encodes one group's batches
+    // the host decides, asks and launches for the next (the device is latency-,
+    // not throughput-bound here, so the groups' batches share it cheaply).
     static const int SPEC = getenv("AMBC_MS_SPEC") ? atoi(getenv("AMBC_MS_SPEC")) : 2;
+    static const int GROUPS = getenv("AMBC_MS_GROUPS") ? std::max(1, std::min(2, atoi(getenv("AMBC_MS_GROUPS")))) : 2;
     uint64_t t_dec = 0, t_req = 0, t_launch = 0, t_wait = 0, t_fill = 0;   // (AMBC_TRACE breakdown)
-    while (!active.empty()) {
+    using Job = std::pair<std::pair<uint32_t, int>, std::vector<uint64_t>>;
+    struct Group {
+        std::vector<Walk> active;
+        std::vector<Job> flight;     // batches on slots slot0.. (at most 8)
+        int slot0 = 0;
+        uint32_t rounds = 0;
+    };
+    Group grp[2];
+    for (int g = 0; g < GROUPS; g++) grp[g].slot0 = 8 * g;
+    for (size_t i = 0; i < active.size(); i++) grp[i % GROUPS].active.push_back(active[i]);
+    auto launch_job = [&](const Job& jb, int slot) -> int {
+        Batch& bb = d.msb[slot];
+        const uint32_t cnt = (uint32_t)jb.second.size();
+        HIPCHK(bb.host_ensure(cnt));
+        std::memcpy(bb.hpos, jb.second.data(), (size_t)cnt * 8);
+        const bool mk = jb.first.second == 1;
+        return launch_batch(bb, d.mss[slot], d_in, n, mk || !lzshare ? p : &po, jb.first.first, bb.hpos, cnt,
+                            ent_of(jb.first.first), true, mk ? subc.data() : nullptr, mk ? nsub : 0);
+    };
+    auto finish_job = [&](const Job& jb, int slot) -> int {
+        uint64_t tl = now_ns();
+        HIPCHK(hipStreamSynchronize(d.mss[slot]));
+        t_wait += now_ns() - tl;
+        tl = now_ns();
+        fill(d.msb[slot], jb.first.first, jb.first.second, jb.second);
+        evaluated += jb.second.size();
+        t_fill += now_ns() - tl;
+        return AMBC_OK;
+    };
+    // the group's batches in flight: wait and take their results
+    auto complete = [&](Group& G) -> int {
+        const uint64_t tk = now_ns();
+        for (size_t j = 0; j < G.flight.size(); j++)
+            if (int rc = finish_job(G.flight[j], G.slot0 + (int)j)) return rc;
+        G.flight.clear();
+        kernel_ns += now_ns() - tk;
+        return AMBC_OK;
+    };
+    // decide as far as known, then ask for the next positions and launch
+    auto advance = [&](Group& G) -> int {
         uint64_t tq = now_ns();
         std::vector<Walk> still;
-        for (Walk w : active) {
+        for (Walk w : G.active) {
             for (;;) {
                 uint32_t sl;
                 PosTable::Page& pg = T.at(w.pos, sl);
@@ -500,15 +543,14 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
         std::sort(still.begin(), still.end(), [](const Walk& x, const Walk& y) { return x.pos < y.pos; });
         still.erase(std::unique(still.begin(), still.end(), [](const Walk& x, const Walk& y) { return x.pos == y.pos; }),
                     still.end());
-        active.swap(still);
+        G.active.swap(still);
         t_dec += now_ns() - tq;
         tq = now_ns();
-        if (active.empty()) break;
-        steps++;
+        if (G.active.empty()) return AMBC_OK;
         req.clear();
         hpos.clear();
         hsize.clear();
-        for (const Walk& w : active) {
+        for (const Walk& w : G.active) {
             uint64_t q = w.pos;
             for (int k = 0; k <= SPEC && q < n; k++, q += w.last) {
                 if (k) {
@@ -518,13 +560,13 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
                 request(q);
             }
         }
-        std::vector<std::pair<std::pair<uint32_t, int>, std::vector<uint64_t>>> jobs;
+        std::vector<Job> jobs;
         for (auto& r : req) {
             const ambc_params* pk = r.first.second == 1 || !lzshare ? p : &po;
             if (int rc = check_size(pk, r.first.first)) {
                 // only an error if a walk itself needs this size (not a speculative position)
                 for (uint64_t q : r.second)
-                    if (std::binary_search(active.begin(), active.end(), Walk{q, 0},
+                    if (std::binary_search(G.active.begin(), G.active.end(), Walk{q, 0},
                                            [](const Walk& x, const Walk& y) { return x.pos < y.pos; }))
                         return rc;
                 // speculative only: never decided from -- forget the requests
@@ -541,45 +583,46 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
             }
             jobs.emplace_back(r.first, std::move(r.second));
         }
+        t_req += now_ns() - tq;
+        if (!jobs.empty()) G.rounds++;
+        // up to 8 batches at once, each on its own stream and batch buffers (the
+        // 64 KiB class runs at 20 workgroups per CU in place: the small ones fill
+        // in); more than 8: the earlier ones are finished here, the last 8 fly
         const uint64_t tk = now_ns();
-        t_req += tk - tq;
-        // up to 8 batches at once, each on its own stream and batch buffers
-        // (the 64 KiB class runs at 20 workgroups per CU in place: the small ones fill in)
         for (size_t j0 = 0; j0 < jobs.size(); j0 += 8) {
             const size_t j1 = std::min(jobs.size(), j0 + 8);
-            uint64_t tl = now_ns();
-            for (size_t j = j0; j < j1; j++) {
-                Batch& bb = d.msb[j - j0];
-                const auto& jb = jobs[j];
-                const uint32_t cnt = (uint32_t)jb.second.size();
-                HIPCHK(bb.host_ensure(cnt));
-                std::memcpy(bb.hpos, jb.second.data(), (size_t)cnt * 8);
-                const bool mk = jb.first.second == 1;
-                int rc = launch_batch(bb, d.mss[j - j0], d_in, n, mk || !lzshare ? p : &po, jb.first.first, bb.hpos,
-                                      cnt, ent_of(jb.first.first), true, mk ? subc.data() : nullptr, mk ? nsub : 0);
-                if (rc) return rc;
-            }
+            const uint64_t tl = now_ns();
+            for (size_t j = j0; j < j1; j++)
+                if (int rc = launch_job(jobs[j], G.slot0 + (int)(j - j0))) return rc;
             t_launch += now_ns() - tl;
-            if (j0 == 0) {                       // the host codecs while the device works
-                int rc = host_round();
-                if (rc) return rc;
-            }
-            for (size_t j = j0; j < j1; j++) {
-                tl = now_ns();
-                HIPCHK(hipStreamSynchronize(d.mss[j - j0]));
-                t_wait += now_ns() - tl;
-                tl = now_ns();
-                fill(d.msb[j - j0], jobs[j].first.first, jobs[j].first.second, jobs[j].second);
-                evaluated += jobs[j].second.size();
-                t_fill += now_ns() - tl;
+            if (j0 == 0)                           // the host codecs while the device works
+                if (int rc = host_round()) return rc;
+            if (j1 < jobs.size()) {
+                for (size_t j = j0; j < j1; j++)
+                    if (int rc = finish_job(jobs[j], G.slot0 + (int)(j - j0))) return rc;
+            } else {
+                for (size_t j = j0; j < j1; j++) G.flight.push_back(std::move(jobs[j]));
             }
         }
-        if (jobs.empty()) {
-            int rc = host_round();
-            if (rc) return rc;
-        }
+        if (jobs.empty())
+            if (int rc = host_round()) return rc;
         kernel_ns += now_ns() - tk;
+        return AMBC_OK;
+    };
+    for (int g = 0; g < GROUPS; g++)
+        if (int rc = advance(grp[g])) return rc;
+    for (;;) {
+        bool any = false;
+        for (int g = 0; g < GROUPS; g++) {
+            Group& G = grp[g];
+            if (G.active.empty() && G.flight.empty()) continue;
+            any = true;
+            if (int rc = complete(G)) return rc;
+            if (int rc = advance(G)) return rc;
+        }
+        if (!any) break;
     }
+    for (int g = 0; g < GROUPS; g++) steps = std::max(steps, grp[g].rounds);
 
     const uint64_t t_walk = now_ns() - t0;
     TRACE("multisize walk ms: decide %.2f requests %.2f launch %.2f wait %.2f fill %.2f host %.2f (total %.2f)",
