@@ -116,7 +116,7 @@ __device__ __forceinline__ void put_bits_plain(uint32_t* words, uint32_t b, uint
     if (o + nb > 32) words[w + 1] |= v >> (32 - o);
 }
 
-template <int CMAX>
+template <int CMAX, bool EV = false>
 struct GdSmem {
     // parse: last[] (4 KB) + 64 bucket masks (512 B); trees: 5 KB; emit: bit staging.
     // Chunks of 16 KiB and more stage their bits over the chunk itself (the
@@ -126,7 +126,8 @@ struct GdSmem {
     static constexpr bool BIG = CMAX >= 16384;
     static constexpr int REGION = (CMAX > 5120 && !BIG ? CMAX : 5120) + 64;
     static constexpr int ROUNDS = (CMAX + 63) / 64;
-    alignas(16) uint8_t chunk[CMAX + 64];  // zero padded
+    // zero padded (EV: decision only, chunks >= 16 KiB read in place from the input)
+    alignas(16) uint8_t chunk[EV ? 16 : CMAX + 64];
     // parse: last[] (u16 x 2048) | trees: sorted/weights/parents | emit: bit staging
     alignas(16) uint32_t region[REGION / 4];
     uint64_t sel[BIG ? 1 : ROUNDS];        // match-start positions, per 64-position round
@@ -392,10 +393,13 @@ __device__ __forceinline__ uint32_t rle_flush(uint8_t* rs, uint8_t* re, uint32_t
     return o;
 }
 
-template <int CMAX>
+// EV (ENC_EVAL, chunks >= 16 KiB, padded input): the decision only -- the chunk is
+// read in place instead of staged (the 64 / 32 KiB LDS copy held the CU to 2 / 3
+// workgroups through the multi-size walk's rounds) and nothing is emitted
+template <int CMAX, bool EV = false>
 __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
-    __shared__ GdSmem<CMAX> S;
-    constexpr int ROUNDS = GdSmem<CMAX>::ROUNDS;
+    __shared__ GdSmem<CMAX, EV> S;
+    constexpr int ROUNDS = GdSmem<CMAX, EV>::ROUNDS;
     const uint32_t lane = threadIdx.x;
     const uint32_t k = blockIdx.x;
     const uint64_t pos0 = A.coff ? A.coff[k] : (uint64_t)k * A.chunk_size;
@@ -415,7 +419,8 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     uint8_t* slot = A.slots + (uint64_t)k * A.slot_stride;
 
     // ---- stage the chunk in LDS ----
-    {
+    const uint8_t* const ch = EV ? src : S.chunk;
+    if constexpr (!EV) {
         const uint32_t nv = n >> 4;
         if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
             for (uint32_t q = lane; q < nv; q += 64)
@@ -434,7 +439,7 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     // n/4 matches)
     uint8_t* const scr = A.gdseq + (uint64_t)k * gd_seq_bytes(CMAX);
     uint64_t* seq = reinterpret_cast<uint64_t*>(scr);
-    uint64_t* const selp = GdSmem<CMAX>::BIG ? reinterpret_cast<uint64_t*>(scr + 2 * CMAX) : S.sel;
+    uint64_t* const selp = GdSmem<CMAX, EV>::BIG ? reinterpret_cast<uint64_t*>(scr + 2 * CMAX) : S.sel;
     uint32_t mcov = 0;  // bytes the matches cover
     unsigned long long* bk = reinterpret_cast<unsigned long long*>(S.region + 1024);  // after last[]
     uint32_t ns = 0;
@@ -466,7 +471,7 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     const int hl = (int)n - 4;  // last hashable position
     uint32_t p = 0;
     int fcarry = 0;  // max match end so far (frequency count)
-    const uint32_t* c32 = reinterpret_cast<const uint32_t*>(S.chunk);
+    const uint32_t* c32 = reinterpret_cast<const uint32_t*>(ch);
 #pragma unroll 1
     for (int r = 0; r < ROUNDS; r++) {
         const int base = r * 64;
@@ -478,7 +483,8 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
         const int i = base + (int)lane;
         const bool act = i <= hl;
         // loads run for every lane (the chunk is zero padded past n + 63)
-        const uint32_t v = ld32(S.chunk, (uint32_t)i);
+        // (EV: lanes past n read nothing -- the input may end 64 bytes after n)
+        const uint32_t v = !EV || i < (int)n ? ld32(ch, (uint32_t)i) : 0u;
         const uint32_t h = (v * 2654435761u) >> 21;
         const uint32_t c16 = last[h];
         // lanes with my 11-bit hash: one shared hash (runs) is the active mask; else
@@ -504,7 +510,7 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
         const uint64_t lower = peers & ((1ull << lane) - 1ull);
         const int cand = lower ? base + 63 - (int)__clzll((long long)lower)
                                : (c16 == 0xFFFFu ? -1 : (int)c16);
-        const uint32_t cv = ld32(S.chunk, (uint32_t)max(cand, 0));
+        const uint32_t cv = ld32(ch, (uint32_t)max(cand, 0));
         const bool valid = act && cand >= 0 && i - cand <= 32768 && cv == v;
         const uint64_t vm = __ballot(valid);
         wave_sync();
@@ -581,7 +587,7 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
                 const uint32_t c = readlane((uint32_t)cand, cur);
                 for (;;) {
                     const uint32_t off = Lp + 4 * lane;
-                    const uint32_t xx = off < lj ? (ld32(S.chunk, c + off) ^ ld32(S.chunk, pj + off)) : 1u;
+                    const uint32_t xx = off < lj ? (ld32(ch, c + off) ^ ld32(ch, pj + off)) : 1u;
                     const uint64_t mm = __ballot(xx != 0);
                     if (mm) {
                         const uint32_t fl = (uint32_t)__builtin_ctzll(mm);
@@ -616,7 +622,7 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
             }
             const int E = max(fcarry, wave_incl_max_i32(e));
             fcarry = max(fcarry, wave_max_i32(e));
-            if (i < (int)n && E <= i) atomicAdd(&S.lf[S.chunk[i]], 1u);
+            if (i < (int)n && E <= i) atomicAdd(&S.lf[ch[i]], 1u);
             mcov += wave_sum_u32(st ? L : 0u);
         }
         ns = ns0 + (uint32_t)__popcll(selm);
@@ -631,7 +637,7 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     // ---- symbol frequencies (the general parse counted them as it went) ----
     if (single) {
         // a literal at 0 and after the last match, then the matches of seq[]
-        if (lane == 0) S.lf[S.chunk[0]] += n - mcov;
+        if (lane == 0) S.lf[ch[0]] += n - mcov;
         wave_sync();
         for (uint32_t j = lane; j < ns; j += 64) {
             const uint32_t Lj = (uint32_t)(seq[j] >> 16) & 0xFFFF;
@@ -763,6 +769,14 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     const uint32_t body = kind == 2 ? dyn_bytes : kind == 1 ? fix_bytes : sto_bytes;
     const uint32_t total = 2 + body + 4;
     if (kind == 0 || total + 18 >= T) GRET;  // a stored block never beats raw
+    if constexpr (EV) {
+        if (lane == 0) {
+            A.ids[k] = 5;
+            A.plen[k] = total;
+            A.sizes[k] = 18ull + total;
+        }
+        return;
+    } else {
 
     // ---- Adler-32 of the chunk (before a BIG chunk's bits overwrite it) ----
     uint32_t adler;
@@ -778,7 +792,7 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
         adler = (uint32_t)(((n + bsum) % 65521) << 16 | ((1 + asum) % 65521));
     }
     // literal bytes during the emission: LDS, or the input (L2) for BIG chunks
-    constexpr bool BIG = GdSmem<CMAX>::BIG;
+    constexpr bool BIG = GdSmem<CMAX, EV>::BIG;
     auto chb = [&](uint32_t q) -> uint32_t { return BIG ? (uint32_t)src[q] : (uint32_t)S.chunk[q]; };
 
     // ---- emission (this chunk's winner) ----
@@ -921,11 +935,18 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     }
     GSTAMP(5);
     GSTAMP_FLUSH;
+    }
 }
 
 template <int CMAX>
 hipError_t launch_deflate_t(const EncArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_deflate<CMAX>, dim3(a.n_chunks), dim3(64), 0, s, a);
+    if constexpr (CMAX >= 16384) {
+        if ((a.flags & ENC_EVAL) && (a.flags & ENC_IN_ALIGNED) && !getenv("AMBC_DEFLATE_EV_LDS")) {
+            hipLaunchKernelGGL((k_deflate<CMAX, true>), dim3(a.n_chunks), dim3(64), 0, s, a);
+            return hipGetLastError();
+        }
+    }
+    hipLaunchKernelGGL((k_deflate<CMAX, false>), dim3(a.n_chunks), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 

@@ -278,11 +278,12 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
     T.init(n, g, nc);
     struct Walk { uint64_t pos; uint32_t last; };      // last: the size it took the step before
     std::vector<Walk> active;
-    // walks: one per 512 KiB, at most 512; speculation: 2 positions ahead (256
-    // MiB of mixed data, reference candidates: best of 1-8 ahead x 256-2048
-    // walks; AMBC_MS_WALKS / AMBC_MS_SPEC override them for such sweeps)
-    static const uint64_t KMAX_ = getenv("AMBC_MS_WALKS") ? strtoull(getenv("AMBC_MS_WALKS"), nullptr, 10) : 512;
-    static const uint64_t SPAN_ = getenv("AMBC_MS_SPAN") ? strtoull(getenv("AMBC_MS_SPAN"), nullptr, 10) : 512 << 10;
+    // walks: one per 256 KiB, at most 1024; speculation: 3 positions ahead (256
+    // MiB of mixed data, reference candidates, {1,3,4,9}, second call: best of
+    // 2-3 ahead x 512-2048 walks, profiles/r3_multisize_sweep.log; AMBC_MS_WALKS /
+    // AMBC_MS_SPAN / AMBC_MS_SPEC override them for such sweeps)
+    static const uint64_t KMAX_ = getenv("AMBC_MS_WALKS") ? strtoull(getenv("AMBC_MS_WALKS"), nullptr, 10) : 1024;
+    static const uint64_t SPAN_ = getenv("AMBC_MS_SPAN") ? strtoull(getenv("AMBC_MS_SPAN"), nullptr, 10) : 256 << 10;
     uint32_t max_cand = 0;
     for (uint32_t c : cands)
         if (hc || any_eligible(p, c)) max_cand = std::max(max_cand, c);
@@ -475,12 +476,13 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
     // per size evaluates each walk's next position and SPEC positions further
     // along the path it would take if it kept its last step size (a guess: a
     // right one saves a round, whose latency -- the slowest 64 KiB encode -- is
-    // the walk's cost; a wrong one costs idle device time only).  The walks run
-    // in GROUPS interleaved groups: while the device encodes one group's batches
-    // the host decides, asks and launches for the next (the device is latency-,
-    // not throughput-bound here, so the groups' batches share it cheaply).
-    static const int SPEC = getenv("AMBC_MS_SPEC") ? atoi(getenv("AMBC_MS_SPEC")) : 2;
-    static const int GROUPS = getenv("AMBC_MS_GROUPS") ? std::max(1, std::min(2, atoi(getenv("AMBC_MS_GROUPS")))) : 2;
+    // the walk's cost; a wrong one costs idle device time only).  AMBC_MS_GROUPS=2
+    // runs the walks as two interleaved groups (the host decides and launches one
+    // group while the device encodes the other's): measured slower -- 256 MiB
+    // {1,3,4,9}: 55.8 -> 81.5 ms of walk at 1024 walks / 3 ahead, the groups'
+    // batches contend on the device -- so one group is the default.
+    static const int SPEC = getenv("AMBC_MS_SPEC") ? atoi(getenv("AMBC_MS_SPEC")) : 3;
+    static const int GROUPS = getenv("AMBC_MS_GROUPS") ? std::max(1, std::min(2, atoi(getenv("AMBC_MS_GROUPS")))) : 1;
     uint64_t t_dec = 0, t_req = 0, t_launch = 0, t_wait = 0, t_fill = 0;   // (AMBC_TRACE breakdown)
     using Job = std::pair<std::pair<uint32_t, int>, std::vector<uint64_t>>;
     struct Group {
