@@ -278,10 +278,10 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
     T.init(n, g, nc);
     struct Walk { uint64_t pos; uint32_t last; };      // last: the size it took the step before
     std::vector<Walk> active;
-    // walks: one per 256 KiB, at most 1024; speculation: 3 positions ahead (256
-    // MiB of mixed data, reference candidates, {1,3,4,9}, second call: best of
-    // 2-3 ahead x 512-2048 walks, profiles/r3_multisize_sweep.log; AMBC_MS_WALKS /
-    // AMBC_MS_SPAN / AMBC_MS_SPEC override them for such sweeps)
+    // walks: one per 256 KiB, at most 1024 (256 MiB of mixed data, reference
+    // candidates, second call: best of 512-2048 walks x 2-4 positions ahead,
+    // profiles/r3_multisize_sweep.log; AMBC_MS_WALKS / AMBC_MS_SPAN / AMBC_MS_SPEC
+    // override them for such sweeps)
     static const uint64_t KMAX_ = getenv("AMBC_MS_WALKS") ? strtoull(getenv("AMBC_MS_WALKS"), nullptr, 10) : 1024;
     static const uint64_t SPAN_ = getenv("AMBC_MS_SPAN") ? strtoull(getenv("AMBC_MS_SPAN"), nullptr, 10) : 256 << 10;
     uint32_t max_cand = 0;
@@ -481,7 +481,11 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
     // group while the device encodes the other's): measured slower -- 256 MiB
     // {1,3,4,9}: 55.8 -> 81.5 ms of walk at 1024 walks / 3 ahead, the groups'
     // batches contend on the device -- so one group is the default.
-    static const int SPEC = getenv("AMBC_MS_SPEC") ? atoi(getenv("AMBC_MS_SPEC")) : 3;
+    // (speculation is cheap where one LZ4 parse serves every size: 4 ahead; where
+    // every size runs its own encoders -- DEFLATE, Dictionary -- 2 ahead: 256 MiB
+    // {1,3,4,9}: 2 / 3 / 4 ahead 71.6 / 70.0 / 63.6 ms, {1,2,3,4,5}: 94.3 / 99.4 ms)
+    static const int SPEC_ENV = getenv("AMBC_MS_SPEC") ? atoi(getenv("AMBC_MS_SPEC")) : -1;
+    const int SPEC = SPEC_ENV >= 0 ? SPEC_ENV : (lzshare ? 4 : 2);
     static const int GROUPS = getenv("AMBC_MS_GROUPS") ? std::max(1, std::min(2, atoi(getenv("AMBC_MS_GROUPS")))) : 1;
     uint64_t t_dec = 0, t_req = 0, t_launch = 0, t_wait = 0, t_fill = 0;   // (AMBC_TRACE breakdown)
     using Job = std::pair<std::pair<uint32_t, int>, std::vector<uint64_t>>;
