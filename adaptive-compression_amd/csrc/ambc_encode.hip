@@ -224,7 +224,12 @@ __device__ bool de_lookback(unsigned long long* st, uint64_t g, uint64_t size, u
 // each, through 1024 latency-bound LZ4 rounds; in place, the work area alone
 // (4 KB) lets 20 workgroups share the CU.  Reads past n stay inside the input's
 // 64 bytes of slack or the next chunk and never reach a result.
-template <int CMAX, bool GL = false>
+// MODE (compile time, so that the headline's kernel carries none of the rest):
+// ENC_MODE_PLAIN compress / plugins; ENC_MODE_WALK the multi-size walk's
+// decision-only batches (ENC_EVAL, lz4sub); ENC_MODE_DIRECT the direct-emission
+// experiment (dstat)
+enum : int { ENC_MODE_PLAIN = 0, ENC_MODE_WALK = 1, ENC_MODE_DIRECT = 2 };
+template <int CMAX, bool GL = false, int MODE = ENC_MODE_PLAIN>
 __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
     constexpr int BS = CMAX >= 4096 ? 64 : CMAX / 64;  // bytes per lane per round
     constexpr int ROUNDS = CMAX / (64 * BS);
@@ -564,11 +569,11 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         if (lane == 0) A.bestpre[k] = best | (uniform ? 0x80000000u : 0u) | (single ? 0x40000000u : 0u);
     }
     const uint32_t best_pre = best;   // before LZ4 (a deferred Huffman compares against it)
-    const bool eval = A.flags & ENC_EVAL;
+    const bool eval = MODE == ENC_MODE_WALK && (A.flags & ENC_EVAL);
     // prefix sizes to report (ENC_EVAL + lz4sub): sub_c[sj..sj_end) -- ascending,
     // below n, within id 9's prefs; they end in order as the parse passes b - 12
     uint32_t sj = 0, sj_end = 0;
-    if (A.lz4sub && ((mm >> 9) & 1u)) {
+    if (MODE == ENC_MODE_WALK && A.lz4sub && ((mm >> 9) & 1u)) {
         while (sj < A.n_subc && A.sub_c[sj] < max(A.pref_min[9], 13u)) sj++;
         sj_end = sj;
         while (sj_end < A.n_subc && A.sub_c[sj_end] < n && A.sub_c[sj_end] <= A.pref_max[9]) sj_end++;
@@ -872,7 +877,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
     // chunk has published its size (LZ4 payloads move from the slot they were
     // built in, raw ones from the chunk, the others are emitted there below)
     bool placed = false;
-    if (A.dstat && !defer && !eval) {
+    if (MODE == ENC_MODE_DIRECT && A.dstat && !defer && !eval) {
         uint64_t pre = 0;
         placed = de_lookback(A.dstat, (uint64_t)A.kbase + k, (uint64_t)HDR + wlen, pre, lane, A.dwait) &&
                  pre + HDR + wlen <= A.dcap;
@@ -1266,11 +1271,21 @@ static hipError_t launch_encode_t(const EncArgs& a, hipStream_t s) {
     static const uint32_t gl_min = getenv("AMBC_ENC_GL_MIN") ? (uint32_t)atoi(getenv("AMBC_ENC_GL_MIN")) : 16384u;
     if constexpr (CMAX >= 4096) {
         if (CMAX >= gl_min && (a.flags & ENC_IN_ALIGNED) && !(a.flags & (ENC_FORCE | ENC_ANALYZE))) {
-            hipLaunchKernelGGL((k_encode<CMAX, true>), dim3(a.n_chunks), dim3(64), 0, s, a);
+            if (a.flags & ENC_EVAL)
+                hipLaunchKernelGGL((k_encode<CMAX, true, ENC_MODE_WALK>), dim3(a.n_chunks), dim3(64), 0, s, a);
+            else if (a.dstat)
+                hipLaunchKernelGGL((k_encode<CMAX, true, ENC_MODE_DIRECT>), dim3(a.n_chunks), dim3(64), 0, s, a);
+            else
+                hipLaunchKernelGGL((k_encode<CMAX, true>), dim3(a.n_chunks), dim3(64), 0, s, a);
             return hipGetLastError();
         }
     }
-    hipLaunchKernelGGL((k_encode<CMAX, false>), dim3(a.n_chunks), dim3(64), 0, s, a);
+    if (a.flags & ENC_EVAL)
+        hipLaunchKernelGGL((k_encode<CMAX, false, ENC_MODE_WALK>), dim3(a.n_chunks), dim3(64), 0, s, a);
+    else if (a.dstat)
+        hipLaunchKernelGGL((k_encode<CMAX, false, ENC_MODE_DIRECT>), dim3(a.n_chunks), dim3(64), 0, s, a);
+    else
+        hipLaunchKernelGGL((k_encode<CMAX, false>), dim3(a.n_chunks), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 

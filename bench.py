@@ -320,13 +320,19 @@ def alt_leg(lib, ctx, d_in, n, args, methods, steps, zlib9=False):
                        "header_walk_ms": round(ds.walk_ns / 1e6, 3), "host_api_GBps": round(n / dwall / 1e9, 3)}}
 
 
-def walk_leg(ctx, d_in, nbytes, methods):
+def walk_leg(ctx, nbytes, methods):
     """The reference's default API path: _adaptive_compress with its eight
-    CHUNK_SIZE_CANDIDATES (the multi-size walk, ambc_compress_multisize) on the
-    first nbytes of the same input, host bytes in and out (upload, walk, final
-    encode, body copy back); the second call is timed; bit-exact decode."""
+    CHUNK_SIZE_CANDIDATES (the multi-size walk, ambc_compress_multisize), host
+    bytes in and out (upload, walk, final encode, body copy back); the second call
+    is timed; bit-exact decode.  Input: runs, text and skewed-random segments of
+    8-64 KiB (scripts/multisize_bench.py) -- on the headline's stream the
+    reference's walk stops at its first incompressible position and stores the
+    rest raw (its remainder rule, adaptive_compressor.py:586-588), which would
+    time almost nothing."""
     from ambc import AdaptiveCompressor
-    data = bytes(d_in.download(nbytes))
+    sys.path.insert(0, os.path.join(REPO, "scripts"))
+    from multisize_bench import mixed
+    data = mixed(nbytes, 7)
     comp = AdaptiveCompressor(methods=methods)
     comp.CHUNK_SIZE_CANDIDATES = list(comp.REFERENCE_CHUNK_SIZE_CANDIDATES)
     comp._adaptive_compress(data)
@@ -337,6 +343,7 @@ def walk_leg(ctx, d_in, nbytes, methods):
     ctx.lib.ambc_last_multisize_info(comp._ctx().h, C.byref(steps), C.byref(ev), C.byref(wns), C.byref(ens))
     ok = comp._adaptive_decompress(body, nbytes) == data
     return {"methods": methods, "candidates": comp.CHUNK_SIZE_CANDIDATES, "bytes": nbytes,
+            "input": "runs / text / skewed random, 8-64 KiB segments (scripts/multisize_bench.py mixed, seed 7)",
             "GBps": round(nbytes / dt / 1e9, 3), "seconds": round(dt, 4), "ratio": round(len(body) / nbytes, 5),
             "packages": comp.chunk_stats["total_chunks"], "walk_rounds": steps.value, "chunk_encodes": ev.value,
             "walk_ms": round(wns.value / 1e6, 2), "final_encode_ms": round(ens.value / 1e6, 2),
@@ -509,7 +516,7 @@ def main():
     if rank == 0 and world == 1 and args.walk_bytes:
         for ms in args.walk_methods.split(";"):
             if ms.strip():
-                w = walk_leg(ctx, d_in, min(n, args.walk_bytes), [int(x) for x in ms.split(",")])
+                w = walk_leg(ctx, args.walk_bytes, [int(x) for x in ms.split(",")])
                 log(f"walk: {w}")
                 walks.append(w)
     if rank == 0 and world == 1 and args.api_bytes:
