@@ -217,7 +217,7 @@ __device__ bool de_lookback(unsigned long long* st, uint64_t g, uint64_t size, u
     return false;
 }
 
-// GL (chunks of 16 KiB and more, no forced / analysed encode, 16-byte aligned
+// GL (chunks of 8 KiB and more, no forced / analysed encode, 16-byte aligned
 // chunk starts): the chunk is read in place from the input through the caches
 // instead of a CMAX-byte LDS copy -- only LZ4 (and id 5's gates) take such
 // chunks, and a 64 KiB chunk in LDS held the CU to 2 workgroups, one wave
@@ -1266,9 +1266,11 @@ __global__ __launch_bounds__(256) void k_equal(const uint8_t* a, const uint8_t* 
 // ---------------------------------------------------------------------------
 template <int CMAX>
 static hipError_t launch_encode_t(const EncArgs& a, hipStream_t s) {
-    // 16 KiB and more: the chunk in place (see k_encode) unless a forced / analysed
-    // encode may take the other methods' LDS-bound paths
-    static const uint32_t gl_min = getenv("AMBC_ENC_GL_MIN") ? (uint32_t)atoi(getenv("AMBC_ENC_GL_MIN")) : 16384u;
+    // 8 KiB and more: the chunk in place (see k_encode) unless a forced / analysed
+    // encode may take the other methods' LDS-bound paths.  Same-box A/B of the
+    // 4 GiB bench (profiles/r3_gl_ab.json): 8 KiB 217.3 -> 274.4 GB/s in place
+    // (12 KB of LDS held the CU to 13 workgroups), 4 KiB 333 -> 300 (stays in LDS)
+    static const uint32_t gl_min = getenv("AMBC_ENC_GL_MIN") ? (uint32_t)atoi(getenv("AMBC_ENC_GL_MIN")) : 8192u;
     if constexpr (CMAX >= 4096) {
         if (CMAX >= gl_min && (a.flags & ENC_IN_ALIGNED) && !(a.flags & (ENC_FORCE | ENC_ANALYZE))) {
             if (a.flags & ENC_EVAL)
