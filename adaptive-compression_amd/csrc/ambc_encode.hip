@@ -63,14 +63,18 @@ static_assert((1u << LZ4_HASH_BITS) * 4 <= 4096, "LZ4 table must fit the work ar
 // per step; the 16-byte body is unrolled, the sub-block loop is not, which
 // keeps the kernel small enough for the instruction cache).
 // f(p, c, nx): position, byte, following byte (zero padding past the data).
+// lim: 16-byte pieces starting at or past lim read as zeros -- a chunk read in
+// place (GL) may end its input there (the input has 64 readable bytes after its
+// end, not a whole lane block's); LDS-staged chunks are zero padded already.
 template <int BS, typename F>
-__device__ __forceinline__ void for_block_bytes(const uint8_t* chunk, uint32_t b0, F&& f) {
+__device__ __forceinline__ void for_block_bytes(const uint8_t* chunk, uint32_t b0, uint32_t lim, F&& f) {
 #pragma unroll 1
     for (int q = 0; q < BS / 16; q++) {
         const uint32_t base = b0 + 16 * q;
-        const uint4 v = *reinterpret_cast<const uint4*>(chunk + base);
+        const bool in = base < lim;
+        const uint4 v = in ? *reinterpret_cast<const uint4*>(chunk + base) : make_uint4(0, 0, 0, 0);
         const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-        const uint32_t nxt = chunk[base + 16];
+        const uint32_t nxt = in ? chunk[base + 16] : 0u;
 #pragma unroll
         for (int t = 0; t < 16; t++) {
             const uint32_t c = (w[t >> 2] >> (8 * (t & 3))) & 0xFFu;
@@ -248,6 +252,8 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
 
     // ---- stage the chunk in LDS (16 B per lane per load, coalesced) ----
     const uint8_t* ch = GL ? src : S.chunk;
+    // (for_block_bytes: in place, nothing is read from 16-byte pieces past n)
+#define GLLIM (GL ? n : 0xFFFFFFFFu)
     if constexpr (GL) {
         for (uint32_t i = lane; i < 256; i += 64) S.hist()[i] = 0;
     } else {
@@ -385,8 +391,8 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
 #pragma unroll 1
         for (int r = 0; r < ROUNDS; r++) {
             const uint32_t b0 = (uint32_t)(r * 64 + lane) * BS;
-            uint32_t prev = b0 ? ch[b0 - 1] : 0x100u;
-            for_block_bytes<BS>(ch, b0, [&](uint32_t p, uint32_t c, uint32_t) {
+            uint32_t prev = b0 ? (b0 - 1 < GLLIM ? (uint32_t)ch[b0 - 1] : 0u) : 0x100u;
+            for_block_bytes<BS>(ch, b0, GLLIM, [&](uint32_t p, uint32_t c, uint32_t) {
                 if (p < n && c != prev) atomicMin(&first[c], p);
                 prev = c;
             });
@@ -925,12 +931,12 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
 #pragma unroll 1
             for (int r = 0; r < ROUNDS; r++) {
                 const uint32_t b0 = (uint32_t)(r * 64 + lane) * BS;
-                const uint32_t prevb = b0 ? ch[b0 - 1] : 0x100u;
+                const uint32_t prevb = b0 ? (b0 - 1 < GLLIM ? (uint32_t)ch[b0 - 1] : 0u) : 0x100u;
                 int lb = -1;
                 uint32_t cnt = 0;
                 {
                     uint32_t prev = prevb;
-                    for_block_bytes<BS>(ch, b0, [&](uint32_t p, uint32_t c, uint32_t) {
+                    for_block_bytes<BS>(ch, b0, GLLIM, [&](uint32_t p, uint32_t c, uint32_t) {
                         if (p < n && c != prev) lb = (int)p;
                         prev = c;
                     });
@@ -939,7 +945,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                 rs_c = max(rs_c, wave_max_i32(lb));
                 const uint32_t off0 = b0 == 0 ? 254u : (uint32_t)((int)(b0 - 1) - rs) % 255u;
                 uint32_t off = off0, prev = prevb;
-                for_block_bytes<BS>(ch, b0, [&](uint32_t p, uint32_t c, uint32_t) {
+                for_block_bytes<BS>(ch, b0, GLLIM, [&](uint32_t p, uint32_t c, uint32_t) {
                     off = c != prev ? 0u : (off == 254u ? 0u : off + 1u);
                     if (p < n && off == 0) cnt++;
                     prev = c;
@@ -947,7 +953,7 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
                 const uint32_t incl = wave_incl_sum(cnt);
                 uint32_t idx = base_idx + incl - cnt;
                 off = off0; prev = prevb;
-                for_block_bytes<BS>(ch, b0, [&](uint32_t p, uint32_t c, uint32_t) {
+                for_block_bytes<BS>(ch, b0, GLLIM, [&](uint32_t p, uint32_t c, uint32_t) {
                     off = c != prev ? 0u : (off == 254u ? 0u : off + 1u);
                     if (p < n && off == 0) {
                         if (idx >= wb && idx < wb + CAPP) ps[idx - wb] = (uint16_t)p;
@@ -998,13 +1004,13 @@ __global__ __launch_bounds__(64) void k_encode(EncArgs A) {
         for (int r = 0; r < ROUNDS; r++) {
             const uint32_t b0 = (uint32_t)(r * 64 + lane) * BS;
             uint32_t my = 0;
-            for_block_bytes<BS>(ch, b0, [&](uint32_t p, uint32_t c, uint32_t) {
+            for_block_bytes<BS>(ch, b0, GLLIM, [&](uint32_t p, uint32_t c, uint32_t) {
                 if (p < n) my += S.clen()[c];
             });
             const uint32_t incl = wave_incl_sum(my);
             uint32_t bp = bitbase + incl - my;
             uint32_t cw = bp >> 5, acc = 0;
-            for_block_bytes<BS>(ch, b0, [&](uint32_t p, uint32_t s, uint32_t) {
+            for_block_bytes<BS>(ch, b0, GLLIM, [&](uint32_t p, uint32_t s, uint32_t) {
                 if (p < n) {
                     const uint32_t L = S.clen()[s], cd = S.code()[s];
                     const uint32_t o = bp & 31, w = bp >> 5;

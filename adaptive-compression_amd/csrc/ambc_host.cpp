@@ -83,8 +83,17 @@ int ambc_init(const int* device_ids, int n_devices, ambc_ctx** out) {
         for (auto& ev : d.ev) HIPCHK(hipEventCreate(&ev));
         for (auto& x : d.xs) HIPCHK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
         for (auto& ev : d.xev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        HIPCHK(hipStreamCreateWithFlags(&d.cs, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&d.ss, hipStreamNonBlocking));   // per-segment statistics
+        // the scan + compaction stream; AMBC_CS_PRIO=1: high priority (measured, §4)
+        if (getenv("AMBC_CS_PRIO") && atoi(getenv("AMBC_CS_PRIO")) > 0) {
+            int lo = 0, hi = 0;
+            HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+            HIPCHK(hipStreamCreateWithPriority(&d.cs, hipStreamNonBlocking, hi));
+        } else {
+            HIPCHK(hipStreamCreateWithFlags(&d.cs, hipStreamNonBlocking));
+        }
         for (auto& ev : d.pev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        for (auto& ev : d.sev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         ctx->devs.push_back(d);
     }
     *out = ctx.release();
@@ -118,6 +127,7 @@ void ambc_destroy(ambc_ctx* ctx) {
         for (auto& ev : d.pev) (void)hipEventDestroy(ev);
         (void)hipStreamSynchronize(d.cs);
         (void)hipStreamDestroy(d.cs);
+        if (d.ss) { (void)hipStreamSynchronize(d.ss); (void)hipStreamDestroy(d.ss); }
         (void)hipStreamDestroy(d.stream);
     }
     delete ctx;
@@ -370,7 +380,8 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
     // or 8 (the last segment's compaction stays exposed, ~0.4 ms), and equal
     // segments beat a short last one (3:3:3:1, 3:3:3:2, 4:4:4:1: +3 % step).  Reference mode
     // needs every verdict before the scan (remainder-raw rule): one range.
-    const uint32_t S = (p->mode != AMBC_MODE_REFERENCE && M >= 16384 && !ea.stamps) ? NSEG : 1;
+    static const uint32_t nseg = getenv("AMBC_NSEG") ? std::max(1, std::min(8, atoi(getenv("AMBC_NSEG")))) : NSEG;
+    const uint32_t S = (p->mode != AMBC_MODE_REFERENCE && M >= 16384 && !ea.stamps) ? nseg : 1;
     d.n_launch = S;
     HIPCHK(hipEventRecord(d.ev[0], s));
     if (S > 1) {
@@ -380,6 +391,8 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
         HIPCHK(d.segbase.ensure((S + 1) * 8));
         HIPCHK(hipMemsetAsync(d.segbase.p, 0, 8, d.cs));
         HIPCHK(hipMemsetAsync(d.acc.p, 0, 260 * 8, d.cs));
+        HIPCHK(hipEventRecord(d.sev[0], d.cs));       // (acc cleared before any statistics)
+        HIPCHK(hipStreamWaitEvent(d.ss, d.sev[0], 0));
         uint64_t* sb = d.segbase.as<uint64_t>();
         for (uint32_t i = 0; i < S; i++) {
             const uint32_t k0 = (uint32_t)((uint64_t)M * i / S), k1 = (uint32_t)((uint64_t)M * (i + 1) / S);
@@ -411,12 +424,18 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
             // queued workgroups for every dispatch); the last one runs alone
             ca.resident = i + 1 < S ? compact_resident() : 0;
             HIPCHK(launch_compact(ca, d.cs));
-            // the segment's statistics beside the next encode too (acc[] accumulates)
+            // the segment's statistics on a stream of their own (acc[] accumulates):
+            // beside an encoder that fills every CU (8 waves per SIMD) a k_stats
+            // launch waits milliseconds for slots, and on d.cs it held the next
+            // segment's compaction back until after the last encode
+            HIPCHK(hipStreamWaitEvent(d.ss, d.pev[i], 0));
             HIPCHK(launch_stats(d.ids.as<uint8_t>() + k0, d.plen.as<uint32_t>() + k0, k1 - k0, ca.n_total, C,
-                                d.acc.as<uint64_t>(), d.cs));
+                                d.acc.as<uint64_t>(), d.ss));
         }
         HIPCHK(hipEventRecord(d.ev[3], d.cs));
         HIPCHK(hipStreamWaitEvent(s, d.ev[3], 0));
+        HIPCHK(hipEventRecord(d.sev[1], d.ss));
+        HIPCHK(hipStreamWaitEvent(s, d.sev[1], 0));
         uint64_t body_len = 0;
         HIPCHK(hipMemcpyAsync(&body_len, sb + S, 8, hipMemcpyDeviceToHost, s));
         std::vector<uint64_t> acc(260);

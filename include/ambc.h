@@ -59,7 +59,7 @@ extern "C" {
                                      advanced_compression.py:76-81; chunk_size <= 65536) instead
                                      of "ambc-deflate v1" */
 #define AMBC_FLAG_INPUT_PADDED 4u /* device-resident calls: at least 64 readable bytes follow the
-                                     input (chunks >= 8 KiB are then read in place instead of
+                                     input (chunks >= 4 KiB are then read in place instead of
                                      through an LDS copy; host-fed calls always qualify) */
 
 /* GPU-routable method ids (bit i of method_mask = method id i) */

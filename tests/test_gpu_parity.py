@@ -232,6 +232,45 @@ def test_bodies_match_oracle(ctx, n, seed, chunk, mode):
     assert comp._adaptive_decompress(body, n) == data
 
 
+@pytest.mark.parametrize("chunk", [4096, 8192, 16384])
+def test_in_place_tail_chunks(ctx, chunk):
+    """Chunks read in place from the input (>= 4 KiB): short last chunks whose
+    winner emits through the lane-block loops (RLE runs, Huffman text, near-7.0
+    entropy) must not read past the input's 64 bytes of slack; device-resident
+    calls with the input ending exactly at its allocation, host calls through
+    the library's own buffer; bodies equal the oracle's."""
+    from ambc import _lib
+    rnd = random.Random(chunk)
+    text = synth.generate(3 * chunk, 41)
+    tails = [bytes(100), bytes([9]) * 777, text[:150], text[:chunk - 1], bytes(rnd.randrange(4) for _ in range(300)),
+             bytes(range(128)) * 2 + bytes(40)]
+    for tail in tails:
+        data = text[:2 * chunk] + tail
+        for mode in ("native", "reference"):
+            comp = _compressor(chunk_size=chunk, mode=mode, methods=(1, 3, 4, 9))
+            body = comp._adaptive_compress(data)
+            ref, _ = orc.compress_body(data, orc.make_params(chunk, mode, (1, 3, 4, 9), n_total=len(data)))
+            assert body == ref, (chunk, len(tail), mode)
+        # device-resident, the input flagged padded and ending 64 bytes before its allocation
+        n = len(data)
+        p, keep = comp._params(n)           # (keep: the entropy tables p points at)
+        p.mode = _lib.MODE_NATIVE
+        p.flags |= _lib.FLAG_INPUT_PADDED
+        d_in = _lib.DeviceBuffer(ctx, n + 64)
+        cap = ctx.lib.ambc_compress_bound(n, chunk)
+        d_out = _lib.DeviceBuffer(ctx, cap + 64)
+        try:
+            d_in.upload(data + bytes(64))
+            olen, st = C.c_uint64(), _lib.Stats()
+            _lib.check(ctx.lib.ambc_compress_device(ctx.h, 0, d_in.ptr, n, C.byref(p), d_out.ptr, cap,
+                                                    C.byref(olen), C.byref(st), None), ctx.lib)
+            nat, _ = orc.compress_body(data, orc.make_params(chunk, "native", (1, 3, 4, 9), n_total=n))
+            assert bytes(d_out.download(olen.value)) == nat
+        finally:
+            d_in.free()
+            d_out.free()
+
+
 def test_random_edge_inputs(ctx):
     rnd = random.Random(5)
     pieces = [bytes(4096), bytes([7]) * 5000, os.urandom(9000), b"abc" * 3000,
