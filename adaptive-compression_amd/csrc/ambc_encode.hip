@@ -221,7 +221,7 @@ __device__ bool de_lookback(unsigned long long* st, uint64_t g, uint64_t size, u
     return false;
 }
 
-// GL (chunks of 8 KiB and more, no forced / analysed encode, 16-byte aligned
+// GL (chunks of 4 KiB and more, no forced / analysed encode, 16-byte aligned
 // chunk starts): the chunk is read in place from the input through the caches
 // instead of a CMAX-byte LDS copy -- only LZ4 (and id 5's gates) take such
 // chunks, and a 64 KiB chunk in LDS held the CU to 2 workgroups, one wave
@@ -233,8 +233,22 @@ __device__ bool de_lookback(unsigned long long* st, uint64_t g, uint64_t size, u
 // decision-only batches (ENC_EVAL, lz4sub); ENC_MODE_DIRECT the direct-emission
 // experiment (dstat)
 enum : int { ENC_MODE_PLAIN = 0, ENC_MODE_WALK = 1, ENC_MODE_DIRECT = 2 };
+// Register allocation for 8 waves per SIMD (64 VGPRs, a few spilled bytes): with
+// the chunk read in place the LDS no longer caps k_encode at 5 waves, and the
+// VALU-issue-bound LZ4 rounds gain from the extra waves -- same-box A/B, 4 GiB
+// (profiles/r3_wpe_ab.json): 4 KiB 3.08 -> 2.86 ms per launch, 8 KiB 3.70 -> 3.48;
+// 6 waves (71 VGPRs) was slower at 8 KiB.  AMBC_WPE=0 builds the compiler's own
+// allocation (94 VGPRs, 5 waves).
+#ifndef AMBC_WPE
+#define AMBC_WPE 8
+#endif
+#if AMBC_WPE
+#define AMBC_ENC_ATTR __attribute__((amdgpu_waves_per_eu(AMBC_WPE, AMBC_WPE)))
+#else
+#define AMBC_ENC_ATTR
+#endif
 template <int CMAX, bool GL = false, int MODE = ENC_MODE_PLAIN>
-__global__ __launch_bounds__(64) void k_encode(EncArgs A) {
+__global__ __launch_bounds__(64) AMBC_ENC_ATTR void k_encode(EncArgs A) {
     constexpr int BS = CMAX >= 4096 ? 64 : CMAX / 64;  // bytes per lane per round
     constexpr int ROUNDS = CMAX / (64 * BS);
     __shared__ EncSmem<CMAX, GL> S;
@@ -1272,11 +1286,12 @@ __global__ __launch_bounds__(256) void k_equal(const uint8_t* a, const uint8_t* 
 // ---------------------------------------------------------------------------
 template <int CMAX>
 static hipError_t launch_encode_t(const EncArgs& a, hipStream_t s) {
-    // 8 KiB and more: the chunk in place (see k_encode) unless a forced / analysed
-    // encode may take the other methods' LDS-bound paths.  Same-box A/B of the
-    // 4 GiB bench (profiles/r3_gl_ab.json): 8 KiB 217.3 -> 274.4 GB/s in place
-    // (12 KB of LDS held the CU to 13 workgroups), 4 KiB 333 -> 300 (stays in LDS)
-    static const uint32_t gl_min = getenv("AMBC_ENC_GL_MIN") ? (uint32_t)atoi(getenv("AMBC_ENC_GL_MIN")) : 8192u;
+    // 4 KiB and more: the chunk in place (see k_encode) unless a forced / analysed
+    // encode may take the other methods' LDS-bound paths.  Same-box A/Bs of the
+    // 4 GiB bench (profiles/r3_gl_ab.json, r3_wpe_ab.json): 8 KiB 217.3 -> 274.4
+    // GB/s in place (12 KB of LDS held the CU to 13 workgroups); 4 KiB in place
+    // pays only with the 8-wave register allocation (333 -> 300 at 5 waves, 340 at 8)
+    static const uint32_t gl_min = getenv("AMBC_ENC_GL_MIN") ? (uint32_t)atoi(getenv("AMBC_ENC_GL_MIN")) : 4096u;
     if constexpr (CMAX >= 4096) {
         if (CMAX >= gl_min && (a.flags & ENC_IN_ALIGNED) && !(a.flags & (ENC_FORCE | ENC_ANALYZE))) {
             if (a.flags & ENC_EVAL)

@@ -2,7 +2,7 @@
 # per-segment statistics fused into k_compact (lib_fused = this tree) vs separate k_stats (lib_new8)
 set -e
 export TMPDIR=/tmp
-O=gpurun_out/ssab
+O=gpurun_out/ssab2
 mkdir -p $O
 timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/tests.log 2>&1
 for r in 1 2 3; do
