@@ -22,7 +22,10 @@ engine runs a single chunk size C (``chunk_size=``, default 4096), i.e.
 With several ``CHUNK_SIZE_CANDIDATES`` (e.g. the reference's default
 ``REFERENCE_CHUNK_SIZE_CANDIDATES``) the reference's multi-size walk runs
 instead, on the device (``_adaptive_compress_multisize`` ->
-ambc_compress_multisize).
+ambc_compress_multisize_ex).  The reference's bz2 / LZMA codecs (ids 6 / 7) have no
+GPU encoder: with them among ``methods`` (reference mode, or several candidates)
+they are scored on host threads beside the device's encoders
+(``hostcodecs.py``).
 
 Defaults differ from the reference's ``AdaptiveCompressor()`` (8-candidate
 walk, every stdlib codec): this class defaults to one 4096-byte chunk size,
@@ -30,7 +33,8 @@ native mode and methods {1, 3, 4, 9} (the throughput configuration; id 9 needs
 an LZ4 decoder on the reading side).  The first compress of an instance built
 with those defaults says so once (``DefaultsWarning``);
 ``AdaptiveCompressor.like_reference()`` builds the closest GPU configuration to
-the reference's default instead.
+the reference's default instead (``full_set=True``: with bz2 / LZMA, byte for
+byte the reference's default).
 """
 import ctypes as C
 import hashlib
