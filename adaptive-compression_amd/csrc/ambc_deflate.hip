@@ -116,7 +116,7 @@ __device__ __forceinline__ void put_bits_plain(uint32_t* words, uint32_t b, uint
     if (o + nb > 32) words[w + 1] |= v >> (32 - o);
 }
 
-template <int CMAX, bool EV = false>
+template <int CMAX, bool NOCHUNK = false>
 struct GdSmem {
     // parse: last[] (4 KB) + 64 bucket masks (512 B); trees: 5 KB; emit: bit staging.
     // Chunks of 16 KiB and more stage their bits over the chunk itself (the
@@ -127,7 +127,7 @@ struct GdSmem {
     static constexpr int REGION = (CMAX > 5120 && !BIG ? CMAX : 5120) + 64;
     static constexpr int ROUNDS = (CMAX + 63) / 64;
     // zero padded (EV: decision only, chunks >= 16 KiB read in place from the input)
-    alignas(16) uint8_t chunk[EV ? 16 : CMAX + 64];
+    alignas(16) uint8_t chunk[NOCHUNK ? 16 : CMAX + 64];
     // parse: last[] (u16 x 2048) | trees: sorted/weights/parents | emit: bit staging
     alignas(16) uint32_t region[REGION / 4];
     uint64_t sel[BIG ? 1 : ROUNDS];        // match-start positions, per 64-position round
@@ -396,10 +396,13 @@ __device__ __forceinline__ uint32_t rle_flush(uint8_t* rs, uint8_t* re, uint32_t
 // EV (ENC_EVAL, chunks >= 16 KiB, padded input): the decision only -- the chunk is
 // read in place instead of staged (the 64 / 32 KiB LDS copy held the CU to 2 / 3
 // workgroups through the multi-size walk's rounds) and nothing is emitted
-template <int CMAX, bool EV = false>
+// IP (chunks up to 8 KiB, padded input): read in place as well, bits still staged
+// in the LDS region (13 -> 9 KB of LDS at 4 KiB)
+template <int CMAX, bool EV = false, bool IP = EV>
 __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
-    __shared__ GdSmem<CMAX, EV> S;
-    constexpr int ROUNDS = GdSmem<CMAX, EV>::ROUNDS;
+    constexpr bool NOCHUNK = EV || (IP && CMAX < 16384);
+    __shared__ GdSmem<CMAX, NOCHUNK> S;
+    constexpr int ROUNDS = GdSmem<CMAX, NOCHUNK>::ROUNDS;
     const uint32_t lane = threadIdx.x;
     const uint32_t k = blockIdx.x;
     const uint64_t pos0 = A.coff ? A.coff[k] : (uint64_t)k * A.chunk_size;
@@ -419,8 +422,8 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     uint8_t* slot = A.slots + (uint64_t)k * A.slot_stride;
 
     // ---- stage the chunk in LDS ----
-    const uint8_t* const ch = EV ? src : S.chunk;
-    if constexpr (!EV) {
+    const uint8_t* const ch = NOCHUNK ? src : S.chunk;
+    if constexpr (!NOCHUNK) {
         const uint32_t nv = n >> 4;
         if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
             for (uint32_t q = lane; q < nv; q += 64)
@@ -439,7 +442,7 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     // n/4 matches)
     uint8_t* const scr = A.gdseq + (uint64_t)k * gd_seq_bytes(CMAX);
     uint64_t* seq = reinterpret_cast<uint64_t*>(scr);
-    uint64_t* const selp = GdSmem<CMAX, EV>::BIG ? reinterpret_cast<uint64_t*>(scr + 2 * CMAX) : S.sel;
+    uint64_t* const selp = GdSmem<CMAX, NOCHUNK>::BIG ? reinterpret_cast<uint64_t*>(scr + 2 * CMAX) : S.sel;
     uint32_t mcov = 0;  // bytes the matches cover
     unsigned long long* bk = reinterpret_cast<unsigned long long*>(S.region + 1024);  // after last[]
     uint32_t ns = 0;
@@ -484,7 +487,7 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
         const bool act = i <= hl;
         // loads run for every lane (the chunk is zero padded past n + 63)
         // (EV: lanes past n read nothing -- the input may end 64 bytes after n)
-        const uint32_t v = !EV || i < (int)n ? ld32(ch, (uint32_t)i) : 0u;
+        const uint32_t v = !NOCHUNK || i < (int)n ? ld32(ch, (uint32_t)i) : 0u;
         const uint32_t h = (v * 2654435761u) >> 21;
         const uint32_t c16 = last[h];
         // lanes with my 11-bit hash: one shared hash (runs) is the active mask; else
@@ -783,7 +786,7 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     {
         uint64_t asum = 0, bsum = 0;
         for (uint32_t i = lane; i < n; i += 64) {
-            const uint32_t c = S.chunk[i];
+            const uint32_t c = ch[i];
             asum += c;
             bsum += (uint64_t)(n - i) * c;
         }
@@ -792,8 +795,8 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
         adler = (uint32_t)(((n + bsum) % 65521) << 16 | ((1 + asum) % 65521));
     }
     // literal bytes during the emission: LDS, or the input (L2) for BIG chunks
-    constexpr bool BIG = GdSmem<CMAX, EV>::BIG;
-    auto chb = [&](uint32_t q) -> uint32_t { return BIG ? (uint32_t)src[q] : (uint32_t)S.chunk[q]; };
+    constexpr bool BIG = GdSmem<CMAX, NOCHUNK>::BIG;
+    auto chb = [&](uint32_t q) -> uint32_t { return BIG || NOCHUNK ? (uint32_t)src[q] : (uint32_t)S.chunk[q]; };
 
     // ---- emission (this chunk's winner) ----
     if (kind == 1) {  // fixed tables
@@ -940,6 +943,12 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
 
 template <int CMAX>
 hipError_t launch_deflate_t(const EncArgs& a, hipStream_t s) {
+    if constexpr (CMAX >= 4096 && CMAX <= 8192) {
+        if ((a.flags & ENC_IN_ALIGNED) && !getenv("AMBC_DEFLATE_LDS")) {
+            hipLaunchKernelGGL((k_deflate<CMAX, false, true>), dim3(a.n_chunks), dim3(64), 0, s, a);
+            return hipGetLastError();
+        }
+    }
     if constexpr (CMAX >= 16384) {
         if ((a.flags & ENC_EVAL) && (a.flags & ENC_IN_ALIGNED) && !getenv("AMBC_DEFLATE_EV_LDS")) {
             hipLaunchKernelGGL((k_deflate<CMAX, true>), dim3(a.n_chunks), dim3(64), 0, s, a);
