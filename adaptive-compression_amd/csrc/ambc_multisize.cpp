@@ -487,9 +487,8 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
     static const int SPEC_ENV = getenv("AMBC_MS_SPEC") ? atoi(getenv("AMBC_MS_SPEC")) : -1;
     // (zlib-9's id 5 is the costliest encoder per position: 1 ahead -- like_reference()
     // on 64 MiB, 1024 walks: 0 / 1 / 2 ahead 0.229 / 0.255 / 0.224 GB/s)
-    const int SPEC = SPEC_ENV >= 0 ? SPEC_ENV
-                                   : (lzshare ? 4 : (eligible(p, cands[0] > 65536 ? 65536 : cands[0], AMBC_M_DEFLATE) &&
-                                                     (p->flags & AMBC_FLAG_ZLIB9)) ? 1 : 2);
+    const bool z9walk = ((p->method_mask >> AMBC_M_DEFLATE) & 1) && (p->flags & AMBC_FLAG_ZLIB9);
+    const int SPEC = SPEC_ENV >= 0 ? SPEC_ENV : (lzshare ? 4 : z9walk ? 1 : 2);
     static const int GROUPS = getenv("AMBC_MS_GROUPS") ? std::max(1, std::min(2, atoi(getenv("AMBC_MS_GROUPS")))) : 1;
     uint64_t t_dec = 0, t_req = 0, t_launch = 0, t_wait = 0, t_fill = 0;   // (AMBC_TRACE breakdown)
     using Job = std::pair<std::pair<uint32_t, int>, std::vector<uint64_t>>;
