@@ -481,14 +481,13 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
     // group while the device encodes the other's): measured slower -- 256 MiB
     // {1,3,4,9}: 55.8 -> 81.5 ms of walk at 1024 walks / 3 ahead, the groups'
     // batches contend on the device -- so one group is the default.
-    // (speculation is cheap where one LZ4 parse serves every size: 4 ahead; where
-    // every size runs its own encoders -- DEFLATE, Dictionary -- 2 ahead: 256 MiB
-    // {1,3,4,9}: 2 / 3 / 4 ahead 71.6 / 70.0 / 63.6 ms, {1,2,3,4,5}: 94.3 / 99.4 ms)
+    // (speculation is cheap where one LZ4 parse serves every size: 6 ahead; where
+    // every size runs its own encoders -- DEFLATE, zlib-9, Dictionary -- 1 ahead:
+    // 256 MiB {1,3,4,9}: 4 / 5 / 6 / 8 ahead 72.4 / 64.1 / 58.4 / 94.9 ms (8 with
+    // 2048 walks), {1,2,3,4,5}: 1 / 2 ahead 86.0 / 90.6 ms, like_reference() on 64
+    // MiB: 0 / 1 / 2 ahead 0.229 / 0.255 / 0.224 GB/s; profiles/r3_multisize_sweep.log)
     static const int SPEC_ENV = getenv("AMBC_MS_SPEC") ? atoi(getenv("AMBC_MS_SPEC")) : -1;
-    // (zlib-9's id 5 is the costliest encoder per position: 1 ahead -- like_reference()
-    // on 64 MiB, 1024 walks: 0 / 1 / 2 ahead 0.229 / 0.255 / 0.224 GB/s)
-    const bool z9walk = ((p->method_mask >> AMBC_M_DEFLATE) & 1) && (p->flags & AMBC_FLAG_ZLIB9);
-    const int SPEC = SPEC_ENV >= 0 ? SPEC_ENV : (lzshare ? 4 : z9walk ? 1 : 2);
+    const int SPEC = SPEC_ENV >= 0 ? SPEC_ENV : (lzshare ? 6 : 1);
     static const int GROUPS = getenv("AMBC_MS_GROUPS") ? std::max(1, std::min(2, atoi(getenv("AMBC_MS_GROUPS")))) : 1;
     uint64_t t_dec = 0, t_req = 0, t_launch = 0, t_wait = 0, t_fill = 0;   // (AMBC_TRACE breakdown)
     using Job = std::pair<std::pair<uint32_t, int>, std::vector<uint64_t>>;
