@@ -1292,7 +1292,7 @@ static hipError_t launch_encode_t(const EncArgs& a, hipStream_t s) {
     // GB/s in place (12 KB of LDS held the CU to 13 workgroups); 4 KiB in place
     // pays only with the 8-wave register allocation (333 -> 300 at 5 waves, 340 at 8)
     static const uint32_t gl_min = getenv("AMBC_ENC_GL_MIN") ? (uint32_t)atoi(getenv("AMBC_ENC_GL_MIN")) : 4096u;
-    if constexpr (CMAX >= 4096) {
+    if constexpr (CMAX >= 1024) {
         if (CMAX >= gl_min && (a.flags & ENC_IN_ALIGNED) && !(a.flags & (ENC_FORCE | ENC_ANALYZE))) {
             if (a.flags & ENC_EVAL)
                 hipLaunchKernelGGL((k_encode<CMAX, true, ENC_MODE_WALK>), dim3(a.n_chunks), dim3(64), 0, s, a);
