@@ -173,17 +173,19 @@ struct PosTable {
         std::vector<Decision> dec;
     };
     uint64_t g = 1;
+    int gsh = -1;                // log2(g) when g is a power of two (the reference's list: 1024)
     uint32_t nc = 0;
     std::vector<std::unique_ptr<Page>> pages;
     void init(uint64_t n, uint64_t g_, uint32_t nc_) {
         g = g_;
+        gsh = (g & (g - 1)) == 0 ? __builtin_ctzll(g) : -1;
         nc = nc_;
         pages.clear();
         pages.resize((size_t)((n / g >> PB) + 1));
     }
     // (page, slot) of position pos, the page created on first use
     Page& at(uint64_t pos, uint32_t& slot) {
-        const uint64_t x = pos / g;
+        const uint64_t x = gsh >= 0 ? pos >> gsh : pos / g;
         slot = (uint32_t)(x & ((1u << PB) - 1));
         std::unique_ptr<Page>& pg = pages[(size_t)(x >> PB)];
         if (!pg) {

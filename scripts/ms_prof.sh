@@ -20,5 +20,6 @@ for _ in range(2):
     print('walk', round(dt, 4), 's', round(len(data) / dt / 1e9, 3), 'GB/s', len(b), flush=True)
 EOF
 AMBC_TRACE=1 timeout -k 10 200 python3 gpurun_out/ms_one.py > gpurun_out/${TAG}_trace.log 2>&1
+[ -n "$NOPROF" ] && exit 0
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- \
     python3 gpurun_out/ms_one.py > gpurun_out/${TAG}_prof.log 2>&1
