@@ -7,6 +7,7 @@ from ._lib import AmbcError, AmbcUnavailable, Context, load  # noqa: F401
 from .compressor import AdaptiveCompressor, DefaultsWarning, entropy_terms  # noqa: F401
 from .methods import (Bzip2Compression, CompressionMethod, DeflateCompression,  # noqa: F401
                       DeltaCompression, DictionaryCompression, HuffmanCompression,
-                      LZ4Compression, LZMACompression, NoCompression, RLECompression)
+                      LZ4Compression, LZMACompression, NoCompression, RLECompression,
+                      ZstdCompression)
 
 __version__ = "0.1.0"

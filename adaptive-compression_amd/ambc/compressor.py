@@ -117,6 +117,9 @@ class AdaptiveCompressor:
         if chunk_size is not None:
             self.CHUNK_SIZE_CANDIDATES = [int(chunk_size)]
         ids = tuple(DEFAULT_METHODS if methods is None else [m for m in methods if m != 255])
+        for i in ids:
+            if i in HOST_SCORED_IDS and i not in DECODE_METHODS:
+                raise ValueError(f"method id {i}: its host library is not available here")
         # validates: GPU encoders, plus the host-scored bz2 / lzma (ids 6 / 7)
         method_mask([i for i in ids if i not in HOST_SCORED_IDS])
         self.compression_methods = [(GPU_METHODS.get(i) or DECODE_METHODS[i])() for i in sorted(set(ids))]

@@ -9,7 +9,8 @@ exceptions raised like the reference's.
   GPU through libambc_hip (single-chunk calls of the same kernels the batched
   path uses; Dictionary emits the reference's own bytes for chunks <= 8192);
 * ids 5, 6, 7 are the reference's own stdlib library wrappers
-  (advanced_compression.py:71-213), registered so that reference-produced files
+  (advanced_compression.py:71-213) and id 8 its zstandard wrapper (:219-261,
+  here over the system libzstd), registered so that reference-produced files
   holding such chunks decode.  When id 5 is among ``methods`` the batched engine
   selects and encodes it on the GPU with "ambc-deflate v1" (k_deflate: a valid
   zlib stream that this wrapper and the reference decode, not zlib level-9
@@ -255,6 +256,10 @@ class DeflateCompression(CompressionMethod):
     def compress(self, data, level=9):
         return zlib.compress(data, level=level) if data else b""
 
+    def should_use(self, data, threshold=0.9):
+        # advanced_compression.py:98-107
+        return len(data) >= 64 and calculate_entropy(data) < 8.0
+
     def decompress(self, data, original_length):
         if not data:
             return b""
@@ -308,8 +313,127 @@ class LZMACompression(CompressionMethod):
             return bytes(original_length)
 
 
+class _Zstd:
+    """The system libzstd (ctypes) with python-zstandard's call semantics -- the
+    reference's id 8 wraps ``zstandard`` (requirements.txt: >=0.15.0), which is
+    not installed here.  Bytes are libzstd's own at level 19; parity unpinned (no
+    reference fixture holds a zstd package)."""
+
+    CONTENTSIZE_UNKNOWN = (1 << 64) - 1
+    CONTENTSIZE_ERROR = (1 << 64) - 2
+
+    class _Buf(C.Structure):               # ZSTD_inBuffer / ZSTD_outBuffer
+        _fields_ = [("ptr", C.c_void_p), ("size", C.c_size_t), ("pos", C.c_size_t)]
+
+    _lib = None
+
+    @classmethod
+    def lib(cls):
+        if cls._lib is None:
+            lib = C.CDLL("libzstd.so.1")
+            lib.ZSTD_compressBound.restype = C.c_size_t
+            lib.ZSTD_compressBound.argtypes = [C.c_size_t]
+            lib.ZSTD_compress.restype = C.c_size_t
+            lib.ZSTD_compress.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_int]
+            lib.ZSTD_isError.restype = C.c_uint
+            lib.ZSTD_isError.argtypes = [C.c_size_t]
+            lib.ZSTD_getFrameContentSize.restype = C.c_ulonglong
+            lib.ZSTD_getFrameContentSize.argtypes = [C.c_void_p, C.c_size_t]
+            lib.ZSTD_createDCtx.restype = C.c_void_p
+            lib.ZSTD_freeDCtx.argtypes = [C.c_void_p]
+            lib.ZSTD_decompressStream.restype = C.c_size_t
+            lib.ZSTD_decompressStream.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+            cls._lib = lib
+        return cls._lib
+
+    @classmethod
+    def available(cls):
+        try:
+            cls.lib()
+            return True
+        except OSError:
+            return False
+
+    @classmethod
+    def compress(cls, data, level):
+        """ZstdCompressor(level=level).compress(data): one frame with its content size."""
+        lib = cls.lib()
+        src = bytes(data)
+        cap = lib.ZSTD_compressBound(len(src))
+        dst = C.create_string_buffer(cap)
+        r = lib.ZSTD_compress(dst, cap, src, len(src), level)
+        if lib.ZSTD_isError(r):
+            raise RuntimeError("zstd compress error")
+        return dst.raw[:r]
+
+    @classmethod
+    def decompress(cls, data, max_output_size):
+        """ZstdDecompressor().decompress(data, max_output_size=...): the first frame;
+        its header's content size when present, else at most max_output_size
+        bytes; raises where python-zstandard raises ZstdError."""
+        lib = cls.lib()
+        src = bytes(data)
+        size = lib.ZSTD_getFrameContentSize(src, len(src))
+        if size == cls.CONTENTSIZE_ERROR:
+            raise ValueError("error determining content size from frame header")
+        if size == 0:
+            return b""
+        if size == cls.CONTENTSIZE_UNKNOWN:
+            if max_output_size == 0:
+                raise ValueError("could not determine content size in frame header")
+            cap, expect = max_output_size, 0
+        else:
+            cap, expect = size, size
+        dst = C.create_string_buffer(max(cap, 1))
+        inb = cls._Buf(C.cast(C.c_char_p(src), C.c_void_p), len(src), 0)
+        outb = cls._Buf(C.cast(dst, C.c_void_p), cap, 0)
+        dctx = lib.ZSTD_createDCtx()
+        if not dctx:
+            raise MemoryError("ZSTD_createDCtx")
+        try:
+            r = lib.ZSTD_decompressStream(dctx, C.byref(outb), C.byref(inb))
+        finally:
+            lib.ZSTD_freeDCtx(dctx)
+        if lib.ZSTD_isError(r):
+            raise ValueError("zstd decompression error")
+        if r:
+            raise ValueError("decompression error: did not decompress full frame")
+        if expect and outb.pos != expect:
+            raise ValueError("decompression error: decompressed size mismatch")
+        return dst.raw[:outb.pos]
+
+
+class ZstdCompression(CompressionMethod):
+    """advanced_compression.py:219-261 (registered when the reference's
+    ``zstandard`` would be: here, when the system libzstd loads)."""
+    type_id = 8
+
+    def compress(self, data):
+        if not data:
+            return b""
+        try:
+            return _Zstd.compress(data, 19)
+        except Exception:  # noqa: BLE001 -- advanced_compression.py:232-234 returns the input
+            return bytes(data)
+
+    def decompress(self, data, original_length):
+        if not data:
+            return b""
+        try:
+            return _fit(_Zstd.decompress(data, original_length), original_length)
+        except Exception:  # noqa: BLE001 -- reference returns zeros on error
+            return bytes(original_length)
+
+    def should_use(self, data, threshold=0.9):
+        # advanced_compression.py:252-261 (entropy > 8.2 is impossible for bytes)
+        return len(data) >= 512 and calculate_entropy(data) <= 8.2
+
+
 GPU_METHODS = {1: RLECompression, 2: DictionaryCompression, 3: HuffmanCompression,
                4: DeltaCompression, 5: DeflateCompression, 9: LZ4Compression}
 DECODE_METHODS = {1: RLECompression, 2: DictionaryCompression, 3: HuffmanCompression,
                   4: DeltaCompression, 5: DeflateCompression, 6: Bzip2Compression,
                   7: LZMACompression, 9: LZ4Compression, 255: NoCompression}
+HAS_ZSTD = _Zstd.available()
+if HAS_ZSTD:
+    DECODE_METHODS[8] = ZstdCompression

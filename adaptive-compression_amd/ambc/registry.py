@@ -25,14 +25,14 @@ REFERENCE_CHUNK_SIZE_CANDIDATES = [131072, 65536, 32768, 16384, 8192, 4096, 2048
 # own Dictionary bytes) takes chunks <= 8192, its preferred maximum
 GPU_ENCODE_IDS = (1, 2, 3, 4, 5, 9)
 DEVICE_DECODE_IDS = (1, 2, 3, 4, 9, 255)
-# ids whose ENCODERS are host libraries in the reference (zlib / bz2 / lzma); on the
-# decode side id 5 is inflated on the GPU (k_decode_inflate), ids 6 / 7 by the
-# reference's stdlib wrappers on the host
-HOST_LIBRARY_IDS = (5, 6, 7)
-# ids the walk scores on the host (the reference's bz2 / lzma wrappers, no GPU
-# encoder): AdaptiveCompressor(methods=(..., 6, 7)) in reference mode or with
-# several CHUNK_SIZE_CANDIDATES -- see hostcodecs.py
-HOST_SCORED_IDS = (6, 7)
+# ids whose ENCODERS are host libraries in the reference (zlib / bz2 / lzma / zstd);
+# on the decode side id 5 is inflated on the GPU (k_decode_inflate), ids 6 / 7 / 8
+# by the reference's library wrappers on the host (id 8 through the system libzstd)
+HOST_LIBRARY_IDS = (5, 6, 7, 8)
+# ids the walk scores on the host (the reference's bz2 / lzma / zstd wrappers, no
+# GPU encoder): AdaptiveCompressor(methods=(..., 6, 7, 8)) in reference mode or
+# with several CHUNK_SIZE_CANDIDATES -- see hostcodecs.py
+HOST_SCORED_IDS = (6, 7, 8)
 DEFAULT_METHODS = (1, 3, 4, 9)         # + 255 always
 DEFAULT_CHUNK_SIZE = 4096
 

@@ -877,7 +877,7 @@ struct Walk {
     std::vector<DecJob> jobs;
     std::vector<uint32_t> src_index;   // job -> package ordinal
     std::vector<uint8_t> kind;         // job -> DEC_KIND_* kernel
-    std::vector<ambc_host_chunk> host;    // decoded by the caller (ids 6, 7)
+    std::vector<ambc_host_chunk> host;    // decoded by the caller (ids 6, 7, 8, ...)
     std::vector<ambc_host_chunk> zlib;    // id 5: inflated here on host threads
     uint64_t total = 0;
     uint64_t scratch = 0;
@@ -929,7 +929,7 @@ bool make_job(const uint8_t* body, uint64_t blen, uint64_t hp, uint32_t ord, con
             j.scratch_cap = orig;
             sneed = (4ull * orig + 15) & ~15ull;
         }
-    } else if (t == 5 || t == 6 || t == 7) {
+    } else if (t == 5 || !device_decodes(t)) {
         j.type = DEC_SKIP;
         kind = DEC_KIND_LIGHT;
     } else {
@@ -2176,7 +2176,7 @@ extern "C" int ambc_decompress_ex(ambc_ctx* ctx, const uint8_t* body, uint64_t b
     if (rc) return rc;
     if (n_host) *n_host = (uint32_t)host.size();
     if (host.size() > host_cap) {
-        if (!host_chunks && !n_host) return fail(AMBC_E_HOSTCODEC, "body has bz2/lzma chunks");
+        if (!host_chunks && !n_host) return fail(AMBC_E_HOSTCODEC, "body has packages for host codecs (bz2 / lzma / zstd)");
         if (host.size() > host_cap) return fail(AMBC_E_CAPACITY, "host_chunks capacity too small");
     }
     for (size_t i = 0; i < host.size(); i++) host_chunks[i] = host[i];
@@ -2187,7 +2187,7 @@ extern "C" int ambc_decompress_batch(ambc_ctx* ctx, const uint8_t* body, uint64_
                                      uint64_t orig_size, uint8_t* out, ambc_stats* st) {
     uint32_t nh = 0;
     int rc = ambc_decompress_ex(ctx, body, body_len, orig_size, nullptr, out, nullptr, 0, &nh, st);
-    if (rc == AMBC_E_CAPACITY && nh) return fail(AMBC_E_HOSTCODEC, "body has bz2/lzma chunks: use ambc_decompress_ex");
+    if (rc == AMBC_E_CAPACITY && nh) return fail(AMBC_E_HOSTCODEC, "body has packages for host codecs (bz2 / lzma / zstd): use ambc_decompress_ex");
     return rc;
 }
 

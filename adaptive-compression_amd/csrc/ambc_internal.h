@@ -121,6 +121,13 @@ constexpr uint32_t DEC_PRODUCED_HOST = 0xFFFFFFFEu;  // k_decode_inflate: output
 constexpr uint32_t DEC_VERBATIM = 256;
 constexpr uint32_t DEC_SKIP = 257;
 
+// ids with a device decoder; any other REGISTERED id (bz2 6, lzma 7, zstd 8, ...)
+// is listed for the caller's host codec (ambc_host_chunk), an unregistered one is
+// copied verbatim (adaptive_compressor.py:432-435)
+__host__ __device__ constexpr bool device_decodes(uint32_t t) {
+    return t == 1 || t == 2 || t == 3 || t == 4 || t == 5 || t == 9 || t == 255;
+}
+
 // ---- the device header walk (ambc_walk.hip), one body piece at a time ----
 constexpr uint64_t WALK_ENDED = ~0ull;   // WalkState::entry once the walk has stopped
 constexpr uint32_t WALK_GRID = 128;      // workgroups of the grid-stride walk kernels (small: they

@@ -414,7 +414,7 @@ __device__ __forceinline__ void walk_job(const WalkArgs& A, uint32_t r, uint64_t
                 j.scratch_cap = orig;
                 sneed = (4ull * orig + 15) & ~15ull;
             }
-        } else if (t == 5 || t == 6 || t == 7) {
+        } else if (t == 5 || !device_decodes(t)) {
             j.type = DEC_SKIP;
             kind = DEC_KIND_LIGHT;
         } else {

@@ -47,7 +47,7 @@ extern "C" {
 #define AMBC_E_RANGE (-4)     /* a u32 chunk field would overflow (reference: struct.error) */
 #define AMBC_E_MARKER (-5)    /* "Marker mismatch in chunk header." (reference ValueError) */
 #define AMBC_E_CAPACITY (-6)  /* output buffer too small */
-#define AMBC_E_HOSTCODEC (-7) /* body holds ids 6/7 chunks: use ambc_decompress_ex */
+#define AMBC_E_HOSTCODEC (-7) /* body holds packages for host codecs (ids 6/7/8): use ambc_decompress_ex */
 #define AMBC_E_CODEC (-8)     /* the codec raises in the reference (e.g. Huffman on 1 or 256 symbols) */
 #define AMBC_E_COMM (-9)      /* RCCL error, or another rank / shard of the call failed */
 
@@ -100,7 +100,8 @@ typedef struct {
     uint64_t host_codec_ns; /* decode: id-5 (zlib) chunks inflated on host threads */
 } ambc_stats;
 
-/* A chunk the library leaves to the caller (ids 6/7: bz2/lzma; id 5 zlib chunks
+/* A chunk the library leaves to the caller: a registered id without a device
+ * decoder (6 bz2, 7 lzma, 8 zstd, ...; id 5 zlib chunks the GPU cannot inflate
  * are inflated inside the library on host threads). */
 typedef struct {
     uint64_t body_off; /* payload offset in the body */
@@ -174,8 +175,9 @@ int ambc_last_multisize_info(ambc_ctx* ctx, uint32_t* steps, uint64_t* evaluated
 int ambc_decompress_batch(ambc_ctx* ctx, const uint8_t* body, uint64_t body_len,
                           uint64_t orig_size, uint8_t* out, ambc_stats* st);
 
-/* As ambc_decompress_batch; ids 6/7 chunks are not decoded but listed in
- * host_chunks (capacity host_cap, count in *n_host) for the caller to fill.
+/* As ambc_decompress_batch; packages of registered ids without a device decoder
+ * (6 bz2, 7 lzma, 8 zstd, ...) are not decoded but listed in host_chunks
+ * (capacity host_cap, count in *n_host) for the caller to fill.
  * registered[id>>6] bit (id&63) marks ids with a registered method
  * (method_lookup); an unregistered id's payload is copied verbatim
  * (adaptive_compressor.py:432-435).  NULL registered = {1,2,3,4,5,6,7,9,255}. */

@@ -1,48 +1,3 @@
-# INTEGRATION — binding the reference to libambc_hip
-
-The reference is pure Python, so its "FFI" for this path is ctypes.  A maintainer
-who wants the reference's own `AdaptiveCompressor` to run its hot loops on MI355X
-drops `integration/ambc_binding.py` (quoted in full below, and tested as it stands:
-`tests/test_gpu_binding.py`) next to `adaptive_compressor.py` and binds the class:
-
-```python
-import adaptive_compressor, ambc_binding
-ambc_binding.bind(adaptive_compressor.AdaptiveCompressor)   # unbind() restores
-```
-
-No reference file changes.  The binding replaces exactly the two loops SURVEY.md
-§8(b) names — `_adaptive_compress` (adaptive_compressor.py:363-394, with
-`_pick_best_chunk_and_method` :537-590 and `_process_chunk` :631-700) and
-`_adaptive_decompress` (:396-454) — and leaves the header, MD5, raw fallback and
-stats code of the reference untouched.  It never drops a method of the instance:
-
-| instance method | where it runs | bytes |
-|---|---|---|
-| 1 RLE, 2 Dictionary, 3 Huffman, 4 Delta | GPU (`k_encode`, `k_dict`) while `method_chunk_prefs` stays in the device domain (Dictionary <= 8192, window 4096 / lookahead 32) | the reference's own (tests/golden) |
-| 5 DEFLATE | GPU zlib-9 (`AMBC_FLAG_ZLIB9`, <= 65536) when the interpreter's zlib is 1.2.11, else host | `zlib.compress(data, 9)`'s own |
-| 9 LZ4 | host (the instance's python-lz4 object) unless `bind(..., gpu_lz4=True)` | python-lz4's, or the GPU's "ambc-lz4 greedy v2" frames |
-| 6 bz2, 7 lzma, 8 zstd, 10 brotli, ... and any id outside the device domain | host threads beside the device (`ambc_compress_multisize_ex` + `ambc_host_codecs`), the instance's own `should_use` / `compress` | the instance's own |
-
-Ties join in id order, which is the reference's list order (its default list —
-basic four, `compression_fix.get_compatible_methods()`'s duplicates, the library
-codecs — meets each id first in ascending order).  Configurations the library
-cannot follow (a list whose first occurrences are not ascending, a non-constant
-marker, candidates above 131072) run the reference's own loop and warn
-`BindingFallback`.  Decoding: `ambc_decompress_ex` decodes ids 1/2/3/4/5/9/255 on
-the GPU and lists packages of the instance's other registered ids (6/7/8/...) for
-its own method objects (zeros on an exception, adaptive_compressor.py:437-442);
-a method returning an unexpected length sends the body to the reference's loop.
-
-`tests/test_gpu_binding.py` applies the binding to a stand-in class with the
-reference's attribute names and method-list shape and checks: the reference's
-default container `tests/golden/files/default_s3_n12288.ambc` (8 candidates,
-methods 1..7) reproduced bit for bit and decoded; every golden reference-loop
-container; bodies and stats equal to the oracle's reference loop with bz2 / lzma
-scored through the instance's objects; id 9 through a host LZ4 object equal to
-the device's LZ4; the fallbacks; host-decoded ids 6/7/8.  `tests/test_abi.py`
-checks the struct layouts against `include/ambc.h` on the CPU.
-
-```python
 """ambc_binding -- puts libambc_hip.so (MI355X) behind the reference's own
 AdaptiveCompressor.  Drop this file next to the reference's adaptive_compressor.py:
 
@@ -430,33 +385,3 @@ if __name__ == "__main__":                  # python ambc_binding.py <reference 
     import adaptive_compressor                 # noqa: E402
     bind(adaptive_compressor.AdaptiveCompressor)
     print("bound:", adaptive_compressor.AdaptiveCompressor._adaptive_compress.__doc__.splitlines()[0])
-```
-
-Notes for the maintainer:
-
-* Python callers that swap the class in: `ambc.AdaptiveCompressor()` defaults to
-  one 4096-byte chunk size, native mode and methods {1, 3, 4, 9} (and says so once,
-  `ambc.DefaultsWarning`, at its first compress);
-  `AdaptiveCompressor.like_reference()` gives the reference's 8-candidate walk in
-  reference mode with its GPU-encodable stdlib codecs {1, 2, 3, 4, 5};
-  `like_reference(full_set=True)` adds bz2 / LZMA scored on the host.
-* One chunk size (`CHUNK_SIZE_CANDIDATES = [C]`): `mode=1` reproduces the
-  reference loop exactly (including its remainder-raw rule), `mode=0` decides each
-  C-byte chunk independently (the parallel mode used for throughput).
-* Several candidates (the reference's default list): `ambc_compress_multisize_ex`
-  runs `_pick_best_chunk_and_method`'s walk on the device.  With `out = NULL` the
-  body stays on the device and `ambc_fetch_body` copies it into a buffer of
-  exactly its size (`*out_len`).
-* Exactness of Huffman's `entropy < 7.0` gate at near-ties: the binding passes
-  numpy's own terms (`p * np.log2(p)` for p = c/C, c = 0..C) for every size
-  Huffman may take (`ent_full` / `ent_tail`, `ent_sizes` / `ent_tabs`).
-* Decoding on N GPUs (one process each): `ambc_split_body` cuts the body at package
-  boundaries into N balanced output ranges, each rank decodes its range into device
-  memory with `ambc_decompress_device`, and the ranges concatenate in rank order
-  (`ambc.distributed.decompress_sharded`).
-* For throughput keep inputs resident on the device and call `ambc_compress_device`
-  (bench.py does); host buffers from `ambc_host_alloc` (pinned) speed up the copies.
-
-The repository's own drop-in (`adaptive-compression_amd/adaptive_compressor.py`,
-re-exporting `ambc.AdaptiveCompressor`) does the same through `ambc/_lib.py`, plus
-multi-GPU sharding (`ambc/distributed.py`).

@@ -6,7 +6,9 @@ of the reference that are easiest to restate in Python:
 * ``decompress_body`` -- ``AdaptiveCompressor._adaptive_decompress``
   (adaptive_compressor.py:396-454) including every lenient path, with the C
   per-codec decoders and stdlib zlib/bz2/lzma for ids 5/6/7
-  (advanced_compression.py:83-96,124-137,187-200).
+  (advanced_compression.py:83-96,124-137,187-200), and id 8 (zstandard,
+  :236-250) restated over the system libzstd -- parity unpinned: the reference
+  holds no zstd fixture and python-zstandard is absent.
 * ``compress_file_bytes`` -- ``AdaptiveCompressor.compress``
   (adaptive_compressor.py:221-255) around the C body loop, with the reference's
   stats dicts (:457-532).
@@ -297,6 +299,73 @@ def _lzma_xz(d):
     return c.compress(d) + c.flush()
 
 
+_zstd = None
+
+
+def zstd_lib():
+    """The system libzstd (python-``zstandard``, the reference's id-8 library,
+    is absent here).  None when it does not load."""
+    global _zstd
+    if _zstd is None:
+        try:
+            z = C.CDLL("libzstd.so.1")
+        except OSError:
+            return None
+        z.ZSTD_getFrameContentSize.restype = C.c_ulonglong
+        z.ZSTD_getFrameContentSize.argtypes = [C.c_char_p, C.c_size_t]
+        z.ZSTD_findFrameCompressedSize.restype = C.c_size_t
+        z.ZSTD_findFrameCompressedSize.argtypes = [C.c_char_p, C.c_size_t]
+        z.ZSTD_decompress.restype = C.c_size_t
+        z.ZSTD_decompress.argtypes = [C.c_void_p, C.c_size_t, C.c_char_p, C.c_size_t]
+        z.ZSTD_compress.restype = C.c_size_t
+        z.ZSTD_compress.argtypes = [C.c_void_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_int]
+        z.ZSTD_compressBound.restype = C.c_size_t
+        z.ZSTD_compressBound.argtypes = [C.c_size_t]
+        z.ZSTD_isError.restype = C.c_uint
+        z.ZSTD_isError.argtypes = [C.c_size_t]
+        _zstd = z
+    return _zstd
+
+
+def zstd_compress(d, level=19):
+    """ZstdCompressor(level=19).compress (advanced_compression.py:224-234): one
+    frame carrying its content size."""
+    z = zstd_lib()
+    cap = z.ZSTD_compressBound(len(d))
+    out = C.create_string_buffer(max(cap, 1))
+    r = z.ZSTD_compress(out, cap, bytes(d), len(d), level)
+    if z.ZSTD_isError(r):
+        raise ValueError("zstd compress")
+    return out.raw[:r]
+
+
+def zstd_decompress(d, max_output_size):
+    """ZstdDecompressor().decompress(d, max_output_size=...) of python-zstandard
+    >= 0.15 (advanced_compression.py:240-241), restated on libzstd's one-shot
+    API: the FIRST frame only (trailing bytes ignored), sized by its header's
+    content size, or by max_output_size when the header has none; raises where
+    python-zstandard raises ZstdError."""
+    z = zstd_lib()
+    d = bytes(d)
+    cs = z.ZSTD_getFrameContentSize(d, len(d))
+    if cs == (1 << 64) - 2:
+        raise ValueError("error determining content size from frame header")
+    if cs == 0:
+        return b""
+    unknown = cs == (1 << 64) - 1
+    if unknown and max_output_size == 0:
+        raise ValueError("could not determine content size in frame header")
+    cap = max_output_size if unknown else cs
+    flen = z.ZSTD_findFrameCompressedSize(d, len(d))
+    if z.ZSTD_isError(flen):
+        raise ValueError("did not decompress full frame")
+    out = C.create_string_buffer(max(cap, 1))
+    r = z.ZSTD_decompress(out, cap, d[:flen], flen)
+    if z.ZSTD_isError(r) or (not unknown and r != cs):
+        raise ValueError("decompression error")
+    return out.raw[:r]
+
+
 def select_reference_set(chunk, ids, prefs=None):
     """_pick_best_chunk_and_method's per-size method loop (adaptive_compressor.py:
     559-579) over the reference's stdlib set {1..7}: should_use, compress, keep the
@@ -325,6 +394,10 @@ def select_reference_set(chunk, ids, prefs=None):
             if n < 8192 or np_entropy(chunk) >= 8.0:
                 continue
             payload = _lzma_xz(chunk)
+        elif mid == 8:
+            if n < 512 or np_entropy(chunk) > 8.2:
+                continue
+            payload = zstd_compress(chunk)
         else:
             raise ValueError(mid)
         if len(payload) + 18 < best:
@@ -334,7 +407,7 @@ def select_reference_set(chunk, ids, prefs=None):
 
 def _encode_reference_set(mid, chunk):
     return {1: rle_encode, 2: dict_encode, 3: huff_encode, 5: deflate_encode,
-            6: lambda d: bz2.compress(d, compresslevel=9), 7: _lzma_xz}[mid](chunk)
+            6: lambda d: bz2.compress(d, compresslevel=9), 7: _lzma_xz, 8: zstd_compress}[mid](chunk)
 
 
 def compress_body_multisize(data, sizes, methods=(1, 3, 4, 255), prefs=None, deflate="gd",
@@ -480,11 +553,12 @@ def decode_chunk(mid, payload, orig):
               4: "orc_delta_decode", 9: "orc_lz4_frame_decode"}[mid]
         r = _c_dec(fn, payload, orig)
         return bytes(orig) if r is None else r
-    if mid in (5, 6, 7):
+    if mid in (5, 6, 7, 8):
         if not payload:
             return b""
         try:
-            raw = {5: zlib.decompress, 6: bz2.decompress, 7: lzma.decompress}[mid](payload)
+            raw = {5: zlib.decompress, 6: bz2.decompress, 7: lzma.decompress,
+                   8: lambda b: zstd_decompress(b, orig)}[mid](payload)
             return _pad_trunc(raw, orig)
         except Exception:  # noqa: BLE001 -- reference wrappers return zeros
             return bytes(orig)

@@ -74,3 +74,41 @@ def test_shard_range_host_only():
     assert lib.ambc_shard_range(32 << 30, 8192, 8, 7, C.byref(b), C.byref(e)) == 0
     assert (b.value, e.value) == (28 << 30, 32 << 30)
     assert lib.ambc_shard_range(100, 16, 0, 0, C.byref(b), C.byref(e)) == _lib.AMBC_E_INVAL
+
+
+def test_binding_module_mirrors_the_abi():
+    """integration/ambc_binding.py (the reference-side binding INTEGRATION.md
+    quotes) declares the same struct layouts as include/ambc.h / ambc._lib, loads
+    the library and, without a device, fails loudly at bind time."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "integration"))
+    import ambc_binding as B
+    from ambc import _lib
+    for a, b in ((B.Params, _lib.Params), (B.Stats, _lib.Stats), (B.HostChunk, _lib.HostChunk)):
+        assert C.sizeof(a) == C.sizeof(b)
+        assert [f[0] for f in a._fields_] == [f[0] for f in b._fields_]
+    from ambc.hostcodecs import HostCodecs
+    assert C.sizeof(B.HostCodecs) == C.sizeof(HostCodecs)
+    lib = B.load_library()
+    assert lib.ambc_compress_bound(4096, 4096) == 4096 + 18 + 16
+    with open(os.path.join(REPO, "INTEGRATION.md")) as f:
+        doc = f.read()
+    assert "integration/ambc_binding.py" in doc
+    if not gpu_present():
+        class K:
+            def _adaptive_compress(self, d):
+                return d
+
+            def _adaptive_decompress(self, d, n):
+                return d
+        with pytest.raises(RuntimeError):
+            B.bind(K)
+        assert K._adaptive_compress(None, b"x") == b"x"
+
+
+def test_integration_doc_quotes_the_binding_verbatim():
+    with open(os.path.join(REPO, "INTEGRATION.md")) as f:
+        doc = f.read()
+    with open(os.path.join(REPO, "integration", "ambc_binding.py")) as f:
+        src = f.read()
+    assert "```python\n" + src + "```" in doc

@@ -271,6 +271,43 @@ def test_in_place_tail_chunks(ctx, chunk):
             d_out.free()
 
 
+@pytest.mark.parametrize("deflate", ["v1", "zlib9"])
+@pytest.mark.parametrize("chunk", [4096, 8192, 16384, 32768, 65536])
+def test_in_place_tail_chunks_deflate(ctx, chunk, deflate):
+    """The in-place reads of id 5's encoders -- k_deflate's in-place variants
+    (4-8 KiB) and its device-scratch variants (16-64 KiB), k_z9_parse and
+    k_z9_parse_big -- on short last chunks: a device-resident input that ends
+    exactly 64 bytes before its allocation (FLAG_INPUT_PADDED), bodies equal to
+    the oracle's (system zlib level 9 for zlib9, "ambc-deflate v1" otherwise)."""
+    from ambc import _lib
+    rnd = random.Random(chunk + 7)
+    text = synth.generate(3 * chunk, 43)
+    tails = [bytes(100), bytes([9]) * 777, text[:150], text[:chunk - 1],
+             bytes(rnd.randrange(4) for _ in range(300)), bytes(range(128)) * 2 + bytes(40), text[:65]]
+    methods = (1, 3, 4, 5)
+    odef = "zlib" if deflate == "zlib9" else "gd"
+    for tail in tails:
+        data = text[:2 * chunk] + tail
+        n = len(data)
+        comp = _compressor(chunk_size=chunk, mode="native", methods=methods, deflate=deflate)
+        nat, _ = orc.compress_body(data, orc.make_params(chunk, "native", methods, n_total=n, deflate=odef))
+        assert comp._adaptive_compress(data) == nat, (chunk, len(tail))
+        p, keep = comp._params(n)           # (keep: the entropy tables p points at)
+        p.flags |= _lib.FLAG_INPUT_PADDED
+        d_in = _lib.DeviceBuffer(ctx, n + 64)
+        cap = ctx.lib.ambc_compress_bound(n, chunk)
+        d_out = _lib.DeviceBuffer(ctx, cap + 64)
+        try:
+            d_in.upload(data + bytes(64))
+            olen, st = C.c_uint64(), _lib.Stats()
+            _lib.check(ctx.lib.ambc_compress_device(ctx.h, 0, d_in.ptr, n, C.byref(p), d_out.ptr, cap,
+                                                    C.byref(olen), C.byref(st), None), ctx.lib)
+            assert bytes(d_out.download(olen.value)) == nat, (chunk, len(tail), "device")
+        finally:
+            d_in.free()
+            d_out.free()
+
+
 def test_random_edge_inputs(ctx):
     rnd = random.Random(5)
     pieces = [bytes(4096), bytes([7]) * 5000, os.urandom(9000), b"abc" * 3000,

@@ -1,0 +1,149 @@
+"""The reference's library-codec plugins on the CPU (advanced_compression.py:71-261):
+DEFLATE's should_use gate (:98-107), the bz2 / LZMA / zstd gates at their
+entropy thresholds, and id 8 (ZstdCompression over the system libzstd, since
+python-zstandard is absent) against the oracle's restatement of
+python-zstandard's decompress semantics (oracle.zstd_decompress): valid frames,
+frames without a content size, damaged and truncated frames, trailing bytes,
+several frames, skippable frames, empty payloads, orig shorter / longer than the
+frame.  Parity of id 8 is unpinned: the reference holds no zstd fixture."""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+sys.path.insert(0, os.path.join(REPO, "adaptive-compression_amd"))
+
+from oracle import oracle as orc  # noqa: E402
+from oracle import synth  # noqa: E402
+
+needs_zstd = pytest.mark.skipif(orc.zstd_lib() is None, reason="libzstd.so.1 not loadable")
+
+
+def _gate_inputs():
+    rng = np.random.default_rng(11)
+    out = [b"", b"x" * 10, b"x" * 63, b"x" * 64, bytes(range(64)), bytes(range(256)),
+           bytes(range(256)) * 4, bytes(range(256)) * 40, b"a" * 511, b"a" * 512,
+           b"a" * 1023, b"a" * 1024, b"a" * 8191, b"a" * 8192]
+    for k in (2, 100, 200, 210, 230, 250, 256):
+        for n in (63, 64, 600, 1100, 9000):
+            out.append(rng.integers(0, k, n, dtype=np.uint8).tobytes())
+    out += [synth.generate(20000, 4), synth.random_bytes(9000, 5)]
+    return out
+
+
+def test_deflate_should_use_matches_reference_gate():
+    """DeflateCompression.should_use: n < 64 -> False, entropy >= 8.0 -> False
+    (advanced_compression.py:98-107), entropy from numpy as the reference."""
+    from ambc.methods import DeflateCompression
+    m = DeflateCompression()
+    seen = set()
+    for d in _gate_inputs():
+        want = len(d) >= 64 and orc.np_entropy(d) < 8.0
+        assert m.should_use(d) == want, len(d)
+        seen.add(want)
+    assert seen == {True, False}
+    assert not m.should_use(bytes(range(256)))            # entropy exactly 8.0
+    assert not m.should_use(b"x" * 63) and m.should_use(b"x" * 64)
+
+
+def test_library_gates_match_oracle_entropy():
+    from ambc.methods import Bzip2Compression, LZMACompression, ZstdCompression
+    gates = {6: (Bzip2Compression(), lambda d: len(d) >= 1024 and orc.np_entropy(d) < 7.7),
+             7: (LZMACompression(), lambda d: len(d) >= 8192 and orc.np_entropy(d) < 8.0),
+             8: (ZstdCompression(), lambda d: len(d) >= 512 and not orc.np_entropy(d) > 8.2)}
+    for mid, (m, want) in gates.items():
+        for d in _gate_inputs():
+            assert m.should_use(d) == want(d), (mid, len(d))
+
+
+def _zstd_no_size(data, level=19):
+    """a frame WITHOUT its content size (ZSTD_c_contentSizeFlag = 0)."""
+    z = C.CDLL("libzstd.so.1")
+    z.ZSTD_createCCtx.restype = C.c_void_p
+    z.ZSTD_CCtx_setParameter.argtypes = [C.c_void_p, C.c_int, C.c_int]
+    z.ZSTD_CCtx_setParameter.restype = C.c_size_t
+    z.ZSTD_compress2.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_char_p, C.c_size_t]
+    z.ZSTD_compress2.restype = C.c_size_t
+    z.ZSTD_freeCCtx.argtypes = [C.c_void_p]
+    cctx = z.ZSTD_createCCtx()
+    z.ZSTD_CCtx_setParameter(cctx, 100, level)          # ZSTD_c_compressionLevel
+    z.ZSTD_CCtx_setParameter(cctx, 200, 0)              # ZSTD_c_contentSizeFlag
+    out = C.create_string_buffer(len(data) + 1024)
+    r = z.ZSTD_compress2(cctx, out, len(data) + 1024, data, len(data))
+    z.ZSTD_freeCCtx(cctx)
+    return out.raw[:r]
+
+
+def zstd_cases():
+    """(payload, orig) pairs covering python-zstandard's decode paths."""
+    a = synth.generate(30000, 21)
+    b = b"hello zstd " * 700
+    fa, fb = orc.zstd_compress(a), orc.zstd_compress(b)
+    na = _zstd_no_size(a)
+    flip = bytearray(fa)
+    flip[len(flip) // 2] ^= 0x5A
+    skippable = (0x184D2A50).to_bytes(4, "little") + (6).to_bytes(4, "little") + b"ignore"
+    return [
+        (fa, len(a)), (fa, len(a) - 1000), (fa, len(a) + 777), (fa, 1),
+        (fb, len(b)), (fb + fa, len(b) + len(a)),            # second frame ignored
+        (fa + b"trailing garbage", len(a)),
+        (fa[:-5], len(a)), (fa[:20], len(a)), (fa[:3], 100),   # truncated
+        (bytes(flip), len(a)),                                 # damaged
+        (na, len(a)), (na, len(a) - 1), (na, len(a) + 5), (na, 0),  # no content size
+        (skippable + fa, len(a)), (b"\x28\xb5\x2f\xfd", 50),  # skippable / header only
+        (b"not a zstd frame at all", 40), (b"", 10), (orc.zstd_compress(b""), 0),
+        (orc.zstd_compress(b""), 7),
+    ]
+
+
+@needs_zstd
+def test_zstd_plugin_matches_oracle_restatement():
+    from ambc.methods import ZstdCompression
+    m = ZstdCompression()
+    assert m.type_id == 8
+    for i, (payload, orig) in enumerate(zstd_cases()):
+        assert m.decompress(payload, orig) == orc.decode_chunk(8, payload, orig), i
+    d = synth.generate(50000, 22)
+    c = m.compress(d)
+    assert c == orc.zstd_compress(d)
+    assert m.decompress(c, len(d)) == d
+    assert m.compress(b"") == b""
+
+
+@needs_zstd
+def test_zstd_registered_like_reference_with_zstandard():
+    """With its requirements installed the reference registers id 8 (adaptive_compressor.
+    py:148-150); the drop-in does when libzstd loads, and scores it on the host."""
+    import advanced_compression
+    from ambc.methods import DECODE_METHODS
+    from ambc.registry import HOST_SCORED_IDS
+    assert advanced_compression.HAS_ZSTD and 8 in DECODE_METHODS and 8 in HOST_SCORED_IDS
+
+
+@needs_zstd
+def test_host_scorer_with_zstd_matches_oracle():
+    from ambc.hostcodecs import HostScorer
+    from ambc.methods import Bzip2Compression, LZMACompression, ZstdCompression
+    from ambc.registry import METHOD_CHUNK_PREFS
+    data = synth.generate(140000, 23) + synth.random_bytes(20000, 24) * 2
+    sc = HostScorer(data, [ZstdCompression(), LZMACompression(), Bzip2Compression()],
+                    dict(METHOD_CHUNK_PREFS), workers=4)
+    wins = set()
+    try:
+        for s in (512, 1024, 4096, 8192, 16384, 65536):
+            for pos in (0, 3 * 1024, 100 * 1024, 140000):
+                if pos + s > len(data):
+                    continue
+                w, pay = sc.best(pos, s)
+                ow, ol = orc.select_reference_set(data[pos:pos + s], (6, 7, 8, 255))
+                assert (w or 255) == ow, (pos, s)
+                if w:
+                    assert len(pay) == ol
+                    wins.add(w)
+    finally:
+        sc.close()
+    assert 8 in wins
