@@ -224,6 +224,9 @@ class Context:
             raise AmbcUnavailable(last_error(self.lib))
         self.h = h
         self.devices = devs
+        # one call at a time per context: its device workspaces (and a body that
+        # ambc_compress_multisize(out=NULL) leaves for ambc_fetch_body) are shared
+        self.lock = threading.RLock()
 
     def close(self):
         if getattr(self, "h", None):

@@ -271,22 +271,28 @@ class AdaptiveCompressor:
         # out = NULL: the body stays on the device until it is fetched into a
         # bytes object of exactly its size (see _adaptive_decompress for why
         # writing into a fresh, private bytes object is sound)
-        try:
-            rc = ctx.lib.ambc_compress_multisize_ex(ctx.h, _lib.addr(src), n, C.byref(p), carr, len(cands),
-                                                    ent_sizes, ent_ptrs, len(tabs),
-                                                    C.addressof(host.struct) if host else None, None, 0,
-                                                    C.byref(olen), C.byref(st))
-        finally:
-            if host:
-                host.close()
-        if host and host.error is not None:
-            raise host.error
-        if rc == _lib.AMBC_E_RANGE:
-            raise struct.error("argument out of range")
-        if rc == _lib.AMBC_E_INVAL:
-            raise NotImplementedError(_lib.last_error(ctx.lib))
-        _lib.check(rc, ctx.lib)
-        del tabs
+        with ctx.lock:                           # the device body below is the context's
+            try:
+                rc = ctx.lib.ambc_compress_multisize_ex(ctx.h, _lib.addr(src), n, C.byref(p), carr, len(cands),
+                                                        ent_sizes, ent_ptrs, len(tabs),
+                                                        C.addressof(host.struct) if host else None, None, 0,
+                                                        C.byref(olen), C.byref(st))
+            finally:
+                if host:
+                    host.close()
+            if host and host.error is not None:
+                raise host.error
+            if rc == _lib.AMBC_E_RANGE:
+                raise struct.error("argument out of range")
+            if rc == _lib.AMBC_E_INVAL:
+                raise NotImplementedError(_lib.last_error(ctx.lib))
+            _lib.check(rc, ctx.lib)
+            del tabs
+            out = bytes(olen.value)
+            if sys.getrefcount(out) != 2:
+                raise RuntimeError("body buffer is shared: refusing to write into it")
+            _lib.check(ctx.lib.ambc_fetch_body(ctx.h, C.cast(C.c_char_p(out), C.POINTER(C.c_uint8)),
+                                               olen.value), ctx.lib)
         self._last_device_stats = st
         self.chunk_stats = {
             "total_chunks": int(st.total_chunks), "compressed_chunks": int(st.compressed_chunks),
@@ -296,11 +302,6 @@ class AdaptiveCompressor:
             "compressed_size_without_overhead": int(st.payload_bytes),
             "overhead_bytes": int(st.overhead_bytes)}
         self.method_usage_ids = [m.type_id for m in self.compression_methods]
-        out = bytes(olen.value)
-        if sys.getrefcount(out) != 2:
-            raise RuntimeError("body buffer is shared: refusing to write into it")
-        _lib.check(ctx.lib.ambc_fetch_body(ctx.h, C.cast(C.c_char_p(out), C.POINTER(C.c_uint8)), olen.value),
-                   ctx.lib)
         return out
 
     def _adaptive_compress(self, file_data):

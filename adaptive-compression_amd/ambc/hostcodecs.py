@@ -1,6 +1,7 @@
 """Host-scored methods of the multi-size walk: the reference's library codecs
-that have no GPU encoder -- BZIP2 (id 6) and LZMA (id 7), advanced_compression.py:
-112-213 -- evaluated on host threads beside the device's encoders.
+that have no GPU encoder -- BZIP2 (id 6), LZMA (id 7) and ZStandard (id 8),
+advanced_compression.py:112-261 -- evaluated on host threads beside the device's
+encoders.
 
 ambc_compress_multisize_ex calls ``eval`` once per walk round with the (position,
 size) pairs the round evaluates (while the device encodes the same pairs) and
@@ -10,9 +11,15 @@ answer is the reference's per-size method loop restricted to these codecs
 strict minimum of len + 18 below the chunk's own length, ids ascending; the
 library then joins it with the GPU's winner in id order.  bz2 / lzma release the
 GIL while they compress, so a thread pool runs the pairs in parallel.
+
+Memory: an LZMA compressor with the reference's 16 MiB dictionary holds about
+190 MiB of encoder state, so at most ``LZMA_JOBS`` (4) of them run at once --
+the rest of the pool keeps bz2 / zstd busy meanwhile; a walk therefore peaks
+near 0.8 GiB of host memory for LZMA (like_reference(full_set=True)).
 """
 import ctypes as C
 import os
+import threading
 from concurrent.futures import ThreadPoolExecutor
 
 EVAL_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), C.c_uint32,
@@ -30,6 +37,7 @@ class HostScorer:
     instances of the host-scored ids; ``prefs``: method_chunk_prefs."""
 
     CACHE_BYTES = 256 << 20          # payloads kept from eval for emit (beyond: recomputed)
+    LZMA_JOBS = 4                    # concurrent LZMA compressors (~190 MiB of state each)
 
     def __init__(self, data, methods, prefs, workers=None):
         self.data = data
@@ -39,6 +47,7 @@ class HostScorer:
         self.cached = 0
         self.error = None
         self.pool = ThreadPoolExecutor(workers or min(32, os.cpu_count() or 4))
+        self._lzma = threading.BoundedSemaphore(self.LZMA_JOBS)
         # the callbacks must outlive the call: keep them on the instance
         self._eval_cb = EVAL_FN(self._eval)
         self._emit_cb = EMIT_FN(self._emit)
@@ -57,7 +66,11 @@ class HostScorer:
             if not lo <= size <= hi or not m.should_use(chunk):
                 continue
             try:
-                c = m.compress(chunk)
+                if m.type_id == 7:
+                    with self._lzma:
+                        c = m.compress(chunk)
+                else:
+                    c = m.compress(chunk)
             except Exception:  # noqa: BLE001 -- the reference's loop skips a raising method
                 continue
             if len(c) < wl:

@@ -110,7 +110,7 @@ void ambc_destroy(ambc_ctx* ctx) {
         for (Buf* b : {&d.in, &d.out, &d.slots, &d.plen, &d.ids, &d.sizes, &d.off, &d.scan_tmp,
                        &d.acc, &d.ent_full, &d.ent_tail, &d.body, &d.jobs, &d.produced, &d.dout,
                        &d.scratch, &d.seg, &d.list, &d.bestpre, &d.gdseq, &d.pending, &d.z9rec, &d.z9scr, &d.segbase, &d.coll, &d.dstat, &d.placed,
-                       &d.inffix})
+                       &d.inffix, &d.ms_out})
             b->release();
         for (auto& b : d.msb) b.release();
         d.dw.release();
@@ -241,8 +241,13 @@ static uint32_t compact_resident() {
     return r;
 }
 
-int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params* p, uint8_t* d_out,
-                      uint64_t out_cap, uint64_t* out_len, ambc_stats* st, const ShardInfo* si) {
+// compress_on's body.  `armed` is set once the pre-flight checks passed (every
+// rank of a sharded call fails those alike) and `joined` once the call entered
+// reference mode's remainder exchange: compress_on joins that exchange on behalf
+// of any later failure, so that no peer waits in it for a rank that left.
+static int compress_on_body(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params* p, uint8_t* d_out,
+                            uint64_t out_cap, uint64_t* out_len, ambc_stats* st, const ShardInfo* si,
+                            bool& armed, bool& joined) {
     int rc = check_params(p);
     if (rc) return rc;
     const uint32_t C = p->chunk_size;
@@ -252,6 +257,9 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
     const bool end = !(p->flags & AMBC_FLAG_NO_END_CHUNK);
     const uint64_t bound = ambc_compress_bound(n, C) - (end ? 0 : END_CHUNK);
     if (out_cap < bound) return fail(AMBC_E_CAPACITY, "device output capacity < ambc_compress_bound");
+    armed = true;
+    if (const char* e = getenv("AMBC_TEST_FAIL_RANK"))   // failure injection for the sharded tests
+        if (si && atoi(e) == si->rank) return fail(AMBC_E_DEVICE, "injected failure (AMBC_TEST_FAIL_RANK)");
     HIPCHK(hipSetDevice(d.id));
     hipStream_t s = d.stream;
     const uint64_t t0 = now_ns();
@@ -452,13 +460,7 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
         return finish_compress(d, p, M, Remainder(), d_out, body_len, acc, d_in, end, out_len, st, t0);
     }
     rc = encode_range(ea);
-    if (rc) {
-        if (si && p->mode == AMBC_MODE_REFERENCE) {   // the peers wait in the remainder exchange
-            uint64_t g = UINT64_MAX;
-            (void)shard_allreduce_min(si->t, &g, rc);
-        }
-        return rc;
-    }
+    if (rc) return rc;
     HIPCHK(hipEventRecord(d.ev[1], s));
     if (ea.stamps) {
         stamps.resize((size_t)M * 8);
@@ -538,6 +540,7 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
             k0 = si->k0;
             n_total = si->n_total;
             if (g != UINT64_MAX) g += k0;
+            joined = true;
             int rc2 = shard_allreduce_min(si->t, &g, AMBC_OK);  // AllReduce(MIN) across the ranks
             if (rc2) return rc2;
         }
@@ -591,6 +594,19 @@ int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params
     HIPCHK(hipStreamSynchronize(s));
     TRACE("stats done body_len=%llu", (unsigned long long)body_len);
     return finish_compress(d, p, R, rm, d_out, body_len, acc, d_in, end, out_len, st, t0);
+}
+
+int ambc::compress_on(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params* p, uint8_t* d_out,
+                      uint64_t out_cap, uint64_t* out_len, ambc_stats* st, const ShardInfo* si) {
+    bool armed = false, joined = false;
+    const int rc = compress_on_body(d, d_in, n, p, d_out, out_cap, out_len, st, si, armed, joined);
+    if (rc && armed && !joined && si && p->mode == AMBC_MODE_REFERENCE) {
+        // every failure after the pre-flight (buffers, launches, an asynchronous
+        // kernel fault seen at a sync) joins the remainder exchange the peers wait in
+        uint64_t g = UINT64_MAX;
+        (void)shard_allreduce_min(si->t, &g, rc);
+    }
+    return rc;
 }
 
 extern "C" int ambc_compress_device(ambc_ctx* ctx, int dev, const void* d_in, uint64_t n,

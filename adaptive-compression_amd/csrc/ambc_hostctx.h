@@ -145,7 +145,8 @@ struct Dev {
     uint32_t ms_steps = 0;      // last multi-size walk: batched evaluation rounds,
     uint64_t ms_evaluated = 0;  //   chunk encodes they ran,
     uint64_t ms_walk_ns = 0, ms_emit_ns = 0;  // and the time of the walk / of the final encode
-    uint64_t ms_body = 0;       // a multi-size body kept in `out` for ambc_fetch_body (0: none)
+    Buf ms_out;                 // the multi-size walk's body (its own buffer: no other call writes it)
+    uint64_t ms_body = 0;       // a multi-size body kept in `ms_out` for ambc_fetch_body (0: none)
     uint64_t t_encode = 0, t_scan = 0, t_compact = 0;
     uint32_t n_launch = 1;      // k_encode launches of the last compress call (pipelined segments)
     hipStream_t cs = nullptr;   // scan + compaction of pipelined segments
@@ -169,6 +170,7 @@ struct ShardInfo {
     Transport* t;
     uint64_t k0;        // global index of this shard's first chunk
     uint64_t n_total;   // bytes of the whole logical input
+    int rank;           // this shard's rank in t
 };
 
 }  // namespace ambc

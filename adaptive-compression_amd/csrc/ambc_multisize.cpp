@@ -243,6 +243,7 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
     if (nc > 32) return fail(AMBC_E_INVAL, "at most 32 distinct candidate sizes");
     const uint64_t t0 = now_ns();
     Dev& d = ctx->devs[0];
+    d.ms_body = 0;                 // a body left by an earlier call is gone from here on
     HIPCHK(hipSetDevice(d.id));
     hipStream_t s = d.stream;
     std::map<uint32_t, const double*> ent;
@@ -659,8 +660,8 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
     if (out && out_cap < body) return fail(AMBC_E_CAPACITY, "output capacity below the body size");
 
     // ---- the chosen chunks, encoded again per size (all methods, bytes), into the body ----
-    HIPCHK(d.out.ensure(body + 64));
-    uint8_t* d_body = d.out.as<uint8_t>();
+    HIPCHK(d.ms_out.ensure(body + 64));
+    uint8_t* d_body = d.ms_out.as<uint8_t>();
     const uint64_t te = now_ns();
     std::map<uint32_t, std::vector<size_t>> groups;
     for (size_t i = 0; i < path.size(); i++)
@@ -775,8 +776,8 @@ extern "C" int ambc_fetch_body(ambc_ctx* ctx, uint8_t* out, uint64_t cap) {
     HIPCHK(hipSetDevice(d.id));
     const uint64_t body = d.ms_body;
     d.ms_body = 0;
-    if (body >= kStageMin) return copy_staged(d, out, d.out.p, body, false);
-    HIPCHK(hipMemcpy(out, d.out.p, body, hipMemcpyDeviceToHost));
+    if (body >= kStageMin) return copy_staged(d, out, d.ms_out.p, body, false);
+    HIPCHK(hipMemcpy(out, d.ms_out.p, body, hipMemcpyDeviceToHost));
     return AMBC_OK;
 }
 

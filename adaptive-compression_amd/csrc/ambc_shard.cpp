@@ -297,7 +297,7 @@ static int shard_compress(Dev& d, Transport& t, const uint8_t* d_shard, uint64_t
                                         : AMBC_OK;
         if ((rc = all_ok(t, pre))) return rc;
     }
-    ShardInfo si{&t, k0, n_total};
+    ShardInfo si{&t, k0, n_total, t.r};
     uint64_t len = 0;
     ambc_stats lst{};
     rc = compress_on(d, d_shard, b1 - b0, &q, d_out, out_cap, &len, &lst, t.W > 1 ? &si : nullptr);
@@ -478,7 +478,8 @@ static int compress_multi_slabs(ambc_ctx* ctx, std::vector<std::unique_ptr<Trans
     std::vector<uint64_t> kern(G, 0), total(G, 0);
     auto slab_len = [&](uint64_t s) { return s < ns ? std::min(SLAB, n - s * SLAB) : 0ull; };
     int rc = run_ranks(ts, [&](int g) -> int {
-        Dev& d = ctx->devs[g];
+      Dev& d = ctx->devs[g];
+      auto rank_body = [&]() -> int {
         Transport& t = *ts[g];
         HIPCHK(hipSetDevice(d.id));
         HIPCHK(d.in.ensure(2 * (SLAB + 64)));
@@ -549,6 +550,17 @@ static int compress_multi_slabs(ambc_ctx* ctx, std::vector<std::unique_ptr<Trans
         sst[g] = tot;
         total[g] = base;
         return AMBC_OK;
+      };
+      const int r = rank_body();
+      // every exit, failures included: no copy on the caller's buffers (the next
+      // slab's H2D from `in`, an earlier round's D2H into `out`) outlives the call
+      (void)hipSetDevice(d.id);
+      const hipError_t e0 = hipStreamSynchronize(d.xs[0]), e1 = hipStreamSynchronize(d.xs[1]),
+                       e2 = hipStreamSynchronize(d.stream);
+      if (r) return r;
+      for (hipError_t e : {e0, e1, e2})
+          if (e != hipSuccess) return fail(AMBC_E_DEVICE, std::string("slab pipeline sync: ") + hipGetErrorString(e));
+      return AMBC_OK;
     });
     if (rc) return rc;
     *out_len = total[0];
