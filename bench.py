@@ -75,6 +75,12 @@ def parse():
     ap.add_argument("--walk-bytes", type=int, default=256 << 20,
                     help="multi-size walk leg (the reference's eight candidates) on this prefix; 0: skip")
     ap.add_argument("--walk-methods", default="1,3,4,9;1,2,3,4,5")
+    ap.add_argument("--ref-walk-bytes", type=int, default=64 << 20,
+                    help="the reference's default compress() path (AdaptiveCompressor.like_reference(): "
+                         "eight candidates, {1,2,3,4,5}, id 5 as zlib-9's bytes) on this many bytes; 0: skip")
+    ap.add_argument("--ref-walk-check-bytes", type=int, default=4 << 20,
+                    help="prefix on which the cpu_baseline leg times the oracle's reference walk and "
+                         "compares its body with the GPU's")
     ap.add_argument("--api-bytes", type=int, default=256 << 20,
                     help="input size of the AdaptiveCompressor.compress(path, path) leg (0: skip)")
     a = ap.parse_args()
@@ -320,6 +326,58 @@ def alt_leg(lib, ctx, d_in, n, args, methods, steps, zlib9=False):
                        "header_walk_ms": round(ds.walk_ns / 1e6, 3), "host_api_GBps": round(n / dwall / 1e9, 3)}}
 
 
+def ref_walk_leg(ctx, nbytes):
+    """The reference's own default compress() path at the reference's bytes:
+    AdaptiveCompressor.like_reference() -- the eight CHUNK_SIZE_CANDIDATES walk
+    (adaptive_compressor.py:61-62,537-590) with {1,2,3,4,5}, id 5 as
+    zlib.compress(chunk, 9)'s own bytes (advanced_compression.py:76-81) at every
+    size -- host bytes in and out, second call timed, bit-exact decode.  Input:
+    multisize_bench's mixed segments (on the headline's stream the walk stores
+    the rest raw at the first random byte run)."""
+    from ambc import AdaptiveCompressor
+    sys.path.insert(0, os.path.join(REPO, "scripts"))
+    from multisize_bench import mixed
+    data = mixed(nbytes, 7)
+    comp = AdaptiveCompressor.like_reference()
+    comp._adaptive_compress(data)
+    t = time.perf_counter()
+    body = comp._adaptive_compress(data)
+    dt = time.perf_counter() - t
+    steps, ev, wns, ens = C.c_uint32(), C.c_uint64(), C.c_uint64(), C.c_uint64()
+    ctx.lib.ambc_last_multisize_info(comp._ctx().h, C.byref(steps), C.byref(ev), C.byref(wns), C.byref(ens))
+    ok = comp._adaptive_decompress(body, nbytes) == data
+    return {"path": "AdaptiveCompressor.like_reference(): the reference's default compress() walk",
+            "methods": [m.type_id for m in comp.compression_methods], "deflate": comp.deflate,
+            "candidates": comp.CHUNK_SIZE_CANDIDATES, "bytes": nbytes,
+            "input": "runs / text / skewed random, 8-64 KiB segments (scripts/multisize_bench.py mixed, seed 7)",
+            "GBps": round(nbytes / dt / 1e9, 3), "seconds": round(dt, 4), "ratio": round(len(body) / nbytes, 5),
+            "packages": comp.chunk_stats["total_chunks"], "method_usage": comp.chunk_stats["method_usage"],
+            "walk_rounds": steps.value, "chunk_encodes": ev.value,
+            "walk_ms": round(wns.value / 1e6, 2), "final_encode_ms": round(ens.value / 1e6, 2),
+            "round_trip_bit_exact": ok}
+
+
+def cpu_baseline_ref_walk(nbytes):
+    """cpu_baseline leg of the like_reference() walk: the oracle's restatement of the
+    reference's walk (oracle.compress_body_multisize with the system zlib at level
+    9 -- one host core, the reference is single-threaded) timed on a bounded prefix
+    of the same input, and its body compared with the GPU's body of that prefix."""
+    from ambc import AdaptiveCompressor
+    from oracle import oracle as orc
+    sys.path.insert(0, os.path.join(REPO, "scripts"))
+    from multisize_bench import mixed
+    data = mixed(nbytes, 7)
+    comp = AdaptiveCompressor.like_reference()
+    body = comp._adaptive_compress(data)
+    t = time.perf_counter()
+    ref, _ = orc.compress_body_multisize(data, comp.CHUNK_SIZE_CANDIDATES, (1, 2, 3, 4, 5, 255), deflate="zlib")
+    dt = time.perf_counter() - t
+    return {"value": round(nbytes / dt / 1e9, 5), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"first {nbytes} bytes of the like_reference leg's input, oracle walk (C restatement, "
+                      "system zlib level 9)", "seconds": round(dt, 3),
+            "gpu_body_equals_oracle": ref == body}
+
+
 def walk_leg(ctx, nbytes, methods):
     """The reference's default API path: _adaptive_compress with its eight
     CHUNK_SIZE_CANDIDATES (the multi-size walk, ambc_compress_multisize), host
@@ -519,6 +577,10 @@ def main():
                 w = walk_leg(ctx, args.walk_bytes, [int(x) for x in ms.split(",")])
                 log(f"walk: {w}")
                 walks.append(w)
+    ref_walk = None
+    if rank == 0 and world == 1 and args.ref_walk_bytes:
+        ref_walk = ref_walk_leg(ctx, args.ref_walk_bytes)
+        log(f"like_reference walk: {ref_walk}")
     if rank == 0 and world == 1 and args.api_bytes:
         api = api_leg(args.api_bytes, args.chunk, args.mode, methods, args.seed)
         log(f"api: {api}")
@@ -548,7 +610,7 @@ def main():
                        "step_ms_p50": round(percentile(step_s, 50) * 1e3, 3),
                        "step_ms_p90": round(percentile(step_s, 90) * 1e3, 3),
                        "e2e_pinned_host": e2e, "api_file": api, "alt_method_sets": alts,
-                       "multisize_walk": walks},
+                       "multisize_walk": walks, "like_reference_walk": ref_walk},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
@@ -560,6 +622,8 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
             result["cpu_baseline"] = cpu_baseline(args, threads, methods)
+            if ref_walk is not None and args.ref_walk_check_bytes:
+                result["cpu_baseline"]["like_reference_walk"] = cpu_baseline_ref_walk(args.ref_walk_check_bytes)
         else:
             result["cpu_baseline"] = None
         print(json.dumps(result), flush=True)
