@@ -31,6 +31,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <new>
 #include <numeric>
 
 #include "ambc_hostctx.h"
@@ -160,52 +161,52 @@ struct Decision {
 // Per walk position (pos = idx * g) and candidate index i: the evaluation of
 // size S_i = min(cands[i], n - pos).  Part "O": the winner of the size's methods
 // other than LZ4 -- or, at the position's LZ4 size M, of all of them; part "L":
-// LZ4's block for S_i < M, from M's launch.  Positions live in pages of 256,
-// allocated when a walk first reaches them.
+// LZ4's block for S_i < M, from M's launch.  One record per position (its state
+// and its nc candidates contiguous: two or three cache lines for the reference's
+// eight candidates, where a field-per-array layout touched a dozen), in pages of
+// 256 positions allocated when a walk first reaches them.
 struct PosTable {
     static constexpr uint32_t PB = 8;
-    struct Page {
-        std::vector<uint32_t> plen, lz, hlen;
-        std::vector<uint8_t> id, hid;               // (hid / hlen: the host codecs' winner, 0: none)
-        std::vector<uint32_t> have, req;            // bit i: part O of candidate i known / asked for
-        std::vector<uint32_t> hhave, hreq;          //   ... the host part of candidate i
-        std::vector<uint8_t> mhave, mreq, decided;  // M's launch known / asked for; decision taken
-        std::vector<Decision> dec;
+    struct Cand {
+        uint32_t plen = 0, lz = 0xFFFFFFFFu, hlen = 0;
+        uint8_t id = 255, hid = 0;                  // (hid / hlen: the host codecs' winner, 0: none)
+        uint16_t pad = 0;
     };
+    struct Rec {
+        uint32_t have = 0, req = 0;                 // bit i: part O of candidate i known / asked for
+        uint32_t hhave = 0, hreq = 0;               //   ... the host part of candidate i
+        uint8_t mhave = 0, mreq = 0, decided = 0;   // M's launch known / asked for; decision taken
+        uint8_t pad = 0;
+        Decision dec{0, 0, 0, 0};
+        Cand* c() { return reinterpret_cast<Cand*>(this + 1); }
+    };
+    static_assert(sizeof(Rec) % alignof(Cand) == 0, "candidates follow the record");
     uint64_t g = 1;
     int gsh = -1;                // log2(g) when g is a power of two (the reference's list: 1024)
     uint32_t nc = 0;
-    std::vector<std::unique_ptr<Page>> pages;
+    size_t rsz = 0;              // bytes per position record
+    std::vector<std::unique_ptr<uint8_t[]>> pages;
     void init(uint64_t n, uint64_t g_, uint32_t nc_) {
         g = g_;
         gsh = (g & (g - 1)) == 0 ? __builtin_ctzll(g) : -1;
         nc = nc_;
+        rsz = sizeof(Rec) + (size_t)nc * sizeof(Cand);
         pages.clear();
         pages.resize((size_t)((n / g >> PB) + 1));
     }
-    // (page, slot) of position pos, the page created on first use
-    Page& at(uint64_t pos, uint32_t& slot) {
+    // the record of position pos, its page created on first use
+    Rec& at(uint64_t pos) {
         const uint64_t x = gsh >= 0 ? pos >> gsh : pos / g;
-        slot = (uint32_t)(x & ((1u << PB) - 1));
-        std::unique_ptr<Page>& pg = pages[(size_t)(x >> PB)];
+        const uint32_t slot = (uint32_t)(x & ((1u << PB) - 1));
+        std::unique_ptr<uint8_t[]>& pg = pages[(size_t)(x >> PB)];
         if (!pg) {
-            pg.reset(new Page);
-            const size_t m = (size_t)1 << PB;
-            pg->plen.assign(m * nc, 0);
-            pg->lz.assign(m * nc, 0xFFFFFFFFu);
-            pg->id.assign(m * nc, 255);
-            pg->hlen.assign(m * nc, 0);
-            pg->hid.assign(m * nc, 0);
-            pg->hhave.assign(m, 0);
-            pg->hreq.assign(m, 0);
-            pg->have.assign(m, 0);
-            pg->req.assign(m, 0);
-            pg->mhave.assign(m, 0);
-            pg->mreq.assign(m, 0);
-            pg->decided.assign(m, 0);
-            pg->dec.assign(m, Decision{0, 0, 0, 0});
+            pg.reset(new uint8_t[rsz << PB]);
+            for (uint32_t q = 0; q < (1u << PB); q++) {
+                Rec* r = new (pg.get() + rsz * q) Rec();
+                for (uint32_t i = 0; i < nc; i++) new (r->c() + i) Cand();
+            }
         }
-        return *pg;
+        return *reinterpret_cast<Rec*>(pg.get() + rsz * slot);
     }
 };
 
@@ -341,20 +342,18 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
     auto ready = [&](uint64_t pos) -> bool {
         Sizes z;
         sizes_at(pos, z);
-        uint32_t sl;
-        PosTable::Page& pg = T.at(pos, sl);
-        if (needs_m(z) && !pg.mhave[sl]) return false;
+        PosTable::Rec& r = T.at(pos);
+        if (needs_m(z) && !r.mhave) return false;
         for (uint32_t i = 0; i < nc; i++)
-            if (((z.canon >> i) & 1) && needs_o(z, i) && !((pg.have[sl] >> i) & 1)) return false;
-        if (hc && (pg.hhave[sl] & z.canon) != z.canon) return false;
+            if (((z.canon >> i) & 1) && needs_o(z, i) && !((r.have >> i) & 1)) return false;
+        if (hc && (r.hhave & z.canon) != z.canon) return false;
         return true;
     };
     // the reference's decision at pos (adaptive_compressor.py:546-590), all parts known
     auto decide = [&](uint64_t pos) -> Decision {
         Sizes z;
         sizes_at(pos, z);
-        uint32_t sl;
-        PosTable::Page& pg = T.at(pos, sl);
+        PosTable::Cand* cd = T.at(pos).c();
         const uint64_t remain = n - pos;
         double best_ratio = 1.0;
         uint32_t best_s = 0, best_plen = 0;
@@ -364,21 +363,21 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
             if (!((z.canon >> i) & 1)) continue;
             const uint32_t sz = z.S[i];
             if (!hc && !any_eligible(p, sz)) continue;
-            const size_t e = (size_t)sl * nc + i;
-            uint32_t plen = pg.plen[e];
-            uint8_t id = pg.id[e];
+            const PosTable::Cand& e = cd[i];
+            uint32_t plen = e.plen;
+            uint8_t id = e.id;
             uint8_t host = 0;
             if (sz != z.M && !needs_o(z, i)) id = 255;            // no other method: raw so far
             if (lzshare && sz < z.M && eligible(p, sz, AMBC_M_LZ4)) {
                 // id 9 comes last in id order: it wins only strictly below the others
-                const uint32_t lb = pg.lz[e];
+                const uint32_t lb = e.lz;
                 const uint32_t other = id == 255 ? sz : plen + HDR;
                 if (lb != 0xFFFFFFFFu && (uint64_t)lb + 41 < other) { plen = lb + 23; id = 9; }
             }
-            if (hc && pg.hid[e] && pg.hlen[e] + HDR < sz) {
+            if (hc && e.hid && e.hlen + HDR < sz) {
                 // the host codecs' winner joins in id order: smaller len, or a tie with a higher id
-                const uint32_t hl = pg.hlen[e];
-                const uint8_t hi = pg.hid[e];
+                const uint32_t hl = e.hlen;
+                const uint8_t hi = e.hid;
                 if (id == 255 || hl < plen || (hl == plen && hi < id)) { plen = hl; id = hi; host = 1; }
             }
             if (id == 255) continue;
@@ -403,22 +402,21 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
     auto request = [&](uint64_t pos) {
         Sizes z;
         sizes_at(pos, z);
-        uint32_t sl;
-        PosTable::Page& pg = T.at(pos, sl);
-        if (needs_m(z) && !pg.mhave[sl] && !pg.mreq[sl]) {
-            pg.mreq[sl] = 1;
+        PosTable::Rec& r = T.at(pos);
+        if (needs_m(z) && !r.mhave && !r.mreq) {
+            r.mreq = 1;
             req[{z.M, 1}].push_back(pos);
         }
         for (uint32_t i = 0; i < nc; i++) {
             if (!((z.canon >> i) & 1)) continue;
-            if (hc && !(((pg.hhave[sl] | pg.hreq[sl]) >> i) & 1)) {
-                pg.hreq[sl] |= 1u << i;
+            if (hc && !(((r.hhave | r.hreq) >> i) & 1)) {
+                r.hreq |= 1u << i;
                 hpos.push_back(pos);
                 hsize.push_back(z.S[i]);
             }
             if (!needs_o(z, i)) continue;
-            if (((pg.have[sl] | pg.req[sl]) >> i) & 1) continue;
-            pg.req[sl] |= 1u << i;
+            if (((r.have | r.req) >> i) & 1) continue;
+            r.req |= 1u << i;
             req[{z.S[i], 0}].push_back(pos);
         }
     };
@@ -436,13 +434,12 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
         for (size_t q = 0; q < hpos.size(); q++) {
             Sizes z;
             sizes_at(hpos[q], z);
-            uint32_t sl;
-            PosTable::Page& pg = T.at(hpos[q], sl);
+            PosTable::Rec& r = T.at(hpos[q]);
             for (uint32_t i = 0; i < nc; i++)
                 if (((z.canon >> i) & 1) && z.S[i] == hsize[q]) {
-                    pg.hid[(size_t)sl * nc + i] = hid_out[q];
-                    pg.hlen[(size_t)sl * nc + i] = hlen_out[q];
-                    pg.hhave[sl] |= 1u << i;
+                    r.c()[i].hid = hid_out[q];
+                    r.c()[i].hlen = hlen_out[q];
+                    r.hhave |= 1u << i;
                 }
         }
         hpos.clear();
@@ -456,19 +453,18 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
             const uint64_t pos = poss[q];
             Sizes z;
             sizes_at(pos, z);
-            uint32_t sl;
-            PosTable::Page& pg = T.at(pos, sl);
+            PosTable::Rec& r = T.at(pos);
+            PosTable::Cand* cd = r.c();
             for (uint32_t i = 0; i < nc; i++) {
                 if (!((z.canon >> i) & 1)) continue;
-                const size_t e = (size_t)sl * nc + i;
                 if (z.S[i] == sz && (kind == 1 || z.S[i] != z.M)) {
-                    pg.plen[e] = bb.hplen[q];
-                    pg.id[e] = bb.hids[q];
-                    pg.have[sl] |= 1u << i;
+                    cd[i].plen = bb.hplen[q];
+                    cd[i].id = bb.hids[q];
+                    r.have |= 1u << i;
                 }
-                if (kind == 1 && z.S[i] < z.M) pg.lz[e] = bb.hlz[q * LZ4_SUB_MAX + jsub[i]];   // (S[i] = cands[i])
+                if (kind == 1 && z.S[i] < z.M) cd[i].lz = bb.hlz[q * LZ4_SUB_MAX + jsub[i]];   // (S[i] = cands[i])
             }
-            if (kind == 1) pg.mhave[sl] = 1;
+            if (kind == 1) r.mhave = 1;
         }
     };
 
@@ -537,13 +533,12 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
         std::vector<Walk> still;
         for (Walk w : G.active) {
             for (;;) {
-                uint32_t sl;
-                PosTable::Page& pg = T.at(w.pos, sl);
-                if (pg.decided[sl]) break;                 // joined a decided path
+                PosTable::Rec& r = T.at(w.pos);
+                if (r.decided) break;                      // joined a decided path
                 if (!ready(w.pos)) { still.push_back(w); break; }
                 const Decision dd = decide(w.pos);
-                pg.decided[sl] = 1;
-                pg.dec[sl] = dd;
+                r.decided = 1;
+                r.dec = dd;
                 if (dd.id == 255) break;                   // the rest is raw: done
                 w.last = dd.s;
                 w.pos += dd.s;
@@ -564,10 +559,7 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
         for (const Walk& w : G.active) {
             uint64_t q = w.pos;
             for (int k = 0; k <= SPEC && q < n; k++, q += w.last) {
-                if (k) {
-                    uint32_t sl;
-                    if (T.at(q, sl).decided[sl]) break;
-                }
+                if (k && T.at(q).decided) break;
                 request(q);
             }
         }
@@ -584,11 +576,10 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
                 for (uint64_t q : r.second) {
                     Sizes z;
                     sizes_at(q, z);
-                    uint32_t sl;
-                    PosTable::Page& pg = T.at(q, sl);
-                    if (r.first.second == 1) pg.mreq[sl] = 0;
+                    PosTable::Rec& rec = T.at(q);
+                    if (r.first.second == 1) rec.mreq = 0;
                     for (uint32_t i = 0; i < nc; i++)
-                        if (z.S[i] == r.first.first) pg.req[sl] &= ~(1u << i);
+                        if (z.S[i] == r.first.first) rec.req &= ~(1u << i);
                 }
                 continue;
             }
@@ -643,10 +634,9 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
     std::vector<Pkg> path;
     uint64_t body = 0;
     for (uint64_t pos = 0; pos < n;) {
-        uint32_t sl;
-        PosTable::Page& pg = T.at(pos, sl);
-        if (!pg.decided[sl]) return fail(AMBC_E_DEVICE, "multi-size walk: undecided position on the path");
-        const Decision& dd = pg.dec[sl];
+        const PosTable::Rec& r = T.at(pos);
+        if (!r.decided) return fail(AMBC_E_DEVICE, "multi-size walk: undecided position on the path");
+        const Decision& dd = r.dec;
         if (dd.id == 255 && n - pos > 0xFFFFFFFFull)
             return fail(AMBC_E_RANGE, "raw remainder exceeds a u32 chunk field");
         path.push_back(Pkg{pos, dd.s, dd.plen, dd.id, dd.host, body});
