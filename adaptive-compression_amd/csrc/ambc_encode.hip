@@ -152,75 +152,6 @@ __device__ __forceinline__ uint32_t hdr_byte(uint32_t q, uint32_t type, uint32_t
     return (clen >> (8 * (q - 14))) & 0xFF;              // compressed_length
 }
 
-// ---- direct emission (measured experiment, EncArgs::dstat) ----
-constexpr unsigned long long DE_AGG = 1ull << 62, DE_INCL = 2ull << 62, DE_VAL = (1ull << 62) - 1;
-
-// aligned dword i of src (GLC: a global buffer this workgroup has just written,
-// read past the vector L1)
-template <bool GLC>
-__device__ __forceinline__ uint32_t de_rd(const uint8_t* src, uint32_t i) {
-    const uint32_t* p = reinterpret_cast<const uint32_t*>(src) + i;
-    if constexpr (GLC) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else return *p;
-}
-
-// dst[0, len) = src[0, len) by the wave (src 4-byte aligned; dword stores where
-// dst is aligned, the 0-3 edge bytes singly)
-template <bool GLC>
-__device__ void de_copy(uint8_t* dst, const uint8_t* src, uint32_t len, uint32_t lane) {
-    const uint32_t head = min(len, (uint32_t)((4 - ((uintptr_t)dst & 3)) & 3));
-    if (lane < head) dst[lane] = (uint8_t)(de_rd<GLC>(src, lane >> 2) >> (8 * (lane & 3)));
-    uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + head);
-    const uint32_t nw = (len - head) >> 2;
-    for (uint32_t w = lane; w < nw; w += 64) {
-        const uint32_t o = head + 4 * w;
-        const uint32_t lo = de_rd<GLC>(src, o >> 2);
-        const uint32_t hi = (o & 3) ? de_rd<GLC>(src, (o >> 2) + 1) : 0u;
-        d32[w] = __builtin_amdgcn_alignbyte(hi, lo, o & 3);
-    }
-    for (uint32_t t = head + 4 * nw + lane; t < len; t += 64)
-        dst[t] = (uint8_t)(de_rd<GLC>(src, t >> 2) >> (8 * (t & 3)));
-}
-
-// Decoupled look-back without waiting: publish chunk g's package size, then sum
-// the predecessors' published sizes back to one that knows its inclusive prefix.
-// false (the chunk goes through its slot and k_compact) as soon as a predecessor
-// has published nothing yet, or after 1024 of them.
-// waits: polls (s_sleep between them) of a window whose first unpublished
-// predecessor blocks the look-back before it gives up (0: none)
-__device__ bool de_lookback(unsigned long long* st, uint64_t g, uint64_t size, uint64_t& pre, uint32_t lane,
-                            uint32_t waits) {
-    if (lane == 0) __hip_atomic_store(&st[g], DE_AGG | size, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint64_t acc = 0;
-    int64_t j = (int64_t)g - 1;
-    uint32_t w = 0;
-#pragma unroll 1
-    for (int it = 0; it < 16; it++, j -= 64) {
-        const int64_t q = j - (int64_t)lane;
-        const unsigned long long v =
-            q >= 0 ? __hip_atomic_load(&st[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : DE_INCL;
-        const uint32_t f = (uint32_t)(v >> 62);
-        const uint64_t stop = __ballot(f != 1u);
-        const uint32_t a = stop ? (uint32_t)__builtin_ctzll(stop) : 64u;
-        if (a < 64 && readlane(f, a) == 0u && w < waits) {   // wait for it: the same window again
-            w++;
-            __builtin_amdgcn_s_sleep(8);
-            it--;
-            j += 64;
-            continue;
-        }
-        acc += wave_sum<uint64_t>((lane < a || (lane == a && f == 2u)) ? (uint64_t)(v & DE_VAL) : 0ull);
-        if (a < 64) {
-            if (readlane(f, a) != 2u) return false;
-            pre = acc;
-            if (lane == 0)
-                __hip_atomic_store(&st[g], DE_INCL | (acc + size), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return true;
-        }
-    }
-    return false;
-}
-
 // GL (chunks of 4 KiB and more, no forced / analysed encode, 16-byte aligned
 // chunk starts): the chunk is read in place from the input through the caches
 // instead of a CMAX-byte LDS copy -- only LZ4 (and id 5's gates) take such
@@ -230,9 +161,9 @@ __device__ bool de_lookback(unsigned long long* st, uint64_t g, uint64_t size, u
 // 64 bytes of slack or the next chunk and never reach a result.
 // MODE (compile time, so that the headline's kernel carries none of the rest):
 // ENC_MODE_PLAIN compress / plugins; ENC_MODE_WALK the multi-size walk's
-// decision-only batches (ENC_EVAL, lz4sub); ENC_MODE_DIRECT the direct-emission
-// experiment (dstat)
-enum : int { ENC_MODE_PLAIN = 0, ENC_MODE_WALK = 1, ENC_MODE_DIRECT = 2 };
+// decision-only batches (ENC_EVAL, lz4sub).  (Direct emission to final offsets
+// was measured in round 3 and removed: profiles/r3_direct_emission_ab.json.)
+enum : int { ENC_MODE_PLAIN = 0, ENC_MODE_WALK = 1 };
 // Register allocation for 8 waves per SIMD (64 VGPRs, a few spilled bytes): with
 // the chunk read in place the LDS no longer caps k_encode at 5 waves, and the
 // VALU-issue-bound LZ4 rounds gain from the extra waves -- same-box A/B, 4 GiB
@@ -259,7 +190,7 @@ __global__ __launch_bounds__(64) AMBC_ENC_ATTR void k_encode(EncArgs A) {
     const uint32_t n = A.coff ? A.clen[k] : (uint32_t)min((uint64_t)A.chunk_size, A.n_total - pos0);
     const uint8_t* src = A.in + pos0;
     uint8_t* const slot0 = A.slots + (uint64_t)k * A.slot_stride;   // the chunk's scratch slot
-    uint8_t* slot = slot0;              // where the payload goes (direct emission: the body)
+    uint8_t* slot = slot0;              // where the payload goes
     // second pass after k_deflate: only the deferred chunks id 5 did not take
     if ((A.flags & ENC_EMIT_PENDING) && (!A.pending[k] || A.ids[k] == 5)) return;
     STAMP_DECL
@@ -800,11 +731,7 @@ __global__ __launch_bounds__(64) AMBC_ENC_ATTR void k_encode(EncArgs A) {
                 // 32-bit offsets from the (uniform) block pointer: saddr stores
                 const uint32_t q0 = emitted + incl - sz;     // token
                 const uint32_t ql = q0 + 1 + xl;             // first literal
-#ifdef AMBC_EXP_NOSTORE
-                if (0) {
-#else
                 if (me && st_on) {
-#endif
                     blk[q0] = (uint8_t)((lit >= 15 ? 15 : lit) << 4 | (ml >= 15 ? 15 : ml));
                     const uint32_t offv = (uint32_t)(i - cand);
                     blk[ql + lit] = (uint8_t)offv;
@@ -823,9 +750,7 @@ __global__ __launch_bounds__(64) AMBC_ENC_ATTR void k_encode(EncArgs A) {
                     const uint64_t rest = sel >> lane;
                     const uint32_t nx = rest ? lane + (uint32_t)__builtin_ctzll(rest) : lane;
                     const uint32_t qn = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(nx << 2), (int)ql);
-#ifndef AMBC_EXP_NOSTORE
                     if (!me && rest && i >= pe) blk[qn + (uint32_t)(i - pe)] = (uint8_t)v;
-#endif
                     if (anchor < (uint32_t)base) {
                         const uint32_t dst = readlane(ql, (uint32_t)__builtin_ctzll(sel));
                         const uint32_t len = (uint32_t)base - anchor;
@@ -893,30 +818,7 @@ __global__ __launch_bounds__(64) AMBC_ENC_ATTR void k_encode(EncArgs A) {
     // launch (ENC_EMIT_PENDING) that repeats this chunk's selection
     const bool defer = A.pending && !(A.flags & ENC_EMIT_PENDING) && (win == 1 || win == 3);
     if (A.pending && !(A.flags & ENC_EMIT_PENDING) && lane == 0) A.pending[k] = defer ? 1 : 0;
-    // direct emission: the package goes to its final offset when every earlier
-    // chunk has published its size (LZ4 payloads move from the slot they were
-    // built in, raw ones from the chunk, the others are emitted there below)
-    bool placed = false;
-    if (MODE == ENC_MODE_DIRECT && A.dstat && !defer && !eval) {
-        uint64_t pre = 0;
-        placed = de_lookback(A.dstat, (uint64_t)A.kbase + k, (uint64_t)HDR + wlen, pre, lane, A.dwait) &&
-                 pre + HDR + wlen <= A.dcap;
-        if (placed) {
-            uint8_t* dst = A.dout + pre;
-            if (lane < HDR) dst[lane] = (uint8_t)hdr_byte(lane, win, n, wlen);
-            if (win == 9) {
-                __threadfence();
-                de_copy<true>(dst + HDR, slot, wlen, lane);
-            } else if (win == 255) {
-                de_copy<false>(dst + HDR, ch, n, lane);
-            }
-            slot = dst + HDR;
-            if (lane == 0) A.placed[k] = 1;
-        } else if (lane == 0) {
-            A.placed[k] = 0;
-        }
-    }
-    if (defer || eval || (placed && (win == 9 || win == 255))) {
+    if (defer || eval) {
     } else if (win == 4) {
         for (uint32_t i = lane; i < n; i += 64)
             slot[i] = i ? (uint8_t)(ch[i] - ch[i - 1]) : ch[0];
@@ -1130,7 +1032,7 @@ __device__ __forceinline__ void compact_package(const CompactArgs& A, uint32_t k
 __global__ __launch_bounds__(256) void k_compact(CompactArgs A) {
     const uint32_t lane = threadIdx.x & 63;
     for (uint32_t k = blockIdx.x * 4 + (threadIdx.x >> 6); k < A.n_chunks; k += gridDim.x * 4)
-        if (!A.placed || !A.placed[k]) compact_package(A, k, lane);
+        compact_package(A, k, lane);
 }
 
 __global__ void k_seg_base(uint64_t* base, const uint64_t* off_last, const uint64_t* size_last) {
@@ -1296,8 +1198,6 @@ static hipError_t launch_encode_t(const EncArgs& a, hipStream_t s) {
         if (CMAX >= gl_min && (a.flags & ENC_IN_ALIGNED) && !(a.flags & (ENC_FORCE | ENC_ANALYZE))) {
             if (a.flags & ENC_EVAL)
                 hipLaunchKernelGGL((k_encode<CMAX, true, ENC_MODE_WALK>), dim3(a.n_chunks), dim3(64), 0, s, a);
-            else if (a.dstat)
-                hipLaunchKernelGGL((k_encode<CMAX, true, ENC_MODE_DIRECT>), dim3(a.n_chunks), dim3(64), 0, s, a);
             else
                 hipLaunchKernelGGL((k_encode<CMAX, true>), dim3(a.n_chunks), dim3(64), 0, s, a);
             return hipGetLastError();
@@ -1305,8 +1205,6 @@ static hipError_t launch_encode_t(const EncArgs& a, hipStream_t s) {
     }
     if (a.flags & ENC_EVAL)
         hipLaunchKernelGGL((k_encode<CMAX, false, ENC_MODE_WALK>), dim3(a.n_chunks), dim3(64), 0, s, a);
-    else if (a.dstat)
-        hipLaunchKernelGGL((k_encode<CMAX, false, ENC_MODE_DIRECT>), dim3(a.n_chunks), dim3(64), 0, s, a);
     else
         hipLaunchKernelGGL((k_encode<CMAX, false>), dim3(a.n_chunks), dim3(64), 0, s, a);
     return hipGetLastError();

@@ -109,7 +109,7 @@ void ambc_destroy(ambc_ctx* ctx) {
         (void)hipStreamSynchronize(d.stream);
         for (Buf* b : {&d.in, &d.out, &d.slots, &d.plen, &d.ids, &d.sizes, &d.off, &d.scan_tmp,
                        &d.acc, &d.ent_full, &d.ent_tail, &d.body, &d.jobs, &d.produced, &d.dout,
-                       &d.scratch, &d.seg, &d.list, &d.bestpre, &d.gdseq, &d.pending, &d.z9rec, &d.z9scr, &d.segbase, &d.coll, &d.dstat, &d.placed,
+                       &d.scratch, &d.seg, &d.list, &d.bestpre, &d.gdseq, &d.pending, &d.z9rec, &d.z9scr, &d.segbase, &d.coll,
                        &d.inffix, &d.ms_out})
             b->release();
         for (auto& b : d.msb) b.release();
@@ -335,20 +335,6 @@ static int compress_on_body(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_
         }
     }
     const bool dict = (p->method_mask >> AMBC_M_DICT) & 1;
-    // direct emission (measured experiment, off by default: DESIGN §4): packages
-    // whose predecessors have all published their sizes go straight to d_out
-    static const bool direct_env = getenv("AMBC_DIRECT_EMIT") != nullptr;
-    const bool direct = direct_env && !deflate && !dict && p->mode != AMBC_MODE_REFERENCE && !si && M > 0;
-    if (direct) {
-        HIPCHK(d.dstat.ensure((size_t)M * 8));
-        HIPCHK(d.placed.ensure((size_t)M));
-        HIPCHK(hipMemsetAsync(d.dstat.p, 0, (size_t)M * 8, s));
-        ea.dstat = d.dstat.as<unsigned long long>();
-        ea.dout = d_out;
-        ea.dcap = out_cap;
-        ea.dwait = (uint32_t)atoi(getenv("AMBC_DIRECT_EMIT"));
-        ea.placed = d.placed.as<uint8_t>();
-    }
     // the kernels of one chunk range [k0, k1): every per-chunk array offset to k0
     auto seg_args = [&](uint32_t k0, uint32_t k1) {
         EncArgs e = ea;
@@ -363,7 +349,6 @@ static int compress_on_body(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_
         if (e.pending) e.pending += k0;
         if (e.gdseq) e.gdseq += (uint64_t)k0 * gd_seq_bytes(gd_cmax);
         if (e.z9rec) e.z9rec += (uint64_t)k0 * z9_rec_words(z9_cmax(C));
-        if (e.placed) e.placed += k0;
         e.kbase = k0;
         return e;
     };
@@ -426,7 +411,6 @@ static int compress_on_body(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_
             ca.chunk_size = C;
             ca.out = d_out;
             ca.in = raw_in_place ? d_in + (uint64_t)k0 * C : nullptr;
-            ca.placed = direct ? d.placed.as<uint8_t>() + k0 : nullptr;
             // beside the next segment's encoder the compaction runs as a resident
             // grid (per-package-group workgroups would wait behind the encoder's
             // queued workgroups for every dispatch); the last one runs alone
@@ -449,14 +433,6 @@ static int compress_on_body(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_
         std::vector<uint64_t> acc(260);
         HIPCHK(hipMemcpyAsync(acc.data(), d.acc.p, 260 * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
-        if (direct && getenv("AMBC_TRACE_DE")) {
-            std::vector<uint8_t> pl(M);
-            HIPCHK(hipMemcpy(pl.data(), d.placed.p, M, hipMemcpyDeviceToHost));
-            uint64_t c = 0;
-            for (uint8_t x : pl) c += x;
-            fprintf(stderr, "[ambc] direct emission: %llu of %u packages placed by k_encode\n",
-                    (unsigned long long)c, M);
-        }
         return finish_compress(d, p, M, Remainder(), d_out, body_len, acc, d_in, end, out_len, st, t0);
     }
     rc = encode_range(ea);
@@ -581,7 +557,6 @@ static int compress_on_body(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_
     ca.chunk_size = C;
     ca.out = d_out;
     ca.in = raw_in_place ? d_in : nullptr;
-    ca.placed = direct ? d.placed.as<uint8_t>() : nullptr;
     HIPCHK(launch_compact(ca, s));
     HIPCHK(hipEventRecord(d.ev[3], s));
     if (trace_on()) { HIPCHK(hipStreamSynchronize(s)); TRACE("compact done"); }

@@ -154,7 +154,6 @@ struct Dev {
     hipEvent_t sev[2] = {};     //   (acc cleared, statistics done)
     hipEvent_t pev[8] = {};     // segment i encoded
     Buf segbase;                // body offset of every segment (device)
-    Buf dstat, placed;          // direct emission (AMBC_DIRECT_EMIT): look-back status, placed flags
     // pinned staging for large pageable copies: 2 buffers + 2 events per copy
     // thread; set 0 uploads, set 1 downloads (the decode pipeline runs both at once)
     std::vector<void*> stage, stage1;

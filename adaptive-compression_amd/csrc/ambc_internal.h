@@ -54,16 +54,7 @@ struct EncArgs {
     uint32_t* lz4sub;
     uint32_t sub_c[LZ4_SUB_MAX];
     uint32_t n_subc;
-    // direct emission (measured experiment, AMBC_DIRECT_EMIT): a chunk whose
-    // predecessors have all published their package sizes (decoupled look-back
-    // over dstat, indexed kbase + k over the whole call) writes its package
-    // straight to dout at its final offset and sets placed[k]; k_compact skips it
-    unsigned long long* dstat;
-    uint32_t kbase;
-    uint8_t* dout;
-    uint64_t dcap;           //   (bytes writable at dout)
-    uint32_t dwait;          //   polls a blocked look-back waits before it gives up (AMBC_DIRECT_EMIT=<n>)
-    uint8_t* placed;
+    uint32_t kbase;          // index of chunk 0 of this launch within the call
 };
 
 // gather the packages into the body at their scanned offsets
@@ -81,7 +72,6 @@ struct CompactArgs {
     uint32_t chunk_size;
     uint8_t* out;
     const uint8_t* in;       // optional (ENC_RAW_IN_PLACE): raw packages read from in + k * chunk_size
-    const uint8_t* placed;   // optional: packages k_encode already wrote (direct emission)
 };
 
 // one decode job per chunk package (built by the host header walk)
