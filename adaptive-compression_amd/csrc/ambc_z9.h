@@ -86,6 +86,18 @@ __device__ __forceinline__ uint32_t grp_max8(uint32_t x) {
     return x;
 }
 __device__ __forceinline__ uint32_t grp8(uint64_t m, uint32_t g) { return (uint32_t)(m >> (8 * g)) & 0xFFu; }
+// the same for lane groups of G = 1, 2, 4 or 8 lanes
+template <int G>
+__device__ __forceinline__ uint32_t grp_max(uint32_t x) {
+    if constexpr (G >= 2) x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, true));
+    if constexpr (G >= 4) x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, true));
+    if constexpr (G >= 8) x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, true));
+    return x;
+}
+template <int G>
+__device__ __forceinline__ uint32_t grp_bits(uint64_t m, uint32_t g) {
+    return (uint32_t)(m >> (G * g)) & ((1u << G) - 1u);
+}
 
 // ---------------------------------------------------------------------------
 // k_z9_heap: zlib's build_tree heap for the literal/length and distance trees,

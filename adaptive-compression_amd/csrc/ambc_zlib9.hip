@@ -57,8 +57,14 @@ namespace {
 #ifndef AMBC_Z9_NW4096
 #define AMBC_Z9_NW4096 8
 #endif
+// lanes per walker (the candidates one search step compares): fewer lanes give
+// more walkers per wave instruction where chains are short
+#ifndef AMBC_Z9_G
+#define AMBC_Z9_G 8
+#endif
 template <int CMAX> struct Z9Cfg {
     static constexpr int NW = CMAX <= 1024 ? 2 : (CMAX <= 2048 ? 4 : (CMAX <= 4096 ? AMBC_Z9_NW4096 : 16));
+    static constexpr int G = AMBC_Z9_G;
 };
 
 template <int CMAX>
@@ -231,12 +237,13 @@ __device__ __forceinline__ void z9_literal_mask(Z9Smem<CMAX>& S, uint32_t n, uin
 // iteration for every active group.
 template <int CMAX>
 __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t wave, uint32_t lane) {
-    constexpr uint32_t NWK = (uint32_t)Z9Cfg<CMAX>::NW * 8u;
+    constexpr uint32_t G = (uint32_t)Z9Cfg<CMAX>::G;
+    constexpr uint32_t NWK = (uint32_t)Z9Cfg<CMAX>::NW * (64u / G);
     typedef __attribute__((address_space(3))) volatile uint32_t lds_vu32;
     lds_vu32* vs = (lds_vu32*)S.seg;
     const uint32_t* c32 = reinterpret_cast<const uint32_t*>(S.ch);
-    const uint32_t g = lane >> 3, r = lane & 7;
-    const uint32_t wid = wave * 8u + g;
+    const uint32_t g = lane / G, r = lane % G;
+    const uint32_t wid = wave * (64u / G) + g;
     // (measured and not kept: starts at n * sqrt(w / NWK), for chains that grow
     // along the chunk -- ASCII 17.3 -> 23.7 ms per 256 MiB: the walkers' overrun
     // until they meet another walker's path, not the chain lengths, sets the time)
@@ -329,7 +336,7 @@ __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t
 #pragma unroll
                 for (int t = 0; t < 4; t++) x[t] = __builtin_amdgcn_alignbyte(w[t + 1], w[t], sh);
                 const bool same = v && z_h15(x[0] & 0xFFFFFFu) == h;
-                const uint32_t sm = grp8(__ballot(same), g);
+                const uint32_t sm = grp_bits<G>(__ballot(same), g);
                 const uint32_t kidx = cnt + (uint32_t)__popc(sm & ((1u << r) - 1u)) + 1u;
                 const bool inwin = s - c <= Z_MAXD;
                 const bool ok = same && inwin && kidx <= Z_CHAIN;
@@ -365,12 +372,12 @@ __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t
                 // the most recent first, 128 bytes a step (lane r compares bytes
                 // [16 r, 16 r + 16) past the known length); once one reaches nice the
                 // older ones cannot win (longest_match stops there)
-                uint32_t em = grp8(__ballot(ok && fm == ~0u && can), g);
+                uint32_t em = grp_bits<G>(__ballot(ok && fm == ~0u && can), g);
 #pragma unroll 1
                 while (__any(em != 0u)) {
                     const bool gact = em != 0u;
                     const uint32_t rr = gact ? (uint32_t)__builtin_ctz(em) : 0u;
-                    const uint32_t src = g * 8u + rr;
+                    const uint32_t src = g * G + rr;
                     const uint32_t cc = (uint32_t)__shfl((int)c, (int)src);
                     const uint32_t ll = (uint32_t)__shfl((int)len, (int)src);
                     const uint32_t off = ll + 16u * r;
@@ -388,10 +395,10 @@ __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t
                     } else if (gact) {
                         f = 0;          // past the longest match zlib takes: the length is capped there
                     }
-                    const uint32_t mm = grp8(__ballot(gact && f != ~0u), g);
+                    const uint32_t mm = grp_bits<G>(__ballot(gact && f != ~0u), g);
                     const uint32_t r0 = mm ? (uint32_t)__builtin_ctz(mm) : 0u;
-                    const uint32_t f0 = (uint32_t)__shfl((int)f, (int)(g * 8u + r0));
-                    const uint32_t L2 = mm ? ll + 16u * r0 + (f0 >> 3) : ll + 128u;
+                    const uint32_t f0 = (uint32_t)__shfl((int)f, (int)(g * G + r0));
+                    const uint32_t L2 = mm ? ll + 16u * r0 + (f0 >> 3) : ll + 16u * G;
                     if (gact && r == rr) len = L2;
                     if (gact && (mm || L2 >= Z_MAXM)) {
                         em &= em - 1u;                                       // this candidate is done
@@ -401,11 +408,11 @@ __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t
 #endif
                 const uint32_t Lp = min(min(len, Z_MAXM), nice);
                 const uint32_t key = ok && can ? (Lp << 16 | c) : 0u;
-                k0 = max(k0, grp_max8(key));
-                k1 = max(k1, grp_max8(ok && kidx <= Z_CHAIN / 4 ? key : 0u));
+                k0 = max(k0, grp_max<G>(key));
+                k1 = max(k1, grp_max<G>(ok && kidx <= Z_CHAIN / 4 ? key : 0u));
                 cnt += (uint32_t)__popc(sm);
-                const uint32_t far = grp8(__ballot(v && !inwin), g);
-                j = j > lo + 8 ? j - 8 : lo;
+                const uint32_t far = grp_bits<G>(__ballot(v && !inwin), g);
+                j = j > lo + G ? j - G : lo;
                 gd = gd || j <= lo || far != 0 || cnt >= Z_CHAIN || (k0 >> 16) >= nice;
             }
         }

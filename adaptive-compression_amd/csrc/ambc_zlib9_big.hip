@@ -48,7 +48,11 @@
 namespace ambc {
 namespace {
 
-constexpr int ZB_NW = 16;                 // waves per chunk in k_z9_parse_big (128 walkers)
+constexpr int ZB_NW = 16;                 // waves per chunk in k_z9_parse_big (64 / ZB_G walkers each)
+#ifndef AMBC_Z9B_G
+#define AMBC_Z9B_G 8
+#endif
+constexpr uint32_t ZB_G = AMBC_Z9B_G;      // lanes per walker (candidates per search step)
 constexpr uint32_t ZB_GRID = 512;         // resident workgroups (2 per CU)
 constexpr uint32_t Z_WSZ = 32768;         // w_size
 constexpr uint32_t Z_SLIDE = 32768 + Z_MAXD;   // strstart that slides the window (65274)
@@ -279,7 +283,8 @@ __device__ __forceinline__ void z9b_walkers(Z9BSmem<CMAX>& S, uint32_t n, const 
                                             uint16_t* sd, const uint8_t* gch, const uint32_t* runb,
                                             const uint16_t* wrs, uint32_t wave, uint32_t lane) {
     constexpr bool CHG = Z9Big<CMAX>::CHG;
-    constexpr uint32_t NWK = (uint32_t)ZB_NW * 8u;
+    constexpr uint32_t G = ZB_G;
+    constexpr uint32_t NWK = (uint32_t)ZB_NW * (64u / G);
     const uint32_t* c32 = reinterpret_cast<const uint32_t*>(S.w.ch);
     const uint32_t* g32 = reinterpret_cast<const uint32_t*>(gch);
     auto W32 = [&](uint32_t i) -> uint32_t {
@@ -291,8 +296,8 @@ __device__ __forceinline__ void z9b_walkers(Z9BSmem<CMAX>& S, uint32_t n, const 
         else return S.w.ch[i];
     };
     const uint16_t* lst = S.w.lst;
-    const uint32_t g = lane >> 3, r = lane & 7;
-    const uint32_t wid = wave * 8u + g;
+    const uint32_t g = lane / G, r = lane % G;
+    const uint32_t wid = wave * (64u / G) + g;
     // the step at which fill_window slides: the first top s >= 65274 with
     // lookahead < 262 (65275 for a 65536-byte input); at s = 65274 a hash head of
     // 32768 reads as NIL (inputs < 65536 only: later heads that far are past MAX_DIST)
@@ -386,7 +391,7 @@ __device__ __forceinline__ void z9b_walkers(Z9BSmem<CMAX>& S, uint32_t n, const 
 #pragma unroll
                 for (int t = 0; t < 5; t++) w[t] = wn[t];
                 // the next step's candidate and its words, issued now
-                idx -= 8;
+                idx -= (int)G;
                 cn = !gd && idx >= (int)lo ? (uint32_t)lst[idx] : 0u;
 #pragma unroll
                 for (int t = 0; t < 5; t++) wn[t] = W32((cn >> 2) + t);
@@ -395,14 +400,14 @@ __device__ __forceinline__ void z9b_walkers(Z9BSmem<CMAX>& S, uint32_t n, const 
 #pragma unroll
                 for (int t = 0; t < 4; t++) x[t] = __builtin_amdgcn_alignbyte(w[t + 1], w[t], v ? sh : 0u);
                 const bool same = v && z_h15(x[0] & 0xFFFFFFu) == h;
-                const uint32_t sm = grp8(__ballot(same), g);
+                const uint32_t sm = grp_bits<G>(__ballot(same), g);
                 const uint32_t kidx = cnt + (uint32_t)__popc(sm & ((1u << r) - 1u)) + 1u;
                 // the hash head may lie MAX_DIST back (deflate_slow's test is <=);
                 // later chain entries must lie above limit = s - MAX_DIST
                 const bool inwin = s - c < Z_MAXD || (s - c == Z_MAXD && kidx == 1u);
                 const bool ok = same && inwin && kidx <= lim;
                 // the slide step: a head of 32768 is NIL, no search at all
-                const bool nilh = grp8(__ballot(same && kidx == 1u && c == Z_WSZ && s == nil_at), g) != 0;
+                const bool nilh = grp_bits<G>(__ballot(same && kidx == 1u && c == Z_WSZ && s == nil_at), g) != 0;
                 uint32_t fm = ~0u;
 #pragma unroll
                 for (int t = 0; t < 4; t++) fm = min(fm, ffbl_raw(x[t] ^ tg[t]) | (uint32_t)t << 5);
@@ -415,12 +420,12 @@ __device__ __forceinline__ void z9b_walkers(Z9BSmem<CMAX>& S, uint32_t n, const 
                 const bool can = fm != ~0u || best < 16 || ext;
                 // the group extends its first-16-equal candidates together, most
                 // recent first, 128 bytes a step, until one reaches nice
-                uint32_t em = grp8(__ballot(ext), g);
+                uint32_t em = grp_bits<G>(__ballot(ext), g);
 #pragma unroll 1
                 while (__any(em != 0u)) {
                     const bool gact = em != 0u;
                     const uint32_t rr = gact ? (uint32_t)__builtin_ctz(em) : 0u;
-                    const uint32_t src = g * 8u + rr;
+                    const uint32_t src = g * G + rr;
                     const uint32_t cc = (uint32_t)__shfl((int)c, (int)src);
                     const uint32_t ll = (uint32_t)__shfl((int)len, (int)src);
                     const uint32_t off = ll + 16u * r;
@@ -438,10 +443,10 @@ __device__ __forceinline__ void z9b_walkers(Z9BSmem<CMAX>& S, uint32_t n, const 
                     } else if (gact) {
                         f = 0;
                     }
-                    const uint32_t mm = grp8(__ballot(gact && f != ~0u), g);
+                    const uint32_t mm = grp_bits<G>(__ballot(gact && f != ~0u), g);
                     const uint32_t r0 = mm ? (uint32_t)__builtin_ctz(mm) : 0u;
-                    const uint32_t f0 = (uint32_t)__shfl((int)f, (int)(g * 8u + r0));
-                    const uint32_t L2 = mm ? ll + 16u * r0 + (f0 >> 3) : ll + 128u;
+                    const uint32_t f0 = (uint32_t)__shfl((int)f, (int)(g * G + r0));
+                    const uint32_t L2 = mm ? ll + 16u * r0 + (f0 >> 3) : ll + 16u * G;
                     if (gact && r == rr) len = L2;
                     if (gact && (mm || L2 >= Z_MAXM)) {
                         em &= em - 1u;
@@ -450,10 +455,10 @@ __device__ __forceinline__ void z9b_walkers(Z9BSmem<CMAX>& S, uint32_t n, const 
                 }
                 const uint32_t Lp = min(min(len, Z_MAXM), nice);
                 const uint32_t key = ok && can && !nilh ? (Lp << 16 | c) : 0u;
-                k0 = nilh ? 0u : max(k0, grp_max8(key));
+                k0 = nilh ? 0u : max(k0, grp_max<G>(key));
                 cnt += (uint32_t)__popc(sm);
-                const uint32_t far = grp8(__ballot(v && s - c >= Z_MAXD), g);
-                j = j > lo + 8 ? j - 8 : lo;
+                const uint32_t far = grp_bits<G>(__ballot(v && s - c >= Z_MAXD), g);
+                j = j > lo + G ? j - G : lo;
                 gd = gd || nilh || j <= lo || far != 0 || cnt >= lim || (k0 >> 16) >= nice;
             }
         }
