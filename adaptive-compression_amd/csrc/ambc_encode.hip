@@ -192,7 +192,7 @@ __global__ __launch_bounds__(64) AMBC_ENC_ATTR void k_encode(EncArgs A) {
     uint8_t* const slot0 = A.slots + (uint64_t)k * A.slot_stride;   // the chunk's scratch slot
     uint8_t* slot = slot0;              // where the payload goes
     // second pass after k_deflate: only the deferred chunks id 5 did not take
-    if ((A.flags & ENC_EMIT_PENDING) && (!A.pending[k] || A.ids[k] == 5)) return;
+    if ((A.flags & ENC_EMIT_PENDING) && (!A.pending[k] || A.ids[k] == 5 || A.ids[k] == 2)) return;
     STAMP_DECL
 
     // ---- stage the chunk in LDS (16 B per lane per load, coalesced) ----

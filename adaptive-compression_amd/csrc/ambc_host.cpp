@@ -318,13 +318,18 @@ static int compress_on_body(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_
     const bool z9 = deflate && (p->flags & AMBC_FLAG_ZLIB9);   // id 5 = zlib-9's bytes
     uint32_t gd_cmax = 1024;                  // launch_deflate's template bucket
     while (gd_cmax < C) gd_cmax <<= 1;
+    const bool dict = (p->method_mask >> AMBC_M_DICT) & 1;
+    if (deflate || dict) {
+        // RLE / Huffman payloads wait for the later encoders' verdict (id 2, id 5);
+        // a second k_encode launch emits the ones they did not replace
+        HIPCHK(d.pending.ensure((size_t)std::max<uint32_t>(M, 1)));
+        ea.pending = d.pending.as<uint8_t>();
+    }
     if (deflate) {
         HIPCHK(d.bestpre.ensure((size_t)std::max<uint32_t>(M, 1) * 4));
         ea.bestpre = d.bestpre.as<uint32_t>();
         HIPCHK(d.gdseq.ensure((size_t)std::max<uint32_t>(M, 1) * gd_seq_bytes(gd_cmax)));
         ea.gdseq = d.gdseq.as<uint8_t>();
-        HIPCHK(d.pending.ensure((size_t)std::max<uint32_t>(M, 1)));
-        ea.pending = d.pending.as<uint8_t>();
         if (z9) {
             HIPCHK(d.z9rec.ensure((size_t)std::max<uint32_t>(M, 1) * z9_rec_words(z9_cmax(C)) * 4));
             ea.z9rec = d.z9rec.as<uint32_t>();
@@ -334,7 +339,6 @@ static int compress_on_body(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_
             }
         }
     }
-    const bool dict = (p->method_mask >> AMBC_M_DICT) & 1;
     // the kernels of one chunk range [k0, k1): every per-chunk array offset to k0
     auto seg_args = [&](uint32_t k0, uint32_t k1) {
         EncArgs e = ea;
@@ -355,10 +359,10 @@ static int compress_on_body(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_
     auto encode_range = [&](const EncArgs& e) -> int {
         HIPCHK(launch_encode(e, s));
         if (dict) HIPCHK(launch_dict(e, dict_cmax(p), s));   // id 2 against k_encode's winner
-        if (deflate) {
-            // id 5 after 1/2/3/4, against LZ4 (ties -> 5)
-            HIPCHK(z9 ? launch_zlib9(e, s) : launch_deflate(e, s));
-            EncArgs ep = e;                 // RLE/Huffman payloads id 5 did not replace
+        // id 5 after 1/2/3/4, against LZ4 (ties -> 5)
+        if (deflate) HIPCHK(z9 ? launch_zlib9(e, s) : launch_deflate(e, s));
+        if (deflate || dict) {
+            EncArgs ep = e;                 // RLE/Huffman payloads ids 2 / 5 did not replace
             ep.flags |= ENC_EMIT_PENDING;
             ep.bestpre = nullptr;
             ep.stamps = nullptr;

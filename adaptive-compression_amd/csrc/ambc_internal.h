@@ -41,7 +41,7 @@ struct EncArgs {
     uint8_t* gdseq;          // k_deflate: n_chunks x chunk-size scratch for the parse's matches
     uint32_t* z9rec;         // k_z9_parse -> k_z9_code: per-chunk match starts + matches (ambc_zlib9.hip)
     uint8_t* z9scr;          // chunks > 8192: k_z9_parse_big's scratch, z9_scratch_bytes(cmax, n_chunks)
-    uint8_t* pending;        // with k_deflate: 1 = the RLE/Huffman payload was not emitted (id 5 may win)
+    uint8_t* pending;        // with k_dict / k_deflate: 1 = the RLE/Huffman payload was not emitted (id 2 / 5 may win)
     uint32_t pref_min[16];
     uint32_t pref_max[16];
     const uint64_t* coff;    // optional chunk table (multi-size walk): chunk k = in[coff[k], coff[k] + clen[k])

@@ -118,13 +118,15 @@ int launch_batch(Batch& b, hipStream_t st, const uint8_t* d_in, uint64_t n, cons
     const bool deflate = eligible(p, s, AMBC_M_DEFLATE);
     uint32_t gd_cmax = 1024;
     while (gd_cmax < C) gd_cmax <<= 1;
+    if ((deflate || dict) && !eval) {       // RLE / Huffman payloads wait for ids 2 / 5
+        HIPCHK(b.pending.ensure((size_t)cnt));
+        ea.pending = b.pending.as<uint8_t>();
+    }
     if (deflate) {
         HIPCHK(b.bestpre.ensure((size_t)cnt * 4));
         HIPCHK(b.gdseq.ensure((size_t)cnt * gd_seq_bytes(gd_cmax)));
-        HIPCHK(b.pending.ensure((size_t)cnt));
         ea.bestpre = b.bestpre.as<uint32_t>();
         ea.gdseq = b.gdseq.as<uint8_t>();
-        ea.pending = b.pending.as<uint8_t>();
         if (p->flags & AMBC_FLAG_ZLIB9) {
             HIPCHK(b.z9rec.ensure((size_t)cnt * z9_rec_words(z9_cmax(C)) * 4));
             ea.z9rec = b.z9rec.as<uint32_t>();
@@ -136,14 +138,12 @@ int launch_batch(Batch& b, hipStream_t st, const uint8_t* d_in, uint64_t n, cons
     }
     HIPCHK(launch_encode(ea, st));
     if (dict) HIPCHK(launch_dict(ea, std::min<uint32_t>(C, p->pref_max[AMBC_M_DICT]), st));
-    if (deflate) {
-        HIPCHK((p->flags & AMBC_FLAG_ZLIB9) ? launch_zlib9(ea, st) : launch_deflate(ea, st));
-        if (!eval) {
-            EncArgs ep = ea;
-            ep.flags |= ENC_EMIT_PENDING;
-            ep.bestpre = nullptr;
-            HIPCHK(launch_encode(ep, st));
-        }
+    if (deflate) HIPCHK((p->flags & AMBC_FLAG_ZLIB9) ? launch_zlib9(ea, st) : launch_deflate(ea, st));
+    if (ea.pending) {
+        EncArgs ep = ea;
+        ep.flags |= ENC_EMIT_PENDING;
+        ep.bestpre = nullptr;
+        HIPCHK(launch_encode(ep, st));
     }
     HIPCHK(hipMemcpyAsync(b.hplen, b.plen.p, (size_t)cnt * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(b.hids, b.ids.p, cnt, hipMemcpyDeviceToHost, st));
