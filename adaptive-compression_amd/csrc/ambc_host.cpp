@@ -474,6 +474,17 @@ static int compress_on_body(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_
             fprintf(stderr, "[ambc stamps] z9 parsed=%.0f wave-0 cycles/chunk: load %.0f sort %.0f walk %.0f "
                     "wait %.0f path %.0f out %.0f\n", gs[7], gs[0] / c, gs[1] / c, gs[2] / c, gs[3] / c,
                     gs[4] / c, gs[5] / c);
+            {   // big kernel, wave 0's walkers: iterations | chain steps << 16 | extension steps << 32 | searches << 48
+                double it = 0, stp = 0, ex = 0, sr = 0;
+                for (uint32_t q = 0; q < M; q++)
+                    if (g[(size_t)q * 8 + 7]) {
+                        const uint64_t w = g[(size_t)q * 8 + 6];
+                        it += (double)(w & 0xFFFF); stp += (double)((w >> 16) & 0xFFFF);
+                        ex += (double)((w >> 32) & 0xFFFF); sr += (double)(w >> 48);
+                    }
+                fprintf(stderr, "[ambc stamps] z9 wave-0 walker loop per chunk: iterations %.0f chain steps %.0f "
+                        "extension steps %.0f searches %.0f\n", it / c, stp / c, ex / c, sr / c);
+            }
             // the spread over chunks: percentiles of a parsed chunk's cycles, and the
             // share of all cycles in the slowest 10 %
             std::vector<double> tot;

@@ -63,56 +63,70 @@ struct RcclTransport : Transport {
     std::vector<ncclComm_t>* group = nullptr;
     std::mutex* group_mu = nullptr;
     RcclTransport(ncclComm_t c, Dev& dev, int nranks, int rank) : comm(c), d(dev) { W = nranks; r = rank; }
-    // this rank's communicator, or null once a failed peer aborted the group
-    ncclComm_t live() {
-        if (!group) return comm;
+    // Enqueue this rank's operations on its communicator.  In-process ranks hold
+    // the group's lock while they enqueue, so a failed peer's abort() never
+    // frees a communicator between the lookup and the enqueue; once enqueued,
+    // an abort cancels the operation in flight (ncclCommAbort's purpose) and the
+    // stream wait that follows, outside the lock, returns.  Null communicator:
+    // a failed peer aborted the group.
+    template <typename F>
+    int enqueue(F&& ops) {
+        if (!group) return ops(comm);
         std::lock_guard<std::mutex> lk(*group_mu);
-        return (*group)[r];
+        ncclComm_t c = (*group)[r];
+        if (!c) return fail(AMBC_E_COMM, "communicator aborted by a failed rank");
+        return ops(c);
     }
 
     int allgather_u64(const uint64_t* mine, uint32_t k, uint64_t* all) override {
-        ncclComm_t comm = live();
-        if (!comm) return fail(AMBC_E_COMM, "communicator aborted by a failed rank");
         HIPCHK(hipSetDevice(d.id));
         HIPCHK(d.coll.ensure((size_t)(W + 1) * k * 8));
         uint64_t* buf = d.coll.as<uint64_t>();
         HIPCHK(hipMemcpyAsync(buf, mine, (size_t)k * 8, hipMemcpyHostToDevice, d.stream));
-        NCCLCHK(ncclAllGather(buf, buf + k, k, ncclUint64, comm, d.stream));
+        int rc = enqueue([&](ncclComm_t c) -> int {
+            NCCLCHK(ncclAllGather(buf, buf + k, k, ncclUint64, c, d.stream));
+            return AMBC_OK;
+        });
+        if (rc) return rc;
         HIPCHK(hipMemcpyAsync(all, buf + k, (size_t)W * k * 8, hipMemcpyDeviceToHost, d.stream));
         HIPCHK(hipStreamSynchronize(d.stream));
         return AMBC_OK;
     }
     int allreduce_u64(uint64_t* v, uint32_t k, int op) override {
-        ncclComm_t comm = live();
-        if (!comm) return fail(AMBC_E_COMM, "communicator aborted by a failed rank");
         HIPCHK(hipSetDevice(d.id));
         HIPCHK(d.coll.ensure((size_t)k * 8));
         uint64_t* buf = d.coll.as<uint64_t>();
         HIPCHK(hipMemcpyAsync(buf, v, (size_t)k * 8, hipMemcpyHostToDevice, d.stream));
         const ncclRedOp_t o = op == AMBC_OP_MIN ? ncclMin : op == AMBC_OP_MAX ? ncclMax : ncclSum;
-        NCCLCHK(ncclAllReduce(buf, buf, k, ncclUint64, o, comm, d.stream));
+        int rc = enqueue([&](ncclComm_t c) -> int {
+            NCCLCHK(ncclAllReduce(buf, buf, k, ncclUint64, o, c, d.stream));
+            return AMBC_OK;
+        });
+        if (rc) return rc;
         HIPCHK(hipMemcpyAsync(v, buf, (size_t)k * 8, hipMemcpyDeviceToHost, d.stream));
         HIPCHK(hipStreamSynchronize(d.stream));
         return AMBC_OK;
     }
     int gather(const uint8_t* src, uint8_t* dst, const uint64_t* offs, const uint64_t* lens, int root) override {
-        ncclComm_t comm = live();
-        if (!comm) return fail(AMBC_E_COMM, "communicator aborted by a failed rank");
         HIPCHK(hipSetDevice(d.id));
         // pieces of at most 1 GiB per send/recv (both sides cut the same way)
         constexpr uint64_t PIECE = 1ull << 30;
-        NCCLCHK(ncclGroupStart());
-        if (r == root) {
-            for (int q = 0; q < W; q++) {
-                if (q == root) continue;
-                for (uint64_t o = 0; o < lens[q]; o += PIECE)
-                    NCCLCHK(ncclRecv(dst + offs[q] + o, std::min(PIECE, lens[q] - o), ncclUint8, q, comm, d.stream));
+        int rc = enqueue([&](ncclComm_t c) -> int {
+            NCCLCHK(ncclGroupStart());
+            if (r == root) {
+                for (int q = 0; q < W; q++) {
+                    if (q == root) continue;
+                    for (uint64_t o = 0; o < lens[q]; o += PIECE)
+                        NCCLCHK(ncclRecv(dst + offs[q] + o, std::min(PIECE, lens[q] - o), ncclUint8, q, c, d.stream));
+                }
+            } else {
+                for (uint64_t o = 0; o < lens[r]; o += PIECE)
+                    NCCLCHK(ncclSend(src + o, std::min(PIECE, lens[r] - o), ncclUint8, root, c, d.stream));
             }
-        } else {
-            for (uint64_t o = 0; o < lens[r]; o += PIECE)
-                NCCLCHK(ncclSend(src + o, std::min(PIECE, lens[r] - o), ncclUint8, root, comm, d.stream));
-        }
-        NCCLCHK(ncclGroupEnd());
+            NCCLCHK(ncclGroupEnd());
+            return AMBC_OK;
+        });
+        if (rc) return rc;
         if (r == root && lens[r] && src != dst + offs[r])
             HIPCHK(hipMemcpyAsync(dst + offs[r], src, lens[r], hipMemcpyDeviceToDevice, d.stream));
         HIPCHK(hipStreamSynchronize(d.stream));

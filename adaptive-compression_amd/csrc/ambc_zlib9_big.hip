@@ -281,7 +281,11 @@ __device__ void z9b_literal_mask(Z9BSmem<CMAX>& S, uint32_t n, const uint16_t* s
 template <int CMAX>
 __device__ __forceinline__ void z9b_walkers(Z9BSmem<CMAX>& S, uint32_t n, const uint16_t* slot, uint32_t* seg,
                                             uint16_t* sd, const uint8_t* gch, const uint32_t* runb,
-                                            const uint16_t* wrs, uint32_t wave, uint32_t lane) {
+                                            const uint16_t* wrs, uint32_t wave, uint32_t lane,
+                                            uint64_t* ctr = nullptr) {
+#ifdef AMBC_STAMPS
+    uint64_t c_it = 0, c_st = 0, c_ex = 0, c_sr = 0;   // loop iterations, chain steps, extension steps, searches
+#endif
     constexpr bool CHG = Z9Big<CMAX>::CHG;
     constexpr uint32_t G = ZB_G;
     constexpr uint32_t NWK = (uint32_t)ZB_NW * (64u / G);
@@ -309,6 +313,9 @@ __device__ __forceinline__ void z9b_walkers(Z9BSmem<CMAX>& S, uint32_t n, const 
     for (;;) {
         if (clean && !done && (q >= n || ((S.vis[q >> 5] >> (q & 31)) & 1u))) done = true;
         if (__all(done)) break;
+#ifdef AMBC_STAMPS
+        c_it++;
+#endif
         // a run of match-less positions from a clean q in one step (at most 512:
         // the path's exit offsets hold 10 bits)
         bool skip = false;
@@ -383,8 +390,14 @@ __device__ __forceinline__ void z9b_walkers(Z9BSmem<CMAX>& S, uint32_t n, const 
             uint32_t wn[5];
 #pragma unroll
             for (int t = 0; t < 5; t++) wn[t] = W32((cn >> 2) + t);
+#ifdef AMBC_STAMPS
+            c_sr += (uint64_t)__popcll(__ballot(act && r == 0));
+#endif
 #pragma unroll 1
             while (__any(!gd)) {
+#ifdef AMBC_STAMPS
+                c_st++;
+#endif
                 const bool v = !gd && idx >= (int)lo;
                 const uint32_t c = v ? cn : 0u;
                 uint32_t w[5];
@@ -423,6 +436,9 @@ __device__ __forceinline__ void z9b_walkers(Z9BSmem<CMAX>& S, uint32_t n, const 
                 uint32_t em = grp_bits<G>(__ballot(ext), g);
 #pragma unroll 1
                 while (__any(em != 0u)) {
+#ifdef AMBC_STAMPS
+                    c_ex++;
+#endif
                     const bool gact = em != 0u;
                     const uint32_t rr = gact ? (uint32_t)__builtin_ctz(em) : 0u;
                     const uint32_t src = g * G + rr;
@@ -501,7 +517,11 @@ __device__ __forceinline__ void z9b_walkers(Z9BSmem<CMAX>& S, uint32_t n, const 
             }
         }
     }
+#ifdef AMBC_STAMPS
+    if (ctr && lane == 0) *ctr = c_it | c_st << 16 | c_ex << 32 | c_sr << 48;
+#endif
 }
+
 
 template <int CMAX>
 __global__ __launch_bounds__(64 * ZB_NW) void k_z9_parse_big(EncArgs A) {
@@ -554,7 +574,13 @@ __global__ __launch_bounds__(64 * ZB_NW) void k_z9_parse_big(EncArgs A) {
         z9b_literal_mask(S, n, slot, gch, runb, wrs, wave, lane);
         __syncthreads();
         BSTAMP(1);
+#ifdef AMBC_STAMPS
+        uint64_t wctr = 0;
+        z9b_walkers(S, n, slot, seg, sd, gch, runb, wrs, wave, lane, wave == 0 ? &wctr : nullptr);
+        if (threadIdx.x == 0) _pa[6] = wctr;
+#else
         z9b_walkers(S, n, slot, seg, sd, gch, runb, wrs, wave, lane);
+#endif
         BSTAMP(2);
         __syncthreads();
         BSTAMP(3);
