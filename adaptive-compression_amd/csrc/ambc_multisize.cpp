@@ -304,8 +304,14 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
         if (n)
             for (uint64_t b0 : starts) active.push_back(Walk{b0, max_cand ? max_cand : cands[0]});
     }
-    for (auto& x : d.mss)
-        if (!x) HIPCHK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+    // slot 0 of each group (the round's largest size: its encode is the round's
+    // latency) on a high-priority stream, the smaller sizes fill in around it
+    for (int i = 0; i < 16; i++) {
+        if (d.mss[i]) continue;
+        int lo = 0, hi = 0;
+        HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIPCHK(hipStreamCreateWithPriority(&d.mss[i], hipStreamNonBlocking, (i % 8) == 0 ? hi : lo));
+    }
     HIPCHK(hipStreamSynchronize(s));                   // (the input upload)
 
     // the sizes at pos: S[i] = min(cands[i], remain); canonical = the first index
@@ -585,6 +591,12 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
             }
             jobs.emplace_back(r.first, std::move(r.second));
         }
+        // the largest size first (slot 0, the high-priority stream)
+        static const bool noprio = getenv("AMBC_MS_NOPRIO") != nullptr;
+        if (!noprio)
+            std::stable_sort(jobs.begin(), jobs.end(), [](const Job& a, const Job& b) {
+                return a.first.first != b.first.first ? a.first.first > b.first.first : a.first.second > b.first.second;
+            });
         t_req += now_ns() - tq;
         if (!jobs.empty()) G.rounds++;
         // up to 8 batches at once, each on its own stream and batch buffers (the
