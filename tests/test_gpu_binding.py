@@ -210,6 +210,7 @@ def test_binding_falls_back_where_it_cannot_follow(Bound):
     data = synth.generate(40000, 95)
     comp = Bound(ids=(1, 3))
     comp.compression_methods.insert(0, M.Bzip2Compression())     # id 6 before id 1: list-order ties
+    comp.method_lookup[6] = comp.compression_methods[0]
     with pytest.warns(ambc_binding_warning()):
         body = comp._adaptive_compress(data)
     assert comp.own_loop_calls == 1
