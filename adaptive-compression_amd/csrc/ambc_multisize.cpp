@@ -665,15 +665,23 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
     HIPCHK(d.ms_out.ensure(body + 64));
     uint8_t* d_body = d.ms_out.as<uint8_t>();
     const uint64_t te = now_ns();
-    std::map<uint32_t, std::vector<size_t>> groups;
+    // grouped by (size, winning id), each group encoded with its winner alone: the
+    // method encoders are deterministic, so the winner's bytes are those of the full
+    // loop, and the losers' encoders (a 64 KiB DEFLATE parse behind an RLE winner)
+    // do not run again.  The plen / id check below still holds every package to the
+    // walk's decision.
+    static const bool allm = getenv("AMBC_MS_FINAL_ALL") != nullptr;
+    std::map<std::pair<uint32_t, uint8_t>, std::vector<size_t>> groups;
     for (size_t i = 0; i < path.size(); i++)
-        if (path[i].id != 255 && !path[i].host) groups[path[i].s].push_back(i);
-    std::vector<std::pair<uint32_t, std::vector<size_t>>> gl(groups.begin(), groups.end());
+        if (path[i].id != 255 && !path[i].host) groups[{path[i].s, allm ? (uint8_t)0 : path[i].id}].push_back(i);
+    std::vector<std::pair<std::pair<uint32_t, uint8_t>, std::vector<size_t>>> gl(groups.begin(), groups.end());
     for (size_t j0 = 0; j0 < gl.size(); j0 += 8) {
         const size_t j1 = std::min(gl.size(), j0 + 8);
         std::vector<std::vector<uint64_t>> offs(j1 - j0);
         for (size_t j = j0; j < j1; j++) {
-            const uint32_t sz = gl[j].first;
+            const uint32_t sz = gl[j].first.first;
+            ambc_params pw = *p;
+            if (gl[j].first.second) pw.method_mask = 1u << gl[j].first.second;
             Batch& bb = d.msb[j - j0];
             hipStream_t xs = d.mss[j - j0];
             const uint32_t cnt = (uint32_t)gl[j].second.size();
@@ -682,7 +690,7 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
                 bb.hpos[q] = path[gl[j].second[q]].pos;
                 offs[j - j0].push_back(path[gl[j].second[q]].off);
             }
-            int rc = launch_batch(bb, xs, d_in, n, p, sz, bb.hpos, cnt, ent_of(sz), false);
+            int rc = launch_batch(bb, xs, d_in, n, &pw, sz, bb.hpos, cnt, ent_of(sz), false);
             if (rc) return rc;
             HIPCHK(bb.off.ensure((size_t)cnt * 8));
             HIPCHK(hipMemcpyAsync(bb.off.p, offs[j - j0].data(), (size_t)cnt * 8, hipMemcpyHostToDevice, xs));
