@@ -396,11 +396,16 @@ __device__ __forceinline__ uint32_t rle_flush(uint8_t* rs, uint8_t* re, uint32_t
 // EV (ENC_EVAL, chunks >= 16 KiB, padded input): the decision only -- the chunk is
 // read in place instead of staged (the 64 / 32 KiB LDS copy held the CU to 2 / 3
 // workgroups through the multi-size walk's rounds) and nothing is emitted
-// IP (chunks up to 8 KiB, padded input): read in place as well, bits still staged
-// in the LDS region (13 -> 9 KB of LDS at 4 KiB)
+// IP (padded input): read in place as well.  Up to 8 KiB the bits are still staged
+// in the LDS region (13 -> 9 KB of LDS at 4 KiB); from 16 KiB (GB) they go straight
+// into the chunk's slot by global atomics, the zlib header and the block header
+// built in the LDS region first: 10 KB of LDS instead of 74 KB at 64 KiB, where the
+// staged copy held a CU to 2 workgroups (half its SIMDs idle) for the multi-size
+// walk's final encode
 template <int CMAX, bool EV = false, bool IP = EV>
 __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
-    constexpr bool NOCHUNK = EV || (IP && CMAX < 16384);
+    constexpr bool NOCHUNK = EV || IP;
+    constexpr bool GB = IP && !EV && CMAX >= 16384;
     __shared__ GdSmem<CMAX, NOCHUNK> S;
     constexpr int ROUNDS = GdSmem<CMAX, NOCHUNK>::ROUNDS;
     const uint32_t lane = threadIdx.x;
@@ -810,14 +815,17 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
         gd_codes<30>(S.dl, S.dc, S.blc, lane);
         gd_codes<19>(S.cl, S.cc, S.blc, lane);
     }
-    uint32_t* bits = BIG ? reinterpret_cast<uint32_t*>(S.chunk) : S.region;
-    const uint32_t nwords = (body + 8) / 4 + 1;
+    // GB: the header words are built in the LDS region from bit 16 (behind 78 DA)
+    uint32_t* bits = GB ? S.region : BIG ? reinterpret_cast<uint32_t*>(S.chunk) : S.region;
+    const uint32_t nwords = GB ? 160u : (body + 8) / 4 + 1;
     for (uint32_t i = lane; i < nwords; i += 64) bits[i] = 0;
     wave_sync();
+    const uint32_t b0 = GB ? 16u : 0u;
     uint32_t bp = 0;
     if (lane == 0) {
-        put_bits_plain(bits, 0, 1u | ((uint32_t)kind << 1), 3);
-        bp = 3;
+        if constexpr (GB) put_bits_plain(bits, 0, 0xDA78u, 16);
+        put_bits_plain(bits, b0, 1u | ((uint32_t)kind << 1), 3);
+        bp = b0 + 3;
         if (kind == 2) {
             put_bits_plain(bits, bp, hlit - 257, 5); bp += 5;
             put_bits_plain(bits, bp, hdist - 1, 5); bp += 5;
@@ -833,6 +841,16 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     }
     bp = readlane(bp, 0);
     wave_sync();
+    if constexpr (GB) {
+        // the header words to the slot, the rest of the package's words zeroed; the
+        // symbols then OR themselves in (the stores complete first)
+        uint32_t* gw = reinterpret_cast<uint32_t*>(slot);
+        const uint32_t hw = (bp + 31) / 32, gn = (2 + body + 4 + 3) / 4 + 1;
+        for (uint32_t i = lane; i < gn; i += 64) gw[i] = i < hw ? bits[i] : 0u;
+        __threadfence();
+        wave_sync();
+        bits = gw;
+    }
     if (n - mcov <= 8 * (ns + 1)) {
         // match-major: lane e emits the literal run before match e and the
         // match (element ns: the literals after the last match); 64 matches per
@@ -919,6 +937,14 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
         }
     }
     wave_sync();
+    if constexpr (GB) {
+        // end of block and Adler-32 (big-endian bytes after the body) by OR as well
+        if (lane == 0) put_bits_atomic(bits, bp, S.lc[256], S.ll[256]);
+        if (lane < 4) {
+            const uint32_t q = 2 + body + lane;
+            atomicOr(&bits[q >> 2], ((adler >> (8 * (3 - lane))) & 0xFFu) << (8 * (q & 3)));
+        }
+    } else {
     if (lane == 0) put_bits_plain(bits, bp, S.lc[256], S.ll[256]);
     wave_sync();
     // ---- the zlib stream into the slot ----
@@ -930,6 +956,7 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
         else if (i < 2 + body) o = bb[i - 2];
         else o = (uint8_t)(adler >> (8 * (3 - (i - 2 - body))));
         slot[i] = o;
+    }
     }
     if (lane == 0) {
         A.ids[k] = 5;
@@ -952,6 +979,11 @@ hipError_t launch_deflate_t(const EncArgs& a, hipStream_t s) {
     if constexpr (CMAX >= 16384) {
         if ((a.flags & ENC_EVAL) && (a.flags & ENC_IN_ALIGNED) && !getenv("AMBC_DEFLATE_EV_LDS")) {
             hipLaunchKernelGGL((k_deflate<CMAX, true>), dim3(a.n_chunks), dim3(64), 0, s, a);
+            return hipGetLastError();
+        }
+        static const bool gb_lds = getenv("AMBC_DEFLATE_GB_LDS") != nullptr;
+        if (!(a.flags & ENC_EVAL) && (a.flags & ENC_IN_ALIGNED) && !gb_lds) {
+            hipLaunchKernelGGL((k_deflate<CMAX, false, true>), dim3(a.n_chunks), dim3(64), 0, s, a);
             return hipGetLastError();
         }
     }
