@@ -323,9 +323,8 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
     uint32_t jsub[32];                                 // subc index of cands[i]
     for (uint32_t i = 0; i < nc; i++)
         jsub[i] = (uint32_t)(std::lower_bound(subc.begin(), subc.end(), cands[i]) - subc.begin());
-    auto sizes_at = [&](uint64_t pos, Sizes& z) {
+    auto sizes_fill = [&](uint64_t pos, Sizes& z) {
         const uint64_t remain = n - pos;
-        if (have_inner && remain >= maxc) { z = inner; return; }
         z.canon = 0;
         z.M = 0;
         for (uint32_t i = 0; i < nc; i++) {
@@ -337,17 +336,24 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
         }
     };
     if (n >= maxc) {
-        sizes_at(0, inner);
+        sizes_fill(0, inner);
         have_inner = true;
     }
+    // the sizes at pos: inner's by reference, a position near the end's in a scratch
+    // record (valid until the next call)
+    Sizes edge;
+    auto sizes_at = [&](uint64_t pos) -> const Sizes& {
+        if (have_inner && n - pos >= maxc) return inner;
+        sizes_fill(pos, edge);
+        return edge;
+    };
     // part O of candidate i at a position: needed (not raw by construction)?
     auto needs_o = [&](const Sizes& z, uint32_t i) {
         return z.S[i] == z.M ? false : any_eligible(lzshare ? &po : p, z.S[i]);
     };
     auto needs_m = [&](const Sizes& z) { return z.M != 0; };
     auto ready = [&](uint64_t pos) -> bool {
-        Sizes z;
-        sizes_at(pos, z);
+        const Sizes& z = sizes_at(pos);
         PosTable::Rec& r = T.at(pos);
         if (needs_m(z) && !r.mhave) return false;
         for (uint32_t i = 0; i < nc; i++)
@@ -357,8 +363,7 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
     };
     // the reference's decision at pos (adaptive_compressor.py:546-590), all parts known
     auto decide = [&](uint64_t pos) -> Decision {
-        Sizes z;
-        sizes_at(pos, z);
+        const Sizes& z = sizes_at(pos);
         PosTable::Cand* cd = T.at(pos).c();
         const uint64_t remain = n - pos;
         double best_ratio = 1.0;
@@ -403,15 +408,39 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
     // host-codec requests of one round: (position, size), and where they go
     std::vector<uint64_t> hpos;
     std::vector<uint32_t> hsize;
-    // requests of one round: (size, kind) -> positions; kind 1 = M's launch
-    std::map<std::pair<uint32_t, int>, std::vector<uint64_t>> req;
+    // requests of one round: (size, kind) -> positions; kind 1 = M's launch.  A
+    // handful of buckets, found by a short scan -- for inner positions (every size
+    // the candidate's own) by a per-candidate cache
+    using ReqKey = std::pair<uint32_t, int>;
+    std::vector<std::pair<ReqKey, std::vector<uint64_t>>> req;
+    int req_in[33];                                    // bucket of inner candidate i (32: M), -1: none yet
+    auto req_clear = [&]() {
+        req.clear();
+        for (int& x : req_in) x = -1;
+    };
+    req_clear();
+    auto req_bucket = [&](ReqKey key) -> std::vector<uint64_t>& {
+        for (auto& b : req)
+            if (b.first == key) return b.second;
+        req.emplace_back(key, std::vector<uint64_t>());
+        return req.back().second;
+    };
+    auto req_push = [&](bool in, int ci, ReqKey key, uint64_t pos) {
+        if (!in) { req_bucket(key).push_back(pos); return; }
+        if (req_in[ci] < 0) {
+            req_bucket(key);
+            for (size_t b = 0; b < req.size(); b++)
+                if (req[b].first == key) req_in[ci] = (int)b;
+        }
+        req[(size_t)req_in[ci]].second.push_back(pos);
+    };
     auto request = [&](uint64_t pos) {
-        Sizes z;
-        sizes_at(pos, z);
+        const Sizes& z = sizes_at(pos);
+        const bool in = &z == &inner;
         PosTable::Rec& r = T.at(pos);
         if (needs_m(z) && !r.mhave && !r.mreq) {
             r.mreq = 1;
-            req[{z.M, 1}].push_back(pos);
+            req_push(in, 32, {z.M, 1}, pos);
         }
         for (uint32_t i = 0; i < nc; i++) {
             if (!((z.canon >> i) & 1)) continue;
@@ -423,7 +452,7 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
             if (!needs_o(z, i)) continue;
             if (((r.have | r.req) >> i) & 1) continue;
             r.req |= 1u << i;
-            req[{z.S[i], 0}].push_back(pos);
+            req_push(in, (int)i, {z.S[i], 0}, pos);
         }
     };
     // the host codecs' answers for the round's pairs into the table
@@ -438,8 +467,7 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
         if (hc->eval(hc->user, hpos.data(), hsize.data(), (uint32_t)hpos.size(), hid_out.data(), hlen_out.data()))
             return fail(AMBC_E_CODEC, "host codec evaluation failed");
         for (size_t q = 0; q < hpos.size(); q++) {
-            Sizes z;
-            sizes_at(hpos[q], z);
+            const Sizes& z = sizes_at(hpos[q]);
             PosTable::Rec& r = T.at(hpos[q]);
             for (uint32_t i = 0; i < nc; i++)
                 if (((z.canon >> i) & 1) && z.S[i] == hsize[q]) {
@@ -457,8 +485,7 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
     auto fill = [&](const Batch& bb, uint32_t sz, int kind, const std::vector<uint64_t>& poss) {
         for (size_t q = 0; q < poss.size(); q++) {
             const uint64_t pos = poss[q];
-            Sizes z;
-            sizes_at(pos, z);
+            const Sizes& z = sizes_at(pos);
             PosTable::Rec& r = T.at(pos);
             PosTable::Cand* cd = r.c();
             for (uint32_t i = 0; i < nc; i++) {
@@ -559,7 +586,7 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
         t_dec += now_ns() - tq;
         tq = now_ns();
         if (G.active.empty()) return AMBC_OK;
-        req.clear();
+        req_clear();
         hpos.clear();
         hsize.clear();
         for (const Walk& w : G.active) {
@@ -580,8 +607,7 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
                         return rc;
                 // speculative only: never decided from -- forget the requests
                 for (uint64_t q : r.second) {
-                    Sizes z;
-                    sizes_at(q, z);
+                    const Sizes& z = sizes_at(q);
                     PosTable::Rec& rec = T.at(q);
                     if (r.first.second == 1) rec.mreq = 0;
                     for (uint32_t i = 0; i < nc; i++)
