@@ -404,7 +404,7 @@ __device__ __forceinline__ uint32_t rle_flush(uint8_t* rs, uint8_t* re, uint32_t
 // walk's final encode
 template <int CMAX, bool EV = false, bool IP = EV>
 __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
-    constexpr bool NOCHUNK = EV || IP;
+    constexpr bool NOCHUNK = IP;
     constexpr bool GB = IP && !EV && CMAX >= 16384;
     __shared__ GdSmem<CMAX, NOCHUNK> S;
     constexpr int ROUNDS = GdSmem<CMAX, NOCHUNK>::ROUNDS;

@@ -968,10 +968,28 @@ __global__ __launch_bounds__(64) AMBC_ENC_ATTR void k_encode(EncArgs A) {
 
 // ---------------------------------------------------------------------------
 // k_compact: header + payload of each package to its byte offset in the body.
-// One wave per package; dwords are assembled with v_alignbyte from two
-// aligned slot loads and stored 4-byte aligned; the 1-3 edge bytes shared
-// with the neighbouring packages are written as single bytes.
+// One wave per package.  The package's interior is written in 16-byte aligned
+// groups of the body, one group per lane and step: each group's 16 source bytes
+// lie at one fixed offset (mod 16) of the 16-byte aligned slot, so two aligned
+// 16-byte loads and four v_alignbyte make it (1 KB per store instruction; the
+// dword version before issued two loads and a store per 4 bytes, 0.39 ms for a
+// 1 GiB segment's 262144 packages alone).  The header and the edge groups shared
+// with the neighbouring packages go byte by byte.
 // ---------------------------------------------------------------------------
+
+__device__ __forceinline__ uint32_t pick_dword(const uint4& a, const uint4& b, uint32_t i) {
+    // dword i (0..7) of the 32-byte window a:b (i wave-uniform per package)
+    switch (i) {
+        case 0: return a.x;
+        case 1: return a.y;
+        case 2: return a.z;
+        case 3: return a.w;
+        case 4: return b.x;
+        case 5: return b.y;
+        case 6: return b.z;
+        default: return b.w;
+    }
+}
 
 __device__ __forceinline__ void compact_package(const CompactArgs& A, uint32_t k, uint32_t lane) {
     const uint64_t o = A.off[k] + (A.base ? *A.base : 0ull);
@@ -981,50 +999,36 @@ __device__ __forceinline__ void compact_package(const CompactArgs& A, uint32_t k
     const uint64_t p0 = (uint64_t)k * A.chunk_size;
     const uint32_t n = A.clen ? A.clen[k] : (uint32_t)min((uint64_t)A.chunk_size, A.n_total - p0);
     const uint8_t* __restrict__ sl = type == 255 && A.in ? A.in + p0 : A.slots + (uint64_t)k * A.slot_stride;
-    const uint64_t d0 = o >> 2, d1 = (o + P - 1) >> 2;
-    uint32_t* __restrict__ out32 = reinterpret_cast<uint32_t*>(A.out);
-    const uint32_t sh = (uint32_t)((0 - o - HDR) & 3u);   // payload byte offset inside a source dword
-    // 256 dwords per step, four per lane at a 64-dword stride (every store
-    // instruction writes 256 contiguous bytes); the interior dwords' loads are
-    // all issued before their stores, the edge dwords go byte by byte
-    for (uint64_t db = d0; db <= d1; db += 256) {
-        uint32_t lo[4], hi[4];
-        bool in[4];
+    uint8_t* const dst = A.out + o;                       // the package's first byte
+    const uint64_t da = reinterpret_cast<uintptr_t>(dst);
+    // interior groups: body-aligned 16-byte groups wholly inside the payload
+    const uint64_t g0 = (da + HDR + 15) >> 4, g1 = (da + P) >> 4;   // [g0, g1)
+    const uint32_t ng = g1 > g0 ? (uint32_t)(g1 - g0) : 0u;
+    const uint32_t head = ng ? (uint32_t)((g0 << 4) - da) : P;     // bytes before the interior
+    const uint32_t tail0 = ng ? head + 16 * ng : P;                 // first byte after it
+    if (ng) {
+        // payload offset of group g0's first byte, and its place in the aligned source
+        const uint32_t t0 = head - HDR;
+        const uint32_t rr = (uint32_t)((reinterpret_cast<uintptr_t>(sl) + t0) & 15u);
+        const uint32_t ds = rr >> 2, bs = (rr & 3u) * 8u;
+        const uint4* src4 = reinterpret_cast<const uint4*>(sl + t0 - rr);
+        uint4* dst4 = reinterpret_cast<uint4*>(g0 << 4);
+        for (uint32_t j = lane; j < ng; j += 64) {
+            const uint4 a = src4[j], b = src4[j + 1];
+            uint32_t w[5];
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint64_t d = db + lane + 64 * j;
-            const int64_t q0 = (int64_t)(d << 2) - (int64_t)o;
-            in[j] = d <= d1 && q0 >= (int64_t)HDR && q0 + 4 <= (int64_t)P;
-            const uint32_t* s32 = reinterpret_cast<const uint32_t*>(sl) + (in[j] ? ((uint32_t)q0 - HDR) >> 2 : 0u);
-            lo[j] = in[j] ? s32[0] : 0u;
-            hi[j] = in[j] && sh ? s32[1] : 0u;
-        }
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint64_t d = db + lane + 64 * j;
-            if (in[j]) {
-                out32[d] = __builtin_amdgcn_alignbyte(hi[j], lo[j], sh);
-            } else if (d <= d1) {
-                const int64_t qd = (int64_t)(d << 2) - (int64_t)o;
-                if (qd >= 0 && qd + 4 <= (int64_t)P) {
-                    uint32_t v = 0;
-                    for (int b = 0; b < 4; b++) {
-                        const uint32_t q = (uint32_t)qd + b;
-                        const uint32_t by = q < HDR ? hdr_byte(q, type, n, pl) : sl[q - HDR];
-                        v |= by << (8 * b);
-                    }
-                    out32[d] = v;
-                } else {
-                    for (int b = 0; b < 4; b++) {
-                        const int64_t q = qd + b;
-                        if (q < 0 || q >= (int64_t)P) continue;
-                        const uint32_t qq = (uint32_t)q;
-                        A.out[(d << 2) + b] = (uint8_t)(qq < HDR ? hdr_byte(qq, type, n, pl) : sl[qq - HDR]);
-                    }
-                }
-            }
+            for (int i = 0; i < 5; i++) w[i] = pick_dword(a, b, ds + i);
+            uint4 v;
+            v.x = (uint32_t)((((uint64_t)w[1] << 32) | w[0]) >> bs);
+            v.y = (uint32_t)((((uint64_t)w[2] << 32) | w[1]) >> bs);
+            v.z = (uint32_t)((((uint64_t)w[3] << 32) | w[2]) >> bs);
+            v.w = (uint32_t)((((uint64_t)w[4] << 32) | w[3]) >> bs);
+            dst4[j] = v;
         }
     }
+    // the header and the edges, byte by byte
+    for (uint32_t q = lane; q < head; q += 64) dst[q] = q < HDR ? hdr_byte(q, type, n, pl) : sl[q - HDR];
+    for (uint32_t q = tail0 + lane; q < P; q += 64) dst[q] = q < HDR ? hdr_byte(q, type, n, pl) : sl[q - HDR];
 }
 
 // a fixed grid of resident workgroups that stride over the packages: launched

@@ -147,6 +147,12 @@ struct Dev {
     uint64_t ms_walk_ns = 0, ms_emit_ns = 0;  // and the time of the walk / of the final encode
     Buf ms_out;                 // the multi-size walk's body (its own buffer: no other call writes it)
     uint64_t ms_body = 0;       // a multi-size body kept in `ms_out` for ambc_fetch_body (0: none)
+    // the multi-size walk's position records, kept across calls (a fresh 40 KB page
+    // per 256 positions cost ~25 ms of page faults and construction per 256 MiB
+    // call): a record belongs to the call whose epoch it carries
+    std::vector<std::vector<uint8_t>> ms_pages;
+    size_t ms_rsz = 0;
+    uint32_t ms_epoch = 0;
     uint64_t t_encode = 0, t_scan = 0, t_compact = 0;
     uint32_t n_launch = 1;      // k_encode launches of the last compress call (pipelined segments)
     hipStream_t cs = nullptr;   // scan + compaction of pipelined segments

@@ -178,6 +178,7 @@ struct PosTable {
         uint8_t mhave = 0, mreq = 0, decided = 0;   // M's launch known / asked for; decision taken
         uint8_t pad = 0;
         Decision dec{0, 0, 0, 0};
+        uint32_t epoch = 0;                         // the call this record belongs to (0: none)
         Cand* c() { return reinterpret_cast<Cand*>(this + 1); }
     };
     static_assert(sizeof(Rec) % alignof(Cand) == 0, "candidates follow the record");
@@ -185,28 +186,41 @@ struct PosTable {
     int gsh = -1;                // log2(g) when g is a power of two (the reference's list: 1024)
     uint32_t nc = 0;
     size_t rsz = 0;              // bytes per position record
-    std::vector<std::unique_ptr<uint8_t[]>> pages;
-    void init(uint64_t n, uint64_t g_, uint32_t nc_) {
+    uint32_t epoch = 0;
+    std::vector<std::vector<uint8_t>>* pages = nullptr;   // the context's pool (Dev::ms_pages)
+    void init(uint64_t n, uint64_t g_, uint32_t nc_, Dev& d) {
         g = g_;
         gsh = (g & (g - 1)) == 0 ? __builtin_ctzll(g) : -1;
         nc = nc_;
         rsz = sizeof(Rec) + (size_t)nc * sizeof(Cand);
-        pages.clear();
-        pages.resize((size_t)((n / g >> PB) + 1));
+        pages = &d.ms_pages;
+        if (d.ms_rsz != rsz) {   // another record layout: the pool starts over
+            d.ms_pages.clear();
+            d.ms_rsz = rsz;
+        }
+        const size_t np = (size_t)((n / g >> PB) + 1);
+        if (d.ms_pages.size() < np) d.ms_pages.resize(np);
+        if (++d.ms_epoch == 0) {   // (wrapped: no record may carry a reused epoch)
+            d.ms_pages.clear();
+            d.ms_pages.resize(np);
+            d.ms_epoch = 1;
+        }
+        epoch = d.ms_epoch;
     }
-    // the record of position pos, its page created on first use
+    // the record of position pos: its page created on first use in the context,
+    // the record reset on first use in this call
     Rec& at(uint64_t pos) {
         const uint64_t x = gsh >= 0 ? pos >> gsh : pos / g;
         const uint32_t slot = (uint32_t)(x & ((1u << PB) - 1));
-        std::unique_ptr<uint8_t[]>& pg = pages[(size_t)(x >> PB)];
-        if (!pg) {
-            pg.reset(new uint8_t[rsz << PB]);
-            for (uint32_t q = 0; q < (1u << PB); q++) {
-                Rec* r = new (pg.get() + rsz * q) Rec();
-                for (uint32_t i = 0; i < nc; i++) new (r->c() + i) Cand();
-            }
+        std::vector<uint8_t>& pg = (*pages)[(size_t)(x >> PB)];
+        if (pg.empty()) pg.resize(rsz << PB);   // (zeros: epoch 0)
+        Rec* r = reinterpret_cast<Rec*>(pg.data() + rsz * slot);
+        if (r->epoch != epoch) {
+            new (r) Rec();
+            r->epoch = epoch;
+            for (uint32_t i = 0; i < nc; i++) new (r->c() + i) Cand();
         }
-        return *reinterpret_cast<Rec*>(pg.get() + rsz * slot);
+        return *r;
     }
 };
 
@@ -279,7 +293,7 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
     uint64_t g = 0;
     for (uint32_t c : cands) g = std::gcd(g, (uint64_t)c);
     PosTable T;
-    T.init(n, g, nc);
+    T.init(n, g, nc, d);
     struct Walk { uint64_t pos; uint32_t last; };      // last: the size it took the step before
     std::vector<Walk> active;
     // walks: one per 256 KiB, at most 1024 (256 MiB of mixed data, reference
@@ -596,6 +610,33 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
                 request(q);
             }
         }
+        // few walks left (the device idles behind one chunk's latency): each walk
+        // also asks for every position its next step can reach, and a guess chain
+        // from each, within BREADTH positions a round -- the next round then decides
+        // at least two steps whatever size wins (AMBC_MS_BREADTH=0: off).  Budget: what
+        // one round's latency hides, ~2048 chunks of 64 KiB ({1,2,3,4,5} 3.55-3.60 ->
+        // 3.79-3.80 GB/s, {1,3,4,9} unchanged); none with zlib-9, whose 64 KiB parse
+        // holds a CU per chunk (like_reference() 0.33 -> 0.20 GB/s with it,
+        // profiles/r4_breadth_ab)
+        static const int64_t BREADTH_ENV = getenv("AMBC_MS_BREADTH") ? atoll(getenv("AMBC_MS_BREADTH")) : -1;
+        const uint64_t BREADTH = BREADTH_ENV >= 0 ? (uint64_t)BREADTH_ENV
+                                                  : ((p->flags & AMBC_FLAG_ZLIB9) && ((p->method_mask >> AMBC_M_DEFLATE) & 1) ? 0 : 2048);
+        if (BREADTH && !G.active.empty() && G.active.size() * nc <= BREADTH) {
+            const uint64_t per = BREADTH / G.active.size();
+            for (const Walk& w : G.active) {
+                const Sizes z = sizes_at(w.pos);           // (a copy: request() reuses the scratch)
+                const uint32_t nsz = (uint32_t)__builtin_popcount(z.canon);
+                const uint64_t depth = std::min<uint64_t>((uint64_t)SPEC + 1, std::max<uint64_t>(1, per / nsz));
+                for (uint32_t i = 0; i < nc; i++) {
+                    if (!((z.canon >> i) & 1) || z.S[i] == w.last) continue;   // (the main chain)
+                    uint64_t q = w.pos + z.S[i];
+                    for (uint64_t k = 0; k < depth && q < n; k++, q += z.S[i]) {
+                        if (T.at(q).decided) break;
+                        request(q);
+                    }
+                }
+            }
+        }
         std::vector<Job> jobs;
         for (auto& r : req) {
             const ambc_params* pk = r.first.second == 1 || !lzshare ? p : &po;
@@ -683,7 +724,6 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
         pos += dd.s;
     }
     body += END_CHUNK;
-    T.pages.clear();
     d.ms_body = 0;
     if (out && out_cap < body) return fail(AMBC_E_CAPACITY, "output capacity below the body size");
 

@@ -780,6 +780,15 @@ __global__ __launch_bounds__(64) void k_z9_code(EncArgs A) {
             const uint32_t bits = kind == 0 ? ((3 + 7) & ~7u) + 32 + 8 * n : 3 + S.misc[8];
             const uint32_t total = 2 + (bits + 7) / 8 + 4;
             if (total + 18 >= T) { ZSTAMP_FLUSH; return; }
+            if (A.flags & ENC_EVAL) {   // the multi-size walk's decision: no bits
+                if (lane == 0) {
+                    A.ids[k] = 5;
+                    A.plen[k] = total;
+                    A.sizes[k] = 18ull + total;
+                }
+                ZSTAMP_FLUSH;
+                return;
+            }
         }
         if (kind == 0) {
             // stored: the 3 header bits, byte alignment, LEN / NLEN, the bytes

@@ -854,6 +854,14 @@ __global__ __launch_bounds__(64) void k_z9_code_big(EncArgs A) {
     }
     const uint32_t total = (bp + 7) / 8 + 4;
     if (total + 18 >= T) return;
+    if (A.flags & ENC_EVAL) {   // the multi-size walk's decision: pass 2 writes nothing it reads
+        if (lane == 0) {
+            A.ids[k] = 5;
+            A.plen[k] = total;
+            A.sizes[k] = 18ull + total;
+        }
+        return;
+    }
 
     // ---- pass 2: the bits ----
     uint32_t* out32 = reinterpret_cast<uint32_t*>(A.slots + (uint64_t)k * A.slot_stride);
