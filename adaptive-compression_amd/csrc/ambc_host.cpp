@@ -110,7 +110,7 @@ void ambc_destroy(ambc_ctx* ctx) {
         for (Buf* b : {&d.in, &d.out, &d.slots, &d.plen, &d.ids, &d.sizes, &d.off, &d.scan_tmp,
                        &d.acc, &d.ent_full, &d.ent_tail, &d.body, &d.jobs, &d.produced, &d.dout,
                        &d.scratch, &d.seg, &d.list, &d.bestpre, &d.gdseq, &d.pending, &d.z9rec, &d.z9scr, &d.segbase, &d.coll,
-                       &d.inffix, &d.ms_out})
+                       &d.inffix, &d.ms_out, &d.ms_ent})
             b->release();
         for (auto& b : d.msb) b.release();
         d.dw.release();

@@ -102,11 +102,9 @@ int launch_batch(Batch& b, hipStream_t st, const uint8_t* d_in, uint64_t n, cons
     bool aligned = ((uintptr_t)d_in & 15) == 0 && !getenv("AMBC_ENC_LDS");
     for (uint32_t q = 0; q < cnt && aligned; q++) aligned = (pos[q] & 15) == 0;
     if (aligned) ea.flags |= ENC_IN_ALIGNED;
-    if (ent) {   // numpy's p*log2(p) terms for an s-byte chunk (Huffman should_use near 7.0)
-        HIPCHK(b.ent.ensure((size_t)(s + 1) * 8));
-        HIPCHK(hipMemcpyAsync(b.ent.p, ent, (size_t)(s + 1) * 8, hipMemcpyHostToDevice, st));
-        if (s == C) ea.ent_full = b.ent.as<double>();
-        else ea.ent_tail = b.ent.as<double>();
+    if (ent) {   // numpy's p*log2(p) terms for an s-byte chunk (Huffman should_use near 7.0), on the device
+        if (s == C) ea.ent_full = ent;
+        else ea.ent_tail = ent;
     }
     if (nsub) {
         HIPCHK(b.lz4sub.ensure((size_t)cnt * LZ4_SUB_MAX * 4));
@@ -261,9 +259,28 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
     d.ms_body = 0;                 // a body left by an earlier call is gone from here on
     HIPCHK(hipSetDevice(d.id));
     hipStream_t s = d.stream;
+    // the entropy tables, uploaded once per call (a per-batch upload from the
+    // caller's pageable arrays held the host until the stream's hardware queue
+    // drained: the round's batches then ran one after another)
     std::map<uint32_t, const double*> ent;
-    for (uint32_t i = 0; i < n_ent; i++)
-        if (ent_tabs && ent_tabs[i]) ent[ent_sizes[i]] = ent_tabs[i];
+    {
+        size_t tot = 0;
+        for (uint32_t i = 0; i < n_ent; i++)
+            if (ent_tabs && ent_tabs[i]) tot += ((size_t)ent_sizes[i] + 1) * 8;
+        if (tot) {
+            HIPCHK(d.ms_ent.ensure(tot));
+            std::vector<uint8_t> stage(tot);
+            size_t o = 0;
+            for (uint32_t i = 0; i < n_ent; i++) {
+                if (!ent_tabs || !ent_tabs[i]) continue;
+                const size_t b = ((size_t)ent_sizes[i] + 1) * 8;
+                std::memcpy(stage.data() + o, ent_tabs[i], b);
+                ent[ent_sizes[i]] = reinterpret_cast<const double*>(d.ms_ent.as<uint8_t>() + o);
+                o += b;
+            }
+            HIPCHK(hipMemcpy(d.ms_ent.p, stage.data(), tot, hipMemcpyHostToDevice));
+        }
+    }
     auto ent_of = [&](uint32_t sz) -> const double* {
         auto it = ent.find(sz);
         return it == ent.end() ? nullptr : it->second;
