@@ -28,16 +28,109 @@
 // slots -- the walk's decision must come out again, or the call fails -- and
 // moved into the body at their offsets (k_compact with per-package lengths).
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <new>
 #include <numeric>
+#include <thread>
+
+#include <unistd.h>
 
 #include "ambc_hostctx.h"
 
 namespace ambc {
 namespace {
+
+// A few host threads for the walk's per-round host work (filling a batch's results
+// into the position table, deciding every walk's steps): between two rounds the
+// device waits for them (~1 ms a round for a thousand walks on one thread).  The
+// workers spin briefly between tasks (the rounds come every few ms), then sleep.
+// AMBC_MS_THREADS sets the count (1: all on the calling thread).
+class WalkPool {
+  public:
+    static WalkPool& get() {
+        static WalkPool pool;
+        return pool;
+    }
+    unsigned size() const { return (unsigned)workers_.size() + 1; }
+    // fn(t, T) for t in [0, T), T = size(); the caller runs t = 0
+    void run(const std::function<void(unsigned, unsigned)>& fn) {
+        const unsigned T = size();
+        if (T == 1) { fn(0, 1); return; }
+        if (getpid() != pid_) {   // a forked child has no workers: every slice here
+            for (unsigned t = 0; t < T; t++) fn(t, T);
+            return;
+        }
+        std::lock_guard<std::mutex> serial(run_mu_);   // one task at a time
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            task_ = &fn;
+            pending_.store(T - 1);
+            gen_.fetch_add(1);
+        }
+        cv_.notify_all();
+        fn(0, T);
+        while (pending_.load() != 0) std::this_thread::yield();
+        task_ = nullptr;
+    }
+    ~WalkPool() {
+        if (getpid() != pid_) {   // (a forked child: the threads are the parent's; leave them be)
+            new std::vector<std::thread>(std::move(workers_));
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+            gen_.fetch_add(1);
+        }
+        cv_.notify_all();
+        for (auto& t : workers_) t.join();
+    }
+
+  private:
+    WalkPool() {
+        const char* e = getenv("AMBC_MS_THREADS");
+        unsigned T = e ? (unsigned)std::max(1, atoi(e)) : std::min(6u, std::max(1u, std::thread::hardware_concurrency() / 2));
+        for (unsigned t = 1; t < T; t++) workers_.emplace_back([this, t] { loop(t); });
+        pid_ = getpid();
+    }
+    void loop(unsigned t) {
+        uint64_t seen = 0;
+        for (;;) {
+            // spin up to ~2 ms for the next task, then sleep on the condition variable
+            const auto t0 = std::chrono::steady_clock::now();
+            while (gen_.load() == seen && std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(2))
+                std::this_thread::yield();
+            if (gen_.load() == seen) {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return gen_.load() != seen; });
+            }
+            seen = gen_.load();
+            if (stop_) return;
+            const std::function<void(unsigned, unsigned)>* f;
+            {
+                std::lock_guard<std::mutex> g(mu_);
+                f = task_;
+            }
+            if (f) (*f)(t, size());
+            pending_.fetch_sub(1);
+        }
+    }
+    std::vector<std::thread> workers_;
+    std::mutex mu_, run_mu_;
+    std::condition_variable cv_;
+    std::atomic<uint64_t> gen_{0};
+    std::atomic<unsigned> pending_{0};
+    const std::function<void(unsigned, unsigned)>* task_ = nullptr;
+    bool stop_ = false;
+    pid_t pid_ = 0;
+};
 
 bool eligible(const ambc_params* p, uint32_t s, uint32_t id) {
     return ((p->method_mask >> id) & 1) && p->pref_min[id] <= s && s <= p->pref_max[id];
@@ -205,6 +298,15 @@ struct PosTable {
         }
         epoch = d.ms_epoch;
     }
+    // the record of position pos if this call touched it already, else null (no
+    // writes: safe beside other readers)
+    Rec* peek(uint64_t pos) {
+        const uint64_t x = gsh >= 0 ? pos >> gsh : pos / g;
+        const std::vector<uint8_t>& pg = (*pages)[(size_t)(x >> PB)];
+        if (pg.empty()) return nullptr;
+        Rec* r = reinterpret_cast<Rec*>(const_cast<uint8_t*>(pg.data()) + rsz * (uint32_t)(x & ((1u << PB) - 1)));
+        return r->epoch == epoch ? r : nullptr;
+    }
     // the record of position pos: its page created on first use in the context,
     // the record reset on first use in this call
     Rec& at(uint64_t pos) {
@@ -311,7 +413,9 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
     for (uint32_t c : cands) g = std::gcd(g, (uint64_t)c);
     PosTable T;
     T.init(n, g, nc, d);
-    struct Walk { uint64_t pos; uint32_t last; };      // last: the size it took the step before
+    // last: the size it took the step before; cq / cs: the guess chain asked for so
+    // far (positions pos + k * cs below cq are requested already)
+    struct Walk { uint64_t pos; uint32_t last; uint64_t cq = 0; uint32_t cs = 0; };
     std::vector<Walk> active;
     // walks: one per 256 KiB, at most 1024 (256 MiB of mixed data, reference
     // candidates, second call: best of 512-2048 walks x 2-4 positions ahead,
@@ -373,19 +477,18 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
     // the sizes at pos: inner's by reference, a position near the end's in a scratch
     // record (valid until the next call)
     Sizes edge;
-    auto sizes_at = [&](uint64_t pos) -> const Sizes& {
+    auto sizes_in = [&](uint64_t pos, Sizes& scratch) -> const Sizes& {   // (thread-safe with its own scratch)
         if (have_inner && n - pos >= maxc) return inner;
-        sizes_fill(pos, edge);
-        return edge;
+        sizes_fill(pos, scratch);
+        return scratch;
     };
+    auto sizes_at = [&](uint64_t pos) -> const Sizes& { return sizes_in(pos, edge); };
     // part O of candidate i at a position: needed (not raw by construction)?
     auto needs_o = [&](const Sizes& z, uint32_t i) {
         return z.S[i] == z.M ? false : any_eligible(lzshare ? &po : p, z.S[i]);
     };
     auto needs_m = [&](const Sizes& z) { return z.M != 0; };
-    auto ready = [&](uint64_t pos) -> bool {
-        const Sizes& z = sizes_at(pos);
-        PosTable::Rec& r = T.at(pos);
+    auto ready_z = [&](const Sizes& z, const PosTable::Rec& r) -> bool {
         if (needs_m(z) && !r.mhave) return false;
         for (uint32_t i = 0; i < nc; i++)
             if (((z.canon >> i) & 1) && needs_o(z, i) && !((r.have >> i) & 1)) return false;
@@ -393,9 +496,8 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
         return true;
     };
     // the reference's decision at pos (adaptive_compressor.py:546-590), all parts known
-    auto decide = [&](uint64_t pos) -> Decision {
-        const Sizes& z = sizes_at(pos);
-        PosTable::Cand* cd = T.at(pos).c();
+    auto decide_z = [&](uint64_t pos, const Sizes& z, PosTable::Rec& rec) -> Decision {
+        const PosTable::Cand* cd = rec.c();
         const uint64_t remain = n - pos;
         double best_ratio = 1.0;
         uint32_t best_s = 0, best_plen = 0;
@@ -513,11 +615,16 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
         return AMBC_OK;
     };
     // a batch's results into the table
-    auto fill = [&](const Batch& bb, uint32_t sz, int kind, const std::vector<uint64_t>& poss) {
-        for (size_t q = 0; q < poss.size(); q++) {
+    // (a batch's positions are distinct and were touched when requested: its
+    // records fill in parallel, read through peek)
+    WalkPool& pool = WalkPool::get();
+    auto fill_range = [&](const Batch& bb, uint32_t sz, int kind, const std::vector<uint64_t>& poss, size_t q0,
+                          size_t q1) {
+        Sizes scr;
+        for (size_t q = q0; q < q1; q++) {
             const uint64_t pos = poss[q];
-            const Sizes& z = sizes_at(pos);
-            PosTable::Rec& r = T.at(pos);
+            const Sizes& z = sizes_in(pos, scr);
+            PosTable::Rec& r = *T.peek(pos);
             PosTable::Cand* cd = r.c();
             for (uint32_t i = 0; i < nc; i++) {
                 if (!((z.canon >> i) & 1)) continue;
@@ -530,6 +637,11 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
             }
             if (kind == 1) r.mhave = 1;
         }
+    };
+    auto fill = [&](const Batch& bb, uint32_t sz, int kind, const std::vector<uint64_t>& poss) {
+        const size_t m = poss.size();
+        if (m < 2048 || pool.size() == 1) { fill_range(bb, sz, kind, poss, 0, m); return; }
+        pool.run([&](unsigned t, unsigned Tn) { fill_range(bb, sz, kind, poss, m * t / Tn, m * (t + 1) / Tn); });
     };
 
     uint32_t steps = 0;
@@ -594,20 +706,51 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
     // decide as far as known, then ask for the next positions and launch
     auto advance = [&](Group& G) -> int {
         uint64_t tq = now_ns();
-        std::vector<Walk> still;
-        for (Walk w : G.active) {
-            for (;;) {
-                PosTable::Rec& r = T.at(w.pos);
-                if (r.decided) break;                      // joined a decided path
-                if (!ready(w.pos)) { still.push_back(w); break; }
-                const Decision dd = decide(w.pos);
-                r.decided = 1;
-                r.dec = dd;
-                if (dd.id == 255) break;                   // the rest is raw: done
-                w.last = dd.s;
-                w.pos += dd.s;
-                if (w.pos >= n) break;
+        // phase 1, in parallel and read-only: every walk's steps as far as its
+        // positions are known; phase 2, in walk order: the steps into the table, a
+        // walk stopping where an earlier one decided already (it joined that path:
+        // the same decisions from there on) -- the sequential loop's outcome
+        const size_t na = G.active.size();
+        struct Trail { std::vector<std::pair<uint64_t, Decision>> steps; Walk end; bool open; };
+        std::vector<Trail> trails(na);
+        auto walk_range = [&](size_t a0, size_t a1) {
+            Sizes scr;
+            for (size_t a = a0; a < a1; a++) {
+                Trail& tr = trails[a];
+                tr.steps.clear();
+                Walk w = G.active[a];
+                tr.open = false;
+                for (;;) {
+                    PosTable::Rec* r = T.peek(w.pos);
+                    if (r && r->decided) break;            // joined a decided path
+                    const Sizes& z = sizes_in(w.pos, scr);
+                    if (!r || !ready_z(z, *r)) { tr.open = true; break; }
+                    const Decision dd = decide_z(w.pos, z, *r);
+                    tr.steps.emplace_back(w.pos, dd);
+                    if (dd.id == 255) break;               // the rest is raw: done
+                    w.last = dd.s;
+                    w.pos += dd.s;
+                    if (w.pos >= n) break;
+                }
+                tr.end = w;
             }
+        };
+        if (na < 64 || pool.size() == 1) walk_range(0, na);
+        else pool.run([&](unsigned t, unsigned Tn) { walk_range(na * t / Tn, na * (t + 1) / Tn); });
+        std::vector<Walk> still;
+        for (size_t a = 0; a < na; a++) {
+            Trail& tr = trails[a];
+            bool joined = false;
+            for (const auto& st : tr.steps) {
+                PosTable::Rec& r = T.at(st.first);
+                if (r.decided) { joined = true; break; }
+                r.decided = 1;
+                r.dec = st.second;
+            }
+            if (joined || !tr.open) continue;
+            PosTable::Rec* r = T.peek(tr.end.pos);
+            if (r && r->decided) continue;                  // (decided by an earlier walk this round)
+            still.push_back(tr.end);
         }
         // (two walks at one position: keep one)
         std::sort(still.begin(), still.end(), [](const Walk& x, const Walk& y) { return x.pos < y.pos; });
@@ -620,12 +763,22 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
         req_clear();
         hpos.clear();
         hsize.clear();
-        for (const Walk& w : G.active) {
+        static const bool rechain = getenv("AMBC_MS_RECHAIN") != nullptr;
+        for (Walk& w : G.active) {
             uint64_t q = w.pos;
-            for (int k = 0; k <= SPEC && q < n; k++, q += w.last) {
+            int k = 0;
+            // still on last round's chain: its requested prefix is skipped (with SPEC
+            // 6 a walk re-asked for six positions a round, most of them known)
+            if (!rechain && w.cs == w.last && w.cq > w.pos && (w.cq - w.pos) % w.last == 0) {
+                k = (int)std::min<uint64_t>((w.cq - w.pos) / w.last, (uint64_t)SPEC + 1);
+                q = w.pos + (uint64_t)k * w.last;
+            }
+            for (; k <= SPEC && q < n; k++, q += w.last) {
                 if (k && T.at(q).decided) break;
                 request(q);
             }
+            w.cs = w.last;
+            w.cq = q;
         }
         // few walks left (the device idles behind one chunk's latency): each walk
         // also asks for every position its next step can reach, and a guess chain
