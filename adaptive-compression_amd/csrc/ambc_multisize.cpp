@@ -279,6 +279,9 @@ struct PosTable {
     size_t rsz = 0;              // bytes per position record
     uint32_t epoch = 0;
     std::vector<std::vector<uint8_t>>* pages = nullptr;   // the context's pool (Dev::ms_pages)
+    std::unique_ptr<std::atomic<uint8_t>[]> pready;       // page i allocated (touch() from several threads)
+    std::mutex pmu;
+    static constexpr uint32_t BUSY = 0xFFFFFFFFu;         // a record being reset by one thread
     void init(uint64_t n, uint64_t g_, uint32_t nc_, Dev& d) {
         g = g_;
         gsh = (g & (g - 1)) == 0 ? __builtin_ctzll(g) : -1;
@@ -297,13 +300,43 @@ struct PosTable {
             d.ms_epoch = 1;
         }
         epoch = d.ms_epoch;
+        pready.reset(new std::atomic<uint8_t>[d.ms_pages.size()]);
+        for (size_t i = 0; i < d.ms_pages.size(); i++) pready[i].store(d.ms_pages[i].empty() ? 0 : 1);
+    }
+    std::vector<uint8_t>& page(size_t i) {
+        if (!pready[i].load(std::memory_order_acquire)) {
+            std::lock_guard<std::mutex> g(pmu);
+            if (!pready[i].load(std::memory_order_relaxed)) {
+                (*pages)[i].resize(rsz << PB);   // (zeros: epoch 0)
+                pready[i].store(1, std::memory_order_release);
+            }
+        }
+        return (*pages)[i];
+    }
+    // at() from several threads at once: the reset claimed by one of them
+    Rec& touch(uint64_t pos) {
+        const uint64_t x = gsh >= 0 ? pos >> gsh : pos / g;
+        Rec* r = reinterpret_cast<Rec*>(page((size_t)(x >> PB)).data() + rsz * (uint32_t)(x & ((1u << PB) - 1)));
+        uint32_t e = __atomic_load_n(&r->epoch, __ATOMIC_ACQUIRE);
+        while (e != epoch) {
+            if (e != BUSY && __atomic_compare_exchange_n(&r->epoch, &e, BUSY, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {
+                Rec fresh;
+                fresh.epoch = BUSY;
+                std::memcpy(static_cast<void*>(r), &fresh, sizeof(Rec));
+                for (uint32_t i = 0; i < nc; i++) new (r->c() + i) Cand();
+                __atomic_store_n(&r->epoch, epoch, __ATOMIC_RELEASE);
+                break;
+            }
+            while ((e = __atomic_load_n(&r->epoch, __ATOMIC_ACQUIRE)) == BUSY) std::this_thread::yield();
+        }
+        return *r;
     }
     // the record of position pos if this call touched it already, else null (no
     // writes: safe beside other readers)
     Rec* peek(uint64_t pos) {
         const uint64_t x = gsh >= 0 ? pos >> gsh : pos / g;
+        if (!pready[(size_t)(x >> PB)].load(std::memory_order_acquire)) return nullptr;
         const std::vector<uint8_t>& pg = (*pages)[(size_t)(x >> PB)];
-        if (pg.empty()) return nullptr;
         Rec* r = reinterpret_cast<Rec*>(const_cast<uint8_t*>(pg.data()) + rsz * (uint32_t)(x & ((1u << PB) - 1)));
         return r->epoch == epoch ? r : nullptr;
     }
@@ -312,9 +345,7 @@ struct PosTable {
     Rec& at(uint64_t pos) {
         const uint64_t x = gsh >= 0 ? pos >> gsh : pos / g;
         const uint32_t slot = (uint32_t)(x & ((1u << PB) - 1));
-        std::vector<uint8_t>& pg = (*pages)[(size_t)(x >> PB)];
-        if (pg.empty()) pg.resize(rsz << PB);   // (zeros: epoch 0)
-        Rec* r = reinterpret_cast<Rec*>(pg.data() + rsz * slot);
+        Rec* r = reinterpret_cast<Rec*>(page((size_t)(x >> PB)).data() + rsz * slot);
         if (r->epoch != epoch) {
             new (r) Rec();
             r->epoch = epoch;
@@ -764,7 +795,9 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
         hpos.clear();
         hsize.clear();
         static const bool rechain = getenv("AMBC_MS_RECHAIN") != nullptr;
-        for (Walk& w : G.active) {
+        // each walk's guess chain; many walks: on the pool, the records claimed by
+        // atomic bit sets, the positions into per-thread buckets merged afterwards
+        auto chain_of = [&](Walk& w, auto&& ask, auto&& rec_of) {
             uint64_t q = w.pos;
             int k = 0;
             // still on last round's chain: its requested prefix is skipped (with SPEC
@@ -774,11 +807,72 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
                 q = w.pos + (uint64_t)k * w.last;
             }
             for (; k <= SPEC && q < n; k++, q += w.last) {
-                if (k && T.at(q).decided) break;
-                request(q);
+                if (k && rec_of(q).decided) break;
+                ask(q);
             }
             w.cs = w.last;
             w.cq = q;
+        };
+        const size_t nw = G.active.size();
+        if (nw < 64 || pool.size() == 1) {
+            for (Walk& w : G.active) chain_of(w, request, [&](uint64_t q) -> PosTable::Rec& { return T.at(q); });
+        } else {
+            struct TL {
+                std::vector<std::pair<ReqKey, std::vector<uint64_t>>> b;
+                int in_idx[33];
+                std::vector<uint64_t> hp;
+                std::vector<uint32_t> hs;
+            };
+            std::vector<TL> tl(pool.size());
+            pool.run([&](unsigned t, unsigned Tn) {
+                TL& L = tl[t];
+                for (int& x : L.in_idx) x = -1;
+                Sizes scr;
+                auto push = [&](bool in, int ci, ReqKey key, uint64_t pos) {
+                    int bi = in ? L.in_idx[ci] : -1;
+                    if (bi < 0) {
+                        for (size_t b = 0; b < L.b.size() && bi < 0; b++)
+                            if (L.b[b].first == key) bi = (int)b;
+                        if (bi < 0) { L.b.emplace_back(key, std::vector<uint64_t>()); bi = (int)L.b.size() - 1; }
+                        if (in) L.in_idx[ci] = bi;
+                    }
+                    L.b[(size_t)bi].second.push_back(pos);
+                };
+                auto ask = [&](uint64_t pos) {
+                    const Sizes& z = sizes_in(pos, scr);
+                    const bool in = &z == &inner;
+                    PosTable::Rec& r = T.touch(pos);
+                    if (needs_m(z) && !r.mhave && !__atomic_exchange_n(&r.mreq, (uint8_t)1, __ATOMIC_ACQ_REL))
+                        push(in, 32, {z.M, 1}, pos);
+                    uint32_t want = 0, hwant = 0;
+                    for (uint32_t i = 0; i < nc; i++) {
+                        if (!((z.canon >> i) & 1)) continue;
+                        if (hc && !((r.hhave >> i) & 1)) hwant |= 1u << i;
+                        if (needs_o(z, i) && !((r.have >> i) & 1)) want |= 1u << i;
+                    }
+                    if (hwant) {
+                        const uint32_t got = hwant & ~__atomic_fetch_or(&r.hreq, hwant, __ATOMIC_ACQ_REL);
+                        for (uint32_t i = 0; i < nc; i++)
+                            if ((got >> i) & 1) { L.hp.push_back(pos); L.hs.push_back(z.S[i]); }
+                    }
+                    if (want) {
+                        const uint32_t got = want & ~__atomic_fetch_or(&r.req, want, __ATOMIC_ACQ_REL);
+                        for (uint32_t i = 0; i < nc; i++)
+                            if ((got >> i) & 1) push(in, (int)i, {z.S[i], 0}, pos);
+                    }
+                };
+                for (size_t a = nw * t / Tn; a < nw * (t + 1) / Tn; a++)
+                    chain_of(G.active[a], ask, [&](uint64_t q) -> PosTable::Rec& { return T.touch(q); });
+            });
+            for (TL& L : tl) {
+                for (auto& b : L.b) {
+                    std::vector<uint64_t>& dst = req_bucket(b.first);
+                    dst.insert(dst.end(), b.second.begin(), b.second.end());
+                }
+                hpos.insert(hpos.end(), L.hp.begin(), L.hp.end());
+                hsize.insert(hsize.end(), L.hs.begin(), L.hs.end());
+            }
+            for (int& x : req_in) x = -1;   // (bucket indices moved: the inner cache starts over)
         }
         // few walks left (the device idles behind one chunk's latency): each walk
         // also asks for every position its next step can reach, and a guess chain
