@@ -83,7 +83,6 @@ int ambc_init(const int* device_ids, int n_devices, ambc_ctx** out) {
         for (auto& ev : d.ev) HIPCHK(hipEventCreate(&ev));
         for (auto& x : d.xs) HIPCHK(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
         for (auto& ev : d.xev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        HIPCHK(hipStreamCreateWithFlags(&d.ss, hipStreamNonBlocking));   // per-segment statistics
         // the scan + compaction stream; AMBC_CS_PRIO=1: high priority (measured, §4)
         if (getenv("AMBC_CS_PRIO") && atoi(getenv("AMBC_CS_PRIO")) > 0) {
             int lo = 0, hi = 0;
@@ -93,7 +92,6 @@ int ambc_init(const int* device_ids, int n_devices, ambc_ctx** out) {
             HIPCHK(hipStreamCreateWithFlags(&d.cs, hipStreamNonBlocking));
         }
         for (auto& ev : d.pev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        for (auto& ev : d.sev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
         ctx->devs.push_back(d);
     }
     *out = ctx.release();
@@ -127,7 +125,6 @@ void ambc_destroy(ambc_ctx* ctx) {
         for (auto& ev : d.pev) (void)hipEventDestroy(ev);
         (void)hipStreamSynchronize(d.cs);
         (void)hipStreamDestroy(d.cs);
-        if (d.ss) { (void)hipStreamSynchronize(d.ss); (void)hipStreamDestroy(d.ss); }
         (void)hipStreamDestroy(d.stream);
     }
     delete ctx;
@@ -388,10 +385,6 @@ static int compress_on_body(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_
         HIPCHK(d.segbase.ensure((S + 1) * 8));
         HIPCHK(hipMemsetAsync(d.segbase.p, 0, 8, d.cs));
         HIPCHK(hipMemsetAsync(d.acc.p, 0, 260 * 8, s));
-#ifdef AMBC_EXP_STATS_PER_SEG
-        HIPCHK(hipEventRecord(d.sev[0], s));          // (acc cleared before any statistics)
-        HIPCHK(hipStreamWaitEvent(d.ss, d.sev[0], 0));
-#endif
         uint64_t* sb = d.segbase.as<uint64_t>();
         for (uint32_t i = 0; i < S; i++) {
             const uint32_t k0 = (uint32_t)((uint64_t)M * i / S), k1 = (uint32_t)((uint64_t)M * (i + 1) / S);
@@ -422,26 +415,15 @@ static int compress_on_body(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_
             // queued workgroups for every dispatch); the last one runs alone
             ca.resident = i + 1 < S ? compact_resident() : 0;
             HIPCHK(launch_compact(ca, d.cs));
-#ifdef AMBC_EXP_STATS_PER_SEG
-            HIPCHK(hipStreamWaitEvent(d.ss, d.pev[i], 0));
-            HIPCHK(launch_stats(d.ids.as<uint8_t>() + k0, d.plen.as<uint32_t>() + k0, k1 - k0, ca.n_total, C,
-                                d.acc.as<uint64_t>(), d.ss));
-#endif
         }
-#ifndef AMBC_EXP_STATS_PER_SEG
         // the statistics once, over every chunk, behind the last encode and beside the
         // last compaction.  Per-segment k_stats launches (round 3, on a stream of
         // their own) waited milliseconds for CU slots beside the next encode, and with
         // 4 hardware queues per process that stream shared one with d.cs: each held
         // the next segment's scan and compaction back (profiles/r4_stats_once_ab)
         HIPCHK(launch_stats(d.ids.as<uint8_t>(), d.plen.as<uint32_t>(), M, n, C, d.acc.as<uint64_t>(), s));
-#endif
         HIPCHK(hipEventRecord(d.ev[3], d.cs));
         HIPCHK(hipStreamWaitEvent(s, d.ev[3], 0));
-#ifdef AMBC_EXP_STATS_PER_SEG
-        HIPCHK(hipEventRecord(d.sev[1], d.ss));
-        HIPCHK(hipStreamWaitEvent(s, d.sev[1], 0));
-#endif
         uint64_t body_len = 0;
         HIPCHK(hipMemcpyAsync(&body_len, sb + S, 8, hipMemcpyDeviceToHost, s));
         std::vector<uint64_t> acc(260);

@@ -157,8 +157,6 @@ struct Dev {
     uint64_t t_encode = 0, t_scan = 0, t_compact = 0;
     uint32_t n_launch = 1;      // k_encode launches of the last compress call (pipelined segments)
     hipStream_t cs = nullptr;   // scan + compaction of pipelined segments
-    hipStream_t ss = nullptr;   // their statistics
-    hipEvent_t sev[2] = {};     //   (acc cleared, statistics done)
     hipEvent_t pev[8] = {};     // segment i encoded
     Buf segbase;                // body offset of every segment (device)
     // pinned staging for large pageable copies: 2 buffers + 2 events per copy
