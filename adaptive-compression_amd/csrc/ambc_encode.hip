@@ -1043,6 +1043,15 @@ __global__ void k_seg_base(uint64_t* base, const uint64_t* off_last, const uint6
     if (threadIdx.x == 0) base[1] = base[0] + off_last[0] + size_last[0];
 }
 
+// the end chunk at the body offset the device holds (a pipelined call's last
+// segment end), and that offset into acc_slot: one copy back for both
+__global__ void k_end_chunk_at(uint8_t* out, const uint64_t* off, uint64_t* acc_slot) {
+    const uint32_t t = threadIdx.x;
+    const uint64_t o = *off;
+    if (out && t < END_CHUNK) out[o + t] = t < 2 ? 0xFF : 0;
+    if (t == 0) acc_slot[0] = o;
+}
+
 __global__ void k_end_chunk(uint8_t* dst) {
     const uint32_t t = threadIdx.x;
     if (t < END_CHUNK) dst[t] = t < 2 ? 0xFF : 0;
@@ -1237,6 +1246,11 @@ hipError_t launch_compact(const CompactArgs& a, hipStream_t s) {
     const uint32_t blocks = a.resident ? std::min<uint32_t>((a.n_chunks + 3) / 4, a.resident)
                                        : (a.n_chunks + 3) / 4;
     hipLaunchKernelGGL(k_compact, dim3(blocks), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_end_chunk_at(uint8_t* out, const uint64_t* off, uint64_t* acc_slot, hipStream_t s) {
+    hipLaunchKernelGGL(k_end_chunk_at, dim3(1), dim3(64), 0, s, out, off, acc_slot);
     return hipGetLastError();
 }
 

@@ -110,6 +110,7 @@ void ambc_destroy(ambc_ctx* ctx) {
                        &d.scratch, &d.seg, &d.list, &d.bestpre, &d.gdseq, &d.pending, &d.z9rec, &d.z9scr, &d.segbase, &d.coll,
                        &d.inffix, &d.ms_out, &d.ms_ent})
             b->release();
+        if (d.hacc) { (void)hipHostFree(d.hacc); d.hacc = nullptr; }
         for (auto& b : d.msb) b.release();
         d.dw.release();
         for (auto& x : d.mss) if (x) { (void)hipStreamSynchronize(x); (void)hipStreamDestroy(x); }
@@ -178,7 +179,7 @@ struct Remainder {
 // after the R packages are in the body and acc[] is on the host
 static int finish_compress(Dev& d, const ambc_params* p, uint32_t R, const Remainder& rm, uint8_t* d_out,
                            uint64_t body_len, const std::vector<uint64_t>& acc, const uint8_t* d_in,
-                           bool end, uint64_t* out_len, ambc_stats* st, uint64_t t0) {
+                           bool end, uint64_t* out_len, ambc_stats* st, uint64_t t0, bool end_written = false) {
     hipStream_t s = d.stream;
     if (rm.hdr) {
         const uint64_t rem = rm.rem_total;
@@ -196,7 +197,7 @@ static int finish_compress(Dev& d, const ambc_params* p, uint32_t R, const Remai
         body_len += rm.copy_len;
     }
     if (end) {
-        HIPCHK(launch_end_chunk(d_out + body_len, s));
+        if (!end_written) HIPCHK(launch_end_chunk(d_out + body_len, s));
         body_len += END_CHUNK;
     }
     HIPCHK(hipEventRecord(d.ev[4], s));
@@ -270,7 +271,7 @@ static int compress_on_body(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_
     HIPCHK(d.ids.ensure((size_t)M + 16));
     HIPCHK(d.sizes.ensure((size_t)(M + 1) * 8));
     HIPCHK(d.off.ensure((size_t)(M + 1) * 8));
-    HIPCHK(d.acc.ensure(260 * 8));
+    HIPCHK(d.acc.ensure(264 * 8));
     // exact entropy tables (optional)
     const double* ef = nullptr;
     const double* et = nullptr;
@@ -426,14 +427,17 @@ static int compress_on_body(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_
         // 4 hardware queues per process that stream shared one with d.cs: each held
         // the next segment's scan and compaction back (profiles/r4_stats_once_ab)
         HIPCHK(launch_stats(d.ids.as<uint8_t>(), d.plen.as<uint32_t>(), M, n, C, d.acc.as<uint64_t>(), s));
+        // the end chunk and the body length behind the last compaction, then one
+        // pinned copy back and one synchronisation (were two pageable copies, a
+        // synchronisation, the end chunk's launch and another)
+        HIPCHK(launch_end_chunk_at(end ? d_out : nullptr, sb + S, d.acc.as<uint64_t>() + 260, d.cs));
         HIPCHK(hipEventRecord(d.ev[3], d.cs));
         HIPCHK(hipStreamWaitEvent(s, d.ev[3], 0));
-        uint64_t body_len = 0;
-        HIPCHK(hipMemcpyAsync(&body_len, sb + S, 8, hipMemcpyDeviceToHost, s));
-        std::vector<uint64_t> acc(260);
-        HIPCHK(hipMemcpyAsync(acc.data(), d.acc.p, 260 * 8, hipMemcpyDeviceToHost, s));
+        if (!d.hacc) HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&d.hacc), 264 * 8, hipHostMallocDefault));
+        HIPCHK(hipMemcpyAsync(d.hacc, d.acc.p, 261 * 8, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
-        return finish_compress(d, p, M, Remainder(), d_out, body_len, acc, d_in, end, out_len, st, t0);
+        std::vector<uint64_t> acc(d.hacc, d.hacc + 260);
+        return finish_compress(d, p, M, Remainder(), d_out, d.hacc[260], acc, d_in, end, out_len, st, t0, true);
     }
     rc = encode_range(ea);
     if (rc) return rc;

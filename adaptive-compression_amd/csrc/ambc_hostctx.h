@@ -147,6 +147,7 @@ struct Dev {
     uint64_t ms_walk_ns = 0, ms_emit_ns = 0;  // and the time of the walk / of the final encode
     Buf ms_out;                 // the multi-size walk's body (its own buffer: no other call writes it)
     Buf ms_ent;                 // the multi-size walk's entropy tables (one upload per call)
+    uint64_t* hacc = nullptr;   // pinned: a pipelined call's statistics and body length, copied back once
     uint64_t ms_body = 0;       // a multi-size body kept in `ms_out` for ambc_fetch_body (0: none)
     // the multi-size walk's position records, kept across calls (a fresh 40 KB page
     // per 256 positions cost ~25 ms of page faults and construction per 256 MiB

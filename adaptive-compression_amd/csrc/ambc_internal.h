@@ -196,6 +196,8 @@ hipError_t launch_zlib9_big(const EncArgs& a, hipStream_t s);
 hipError_t launch_zlib9(const EncArgs& a, hipStream_t s);
 hipError_t launch_compact(const CompactArgs& a, hipStream_t s);
 hipError_t launch_end_chunk(uint8_t* dst, hipStream_t s);
+// out == null: only *off into acc_slot[0]
+hipError_t launch_end_chunk_at(uint8_t* out, const uint64_t* off, uint64_t* acc_slot, hipStream_t s);
 // base[1] = base[0] + off_last[0] + size_last[0] (a pipelined segment's end offset)
 hipError_t launch_seg_base(uint64_t* base, const uint64_t* off_last, const uint64_t* size_last, hipStream_t s);
 hipError_t launch_stats(const uint8_t* ids, const uint32_t* plen, uint32_t n_chunks,
