@@ -76,13 +76,15 @@ struct Batch {
     uint8_t* hids = nullptr;
     uint32_t* hlz = nullptr;
     uint64_t* hpos = nullptr;   // pinned chunk positions (the upload's source)
+    uint64_t* hoff = nullptr;   // pinned body offsets (a final encode's compaction)
     size_t hcap = 0;
     void host_free() {
         if (hplen) (void)hipHostFree(hplen);
         if (hids) (void)hipHostFree(hids);
         if (hlz) (void)hipHostFree(hlz);
         if (hpos) (void)hipHostFree(hpos);
-        hplen = nullptr; hids = nullptr; hlz = nullptr; hpos = nullptr; hcap = 0;
+        if (hoff) (void)hipHostFree(hoff);
+        hplen = nullptr; hids = nullptr; hlz = nullptr; hpos = nullptr; hoff = nullptr; hcap = 0;
     }
     hipError_t host_ensure(size_t n) {
         if (n <= hcap) return hipSuccess;
@@ -92,6 +94,7 @@ struct Batch {
         if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&hids), n);
         if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&hlz), n * 4 * LZ4_SUB_MAX);
         if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&hpos), n * 8);
+        if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&hoff), n * 8);
         if (e == hipSuccess) hcap = n;
         return e;
     }

@@ -954,6 +954,121 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
         kernel_ns += now_ns() - tk;
         return AMBC_OK;
     };
+    // ---- the reference's walk from 0, read off the decisions as they come, and its
+    // packages encoded once more (bytes) beside the walk's later rounds ----
+    struct Pkg { uint64_t pos; uint32_t s, plen; uint8_t id, host; uint64_t off; };
+    std::vector<Pkg> path;
+    uint64_t body = 0, path_pos = 0;
+    bool path_end = false;
+    // the body buffer at its largest: every package is smaller than its chunk but
+    // the raw remainder, each adds a header
+    const uint64_t body_cap = n + (uint64_t)HDR * (n / *std::min_element(cands.begin(), cands.end()) + 2) + END_CHUNK;
+    HIPCHK(d.ms_out.ensure(body_cap + 64));
+    uint8_t* d_body = d.ms_out.as<uint8_t>();
+    auto extend_path = [&]() -> int {
+        while (!path_end) {
+            if (path_pos >= n) { path_end = true; break; }
+            PosTable::Rec* r = T.peek(path_pos);
+            if (!r || !r->decided) break;
+            const Decision dd = r->dec;
+            if (dd.id == 255 && n - path_pos > 0xFFFFFFFFull)
+                return fail(AMBC_E_RANGE, "raw remainder exceeds a u32 chunk field");
+            path.push_back(Pkg{path_pos, dd.s, dd.plen, dd.id, dd.host, body});
+            body += HDR + (uint64_t)dd.plen;
+            if (dd.id == 255) { path_end = true; break; }
+            path_pos += dd.s;
+        }
+        return AMBC_OK;
+    };
+    // The final encode, after the walk: grouped by (size, winning id), each group
+    // encoded with its winner alone -- the method encoders are deterministic, so the
+    // winner's bytes are those of the full loop, and the losers' encoders (a 64 KiB
+    // DEFLATE parse behind an RLE winner) do not run again; every package's plen / id
+    // is checked against the walk's decision when its slot is done.  The groups go
+    // onto all 15 batch slots as they free up (polled), not 8 at a time.  (Encoding
+    // the path's packages beside the walk's later rounds was measured slower: the
+    // walk's latency-bound rounds lose more than the final encode saves.)
+    constexpr int FSN = 15;
+    auto fslot = [](int k) { return k < 7 ? 9 + k : k - 7; };   // slots 9..15, then 0..7
+    struct FinalJob { std::vector<size_t> idx; bool busy = false; };
+    FinalJob fj[FSN];
+    static const bool allm = getenv("AMBC_MS_FINAL_ALL") != nullptr;
+    // verify slot k's group: blocking, or only if its stream is done (false: busy)
+    auto final_finish = [&](int k, bool wait) -> int {
+        if (!fj[k].busy) return AMBC_OK;
+        if (wait) {
+            HIPCHK(hipStreamSynchronize(d.mss[fslot(k)]));
+        } else {
+            const hipError_t q = hipStreamQuery(d.mss[fslot(k)]);
+            if (q == hipErrorNotReady) return AMBC_OK;
+            HIPCHK(q);
+        }
+        const Batch& bb = d.msb[fslot(k)];
+        for (size_t q = 0; q < fj[k].idx.size(); q++) {
+            const Pkg& pk = path[fj[k].idx[q]];
+            if (bb.hplen[q] != pk.plen || bb.hids[q] != pk.id)
+                return fail(AMBC_E_DEVICE, "multi-size walk: re-encode differs");
+        }
+        fj[k].busy = false;
+        return AMBC_OK;
+    };
+    using FGroup = std::pair<std::pair<uint32_t, uint8_t>, std::vector<size_t>>;
+    std::vector<FGroup> fpend;                       // groups waiting for a free slot
+    auto final_group = [&](size_t i0, size_t i1) {
+        std::map<std::pair<uint32_t, uint8_t>, std::vector<size_t>> groups;
+        for (size_t i = i0; i < i1; i++)
+            if (path[i].id != 255 && !path[i].host) groups[{path[i].s, allm ? (uint8_t)0 : path[i].id}].push_back(i);
+        for (auto& gr : groups) fpend.emplace_back(gr.first, std::move(gr.second));
+    };
+    auto final_launch = [&](int k, FGroup& gr) -> int {
+        const uint32_t sz = gr.first.first;
+        ambc_params pw = *p;
+        if (gr.first.second) pw.method_mask = 1u << gr.first.second;
+        Batch& bb = d.msb[fslot(k)];
+        hipStream_t xs = d.mss[fslot(k)];
+        const uint32_t cnt = (uint32_t)gr.second.size();
+        HIPCHK(bb.host_ensure(cnt));
+        for (uint32_t q = 0; q < cnt; q++) {
+            bb.hpos[q] = path[gr.second[q]].pos;
+            bb.hoff[q] = path[gr.second[q]].off;
+        }
+        if (int rc = launch_batch(bb, xs, d_in, n, &pw, sz, bb.hpos, cnt, ent_of(sz), false)) return rc;
+        HIPCHK(bb.off.ensure((size_t)cnt * 8));
+        HIPCHK(hipMemcpyAsync(bb.off.p, bb.hoff, (size_t)cnt * 8, hipMemcpyHostToDevice, xs));
+        CompactArgs ca{};
+        ca.slots = bb.slots.as<uint8_t>();
+        ca.slot_stride = slot_stride_for((sz + 15) & ~15u);
+        ca.plen = bb.plen.as<uint32_t>();
+        ca.ids = bb.ids.as<uint8_t>();
+        ca.off = bb.off.as<uint64_t>();
+        ca.n_chunks = cnt;
+        ca.clen = bb.clen.as<uint32_t>();
+        ca.n_total = n;
+        ca.chunk_size = (sz + 15) & ~15u;
+        ca.out = d_body;
+        HIPCHK(launch_compact(ca, xs));
+        fj[k].idx = std::move(gr.second);
+        fj[k].busy = true;
+        return AMBC_OK;
+    };
+    // the groups onto slots as they free up, then every slot done and checked
+    auto final_run = [&]() -> int {
+        size_t gi = 0;
+        while (gi < fpend.size()) {
+            bool launched = false;
+            for (int k = 0; k < FSN && gi < fpend.size(); k++) {
+                if (int rc = final_finish(k, false)) return rc;
+                if (fj[k].busy) continue;
+                if (int rc = final_launch(k, fpend[gi++])) return rc;
+                launched = true;
+            }
+            if (!launched) std::this_thread::yield();
+        }
+        fpend.clear();
+        for (int k = 0; k < FSN; k++)
+            if (int rc = final_finish(k, true)) return rc;
+        return AMBC_OK;
+    };
     for (int g = 0; g < GROUPS; g++)
         if (int rc = advance(grp[g])) return rc;
     for (;;) {
@@ -972,81 +1087,16 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
     const uint64_t t_walk = now_ns() - t0;
     TRACE("multisize walk ms: decide %.2f requests %.2f launch %.2f wait %.2f fill %.2f host %.2f (total %.2f)",
           t_dec / 1e6, t_req / 1e6, t_launch / 1e6, t_wait / 1e6, t_fill / 1e6, t_host / 1e6, t_walk / 1e6);
-    // ---- the reference's walk from 0, read off the decisions ----
-    struct Pkg { uint64_t pos; uint32_t s, plen; uint8_t id, host; uint64_t off; };
-    std::vector<Pkg> path;
-    uint64_t body = 0;
-    for (uint64_t pos = 0; pos < n;) {
-        const PosTable::Rec& r = T.at(pos);
-        if (!r.decided) return fail(AMBC_E_DEVICE, "multi-size walk: undecided position on the path");
-        const Decision& dd = r.dec;
-        if (dd.id == 255 && n - pos > 0xFFFFFFFFull)
-            return fail(AMBC_E_RANGE, "raw remainder exceeds a u32 chunk field");
-        path.push_back(Pkg{pos, dd.s, dd.plen, dd.id, dd.host, body});
-        body += HDR + (uint64_t)dd.plen;
-        if (dd.id == 255) break;
-        pos += dd.s;
-    }
+    if (int rc = extend_path()) return rc;
+    if (!path_end) return fail(AMBC_E_DEVICE, "multi-size walk: undecided position on the path");
     body += END_CHUNK;
     d.ms_body = 0;
     if (out && out_cap < body) return fail(AMBC_E_CAPACITY, "output capacity below the body size");
-
-    // ---- the chosen chunks, encoded again per size (all methods, bytes), into the body ----
-    HIPCHK(d.ms_out.ensure(body + 64));
-    uint8_t* d_body = d.ms_out.as<uint8_t>();
     const uint64_t te = now_ns();
-    // grouped by (size, winning id), each group encoded with its winner alone: the
-    // method encoders are deterministic, so the winner's bytes are those of the full
-    // loop, and the losers' encoders (a 64 KiB DEFLATE parse behind an RLE winner)
-    // do not run again.  The plen / id check below still holds every package to the
-    // walk's decision.
-    static const bool allm = getenv("AMBC_MS_FINAL_ALL") != nullptr;
-    std::map<std::pair<uint32_t, uint8_t>, std::vector<size_t>> groups;
-    for (size_t i = 0; i < path.size(); i++)
-        if (path[i].id != 255 && !path[i].host) groups[{path[i].s, allm ? (uint8_t)0 : path[i].id}].push_back(i);
-    std::vector<std::pair<std::pair<uint32_t, uint8_t>, std::vector<size_t>>> gl(groups.begin(), groups.end());
-    for (size_t j0 = 0; j0 < gl.size(); j0 += 8) {
-        const size_t j1 = std::min(gl.size(), j0 + 8);
-        std::vector<std::vector<uint64_t>> offs(j1 - j0);
-        for (size_t j = j0; j < j1; j++) {
-            const uint32_t sz = gl[j].first.first;
-            ambc_params pw = *p;
-            if (gl[j].first.second) pw.method_mask = 1u << gl[j].first.second;
-            Batch& bb = d.msb[j - j0];
-            hipStream_t xs = d.mss[j - j0];
-            const uint32_t cnt = (uint32_t)gl[j].second.size();
-            HIPCHK(bb.host_ensure(cnt));
-            for (uint32_t q = 0; q < cnt; q++) {
-                bb.hpos[q] = path[gl[j].second[q]].pos;
-                offs[j - j0].push_back(path[gl[j].second[q]].off);
-            }
-            int rc = launch_batch(bb, xs, d_in, n, &pw, sz, bb.hpos, cnt, ent_of(sz), false);
-            if (rc) return rc;
-            HIPCHK(bb.off.ensure((size_t)cnt * 8));
-            HIPCHK(hipMemcpyAsync(bb.off.p, offs[j - j0].data(), (size_t)cnt * 8, hipMemcpyHostToDevice, xs));
-            CompactArgs ca{};
-            ca.slots = bb.slots.as<uint8_t>();
-            ca.slot_stride = slot_stride_for((sz + 15) & ~15u);
-            ca.plen = bb.plen.as<uint32_t>();
-            ca.ids = bb.ids.as<uint8_t>();
-            ca.off = bb.off.as<uint64_t>();
-            ca.n_chunks = cnt;
-            ca.clen = bb.clen.as<uint32_t>();
-            ca.n_total = n;
-            ca.chunk_size = (sz + 15) & ~15u;
-            ca.out = d_body;
-            HIPCHK(launch_compact(ca, xs));
-        }
-        for (size_t j = j0; j < j1; j++) {
-            HIPCHK(hipStreamSynchronize(d.mss[j - j0]));
-            const Batch& bb = d.msb[j - j0];
-            for (size_t q = 0; q < gl[j].second.size(); q++) {
-                const Pkg& pk = path[gl[j].second[q]];
-                if (bb.hplen[q] != pk.plen || bb.hids[q] != pk.id)
-                    return fail(AMBC_E_DEVICE, "multi-size walk: re-encode differs");
-            }
-        }
-    }
+    // (largest chunks first: their encodes are the longest)
+    final_group(0, path.size());
+    std::stable_sort(fpend.begin(), fpend.end(), [](const FGroup& x, const FGroup& y) { return x.first.first > y.first.first; });
+    if (int rc = final_run()) return rc;
     {   // host-scored packages: header + the caller's payload bytes
         std::vector<uint8_t> hb;
         for (const Pkg& pk : path) {
