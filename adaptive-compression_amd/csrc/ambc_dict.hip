@@ -535,7 +535,7 @@ __global__ __launch_bounds__(64 * DictCfg<CMAX>::NW) void k_dict(EncArgs A) {
     uint8_t* slot = A.slots + (uint64_t)k * A.slot_stride;
     uint16_t* s16 = reinterpret_cast<uint16_t*>(slot);
     const uint32_t o = S.olen;
-    {
+    if (!(A.flags & ENC_EVAL)) {   // (the multi-size walk's decision-only batches: no bytes)
         uint32_t e = S.path.be[wave], ob = S.path.bo[wave];
 #pragma unroll 1
         for (uint32_t i = 0; i < wpb; i++) {
