@@ -937,8 +937,14 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
         for (size_t j0 = 0; j0 < jobs.size(); j0 += 8) {
             const size_t j1 = std::min(jobs.size(), j0 + 8);
             const uint64_t tl = now_ns();
-            for (size_t j = j0; j < j1; j++)
+            // the largest size first (its own high-priority stream), then the rest
+            // smallest first: streams share hardware queues, and a 1 KiB batch
+            // queued behind an 8 KiB Dictionary chain ended the round
+            static const bool desc = getenv("AMBC_MS_LAUNCH_DESC") != nullptr;
+            for (size_t x = 0; x < j1 - j0; x++) {
+                const size_t j = desc || x == 0 ? j0 + x : j1 - x;
                 if (int rc = launch_job(jobs[j], G.slot0 + (int)(j - j0))) return rc;
+            }
             t_launch += now_ns() - tl;
             if (j0 == 0)                           // the host codecs while the device works
                 if (int rc = host_round()) return rc;
