@@ -109,6 +109,14 @@ __device__ __forceinline__ void put_bits_atomic(uint32_t* words, uint32_t b, uin
     if (o + nb > 32) atomicOr(&words[w + 1], v >> (32 - o));
 }
 
+// put_bits_atomic into a ring of rm + 1 words (a power of two)
+__device__ __forceinline__ void put_bits_ring(uint32_t* ring, uint32_t b, uint32_t v, uint32_t nb, uint32_t rm) {
+    if (!nb) return;
+    const uint32_t w = b >> 5, o = b & 31;
+    atomicOr(&ring[w & rm], v << o);
+    if (o + nb > 32) atomicOr(&ring[(w + 1) & rm], v >> (32 - o));
+}
+
 __device__ __forceinline__ void put_bits_plain(uint32_t* words, uint32_t b, uint32_t v, uint32_t nb) {
     if (!nb) return;
     const uint32_t w = b >> 5, o = b & 31;
@@ -815,9 +823,14 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
         gd_codes<30>(S.dl, S.dc, S.blc, lane);
         gd_codes<19>(S.cl, S.cc, S.blc, lane);
     }
-    // GB: the header words are built in the LDS region from bit 16 (behind 78 DA)
+    // GB: the stream goes through a 4 KB ring in the LDS region (the header from
+    // bit 16, behind 78 DA), its finished words stored to the slot after every
+    // 64-position round: LDS atomics instead of global ones (same-address ORs
+    // serialised in L2: a 64 KiB chunk's emission cost more than its parse)
+    constexpr uint32_t RW = 1024, RM = RW - 1;
+    static_assert(!GB || GdSmem<CMAX, NOCHUNK>::REGION >= 4 * (int)RW, "the ring fits the region");
     uint32_t* bits = GB ? S.region : BIG ? reinterpret_cast<uint32_t*>(S.chunk) : S.region;
-    const uint32_t nwords = GB ? 160u : (body + 8) / 4 + 1;
+    const uint32_t nwords = GB ? RW : (body + 8) / 4 + 1;
     for (uint32_t i = lane; i < nwords; i += 64) bits[i] = 0;
     wave_sync();
     const uint32_t b0 = GB ? 16u : 0u;
@@ -841,17 +854,23 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     }
     bp = readlane(bp, 0);
     wave_sync();
-    if constexpr (GB) {
-        // the header words to the slot, the rest of the package's words zeroed; the
-        // symbols then OR themselves in (the stores complete first)
-        uint32_t* gw = reinterpret_cast<uint32_t*>(slot);
-        const uint32_t hw = (bp + 31) / 32, gn = (2 + body + 4 + 3) / 4 + 1;
-        for (uint32_t i = lane; i < gn; i += 64) gw[i] = i < hw ? bits[i] : 0u;
-        __threadfence();
+    uint32_t* const gw = reinterpret_cast<uint32_t*>(slot);
+    uint32_t flushed = 0;   // GB: words [0, flushed) are in the slot
+    auto flush = [&](uint32_t upto) {
         wave_sync();
-        bits = gw;
-    }
-    if (n - mcov <= 8 * (ns + 1)) {
+        for (uint32_t w = flushed + lane; w < upto; w += 64) {
+            gw[w] = S.region[w & RM];
+            S.region[w & RM] = 0;
+        }
+        wave_sync();
+        flushed = upto;
+    };
+    auto put = [&](uint32_t b, uint32_t v, uint32_t nb) {
+        if constexpr (GB) put_bits_ring(S.region, b, v, nb, RM);
+        else put_bits_atomic(bits, b, v, nb);
+    };
+    // (GB: position-major only, so that a round's bits are bounded by the ring)
+    if (!GB && n - mcov <= 8 * (ns + 1)) {
         // match-major: lane e emits the literal run before match e and the
         // match (element ns: the literals after the last match); 64 matches per
         // step instead of 64 positions
@@ -925,25 +944,28 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
             const uint32_t incl = wave_incl_sum(cost);
             uint32_t b = bp + incl - cost;
             if (lit) {
-                put_bits_atomic(bits, b, S.lc[c], S.ll[c]);
+                put(b, S.lc[c], S.ll[c]);
             } else if (st) {
                 const uint32_t l1 = S.ll[257 + lcd], l2 = S.dl[dcd];
-                put_bits_atomic(bits, b, S.lc[257 + lcd] | (Lx - c_lbase[lcd]) << l1, l1 + c_lext[lcd]);
+                put(b, S.lc[257 + lcd] | (Lx - c_lbase[lcd]) << l1, l1 + c_lext[lcd]);
                 b += l1 + c_lext[lcd];
-                put_bits_atomic(bits, b, S.dc[dcd] | (Dx - c_dbase[dcd]) << l2, l2 + c_dext[dcd]);
+                put(b, S.dc[dcd] | (Dx - c_dbase[dcd]) << l2, l2 + c_dext[dcd]);
             }
             bp += readlane(incl, 63);
             sb += (uint32_t)__popcll(sm);
+            if constexpr (GB) flush(bp >> 5);
         }
     }
     wave_sync();
     if constexpr (GB) {
-        // end of block and Adler-32 (big-endian bytes after the body) by OR as well
-        if (lane == 0) put_bits_atomic(bits, bp, S.lc[256], S.ll[256]);
+        // end of block and Adler-32 (big-endian bytes after the body) into the ring,
+        // then its last words to the slot
+        if (lane == 0) put_bits_ring(S.region, bp, S.lc[256], S.ll[256], RM);
         if (lane < 4) {
             const uint32_t q = 2 + body + lane;
-            atomicOr(&bits[q >> 2], ((adler >> (8 * (3 - lane))) & 0xFFu) << (8 * (q & 3)));
+            atomicOr(&S.region[(q >> 2) & RM], ((adler >> (8 * (3 - lane))) & 0xFFu) << (8 * (q & 3)));
         }
+        flush((total + 3) / 4);
     } else {
     if (lane == 0) put_bits_plain(bits, bp, S.lc[256], S.ll[256]);
     wave_sync();
