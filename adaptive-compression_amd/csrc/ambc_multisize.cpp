@@ -692,8 +692,12 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
     // 256 MiB {1,3,4,9}: 4 / 5 / 6 / 8 ahead 72.4 / 64.1 / 58.4 / 94.9 ms (8 with
     // 2048 walks), {1,2,3,4,5}: 1 / 2 ahead 86.0 / 90.6 ms, like_reference() on 64
     // MiB: 0 / 1 / 2 ahead 0.229 / 0.255 / 0.224 GB/s; profiles/r3_multisize_sweep.log)
+    // (round 4, with breadth speculation for the last walks: {1,2,3,4,5} 0 / 1 / 2
+    // ahead 4.61-4.77 / 4.48-4.53 / 3.93-3.97 GB/s; like_reference() -- no breadth --
+    // 0.31 / 0.34 / 0.28, profiles/r4_spec_ab)
     static const int SPEC_ENV = getenv("AMBC_MS_SPEC") ? atoi(getenv("AMBC_MS_SPEC")) : -1;
-    const int SPEC = SPEC_ENV >= 0 ? SPEC_ENV : (lzshare ? 6 : 1);
+    const bool z9walk = (p->flags & AMBC_FLAG_ZLIB9) && ((p->method_mask >> AMBC_M_DEFLATE) & 1);
+    const int SPEC = SPEC_ENV >= 0 ? SPEC_ENV : (lzshare ? 6 : z9walk ? 1 : 0);
     static const int GROUPS = getenv("AMBC_MS_GROUPS") ? std::max(1, std::min(2, atoi(getenv("AMBC_MS_GROUPS")))) : 1;
     uint64_t t_dec = 0, t_req = 0, t_launch = 0, t_wait = 0, t_fill = 0;   // (AMBC_TRACE breakdown)
     using Job = std::pair<std::pair<uint32_t, int>, std::vector<uint64_t>>;
@@ -884,7 +888,7 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
         // profiles/r4_breadth_ab)
         static const int64_t BREADTH_ENV = getenv("AMBC_MS_BREADTH") ? atoll(getenv("AMBC_MS_BREADTH")) : -1;
         const uint64_t BREADTH = BREADTH_ENV >= 0 ? (uint64_t)BREADTH_ENV
-                                                  : ((p->flags & AMBC_FLAG_ZLIB9) && ((p->method_mask >> AMBC_M_DEFLATE) & 1) ? 0 : 2048);
+                                                  : (z9walk ? 0 : 2048);
         if (BREADTH && !G.active.empty() && G.active.size() * nc <= BREADTH) {
             const uint64_t per = BREADTH / G.active.size();
             for (const Walk& w : G.active) {
