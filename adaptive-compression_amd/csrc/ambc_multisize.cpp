@@ -420,9 +420,20 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
     };
     // the input, uploaded once (64 bytes of slack for the encoders' padded loads)
     HIPCHK(d.in.ensure(n + 64));
+    // (a large upload runs on a thread of its own while the first round is planned;
+    // the first launch waits for it)
+    std::thread upload;
+    int upload_rc = AMBC_OK;
+    struct Joiner {
+        std::thread& t;
+        ~Joiner() { if (t.joinable()) t.join(); }
+    } upload_join{upload};
+    auto await_upload = [&]() -> int {
+        if (upload.joinable()) upload.join();
+        return upload_rc;
+    };
     if (n >= kStageMin) {
-        int rc = copy_staged(d, d.in.p, in, n, true);
-        if (rc) return rc;
+        upload = std::thread([&] { upload_rc = copy_staged(d, d.in.p, in, n, true, 0, 8); });
     } else if (n) {
         HIPCHK(hipMemcpyAsync(d.in.p, in, n, hipMemcpyHostToDevice, s));
     }
@@ -938,6 +949,8 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
         // 64 KiB class runs at 20 workgroups per CU in place: the small ones fill
         // in); more than 8: the earlier ones are finished here, the last 8 fly
         const uint64_t tk = now_ns();
+        if (!jobs.empty())
+            if (int rc = await_upload()) return rc;
         for (size_t j0 = 0; j0 < jobs.size(); j0 += 8) {
             const size_t j1 = std::min(jobs.size(), j0 + 8);
             const uint64_t tl = now_ns();
@@ -1097,6 +1110,7 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
     const uint64_t t_walk = now_ns() - t0;
     TRACE("multisize walk ms: decide %.2f requests %.2f launch %.2f wait %.2f fill %.2f host %.2f (total %.2f)",
           t_dec / 1e6, t_req / 1e6, t_launch / 1e6, t_wait / 1e6, t_fill / 1e6, t_host / 1e6, t_walk / 1e6);
+    if (int rc = await_upload()) return rc;
     if (int rc = extend_path()) return rc;
     if (!path_end) return fail(AMBC_E_DEVICE, "multi-size walk: undecided position on the path");
     body += END_CHUNK;
