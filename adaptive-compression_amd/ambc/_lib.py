@@ -47,6 +47,7 @@ EXPORTS = (
     "ambc_compress_shard", "ambc_decompress_shard", "ambc_decompress_multi",
     "ambc_synth_device_range", "ambc_device_equal", "ambc_compress_multisize",
     "ambc_last_multisize_info", "ambc_fetch_body", "ambc_compress_multisize_ex", "ambc_debug_walk",
+    "ambc_test_inject_failure",
 )
 
 
@@ -148,6 +149,7 @@ def _declare(lib):
                                         C.POINTER(C.c_void_p), u32, vp, u8p, u64, C.POINTER(u64),
                                         C.POINTER(Stats)], i32),
         "ambc_debug_walk": ([u8p, u64, u64, u32, C.POINTER(u64), C.POINTER(u64), C.POINTER(u64)], i32),
+        "ambc_test_inject_failure": ([i32], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -225,7 +227,9 @@ class Context:
         self.h = h
         self.devices = devs
         # one call at a time per context: its device workspaces (and a body that
-        # ambc_compress_multisize(out=NULL) leaves for ambc_fetch_body) are shared
+        # ambc_compress_multisize(out=NULL) leaves for ambc_fetch_body) are shared.
+        # Every libambc call on the context's workspaces takes it (compressor.py,
+        # methods.py, distributed.py)
         self.lock = threading.RLock()
 
     def close(self):
@@ -292,6 +296,7 @@ class DeviceBuffer:
 
 
 _ctx = None
+_plugin_ctx = None
 
 
 def default_context(devices=None):
@@ -300,3 +305,15 @@ def default_context(devices=None):
         if _ctx is None or (devices and list(devices) != _ctx.devices):
             _ctx = Context(devices)
         return _ctx
+
+
+def plugin_context():
+    """The per-chunk plugins' own context (methods.py): a plugin called from a
+    host-codec callback while a walk holds the default context's lock (the
+    reference-side binding scores the instance's own method objects on host
+    threads) must not wait for that lock."""
+    global _plugin_ctx
+    with _lock:
+        if _plugin_ctx is None:
+            _plugin_ctx = Context()
+        return _plugin_ctx

@@ -322,8 +322,9 @@ class AdaptiveCompressor:
         out = bytearray(cap)
         olen = C.c_uint64()
         st = _lib.Stats()
-        rc = ctx.lib.ambc_compress_batch(ctx.h, _lib.addr(file_data), n, C.byref(p),
-                                         _lib.addr(out), cap, C.byref(olen), C.byref(st))
+        with ctx.lock:
+            rc = ctx.lib.ambc_compress_batch(ctx.h, _lib.addr(file_data), n, C.byref(p),
+                                             _lib.addr(out), cap, C.byref(olen), C.byref(st))
         if rc == _lib.AMBC_E_RANGE:
             import struct
             raise struct.error("argument out of range")
@@ -371,8 +372,9 @@ class AdaptiveCompressor:
             nh = C.c_uint32()
             st = _lib.Stats()
             optr = C.cast(C.c_char_p(out), C.POINTER(C.c_uint8)) if direct else _lib.addr(out)
-            rc = ctx.lib.ambc_decompress_ex(ctx.h, _lib.addr(data), len(data), orig_size, reg,
-                                            optr, hc, cap, C.byref(nh), C.byref(st))
+            with ctx.lock:
+                rc = ctx.lib.ambc_decompress_ex(ctx.h, _lib.addr(data), len(data), orig_size, reg,
+                                                optr, hc, cap, C.byref(nh), C.byref(st))
             if rc == _lib.AMBC_E_CAPACITY and nh.value > cap:
                 cap = nh.value
                 continue

@@ -62,8 +62,9 @@ def compress_shard(group, d_shard, n_total, params, d_out, out_cap, root=-1):
     ``group`` is a GpuGroup (or a one-device Context: one rank)."""
     ctx = getattr(group, "ctx", group)
     info, st = _lib.ShardInfo(), _lib.Stats()
-    rc = ctx.lib.ambc_compress_shard(ctx.h, int(d_shard), n_total, C.byref(params), int(d_out), out_cap,
-                                     root, C.byref(info), C.byref(st))
+    with ctx.lock:
+        rc = ctx.lib.ambc_compress_shard(ctx.h, int(d_shard), n_total, C.byref(params), int(d_out), out_cap,
+                                         root, C.byref(info), C.byref(st))
     if rc == _lib.AMBC_E_RANGE:
         import struct
         raise struct.error("argument out of range")
@@ -76,8 +77,9 @@ def gather(group, d_src, nbytes, d_dst=None, dst_cap=0):
     (this rank's offset, total)."""
     ctx = getattr(group, "ctx", group)
     off, tot = C.c_uint64(), C.c_uint64()
-    _lib.check(ctx.lib.ambc_comm_gather(ctx.h, int(d_src), nbytes, int(d_dst) if d_dst else None, dst_cap,
-                                        C.byref(off), C.byref(tot)), ctx.lib)
+    with ctx.lock:
+        _lib.check(ctx.lib.ambc_comm_gather(ctx.h, int(d_src), nbytes, int(d_dst) if d_dst else None, dst_cap,
+                                            C.byref(off), C.byref(tot)), ctx.lib)
     return off.value, tot.value
 
 
@@ -107,9 +109,10 @@ def decompress_shard(group, body, orig_size, d_out, out_cap, root=0, registered=
     ctx = getattr(group, "ctx", group)
     arr = np.frombuffer(body, dtype=np.uint8)
     info, st = _lib.ShardInfo(), _lib.Stats()
-    rc = ctx.lib.ambc_decompress_shard(ctx.h, arr.ctypes.data if len(arr) else None, len(arr), orig_size,
-                                       registered_array(registered), int(d_out), out_cap, root,
-                                       C.byref(info), C.byref(st))
+    with ctx.lock:
+        rc = ctx.lib.ambc_decompress_shard(ctx.h, arr.ctypes.data if len(arr) else None, len(arr), orig_size,
+                                           registered_array(registered), int(d_out), out_cap, root,
+                                           C.byref(info), C.byref(st))
     if rc == _lib.AMBC_E_MARKER:
         raise ValueError("Marker mismatch in chunk header.")
     _lib.check(rc, ctx.lib)
@@ -122,8 +125,9 @@ def decompress_multi(ctx, body, orig_size, registered=DEFAULT_REGISTERED):
     arr = np.frombuffer(body, dtype=np.uint8)
     out = bytearray(max(orig_size, 1))
     st = _lib.Stats()
-    rc = ctx.lib.ambc_decompress_multi(ctx.h, arr.ctypes.data if len(arr) else None, len(arr), orig_size,
-                                       registered_array(registered), _lib.addr(out), C.byref(st))
+    with ctx.lock:
+        rc = ctx.lib.ambc_decompress_multi(ctx.h, arr.ctypes.data if len(arr) else None, len(arr), orig_size,
+                                           registered_array(registered), _lib.addr(out), C.byref(st))
     if rc == _lib.AMBC_E_MARKER:
         raise ValueError("Marker mismatch in chunk header.")
     _lib.check(rc, ctx.lib)

@@ -1014,7 +1014,10 @@ __device__ __forceinline__ void compact_package(const CompactArgs& A, uint32_t k
         const uint4* src4 = reinterpret_cast<const uint4*>(sl + t0 - rr);
         uint4* dst4 = reinterpret_cast<uint4*>(g0 << 4);
         for (uint32_t j = lane; j < ng; j += 64) {
-            const uint4 a = src4[j], b = src4[j + 1];
+            // (a source on the 16-byte grid needs no second block: never read it --
+            // for a raw package compacted from the caller's input it may lie past
+            // the input's last byte, in unmapped memory)
+            const uint4 a = src4[j], b = rr ? src4[j + 1] : make_uint4(0u, 0u, 0u, 0u);
             uint32_t w[5];
 #pragma unroll
             for (int i = 0; i < 5; i++) w[i] = pick_dword(a, b, ds + i);

@@ -247,6 +247,9 @@ static uint32_t compact_resident() {
 // rank of a sharded call fails those alike) and `joined` once the call entered
 // reference mode's remainder exchange: compress_on joins that exchange on behalf
 // of any later failure, so that no peer waits in it for a rank that left.
+// the sharded tests' failure injection (ambc_test_inject_failure; -1: none)
+static std::atomic<int> g_fail_rank{-1};
+
 static int compress_on_body(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_params* p, uint8_t* d_out,
                             uint64_t out_cap, uint64_t* out_len, ambc_stats* st, const ShardInfo* si,
                             bool& armed, bool& joined) {
@@ -260,8 +263,8 @@ static int compress_on_body(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_
     const uint64_t bound = ambc_compress_bound(n, C) - (end ? 0 : END_CHUNK);
     if (out_cap < bound) return fail(AMBC_E_CAPACITY, "device output capacity < ambc_compress_bound");
     armed = true;
-    if (const char* e = getenv("AMBC_TEST_FAIL_RANK"))   // failure injection for the sharded tests
-        if (si && atoi(e) == si->rank) return fail(AMBC_E_DEVICE, "injected failure (AMBC_TEST_FAIL_RANK)");
+    if (si && g_fail_rank.load(std::memory_order_relaxed) == si->rank)   // (ambc_test_inject_failure)
+        return fail(AMBC_E_DEVICE, "injected failure (ambc_test_inject_failure)");
     HIPCHK(hipSetDevice(d.id));
     hipStream_t s = d.stream;
     const uint64_t t0 = now_ns();
@@ -2212,6 +2215,8 @@ extern "C" int ambc_decompress_device(ambc_ctx* ctx, int dev, const uint8_t* bod
 
 // host code only (diagnostics): the threaded header walk of the decode path on
 // a host body -> packages, output bytes, wall ns (threads: 0 = default)
+extern "C" int ambc_test_inject_failure(int rank) { return g_fail_rank.exchange(rank); }
+
 extern "C" int ambc_debug_walk(const uint8_t* body, uint64_t blen, uint64_t orig_size, uint32_t threads,
                                uint64_t* n_pkgs, uint64_t* total, uint64_t* ns) {
     uint64_t reg[4];

@@ -14,6 +14,7 @@
 
 #include "../../include/ambc.h"
 #include "ambc_internal.h"
+#include "ambc_sync.h"
 
 namespace ambc {
 
@@ -192,7 +193,7 @@ struct ambc_ctx {
     // in-process multi-device communicators (ncclCommInitAll over distinct devices),
     // created on the first sharded call
     std::vector<ncclComm_t> dev_comms;
-    std::mutex comm_mu;          // guards dev_comms against a concurrent abort
+    ambc::AbortGate comm_gate;         // a failed rank's abort against enqueues in progress (ambc_shard.cpp)
 };
 
 namespace ambc {

@@ -47,92 +47,7 @@
 namespace ambc {
 namespace {
 
-// A few host threads for the walk's per-round host work (filling a batch's results
-// into the position table, deciding every walk's steps): between two rounds the
-// device waits for them (~1 ms a round for a thousand walks on one thread).  The
-// workers spin briefly between tasks (the rounds come every few ms), then sleep.
-// AMBC_MS_THREADS sets the count (1: all on the calling thread; 10 by default where
-// the host has the cores: {1,3,4,9} walk 40.2-41.4 -> 38.4 ms against 6,
-// profiles/r4_walk_threads_ab3).
-class WalkPool {
-  public:
-    static WalkPool& get() {
-        static WalkPool pool;
-        return pool;
-    }
-    unsigned size() const { return (unsigned)workers_.size() + 1; }
-    // fn(t, T) for t in [0, T), T = size(); the caller runs t = 0
-    void run(const std::function<void(unsigned, unsigned)>& fn) {
-        const unsigned T = size();
-        if (T == 1) { fn(0, 1); return; }
-        if (getpid() != pid_) {   // a forked child has no workers: every slice here
-            for (unsigned t = 0; t < T; t++) fn(t, T);
-            return;
-        }
-        std::lock_guard<std::mutex> serial(run_mu_);   // one task at a time
-        {
-            std::lock_guard<std::mutex> g(mu_);
-            task_ = &fn;
-            pending_.store(T - 1);
-            gen_.fetch_add(1);
-        }
-        cv_.notify_all();
-        fn(0, T);
-        while (pending_.load() != 0) std::this_thread::yield();
-        task_ = nullptr;
-    }
-    ~WalkPool() {
-        if (getpid() != pid_) {   // (a forked child: the threads are the parent's; leave them be)
-            new std::vector<std::thread>(std::move(workers_));
-            return;
-        }
-        {
-            std::lock_guard<std::mutex> g(mu_);
-            stop_ = true;
-            gen_.fetch_add(1);
-        }
-        cv_.notify_all();
-        for (auto& t : workers_) t.join();
-    }
-
-  private:
-    WalkPool() {
-        const char* e = getenv("AMBC_MS_THREADS");
-        unsigned T = e ? (unsigned)std::max(1, atoi(e)) : std::min(10u, std::max(1u, std::thread::hardware_concurrency() / 2));
-        for (unsigned t = 1; t < T; t++) workers_.emplace_back([this, t] { loop(t); });
-        pid_ = getpid();
-    }
-    void loop(unsigned t) {
-        uint64_t seen = 0;
-        for (;;) {
-            // spin up to ~2 ms for the next task, then sleep on the condition variable
-            const auto t0 = std::chrono::steady_clock::now();
-            while (gen_.load() == seen && std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(2))
-                std::this_thread::yield();
-            if (gen_.load() == seen) {
-                std::unique_lock<std::mutex> lk(mu_);
-                cv_.wait(lk, [&] { return gen_.load() != seen; });
-            }
-            seen = gen_.load();
-            if (stop_) return;
-            const std::function<void(unsigned, unsigned)>* f;
-            {
-                std::lock_guard<std::mutex> g(mu_);
-                f = task_;
-            }
-            if (f) (*f)(t, size());
-            pending_.fetch_sub(1);
-        }
-    }
-    std::vector<std::thread> workers_;
-    std::mutex mu_, run_mu_;
-    std::condition_variable cv_;
-    std::atomic<uint64_t> gen_{0};
-    std::atomic<unsigned> pending_{0};
-    const std::function<void(unsigned, unsigned)>* task_ = nullptr;
-    bool stop_ = false;
-    pid_t pid_ = 0;
-};
+// (WalkPool, the per-round host threads: ambc_sync.h)
 
 bool eligible(const ambc_params* p, uint32_t s, uint32_t id) {
     return ((p->method_mask >> id) & 1) && p->pref_min[id] <= s && s <= p->pref_max[id];
@@ -822,6 +737,11 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
             if (!rechain && w.cs == w.last && w.cq > w.pos && (w.cq - w.pos) % w.last == 0) {
                 k = (int)std::min<uint64_t>((w.cq - w.pos) / w.last, (uint64_t)SPEC + 1);
                 q = w.pos + (uint64_t)k * w.last;
+                // the walk's own position is always asked for again (its record
+                // knows what is requested already): a speculative request there
+                // may have been forgotten (a size check_size refuses), and the walk
+                // would otherwise wait for it forever
+                ask(w.pos);
             }
             for (; k <= SPEC && q < n; k++, q += w.last) {
                 if (k && rec_of(q).decided) break;

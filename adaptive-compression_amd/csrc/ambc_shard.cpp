@@ -33,6 +33,7 @@
 #include "../../include/ambc.h"
 #include "ambc_hostctx.h"
 #include "ambc_internal.h"
+#include "ambc_sync.h"
 
 namespace ambc {
 
@@ -61,21 +62,22 @@ struct RcclTransport : Transport {
     // rank aborts all of them (ncclCommAbort releases peers blocked in a
     // collective); the ctx builds fresh ones on its next sharded call
     std::vector<ncclComm_t>* group = nullptr;
-    std::mutex* group_mu = nullptr;
+    AbortGate* gate = nullptr;
     RcclTransport(ncclComm_t c, Dev& dev, int nranks, int rank) : comm(c), d(dev) { W = nranks; r = rank; }
-    // Enqueue this rank's operations on its communicator.  In-process ranks hold
-    // the group's lock while they enqueue, so a failed peer's abort() never
-    // frees a communicator between the lookup and the enqueue; once enqueued,
-    // an abort cancels the operation in flight (ncclCommAbort's purpose) and the
-    // stream wait that follows, outside the lock, returns.  Null communicator:
-    // a failed peer aborted the group.
+    // Enqueue this rank's operations on its communicator.  No lock spans the
+    // enqueue (a peer's first collective may wait inside its call for this rank):
+    // in-process ranks pass the group's AbortGate, so a failed peer's abort()
+    // waits for the enqueue to return before it frees the communicators, and an
+    // enqueue after the abort fails.  Once enqueued, an abort cancels the
+    // operation in flight (ncclCommAbort's purpose) and the stream wait that
+    // follows returns.
     template <typename F>
     int enqueue(F&& ops) {
         if (!group) return ops(comm);
-        std::lock_guard<std::mutex> lk(*group_mu);
-        ncclComm_t c = (*group)[r];
-        if (!c) return fail(AMBC_E_COMM, "communicator aborted by a failed rank");
-        return ops(c);
+        if (!gate->enter()) return fail(AMBC_E_COMM, "communicator aborted by a failed rank");
+        const int rc = ops((*group)[r]);
+        gate->leave();
+        return rc;
     }
 
     int allgather_u64(const uint64_t* mine, uint32_t k, uint64_t* all) override {
@@ -134,45 +136,16 @@ struct RcclTransport : Transport {
     }
     void abort() override {
         if (!group) return;   // a process per GPU: the status exchanges keep the ranks in step
-        std::lock_guard<std::mutex> lk(*group_mu);
-        for (ncclComm_t& c : *group)
-            if (c) { (void)ncclCommAbort(c); c = nullptr; }
+        gate->abort([&] {
+            for (ncclComm_t& c : *group)
+                if (c) { (void)ncclCommAbort(c); c = nullptr; }
+        });
     }
 };
 
 // ---------------------------------------------------------------------------
 // host threads of one process (a ctx that lists a device more than once)
 // ---------------------------------------------------------------------------
-struct Hub {
-    explicit Hub(int w) : W(w), vals(w), srcs(w, nullptr) {}
-    std::mutex m;
-    std::condition_variable cv;
-    int W, arrived = 0;
-    uint64_t gen = 0;
-    bool failed = false;
-    std::vector<std::vector<uint64_t>> vals;
-    std::vector<const uint8_t*> srcs;
-    // false when some rank failed (every waiter returns)
-    bool wait() {
-        std::unique_lock<std::mutex> lk(m);
-        if (failed) return false;
-        const uint64_t g = gen;
-        if (++arrived == W) {
-            arrived = 0;
-            gen++;
-            cv.notify_all();
-            return true;
-        }
-        cv.wait(lk, [&] { return gen != g || failed; });
-        return !failed;
-    }
-    void fail() {
-        std::lock_guard<std::mutex> lk(m);
-        failed = true;
-        cv.notify_all();
-    }
-};
-
 struct LocalTransport : Transport {
     Hub& hub;
     Dev& d;
@@ -418,6 +391,56 @@ static int shard_decompress(Dev& d, Transport& t, const uint8_t* body, uint64_t 
     return AMBC_OK;
 }
 
+// One thread issues, as one group over every communicator of the ctx, each
+// collective kind the in-process ranks use -- AllGather and AllReduce of u64 at
+// the sizes the calls exchange, and every rank's Send / Recv to rank 0 (the
+// gather) -- so that every connection exists before the rank threads start:
+// after this no enqueue waits for a peer.  (This is the single-process multi-GPU
+// pattern of SURVEY.md §5; it stays unverified until an 8-GPU node runs it.)
+static int connect_group(ambc_ctx* ctx) {
+    const int G = (int)ctx->devs.size();
+    constexpr uint32_t K = 262;            // (NSTAT: the largest u64 exchange)
+    for (int g = 0; g < G; g++) {
+        Dev& d = ctx->devs[g];
+        HIPCHK(hipSetDevice(d.id));
+        HIPCHK(d.coll.ensure((size_t)(G + 1) * K * 8));
+        HIPCHK(hipMemsetAsync(d.coll.p, 0, (size_t)(G + 1) * K * 8, d.stream));
+        HIPCHK(hipStreamSynchronize(d.stream));
+    }
+    for (uint32_t k : {1u, 3u, K}) {
+        NCCLCHK(ncclGroupStart());
+        for (int g = 0; g < G; g++) {
+            Dev& d = ctx->devs[g];
+            uint64_t* buf = d.coll.as<uint64_t>();
+            NCCLCHK(ncclAllGather(buf, buf + k, k, ncclUint64, ctx->dev_comms[g], d.stream));
+        }
+        NCCLCHK(ncclGroupEnd());
+        NCCLCHK(ncclGroupStart());
+        for (int g = 0; g < G; g++) {
+            Dev& d = ctx->devs[g];
+            uint64_t* buf = d.coll.as<uint64_t>();
+            NCCLCHK(ncclAllReduce(buf, buf, k, ncclUint64, ncclSum, ctx->dev_comms[g], d.stream));
+        }
+        NCCLCHK(ncclGroupEnd());
+    }
+    NCCLCHK(ncclGroupStart());
+    for (int g = 0; g < G; g++) {
+        Dev& d = ctx->devs[g];
+        uint8_t* buf = d.coll.as<uint8_t>();
+        if (g == 0) {
+            for (int q = 1; q < G; q++) NCCLCHK(ncclRecv(buf + 8 * q, 8, ncclUint8, q, ctx->dev_comms[0], d.stream));
+        } else {
+            NCCLCHK(ncclSend(buf, 8, ncclUint8, 0, ctx->dev_comms[g], d.stream));
+        }
+    }
+    NCCLCHK(ncclGroupEnd());
+    for (int g = 0; g < G; g++) {
+        HIPCHK(hipSetDevice(ctx->devs[g].id));
+        HIPCHK(hipStreamSynchronize(ctx->devs[g].stream));
+    }
+    return AMBC_OK;
+}
+
 // in-process multi-device: one transport per device
 static int make_transports(ambc_ctx* ctx, std::unique_ptr<Hub>& hub, std::vector<std::unique_ptr<Transport>>& ts) {
     const int G = (int)ctx->devs.size();
@@ -431,12 +454,21 @@ static int make_transports(ambc_ctx* ctx, std::unique_ptr<Hub>& hub, std::vector
             std::vector<int> dl;
             for (auto& d : ctx->devs) dl.push_back(d.id);
             ctx->dev_comms.assign(G, nullptr);
+            // every connection at init (RCCL 2.27 connects lazily inside a rank's
+            // first collective, where it waits for its peers) -- unless the caller
+            // chose otherwise -- and the warm-up below connects the rest
+            setenv("NCCL_RUNTIME_CONNECT", "0", 0);
             NCCLCHK(ncclCommInitAll(ctx->dev_comms.data(), G, dl.data()));
+            ctx->comm_gate.reset();
+            if (int rc = connect_group(ctx)) {
+                for (ncclComm_t& c : ctx->dev_comms) if (c) { (void)ncclCommAbort(c); c = nullptr; }
+                return rc;
+            }
         }
         for (int g = 0; g < G; g++) {
             RcclTransport* rt = new RcclTransport(ctx->dev_comms[g], ctx->devs[g], G, g);
             rt->group = &ctx->dev_comms;
-            rt->group_mu = &ctx->comm_mu;
+            rt->gate = &ctx->comm_gate;
             ts.emplace_back(rt);
         }
     } else {

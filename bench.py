@@ -67,8 +67,9 @@ def parse():
     ap.add_argument("--py-seconds", type=float, default=12.0,
                     help="budget of the single-core pure-Python restatement leg")
     ap.add_argument("--no-e2e", action="store_true", help="skip the pinned host-to-host leg")
-    ap.add_argument("--alt-methods", default="1,3,4,5;1,2,3,4;1,3,4,5z",
+    ap.add_argument("--alt-methods", default="1,3,4;1,3,4,5;1,2,3,4;1,3,4,5z",
                     help="';'-separated method sets reported beside the headline ('' to skip): "
+                         "1,3,4 = the reference's per-chunk GPU-routable set (BASELINE.md's CPU row); "
                          "1,3,4,5 = every package decodable by the stdlib-only reference; "
                          "a trailing z = id 5 as zlib.compress(data, 9)'s own bytes; "
                          "1,2,3,4 = the reference's own bytes (byte-pinned set)")
@@ -81,6 +82,12 @@ def parse():
     ap.add_argument("--ref-walk-check-bytes", type=int, default=4 << 20,
                     help="prefix on which the cpu_baseline leg times the oracle's reference walk and "
                          "compares its body with the GPU's")
+    ap.add_argument("--ref-full-walk-bytes", type=int, default=4 << 20,
+                    help="the reference's default compress() path with its whole stdlib method set "
+                         "(like_reference(full_set=True): {1..7}, bz2 / LZMA scored on host threads) "
+                         "on this many bytes; 0: skip")
+    ap.add_argument("--ref-full-walk-check-bytes", type=int, default=1 << 20,
+                    help="prefix on which that leg's body is compared with the oracle's reference loop")
     ap.add_argument("--api-bytes", type=int, default=256 << 20,
                     help="input size of the AdaptiveCompressor.compress(path, path) leg (0: skip)")
     a = ap.parse_args()
@@ -326,19 +333,24 @@ def alt_leg(lib, ctx, d_in, n, args, methods, steps, zlib9=False):
                        "header_walk_ms": round(ds.walk_ns / 1e6, 3), "host_api_GBps": round(n / dwall / 1e9, 3)}}
 
 
-def ref_walk_leg(ctx, nbytes):
+def ref_walk_leg(ctx, nbytes, full_set=False, check_bytes=0):
     """The reference's own default compress() path at the reference's bytes:
     AdaptiveCompressor.like_reference() -- the eight CHUNK_SIZE_CANDIDATES walk
-    (adaptive_compressor.py:61-62,537-590) with {1,2,3,4,5}, id 5 as
-    zlib.compress(chunk, 9)'s own bytes (advanced_compression.py:76-81) at every
-    size -- host bytes in and out, second call timed, bit-exact decode.  Input:
-    multisize_bench's mixed segments (on the headline's stream the walk stores
-    the rest raw at the first random byte run)."""
+    (adaptive_compressor.py:61-62,537-590), id 5 as zlib.compress(chunk, 9)'s own
+    bytes (advanced_compression.py:76-81) at every size -- host bytes in and out,
+    second call timed, bit-exact decode.  full_set=False: its GPU-encodable
+    stdlib codecs {1,2,3,4,5} (ids 6 / 7 left out); full_set=True: the reference's
+    whole default set {1..7} (adaptive_compressor.py:129-176, compression_fix.py:
+    60-125), bz2 / LZMA scored on host threads beside the device, and the body of
+    a check_bytes prefix compared with the oracle's restatement of the reference
+    loop with the same stdlib calls.  Input: multisize_bench's mixed segments (on
+    the headline's stream the walk stores the rest raw at the first random byte
+    run)."""
     from ambc import AdaptiveCompressor
     sys.path.insert(0, os.path.join(REPO, "scripts"))
     from multisize_bench import mixed
     data = mixed(nbytes, 7)
-    comp = AdaptiveCompressor.like_reference()
+    comp = AdaptiveCompressor.like_reference(full_set=full_set)
     comp._adaptive_compress(data)
     t = time.perf_counter()
     body = comp._adaptive_compress(data)
@@ -346,8 +358,23 @@ def ref_walk_leg(ctx, nbytes):
     steps, ev, wns, ens = C.c_uint32(), C.c_uint64(), C.c_uint64(), C.c_uint64()
     ctx.lib.ambc_last_multisize_info(comp._ctx().h, C.byref(steps), C.byref(ev), C.byref(wns), C.byref(ens))
     ok = comp._adaptive_decompress(body, nbytes) == data
-    return {"path": "AdaptiveCompressor.like_reference(): the reference's default compress() walk",
-            "methods": [m.type_id for m in comp.compression_methods], "deflate": comp.deflate,
+    ids = [m.type_id for m in comp.compression_methods]
+    check = None
+    if full_set and check_bytes:
+        from oracle import oracle as orc
+        pre = data[:check_bytes]
+        t = time.perf_counter()
+        ref, _ = orc.compress_body_multisize(pre, comp.CHUNK_SIZE_CANDIDATES, tuple(ids), deflate="zlib",
+                                             reference_set=True)
+        dto = time.perf_counter() - t
+        check = {"bytes": check_bytes, "gpu_body_equals_oracle": comp._adaptive_compress(pre) == ref,
+                 "oracle_seconds": round(dto, 3), "oracle_GBps_1core": round(check_bytes / dto / 1e9, 6)}
+    path = ("AdaptiveCompressor.like_reference(full_set=True): the reference's default compress() walk with "
+            "its whole stdlib method set {1,2,3,4,5,6,7} (bz2 / LZMA scored on host threads)" if full_set else
+            "AdaptiveCompressor.like_reference(): the reference's default compress() walk restricted to its "
+            "GPU-encodable stdlib codecs {1,2,3,4,5} (ids 6 / 7 left out: like_reference_full_walk has them)")
+    return {"path": path, **({"oracle_check": check} if check else {}),
+            "methods": ids, "deflate": comp.deflate,
             "candidates": comp.CHUNK_SIZE_CANDIDATES, "bytes": nbytes,
             "input": "runs / text / skewed random, 8-64 KiB segments (scripts/multisize_bench.py mixed, seed 7)",
             "GBps": round(nbytes / dt / 1e9, 3), "seconds": round(dt, 4), "ratio": round(len(body) / nbytes, 5),
@@ -577,10 +604,14 @@ def main():
                 w = walk_leg(ctx, args.walk_bytes, [int(x) for x in ms.split(",")])
                 log(f"walk: {w}")
                 walks.append(w)
-    ref_walk = None
+    ref_walk = ref_full = None
     if rank == 0 and world == 1 and args.ref_walk_bytes:
         ref_walk = ref_walk_leg(ctx, args.ref_walk_bytes)
         log(f"like_reference walk: {ref_walk}")
+    if rank == 0 and world == 1 and args.ref_full_walk_bytes:
+        ref_full = ref_walk_leg(ctx, args.ref_full_walk_bytes, full_set=True,
+                                check_bytes=args.ref_full_walk_check_bytes)
+        log(f"like_reference full walk: {ref_full}")
     if rank == 0 and world == 1 and args.api_bytes:
         api = api_leg(args.api_bytes, args.chunk, args.mode, methods, args.seed)
         log(f"api: {api}")
@@ -610,7 +641,8 @@ def main():
                        "step_ms_p50": round(percentile(step_s, 50) * 1e3, 3),
                        "step_ms_p90": round(percentile(step_s, 90) * 1e3, 3),
                        "e2e_pinned_host": e2e, "api_file": api, "alt_method_sets": alts,
-                       "multisize_walk": walks, "like_reference_walk": ref_walk},
+                       "multisize_walk": walks, "like_reference_walk": ref_walk,
+                       "like_reference_full_walk": ref_full},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,

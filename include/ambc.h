@@ -326,6 +326,12 @@ int ambc_last_encode_launches(ambc_ctx* ctx, int dev, uint32_t* n_launch);
 int ambc_debug_walk(const uint8_t* body, uint64_t body_len, uint64_t orig_size, uint32_t threads,
                     uint64_t* n_pkgs, uint64_t* total, uint64_t* ns);
 
+/* test hook, never set by the library itself: the sharded compress of rank
+ * `rank` fails right after its pre-flight (-1, the default: no injection) --
+ * tests/test_gpu_distributed.py drives the failure paths with it.  Process-wide;
+ * returns the previous value. */
+int ambc_test_inject_failure(int rank);
+
 #ifdef __cplusplus
 }
 #endif

@@ -142,11 +142,20 @@ class _HostScorer:
     """ambc_host_codecs over the instance's own method objects: per (position,
     size) pair the reference's per-size method loop restricted to them
     (adaptive_compressor.py:559-579: prefs, should_use, compress, exceptions
-    skipped, strict minimum of len + 18 below the chunk's length, list order)."""
+    skipped, strict minimum of len + 18 below the chunk's length, list order).
+    The walk scores every candidate size at every position it asks for, so the
+    payloads kept for ``emit`` are capped (beyond the cap ``emit`` recomputes) and
+    at most LZMA_JOBS LZMA compressors (the reference's 16 MiB dictionary: ~190
+    MiB of encoder state each) run at once -- the limits of the package's own
+    scorer, ambc/hostcodecs.py, kept here so this file stays standalone."""
+
+    CACHE_BYTES = 256 << 20
+    LZMA_JOBS = 4
 
     def __init__(self, data, methods, prefs, workers):
         self.data, self.methods, self.prefs = data, methods, prefs
-        self.cache, self.error = {}, None
+        self.cache, self.cached, self.error = {}, 0, None
+        self._lzma = threading.BoundedSemaphore(self.LZMA_JOBS)
         self.pool = ThreadPoolExecutor(workers)
         self._eval_cb, self._emit_cb = EVAL_FN(self._eval), EMIT_FN(self._emit)
         self.struct = HostCodecs(self._eval_cb, self._emit_cb, None)
@@ -159,7 +168,11 @@ class _HostScorer:
             if not lo <= size <= hi or not m.should_use(chunk):
                 continue
             try:
-                c = m.compress(chunk)
+                if m.type_id == 7:
+                    with self._lzma:
+                        c = m.compress(chunk)
+                else:
+                    c = m.compress(chunk)
             except Exception:  # noqa: BLE001 -- the reference's loop skips a raising method
                 continue
             if len(c) < wl:
@@ -171,8 +184,9 @@ class _HostScorer:
             pairs = [(int(pos[i]), int(size[i])) for i in range(count)]
             for i, (w, pay) in enumerate(self.pool.map(lambda ps: self.best(*ps), pairs)):
                 out_id[i], out_len[i] = w, (len(pay) if w else 0)
-                if w:
+                if w and self.cached + len(pay) <= self.CACHE_BYTES:
                     self.cache[pairs[i]] = (w, pay)
+                    self.cached += len(pay)
             return 0
         except BaseException as e:  # noqa: BLE001 -- must not unwind through C
             self.error = e

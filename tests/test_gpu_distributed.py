@@ -375,19 +375,19 @@ def test_rccl_multi_rank_shards(hip_lib):
 
 @pytest.mark.parametrize("fail_rank", [0, 1, 2])
 def test_sharded_reference_mode_failure_leaves_together(hip_lib, fail_rank):
-    """A rank that fails after the pre-flight (AMBC_TEST_FAIL_RANK injects it)
+    """A rank that fails after the pre-flight (ambc_test_inject_failure injects it)
     still joins the reference mode's remainder exchange and the size exchange:
     every rank returns an error, none waits for it, and the ctx works afterwards."""
     from ambc import _lib
     chunk, nchunks = 1024, 24
     data = _ref_mode_input(chunk, nchunks, 9)
     multi = _ctx([0] * 3)
-    os.environ["AMBC_TEST_FAIL_RANK"] = str(fail_rank)
+    multi.lib.ambc_test_inject_failure(fail_rank)
     try:
         with pytest.raises(_lib.AmbcError):
             _compress(multi, data, chunk, (1, 3, 4), mode="reference")
     finally:
-        del os.environ["AMBC_TEST_FAIL_RANK"]
+        multi.lib.ambc_test_inject_failure(-1)
     ref, _ = orc.compress_body(data, orc.make_params(chunk, "reference", (1, 3, 4, 255), n_total=len(data)))
     got, _ = _compress(multi, data, chunk, (1, 3, 4), mode="reference")
     assert got == ref

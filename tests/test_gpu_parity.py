@@ -812,6 +812,26 @@ def test_multisize_many_walks_match_oracle(ctx):
         assert comp._adaptive_decompress(body, len(data)) == data
 
 
+@pytest.mark.timeout(120)
+def test_multisize_refused_size_near_the_end_fails_not_hangs(ctx):
+    """Dictionary's prefs widened to 12288 (its GPU encoder takes <= 8192): the
+    remainder-clamped candidate near the end is refused by check_size.  A walk's
+    speculative request there is forgotten; a walk that later stands there must
+    ask again and fail (NotImplementedError), not wait forever.  Without that
+    position on the path the body equals the oracle's walk."""
+    text = synth.generate(5 * 4096 + 10000, 7)
+    for data in (text, bytes(4096) + text[4096:], bytes(len(text))):
+        comp = _compressor(methods=(1, 2, 3, 4, 9))
+        comp.CHUNK_SIZE_CANDIDATES = [16384, 4096]
+        comp.method_chunk_prefs = dict(comp.method_chunk_prefs)
+        comp.method_chunk_prefs[2] = (128, 12288)
+        try:
+            body = comp._adaptive_compress(data)
+        except NotImplementedError:
+            continue
+        assert comp._adaptive_decompress(body, len(data)) == data
+
+
 def _lz4_prefix_inputs():
     """Inputs whose LZ4 parses cross the candidate prefixes in every way: long
     matches over several prefix ends at once (zero runs), short periods (matches
