@@ -12,14 +12,14 @@ strict minimum of len + 18 below the chunk's own length, ids ascending; the
 library then joins it with the GPU's winner in id order.  bz2 / lzma release the
 GIL while they compress, so a thread pool runs the pairs in parallel.
 
-Memory: an LZMA compressor with the reference's 16 MiB dictionary holds about
-190 MiB of encoder state, so at most ``LZMA_JOBS`` (4) of them run at once --
-the rest of the pool keeps bz2 / zstd busy meanwhile; a walk therefore peaks
-near 0.8 GiB of host memory for LZMA (like_reference(full_set=True)).
+Memory: an LZMA encoder with the reference's 16 MiB dictionary holds about
+190 MiB of state; methods.py keeps at most 8 of them (re-initialised, not
+rebuilt, per call) and a call waits for a free one, so the rest of the pool keeps
+bz2 / zstd busy meanwhile: a walk peaks near 1.5 GiB of host memory for LZMA
+(like_reference(full_set=True)).
 """
 import ctypes as C
 import os
-import threading
 from concurrent.futures import ThreadPoolExecutor
 
 EVAL_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), C.c_uint32,
@@ -37,7 +37,6 @@ class HostScorer:
     instances of the host-scored ids; ``prefs``: method_chunk_prefs."""
 
     CACHE_BYTES = 256 << 20          # payloads kept from eval for emit (beyond: recomputed)
-    LZMA_JOBS = 4                    # concurrent LZMA compressors (~190 MiB of state each)
 
     def __init__(self, data, methods, prefs, workers=None):
         self.data = data
@@ -47,7 +46,6 @@ class HostScorer:
         self.cached = 0
         self.error = None
         self.pool = ThreadPoolExecutor(workers or min(32, os.cpu_count() or 4))
-        self._lzma = threading.BoundedSemaphore(self.LZMA_JOBS)
         # the callbacks must outlive the call: keep them on the instance
         self._eval_cb = EVAL_FN(self._eval)
         self._emit_cb = EMIT_FN(self._emit)
@@ -66,11 +64,7 @@ class HostScorer:
             if not lo <= size <= hi or not m.should_use(chunk):
                 continue
             try:
-                if m.type_id == 7:
-                    with self._lzma:
-                        c = m.compress(chunk)
-                else:
-                    c = m.compress(chunk)
+                c = m.compress(chunk)
             except Exception:  # noqa: BLE001 -- the reference's loop skips a raising method
                 continue
             if len(c) < wl:

@@ -22,7 +22,9 @@ C-ABI call for the whole body.
 import bz2
 import ctypes as C
 import lzma
+import queue
 import struct
+import threading
 import zlib
 from abc import ABC, abstractmethod
 
@@ -292,6 +294,104 @@ class Bzip2Compression(CompressionMethod):
             return bytes(original_length)
 
 
+class _XZEncoders:
+    """The reference's LZMA call -- ``lzma.LZMACompressor(format=FORMAT_XZ,
+    check=CHECK_CRC64, filters=[{"id": FILTER_LZMA2, "dict_size": 1 << 24}])``,
+    advanced_compression.py:163-182 -- made through the liblzma that Python's
+    own ``_lzma`` module links, on encoders that are kept and re-initialised
+    instead of built per call: a fresh encoder faults in ~190 MiB of match-finder
+    state each time (8 KiB chunk: 25 -> 10 ms; the walk scores LZMA at every
+    candidate size of 8 KiB and more).  Same library, same filter chain (preset
+    6 with the 16 MiB dictionary: what _lzma builds from that spec), same
+    check, one LZMA_FINISH pass: the same bytes -- checked against Python's lzma
+    on a probe when the pool is first used; a mismatch (or no liblzma) leaves
+    Python's lzma in charge.  At most SIZE encoders exist; a caller waits for one."""
+
+    SIZE = 8
+
+    class _Stream(C.Structure):          # lzma_stream (LZMA_STREAM_INIT: all zeros)
+        _fields_ = [("next_in", C.c_void_p), ("avail_in", C.c_size_t), ("total_in", C.c_uint64),
+                    ("next_out", C.c_void_p), ("avail_out", C.c_size_t), ("total_out", C.c_uint64),
+                    ("allocator", C.c_void_p), ("internal", C.c_void_p), ("reserved", C.c_uint8 * 128)]
+
+    class _Filter(C.Structure):          # lzma_filter
+        _fields_ = [("id", C.c_uint64), ("options", C.c_void_p)]
+
+    _pool = None
+    _lock = threading.Lock()
+
+    @classmethod
+    def pool(cls):
+        """the encoder pool, or None when the liblzma path is unavailable"""
+        with cls._lock:
+            if cls._pool is None:
+                cls._pool = False
+                try:
+                    lib = C.CDLL("liblzma.so.5")
+                    lib.lzma_lzma_preset.argtypes = [C.c_void_p, C.c_uint32]
+                    lib.lzma_lzma_preset.restype = C.c_int
+                    lib.lzma_stream_encoder.argtypes = [C.POINTER(cls._Stream), C.c_void_p, C.c_int]
+                    lib.lzma_stream_encoder.restype = C.c_int
+                    lib.lzma_code.argtypes = [C.POINTER(cls._Stream), C.c_int]
+                    lib.lzma_code.restype = C.c_int
+                    lib.lzma_stream_buffer_bound.argtypes = [C.c_size_t]
+                    lib.lzma_stream_buffer_bound.restype = C.c_size_t
+                    lib.lzma_end.argtypes = [C.POINTER(cls._Stream)]
+                    cls.lib = lib
+                    free = queue.LifoQueue()
+                    for _ in range(cls.SIZE):
+                        free.put(cls())
+                    probe = bytes(range(256)) * 40 + b"abcabcabd" * 300
+                    if cls._encode(free, probe) == cls._python(probe):
+                        cls._pool = free
+                except (OSError, AttributeError, RuntimeError):
+                    cls._pool = False
+            return cls._pool or None
+
+    def __init__(self):
+        lib = type(self).lib
+        self.opt = (C.c_uint8 * 512)()        # lzma_options_lzma (and slack)
+        if lib.lzma_lzma_preset(self.opt, 6):
+            raise RuntimeError("lzma_lzma_preset")
+        C.c_uint32.from_buffer(self.opt, 0).value = 1 << 24     # dict_size, the struct's first field
+        self.flt = (self._Filter * 2)(self._Filter(0x21, C.addressof(self.opt)),   # LZMA_FILTER_LZMA2
+                                      self._Filter((1 << 64) - 1, None))           # LZMA_VLI_UNKNOWN
+        self.strm = self._Stream()
+
+    def run(self, data):
+        lib = type(self).lib
+        if lib.lzma_stream_encoder(C.byref(self.strm), self.flt, 4):      # LZMA_CHECK_CRC64
+            raise RuntimeError("lzma_stream_encoder")
+        cap = lib.lzma_stream_buffer_bound(len(data))
+        out = C.create_string_buffer(cap)
+        src = C.c_char_p(data)
+        self.strm.next_in, self.strm.avail_in = C.cast(src, C.c_void_p), len(data)
+        self.strm.next_out, self.strm.avail_out = C.addressof(out), cap
+        if lib.lzma_code(C.byref(self.strm), 3) != 1:                    # LZMA_FINISH -> LZMA_STREAM_END
+            raise RuntimeError("lzma_code")
+        return out.raw[:cap - self.strm.avail_out]
+
+    @staticmethod
+    def _encode(free, data):
+        enc = free.get()
+        try:
+            return enc.run(data)
+        finally:
+            free.put(enc)
+
+    @staticmethod
+    def _python(data):
+        c = lzma.LZMACompressor(format=lzma.FORMAT_XZ, check=lzma.CHECK_CRC64,
+                                filters=[{"id": lzma.FILTER_LZMA2, "dict_size": 1 << 24}])
+        return c.compress(data) + c.flush()
+
+    @classmethod
+    def compress(cls, data):
+        free = cls.pool()
+        data = bytes(data)
+        return cls._encode(free, data) if free is not None else cls._python(data)
+
+
 class LZMACompression(CompressionMethod):
     """advanced_compression.py:155-213"""
     type_id = 7
@@ -300,9 +400,7 @@ class LZMACompression(CompressionMethod):
         if not data:
             return b""
         try:
-            c = lzma.LZMACompressor(format=lzma.FORMAT_XZ, check=lzma.CHECK_CRC64,
-                                    filters=[{"id": lzma.FILTER_LZMA2, "dict_size": 1 << 24}])
-            return c.compress(data) + c.flush()
+            return _XZEncoders.compress(data)
         except Exception:  # noqa: BLE001 -- advanced_compression.py:183-185 returns the input
             return data
 

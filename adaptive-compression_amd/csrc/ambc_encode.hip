@@ -33,14 +33,19 @@ namespace ambc {
 
 template <int CMAX, bool GL = false>
 struct EncSmem {
-    // work = union, by lifetime.  Selection: hist | code | clen | Huffman tree
-    // (parent/pbit), whose space the first occurrences (first/order) reuse once
-    // the tree is built.  LZ4: the hash table (u32 per bucket).  Emit: RLE pair
-    // starts | Huffman bit staging behind hist/code/clen.  8 KB per workgroup at
-    // C = 4096 -> 20 workgroups per CU (12 KB / 13 at 8192, 20 KB / 8 at 16384).
-    static constexpr int WORK = 4096;   // every chunk size; larger Huffman payloads stage in the slot
-    static constexpr int STAGE_OFF = 2304;                  // Huffman bit staging
-    static constexpr int STAGE = WORK - STAGE_OFF;
+    // work = union, by lifetime.  Selection: hist | Huffman tree (parent / pbit,
+    // whose space the first occurrences first / order reuse once the codes are
+    // known) | clen | code.  LZ4: the hash table (u32 per bucket) over all of it.
+    // Emit: RLE pair starts, or the Huffman bit stage over everything below clen
+    // (the table is written before the stage is filled).  4 KB per workgroup: 32
+    // workgroups (8 waves per SIMD) fit a CU.
+    //   0    .. 1023  hist u32[256]                        | stage
+    //   1024 .. 2047  parent u16[512]  | first u32[256]     | stage
+    //   2048 .. 2559  pbit u8[512]     | order u8[256]      | stage
+    //   2816 .. 3071  clen u8[256]
+    //   3072 .. 4095  code u32[256]
+    static constexpr int WORK = 4096;   // every chunk size
+    static constexpr int STAGE = 2816;  // Huffman bit stage (a larger payload goes in windows)
     // zero padded up to CMAX; reads past CMAX (the LZ4 loads of lanes beyond n,
     // match lengths capped below n) land in work[], which follows: in bounds,
     // and never part of a result
@@ -48,14 +53,14 @@ struct EncSmem {
     alignas(16) uint32_t work[WORK / 4];
     __device__ __forceinline__ uint8_t* wb() { return reinterpret_cast<uint8_t*>(work); }
     __device__ __forceinline__ uint32_t* hist() { return work; }
-    __device__ __forceinline__ uint32_t* code() { return work + 256; }
-    __device__ __forceinline__ uint8_t* clen() { return wb() + 2048; }
-    __device__ __forceinline__ uint16_t* parent() { return reinterpret_cast<uint16_t*>(wb() + 2304); }
-    __device__ __forceinline__ uint8_t* pbit() { return wb() + 3328; }
-    __device__ __forceinline__ uint32_t* first() { return reinterpret_cast<uint32_t*>(wb() + 2304); }
-    __device__ __forceinline__ uint8_t* order() { return wb() + 3328; }
+    __device__ __forceinline__ uint16_t* parent() { return reinterpret_cast<uint16_t*>(wb() + 1024); }
+    __device__ __forceinline__ uint8_t* pbit() { return wb() + 2048; }
+    __device__ __forceinline__ uint32_t* first() { return reinterpret_cast<uint32_t*>(wb() + 1024); }
+    __device__ __forceinline__ uint8_t* order() { return wb() + 2048; }
+    __device__ __forceinline__ uint8_t* clen() { return wb() + 2816; }
+    __device__ __forceinline__ uint32_t* code() { return reinterpret_cast<uint32_t*>(wb() + 3072); }
     __device__ __forceinline__ uint32_t* last() { return work; }
-    __device__ __forceinline__ uint32_t* stage() { return reinterpret_cast<uint32_t*>(wb() + STAGE_OFF); }
+    __device__ __forceinline__ uint32_t* stage() { return work; }
 };
 static_assert((1u << LZ4_HASH_BITS) * 4 <= 4096, "LZ4 table must fit the work area");
 
@@ -121,6 +126,32 @@ __device__ __forceinline__ uint8_t lz4_hdr_byte(uint32_t q, uint32_t n, uint32_t
     if (q < 14) return q < 10 ? (uint8_t)(n >> (8 * (q - 6))) : 0;
     if (q == 14) return (uint8_t)((xxh32_desc(n) >> 8) & 0xFF);
     return (uint8_t)(bs >> (8 * (q - 15)));
+}
+
+// len bytes from LDS (src: 4-byte aligned) to global memory at any alignment: the
+// destination's aligned 16-byte groups one per lane and step (five LDS dwords
+// shifted into place), the bytes before and after them one per lane
+__device__ __forceinline__ void lds_store_bytes(uint8_t* dst, const uint8_t* src, uint32_t len, uint32_t lane) {
+    const uint64_t da = reinterpret_cast<uintptr_t>(dst);
+    const uint64_t g0 = (da + 15) >> 4, g1 = (da + len) >> 4;
+    const uint32_t ng = g1 > g0 ? (uint32_t)(g1 - g0) : 0u;
+    const uint32_t head = ng ? (uint32_t)((g0 << 4) - da) : len;
+    const uint32_t tail0 = ng ? head + 16 * ng : len;
+    const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src);
+    const uint32_t sh = head & 3u;
+    for (uint32_t j = lane; j < ng; j += 64) {
+        const uint32_t q = (head >> 2) + 4 * j;
+        const uint32_t a0 = s32[q], a1 = s32[q + 1], a2 = s32[q + 2], a3 = s32[q + 3];
+        const uint32_t a4 = sh ? s32[q + 4] : 0u;
+        uint4 v;
+        v.x = __builtin_amdgcn_alignbyte(a1, a0, sh);
+        v.y = __builtin_amdgcn_alignbyte(a2, a1, sh);
+        v.z = __builtin_amdgcn_alignbyte(a3, a2, sh);
+        v.w = __builtin_amdgcn_alignbyte(a4, a3, sh);
+        reinterpret_cast<uint4*>(g0 << 4)[j] = v;
+    }
+    for (uint32_t q = lane; q < head; q += 64) dst[q] = src[q];
+    for (uint32_t q = tail0 + lane; q < len; q += 64) dst[q] = src[q];
 }
 
 #ifdef AMBC_STAMPS
@@ -337,94 +368,54 @@ __global__ __launch_bounds__(64) AMBC_ENC_ATTR void k_encode(EncArgs A) {
         for (int r = 0; r < ROUNDS; r++) {
             const uint32_t b0 = (uint32_t)(r * 64 + lane) * BS;
             uint32_t prev = b0 ? (b0 - 1 < GLLIM ? (uint32_t)ch[b0 - 1] : 0u) : 0x100u;
+            // (the read first: once a lower block has posted a symbol, later
+            // occurrences skip the atomic -- most bytes of a text chunk)
             for_block_bytes<BS>(ch, b0, GLLIM, [&](uint32_t p, uint32_t c, uint32_t) {
-                if (p < n && c != prev) atomicMin(&first[c], p);
+                if (p < n && c != prev && first[c] > p) atomicMin(&first[c], p);
                 prev = c;
             });
         }
         wave_sync();
-        uint32_t f[4], rk[4] = {0, 0, 0, 0};
+        // the present symbols as (first position << 8 | symbol), compacted in
+        // symbol order over first[], then each ranked by the positions before it
+        uint32_t f[4];
 #pragma unroll
         for (int j = 0; j < 4; j++) f[j] = first[lane + 64 * j];
-#pragma unroll 4
-        for (int t = 0; t < 256; t++) {
-            const uint32_t ft = first[t];
+        wave_sync();
+        uint32_t K = 0;
+        const uint64_t lt = (1ull << lane) - 1ull;
 #pragma unroll
-            for (int j = 0; j < 4; j++) rk[j] += ft < f[j];
+        for (int j = 0; j < 4; j++) {
+            const bool pr = f[j] != 0xFFFFFFFFu;
+            const uint64_t m = __ballot(pr);
+            if (pr) first[K + (uint32_t)__popcll(m & lt)] = f[j] << 8 | (lane + 64 * j);
+            K += (uint32_t)__popcll(m);
         }
-#pragma unroll
-        for (int j = 0; j < 4; j++)
-            if (f[j] != 0xFFFFFFFFu) S.order()[rk[j]] = (uint8_t)(lane + 64 * j);
+        wave_sync();
+        for (uint32_t q = lane; q < K; q += 64) {
+            const uint32_t key = first[q];
+            uint32_t rk = 0;
+#pragma unroll 4
+            for (uint32_t t = 0; t < K; t++) rk += first[t] < key;
+            S.order()[rk] = (uint8_t)key;
+        }
         wave_sync();
     };
 
     uint32_t kdist = 0;
-    // Huffman code lengths/codes into clen[]/code[] from hist[] (kdist >= 2 symbols)
-    auto huff_tree = [&](uint32_t& nb, uint32_t& maxlen) {
-        // tree: slot s holds the active node whose first symbol is s; merge the two
-        // smallest (weight, first symbol) keys (heapq order, :482-494)
-        uint32_t key[4];
-        uint32_t nid[4];
+    // Huffman payload bits by the merges of the heapq order (:482-494): merge the
+    // two smallest (weight, first symbol) keys -- slot s holds the active node
+    // whose first symbol is s -- and every merge adds its weight once per level
+    // below it, so the encoded length is the sum of the merged weights.  The tree
+    // is recorded on the way (parent / pbit of each merged node) for the emission.
+    bool tree_ok = false;    // parent / pbit hold this chunk's tree (the LZ4 table overlays them)
+    auto huff_merge = [&]() -> uint32_t {
+        uint32_t key[4], nid[4];
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            const uint32_t s = lane + 64 * j, c = S.hist()[s];
-            key[j] = c ? (c << 8 | s) : 0xFFFFFFFFu;
-            nid[j] = s;
-        }
-#pragma unroll 1
-        for (uint32_t m = 0; m + 1 < kdist; m++) {
-            uint32_t lm = min(min(key[0], key[1]), min(key[2], key[3]));
-            const uint32_t k1 = wave_min_u32(lm);
-            uint32_t lm2 = 0xFFFFFFFFu;
-#pragma unroll
-            for (int j = 0; j < 4; j++) if (key[j] != k1) lm2 = min(lm2, key[j]);
-            const uint32_t k2 = wave_min_u32(lm2);
-            const uint32_t s1 = k1 & 255u, s2 = k2 & 255u;
-            const uint32_t merged = ((k1 >> 8) + (k2 >> 8)) << 8 | s1;
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                if (lane + 64 * j == s1) {
-                    S.parent()[nid[j]] = (uint16_t)(256 + m); S.pbit()[nid[j]] = 0;
-                    key[j] = merged; nid[j] = 256 + m;
-                } else if (lane + 64 * j == s2) {
-                    S.parent()[nid[j]] = (uint16_t)(256 + m); S.pbit()[nid[j]] = 1;
-                    key[j] = 0xFFFFFFFFu;
-                }
-            }
-        }
-        wave_sync();
-        const uint32_t root = 256 + kdist - 2;
-        nb = 0; maxlen = 0;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t s = lane + 64 * j, c = S.hist()[s];
-            if (c) {
-                uint32_t nd = s, len = 0, code = 0;
-                while (nd != root) {
-                    if (len < 32) code |= (uint32_t)S.pbit()[nd] << len;
-                    len++;
-                    nd = S.parent()[nd];
-                }
-                S.clen()[s] = (uint8_t)min(len, 255u);
-                S.code()[s] = code;
-                nb += c * len;
-                maxlen = max(maxlen, len);
-            }
-        }
-        nb = wave_sum_u32(nb);
-        maxlen = (uint32_t)wave_max_i32((int)maxlen);
-        wave_sync();
-    };
-
-    // Huffman payload bits without the tree: every merge of the heapq order
-    // (:482-494) adds its weight once per level below it, so the encoded length
-    // is the sum of the merged weights
-    auto huff_bits = [&]() -> uint32_t {
-        uint32_t key[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t s = lane + 64 * j, c = S.hist()[s];
-            key[j] = c ? (c << 8 | s) : 0xFFFFFFFFu;
+            const uint32_t sy = lane + 64 * j, c = S.hist()[sy];
+            key[j] = c ? (c << 8 | sy) : 0xFFFFFFFFu;
+            nid[j] = sy;
         }
         uint32_t nb = 0;
 #pragma unroll 1
@@ -440,11 +431,38 @@ __global__ __launch_bounds__(64) AMBC_ENC_ATTR void k_encode(EncArgs A) {
             nb += wsum;
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                if (lane + 64 * j == s1) key[j] = wsum << 8 | s1;
-                else if (lane + 64 * j == s2) key[j] = 0xFFFFFFFFu;
+                if (lane + 64 * j == s1) {
+                    S.parent()[nid[j]] = (uint16_t)(256 + m); S.pbit()[nid[j]] = 0;
+                    key[j] = wsum << 8 | s1; nid[j] = 256 + m;
+                } else if (lane + 64 * j == s2) {
+                    S.parent()[nid[j]] = (uint16_t)(256 + m); S.pbit()[nid[j]] = 1;
+                    key[j] = 0xFFFFFFFFu;
+                }
             }
         }
+        wave_sync();
+        tree_ok = true;
         return nb;
+    };
+    // code lengths / codes into clen[] / code[] from the recorded tree (kdist >= 2):
+    // every symbol walks to the root; the edge next to the root is the code's MSB
+    auto huff_codes = [&]() {
+        const uint32_t root = 256 + kdist - 2;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t sy = lane + 64 * j;
+            if (S.hist()[sy]) {
+                uint32_t nd = sy, len = 0, cd = 0;
+                while (nd != root) {
+                    if (len < 32) cd |= (uint32_t)S.pbit()[nd] << len;
+                    len++;
+                    nd = S.parent()[nd];
+                }
+                S.clen()[sy] = (uint8_t)min(len, 255u);
+                S.code()[sy] = cd;
+            }
+        }
+        wave_sync();
     };
 
     bool huff_su = false;
@@ -490,7 +508,7 @@ __global__ __launch_bounds__(64) AMBC_ENC_ATTR void k_encode(EncArgs A) {
                 huff_lb = 1 + 5 * kdist + 4 + (uint32_t)floor((double)n * H * (1.0 - 1e-9) / 8.0);
             } else {
                 // (code lengths stay <= 23 for n <= 65536: a Fibonacci-weighted tree)
-                const uint32_t nb = huff_bits();
+                const uint32_t nb = huff_merge();
                 const uint32_t l = 1 + 5 * kdist + 4 + (nb + 7) / 8;
                 if (l + HDR < best) { best = l + HDR; win = 3; wlen = l; }
             }
@@ -534,7 +552,8 @@ __global__ __launch_bounds__(64) AMBC_ENC_ATTR void k_encode(EncArgs A) {
     // 18-B header it cannot win unless best > 51 + ext(n - 10) (zero runs: RLE 52)
     const bool lz4_main = eligible(9) && (force || (n >= 1024 && best > 51 + ext_len(n - 10)));
     if (lz4_main || sj < sj_end) {
-        // the walk's hash table overlays hist[]: keep the counts in registers
+        // the walk's hash table overlays hist[] and the tree: keep the counts in registers
+        tree_ok = false;
         uint32_t hsave[4];
 #pragma unroll
         for (int j = 0; j < 4; j++) hsave[j] = S.hist()[lane + 64 * j];
@@ -804,7 +823,7 @@ __global__ __launch_bounds__(64) AMBC_ENC_ATTR void k_encode(EncArgs A) {
 
     if (huff_defer && huff_lb + HDR < best_pre && (win != 9 || huff_lb <= wlen)) {
         // Huffman comes before LZ4 in id order: it wins a tie with LZ4
-        const uint32_t nb = huff_bits();
+        const uint32_t nb = huff_merge();
         const uint32_t l = 1 + 5 * kdist + 4 + (nb + 7) / 8;
         if (l + HDR < best_pre && (win != 9 || l <= wlen)) { best = l + HDR; win = 3; wlen = l; }
     }
@@ -890,70 +909,87 @@ __global__ __launch_bounds__(64) AMBC_ENC_ATTR void k_encode(EncArgs A) {
             wave_sync();
         }
     } else if (win == 3) {
-        {
-            uint32_t nb2, ml2;
-            huff_tree(nb2, ml2);   // codes and lengths of the winner's tree
-        }
-        compute_first();   // (the LZ4 table may have overwritten an earlier order[])
-        uint32_t* bits = S.stage();
+        // the table: [k][sym, count u32le] x k (first-occurrence order), [nbits
+        // u32le], then the bits MSB-first (compression_methods.py:354-405)
+        if (!tree_ok) (void)huff_merge();   // (the LZ4 table overwrote the sizing pass's tree)
+        huff_codes();
+        compute_first();
         const uint32_t kk = kdist;
-        // table: [k][sym, count u32le] x k (first-occurrence order) [nbits u32le]
         if (lane == 0) slot[0] = (uint8_t)kk;
         for (uint32_t q = lane; q < kk; q += 64) {
-            const uint32_t s = S.order()[q], c = S.hist()[s];
+            const uint32_t sy = S.order()[q], c = S.hist()[sy];
             uint8_t* e = slot + 1 + 5 * q;
-            e[0] = (uint8_t)s; e[1] = (uint8_t)c; e[2] = (uint8_t)(c >> 8);
+            e[0] = (uint8_t)sy; e[1] = (uint8_t)c; e[2] = (uint8_t)(c >> 8);
             e[3] = (uint8_t)(c >> 16); e[4] = (uint8_t)(c >> 24);
         }
         const uint32_t hb = 1 + 5 * kk;
         const uint32_t nbytes = wlen - hb - 4;
-        const uint32_t nwords = (nbytes + 3) >> 2;
-        // forced encodes of high-entropy data can outgrow the LDS region: stage the
-        // bit words in the slot behind the payload instead (slot holds 3C + 1344 B)
-        const bool gstage = (nwords + 1) * 4 > (uint32_t)EncSmem<CMAX, GL>::STAGE;
-        if (gstage) bits = reinterpret_cast<uint32_t*>(slot0 + ((wlen + 15) & ~15u));   // (always the slot)
-        for (uint32_t w = lane; w < nwords + 1; w += 64) bits[w] = 0;
-        if (gstage) __threadfence();
-        wave_sync();
-        uint32_t bitbase = 0;
+        uint8_t* const pay = slot + hb + 4;
+        wave_sync();   // hist / first / order are done with: the stage overlays them
+        // The bits go through an LDS stage of CAPB bytes, a window of the payload
+        // at a time (one window for every Huffman winner of a 4 KiB chunk; forced
+        // high-entropy encodes take several): each lane packs its block's codes
+        // into 32-bit words, byte-swapped so that the stage holds the payload's
+        // bytes in order, ORs them in (LDS atomics: the words at the lanes' edges
+        // are shared), and the window is stored with aligned 16-byte stores.
+        constexpr uint32_t CAPB = EncSmem<CMAX, GL>::STAGE;
+        uint32_t* bits = S.stage();
+        uint32_t nbits = 0;
 #pragma unroll 1
-        for (int r = 0; r < ROUNDS; r++) {
-            const uint32_t b0 = (uint32_t)(r * 64 + lane) * BS;
-            uint32_t my = 0;
-            for_block_bytes<BS>(ch, b0, GLLIM, [&](uint32_t p, uint32_t c, uint32_t) {
-                if (p < n) my += S.clen()[c];
-            });
-            const uint32_t incl = wave_incl_sum(my);
-            uint32_t bp = bitbase + incl - my;
-            uint32_t cw = bp >> 5, acc = 0;
-            for_block_bytes<BS>(ch, b0, GLLIM, [&](uint32_t p, uint32_t s, uint32_t) {
-                if (p < n) {
-                    const uint32_t L = S.clen()[s], cd = S.code()[s];
-                    const uint32_t o = bp & 31, w = bp >> 5;
-                    if (w != cw) { if (acc) atomicOr(&bits[cw], acc); cw = w; acc = 0; }
-                    if (o + L <= 32) {
-                        acc |= cd << (32 - o - L);
-                    } else {
-                        acc |= cd >> (o + L - 32);
-                        atomicOr(&bits[cw], acc);
-                        cw = w + 1;
-                        acc = cd << (64 - o - L);
-                    }
-                    bp += L;
+        for (uint32_t w0 = 0; w0 < nbytes; w0 += CAPB) {
+            const uint32_t wl = min(CAPB, nbytes - w0);
+            const uint32_t B0 = 8 * w0, B1 = 8 * (w0 + wl);    // the window's stream bits
+            for (uint32_t w = lane; w < (wl + 3) / 4; w += 64) bits[w] = 0;
+            wave_sync();
+            uint32_t bitbase = 0;
+#pragma unroll 1
+            for (int r = 0; r < ROUNDS; r++) {
+                const uint32_t b0 = (uint32_t)(r * 64 + lane) * BS;
+                uint32_t my = 0;
+                for_block_bytes<BS>(ch, b0, GLLIM, [&](uint32_t p, uint32_t c, uint32_t) {
+                    if (p < n) my += S.clen()[c];
+                });
+                const uint32_t incl = wave_incl_sum(my);
+                const uint32_t tot = readlane(incl, 63);
+                uint32_t bp = bitbase + incl - my;
+                if (my && bp < B1 && bp + my > B0) {
+                    uint32_t cw = (max(bp, B0) - B0) >> 5, acc = 0;
+                    for_block_bytes<BS>(ch, b0, GLLIM, [&](uint32_t p, uint32_t sy, uint32_t) {
+                        if (p < n) {
+                            uint32_t L = S.clen()[sy], cd = S.code()[sy];
+                            const uint32_t e = bp + L;
+                            if (e > B0 && bp < B1) {
+                                uint32_t at = bp;
+                                if (bp < B0) { L = e - B0; cd &= (1u << L) - 1u; at = B0; }   // (the rest was the last window's)
+                                if (e > B1) { cd >>= e - B1; L -= e - B1; }                 // (the rest is the next window's)
+                                const uint32_t rel = at - B0, o = rel & 31, w = rel >> 5;
+                                if (w != cw) {
+                                    if (acc) atomicOr(&bits[cw], __builtin_bswap32(acc));
+                                    cw = w;
+                                    acc = 0;
+                                }
+                                if (o + L <= 32) {
+                                    acc |= cd << (32 - o - L);
+                                } else {
+                                    acc |= cd >> (o + L - 32);
+                                    atomicOr(&bits[cw], __builtin_bswap32(acc));
+                                    cw = w + 1;
+                                    acc = cd << (64 - o - L);
+                                }
+                            }
+                            bp = e;
+                        }
+                    });
+                    if (acc) atomicOr(&bits[cw], __builtin_bswap32(acc));
                 }
-            });
-            if (acc) atomicOr(&bits[cw], acc);
-            bitbase += readlane(incl, 63);
+                bitbase += tot;
+            }
+            nbits = bitbase;
+            wave_sync();
+            lds_store_bytes(pay + w0, reinterpret_cast<const uint8_t*>(bits), wl, lane);
+            wave_sync();
         }
-        if (gstage) __threadfence();
-        wave_sync();
-        if (lane < 4) slot[hb + lane] = (uint8_t)(bitbase >> (8 * lane));
-        for (uint32_t q = lane; q < nbytes; q += 64) {
-            const uint32_t w = gstage ? __hip_atomic_load(&bits[q >> 2], __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_AGENT)
-                                      : bits[q >> 2];
-            slot[hb + 4 + q] = (uint8_t)(w >> (24 - 8 * (q & 3)));
-        }
+        if (lane < 4) slot[hb + lane] = (uint8_t)(nbits >> (8 * lane));
     }
 
     STAMP(6);

@@ -14,16 +14,11 @@
 
 #include "../../include/ambc.h"
 #include "ambc_internal.h"
+#include "ambc_hostutil.h"
 #include "ambc_sync.h"
+#include "ambc_walkcore.h"
 
 namespace ambc {
-
-extern thread_local std::string g_err;
-
-inline int fail(int code, const std::string& msg) {
-    g_err = msg;
-    return code;
-}
 
 #define HIPCHK(expr)                                                                   \
     do {                                                                               \
@@ -38,22 +33,6 @@ inline int fail(int code, const std::string& msg) {
         if (_r != ncclSuccess)                                                         \
             return ::ambc::fail(AMBC_E_COMM, std::string(#expr) + ": " + ncclGetErrorString(_r)); \
     } while (0)
-
-inline bool trace_on() {
-    static int on = -1;
-    if (on < 0) on = getenv("AMBC_TRACE") ? 1 : 0;
-    return on == 1;
-}
-#define TRACE(...)                                                   \
-    do {                                                             \
-        if (::ambc::trace_on()) { fprintf(stderr, "[ambc] " __VA_ARGS__); fputc('\n', stderr); fflush(stderr); } \
-    } while (0)
-
-inline uint64_t now_ns() {
-    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
-               std::chrono::steady_clock::now().time_since_epoch())
-        .count();
-}
 
 struct Buf {
     void* p = nullptr;
@@ -153,12 +132,7 @@ struct Dev {
     Buf ms_ent;                 // the multi-size walk's entropy tables (one upload per call)
     uint64_t* hacc = nullptr;   // pinned: a pipelined call's statistics and body length, copied back once
     uint64_t ms_body = 0;       // a multi-size body kept in `ms_out` for ambc_fetch_body (0: none)
-    // the multi-size walk's position records, kept across calls (a fresh 40 KB page
-    // per 256 positions cost ~25 ms of page faults and construction per 256 MiB
-    // call): a record belongs to the call whose epoch it carries
-    std::vector<std::vector<uint8_t>> ms_pages;
-    size_t ms_rsz = 0;
-    uint32_t ms_epoch = 0;
+    WalkMemory ms_mem;          // the multi-size walk's position records, kept across calls (ambc_walkcore.h)
     uint64_t t_encode = 0, t_scan = 0, t_compact = 0;
     uint32_t n_launch = 1;      // k_encode launches of the last compress call (pipelined segments)
     hipStream_t cs = nullptr;   // scan + compaction of pipelined segments

@@ -147,3 +147,32 @@ def test_host_scorer_with_zstd_matches_oracle():
     finally:
         sc.close()
     assert 8 in wins
+
+
+def test_lzma_plugin_equals_python_lzma():
+    """LZMACompression.compress runs on kept liblzma encoders (methods._XZEncoders)
+    and must give exactly the bytes of the reference's call, Python's
+    lzma.LZMACompressor(FORMAT_XZ, CHECK_CRC64, LZMA2 with a 16 MiB dictionary)
+    (advanced_compression.py:163-182), for every input, from several threads at
+    once; on an exception it returns the input (:183-185)."""
+    import lzma
+    from concurrent.futures import ThreadPoolExecutor
+    from ambc.methods import LZMACompression, _XZEncoders
+
+    def ref(d):
+        c = lzma.LZMACompressor(format=lzma.FORMAT_XZ, check=lzma.CHECK_CRC64,
+                                filters=[{"id": lzma.FILTER_LZMA2, "dict_size": 1 << 24}])
+        return c.compress(d) + c.flush()
+
+    assert _XZEncoders.pool() is not None, "liblzma.so.5 path unavailable"
+    rng = np.random.default_rng(3)
+    text = synth.generate(200000, 9)
+    cases = [b"x", bytes(7), bytes(range(256)) * 64, synth.random_bytes(70000, 2)]
+    cases += [text[int(s):int(s) + int(n)] for s, n in zip(rng.integers(0, 60000, 24), rng.integers(1, 131072, 24))]
+    m = LZMACompression()
+    with ThreadPoolExecutor(12) as ex:
+        got = list(ex.map(m.compress, cases))
+    for d, g in zip(cases, got):
+        assert g == ref(d), len(d)
+    assert m.compress(b"") == b""
+    assert m.compress("not bytes") == "not bytes"          # the reference's except: return data
