@@ -14,3 +14,4 @@ done
 AMBC_LIB=$PWD/adaptive-compression_amd/ambc/libambc_hip_old.so timeout -k 10 200 python3 -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --api-bytes 0 --no-e2e --alt-methods "1,3,4" --walk-bytes 0 --ref-walk-bytes 0 --ref-full-walk-bytes 0 > $O/bench_old.json 2> $O/bench_old.err
 timeout -k 10 200 python3 -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --api-bytes 0 --no-e2e --alt-methods "1,3,4" --walk-bytes 0 --ref-walk-bytes 0 --ref-full-walk-bytes 0 > $O/bench_new.json 2> $O/bench_new.err
 timeout -k 10 300 python3 -u bench.py --steps 1 --warmup 0 --no-cpu-baseline --api-bytes 0 --no-e2e --alt-methods "" --walk-bytes 0 --ref-walk-bytes 0 --no-verify > $O/bench_fullwalk.json 2> $O/bench_fullwalk.err
+AMBC_TRACE=1 timeout -k 10 300 python3 -u bench.py --no-cpu-baseline --api-bytes 0 --no-e2e --no-verify --size 268435456 --alt-methods "" --ref-full-walk-bytes 0 --steps 1 --warmup 1 > $O/walktrace.json 2> $O/walktrace.err

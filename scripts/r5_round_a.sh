@@ -1,0 +1,22 @@
+#!/bin/bash
+# Round 5 pass A: the GPU suite on this library; same-box A/Bs of the Huffman
+# emitter (libambc_hip_old.so: the round's first commit) and of the zlib-9 pair
+# path (libambc_hip_exp.so: built with -DAMBC_Z9_PAIRS=0); the walk legs' host
+# breakdown (AMBC_TRACE); the full-set reference walk.  Each step under its own limit.
+set -e
+export TMPDIR=/tmp
+O=gpurun_out/r5a
+mkdir -p $O
+L=$PWD/adaptive-compression_amd/ambc
+timeout -k 10 700 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1
+for lib in old new; do
+  f=$L/libambc_hip.so; [ $lib = old ] && f=$L/libambc_hip_old.so
+  AMBC_LIB=$f timeout -k 10 200 python3 -u scripts/kbench.py --msets "1,3,4;1,3,4,9" --inputs zero,random,ascii,mixed --reps 3 > $O/kbench_huff_$lib.log 2>&1
+done
+for lib in nopairs pairs; do
+  f=$L/libambc_hip.so; [ $lib = nopairs ] && f=$L/libambc_hip_exp.so
+  AMBC_LIB=$f timeout -k 10 200 python3 -u scripts/kbench.py --msets "1,3,4,5" --flags 2 --inputs zero,random,ascii,mixed --reps 3 > $O/kbench_z9_$lib.log 2>&1
+done
+timeout -k 10 400 python3 -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --api-bytes 0 --no-e2e --alt-methods "1,3,4;1,3,4,5z" --walk-bytes 0 --ref-full-walk-bytes 0 > $O/bench.json 2> $O/bench.err
+AMBC_TRACE=1 timeout -k 10 300 python3 -u bench.py --no-cpu-baseline --api-bytes 0 --no-e2e --no-verify --size 268435456 --alt-methods "" --ref-full-walk-bytes 0 --steps 1 --warmup 1 > $O/walktrace.json 2> $O/walktrace.err
+timeout -k 10 300 python3 -u bench.py --steps 1 --warmup 0 --no-cpu-baseline --api-bytes 0 --no-e2e --alt-methods "" --walk-bytes 0 --ref-walk-bytes 0 --no-verify > $O/fullwalk.json 2> $O/fullwalk.err
