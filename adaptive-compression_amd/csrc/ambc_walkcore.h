@@ -683,10 +683,11 @@ int walk_decide(B& be, WalkMemory& mem, WalkPool& pool, const WalkConfig& cfg, u
         // from each, within BREADTH positions a round -- the next round then decides
         // at least two steps whatever size wins (breadth 0: off).  Budget: what
         // one round's latency hides, ~2048 chunks of 64 KiB ({1,2,3,4,5} 3.55-3.60 ->
-        // 3.79-3.80 GB/s, {1,3,4,9} unchanged); none with zlib-9, whose 64 KiB parse
-        // holds a CU per chunk (like_reference() 0.33 -> 0.20 GB/s with it,
-        // profiles/r4_breadth_ab)
-        const uint64_t BREADTH = cfg.breadth >= 0 ? (uint64_t)cfg.breadth : (z9walk ? 0 : 2048);
+        // 3.79-3.80 GB/s, {1,3,4,9} unchanged); with zlib-9, whose 64 KiB parse holds
+        // a CU per chunk, about one chunk per CU: 256 (like_reference() 0 / 128 / 256
+        // / 512 / 2048: 0.33 / 0.356 / 0.363 / 0.355 / 0.20 GB/s, profiles/r4_breadth_ab,
+        // r5_breadth_ab)
+        const uint64_t BREADTH = cfg.breadth >= 0 ? (uint64_t)cfg.breadth : (z9walk ? 256 : 2048);
         if (BREADTH && !G.active.empty() && G.active.size() * nc <= BREADTH) {
             const uint64_t per = BREADTH / G.active.size();
             for (const Walk& w : G.active) {

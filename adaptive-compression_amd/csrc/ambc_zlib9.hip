@@ -457,144 +457,6 @@ __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t
     }
 }
 
-// ---------------------------------------------------------------------------
-// The pair path (chunks of 4 and 8 KiB whose sort buckets hold at most Z9P_LIM
-// positions).  For such a chunk no hash chain reaches zlib's limits (1024 entries
-// after a good match, 4096 otherwise; MAX_DIST is beyond the chunk), so
-// longest_match(s) is fully determined by the chain's content: the longest match
-// among the earlier positions with s's three bytes (capped at min(258, n - s)),
-// the most recent of the longest -- a colliding hash's entries match fewer than
-// three bytes and never win.  Instead of walkers scanning chains per visited
-// position, every pair (c, s), c < s, of a bucket is compared once -- all pairs
-// of all buckets flattened over every lane of the workgroup, balanced -- and
-// table[s] = max(len << 16 | c) by LDS atomicMax; then every position's segment
-// (deflate_slow from a clean position: a literal, or the lazy chain's literals
-// and the match that ends it) is a few table lookups, for all positions at once.
-// The path from 0 is read off the segments as before.  A chunk with a larger
-// bucket (byte runs, short periods) keeps the walkers.
-#ifndef AMBC_Z9_PAIRS
-#define AMBC_Z9_PAIRS 1
-#endif
-constexpr uint32_t Z9P_LIM = 192;   // largest bucket of a pair-path chunk (<= 1024: no chain limit binds)
-template <int CMAX> struct Z9Pairs {
-    // the per-bucket pair prefix lives in slot[] (ZNB u32), unused on this path
-    static constexpr bool ok = AMBC_Z9_PAIRS && CMAX >= 4096 && CMAX <= 8192;
-};
-
-// the bucket pair counts' exclusive prefix into pre[] (u32 per bucket) and the
-// total into *tot; false when a bucket holds more than Z9P_LIM positions
-template <int CMAX>
-__device__ bool z9_pair_prefix(Z9Smem<CMAX>& S, uint32_t* pre, uint32_t* tot, uint32_t wave, uint32_t lane) {
-    if (wave == 0) {
-        constexpr uint32_t PER = ZNB / 64;
-        uint32_t sum = 0, big = 0;
-#pragma unroll 4
-        for (uint32_t t = 0; t < PER; t++) {
-            const uint32_t h = lane * PER + t;
-            const uint32_t m = (uint32_t)S.bend()[h] - S.bstart(h);
-            big |= m > Z9P_LIM;
-            sum += m * (m - 1) / 2;
-        }
-        uint32_t run = wave_incl_sum(sum) - sum;
-        const uint32_t total = readlane(run + sum, 63);
-        const bool any_big = __any(big != 0);
-#pragma unroll 4
-        for (uint32_t t = 0; t < PER; t++) {
-            const uint32_t h = lane * PER + t;
-            const uint32_t m = (uint32_t)S.bend()[h] - S.bstart(h);
-            pre[h] = run;
-            run += m * (m - 1) / 2;
-        }
-        if (lane == 0) *tot = any_big ? 0xFFFFFFFFu : total;
-    }
-    __syncthreads();
-    return *tot != 0xFFFFFFFFu;
-}
-
-// every pair (c, s) of every bucket: table[s] = max over c of min(len, nice) << 16 | c
-// for len >= 3 (table = seg[], zeroed)
-template <int CMAX>
-__device__ void z9_pair_table(Z9Smem<CMAX>& S, uint32_t n, const uint32_t* pre, uint32_t tot, uint32_t tid,
-                              uint32_t T) {
-    const uint32_t* c32 = reinterpret_cast<const uint32_t*>(S.ch);
-#pragma unroll 1
-    for (uint32_t p = tid; p < tot; p += T) {
-        // the bucket: the last with pre[h] <= p
-        uint32_t h = 0;
-#pragma unroll
-        for (uint32_t st = ZNB / 2; st; st >>= 1)
-            if (pre[h + st] <= p) h += st;
-        const uint32_t q = p - pre[h];
-        // q -> (i, j), i < j: q = j (j - 1) / 2 + i
-        uint32_t j = (uint32_t)((1.0f + sqrtf(1.0f + 8.0f * (float)q)) * 0.5f);
-        while (j * (j - 1) / 2 > q) j--;
-        while ((j + 1) * j / 2 <= q) j++;
-        const uint32_t i = q - j * (j - 1) / 2;
-        const uint32_t b0 = S.bstart(h);
-        const uint32_t c = S.lst[b0 + i], s = S.lst[b0 + j];   // c < s (ascending in a bucket)
-        const uint32_t nice = min(Z_MAXM, n - s);
-        uint32_t len = 0;
-        for (;;) {
-            const uint32_t ac = (c + len) >> 2, as = (s + len) >> 2, cs = (c + len) & 3u, ss = (s + len) & 3u;
-            uint32_t wc[5], ws[5];
-#pragma unroll
-            for (int t = 0; t < 5; t++) { wc[t] = c32[ac + t]; ws[t] = c32[as + t]; }
-            uint32_t f = ~0u;
-#pragma unroll
-            for (int t = 0; t < 4; t++)
-                f = min(f, ffbl_raw(__builtin_amdgcn_alignbyte(wc[t + 1], wc[t], cs) ^
-                                    __builtin_amdgcn_alignbyte(ws[t + 1], ws[t], ss)) | (uint32_t)t << 5);
-            if (f != ~0u) { len += f >> 3; break; }
-            len += 16;
-            if (len >= nice) break;
-        }
-        len = min(len, nice);
-        if (len >= 3) atomicMax(&S.seg[s], len << 16 | c);
-    }
-}
-
-// every position's segment from the table: deflate_slow from a clean q (the
-// walkers' state machine with table lookups for longest_match), into seg[] / sd[]
-template <int CMAX>
-__device__ void z9_pair_segments(Z9Smem<CMAX>& S, uint32_t n, uint32_t tid, uint32_t T) {
-    constexpr uint32_t PER = (uint32_t)CMAX / (64u * (uint32_t)Z9Cfg<CMAX>::NW);
-    uint32_t rec[PER], rd[PER];
-#pragma unroll
-    for (uint32_t k = 0; k < PER; k++) {
-        const uint32_t q = tid + k * T;
-        rec[k] = 0;
-        rd[k] = 0;
-        if (q >= n) continue;
-        uint32_t P = 2, Pd = 0, c = 0, s = q;
-        bool clean = true;
-#pragma unroll 1
-        for (;;) {
-            uint32_t ML = 2, MD = 0;
-            if (s >= 1 && s + 3 <= n && P < Z_MAXM) {
-                const uint32_t key = S.seg[s];
-                const uint32_t L = key >> 16, d = s - (key & 0xFFFFu);
-                if (L >= 3 && !(L == 3 && d > Z_TOOFAR)) { ML = L; MD = d; }
-            }
-            if (clean) {
-                if (ML < 3) { rec[k] = 0x80000000u | 1u; break; }
-                P = ML; Pd = MD; c = 0; s = q + 1; clean = false;
-            } else if (ML <= P) {
-                rec[k] = 0x80000000u | P << 16 | c;
-                rd[k] = Pd;
-                break;
-            } else {
-                c++; P = ML; Pd = MD; s++;
-            }
-        }
-    }
-    __syncthreads();   // (every lookup is done: the table becomes the segments)
-#pragma unroll
-    for (uint32_t k = 0; k < PER; k++) {
-        const uint32_t q = tid + k * T;
-        if (q < (uint32_t)CMAX) { S.seg[q] = rec[k]; S.sd[q] = (uint16_t)rd[k]; }
-    }
-}
-
 #ifdef AMBC_STAMPS
 // diagnostic build only: wave 0's phase cycles per parsed chunk in
 // A.stamps[(2 M + k) * 8 + phase] (k_dict's slots; phase 7 = 1 marks a parse)
@@ -646,27 +508,12 @@ __global__ __launch_bounds__(64 * Z9Cfg<CMAX>::NW) void k_z9_parse(EncArgs A) {
     PSTAMP(0);
     z9_sort(S, n - 2, wave, lane);
     for (uint32_t i = threadIdx.x; i < (uint32_t)CMAX; i += 64u * NW) S.seg[i] = 0;
-    bool paired = false;
-    if constexpr (Z9Pairs<CMAX>::ok) {
-        uint32_t* pre = reinterpret_cast<uint32_t*>(S.slot);   // (the walkers' slot[] is not used here)
-        if (z9_pair_prefix(S, pre, &S.nmatch, wave, lane)) {
-            paired = true;
-            z9_pair_table(S, n, pre, S.nmatch, threadIdx.x, 64u * NW);
-            __syncthreads();
-            PSTAMP(1);
-            z9_pair_segments(S, n, threadIdx.x, 64u * NW);
-            PSTAMP(2);
-            __syncthreads();
-        }
-    }
-    if (!paired) {
-        z9_literal_mask(S, n, wave, lane);
-        __syncthreads();
-        PSTAMP(1);
-        z9_walkers(S, n, wave, lane);
-        PSTAMP(2);
-        __syncthreads();
-    }
+    z9_literal_mask(S, n, wave, lane);
+    __syncthreads();
+    PSTAMP(1);
+    z9_walkers(S, n, wave, lane);
+    PSTAMP(2);
+    __syncthreads();
     PSTAMP(3);
     // ---- the path from 0.  Per 64-position window, pointer doubling over the
     // lanes gives every clean position's exit from the window (the first path

@@ -129,7 +129,6 @@ struct Z9BSmem {
     uint32_t litm[CMAX / 32];                          // the walk: positions that take no match (z9b_literal_mask)
     uint32_t runb[CHG ? 1 : CMAX / 32];                //   byte-run starts, and every position >= n (CHG: scratch)
     uint16_t wrs[CHG ? 1 : CMAX / 32];                 //   the run holding position 32 w starts here (CHG: scratch)
-    uint32_t wk[CMAX / 64 + 1];                        // the walk's estimated work per 64 positions -> prefix, total
     uint32_t bnd[8];                                   // block ends (boundary positions)
     uint32_t btop[8];                                  // the step top that flushed block b
     uint32_t nbnd, nmatch;
@@ -254,45 +253,13 @@ __device__ void z9b_literal_mask(Z9BSmem<CMAX>& S, uint32_t n, const uint16_t* s
             }
         }
         const uint64_t m = __ballot(lit);
-        const bool rs = p == 0 || p >= n || B8(p) != B8(p - 1);
-        const uint64_t rm = __ballot(rs);
-        // the walk's work at p, estimated: nothing for a match-less position (a
-        // run of them is one step), little inside a byte run (the run shortcut),
-        // else a search over its bucket's earlier entries, 8 a step
-        uint32_t cost = 0;
-        if (!lit) {
-            const bool inrun = !rs && p >= 2 && B8(p - 1) == B8(p - 2);
-            const uint32_t h = z_h15(gram(p));
-            cost = inrun ? 2u : 4u + min((uint32_t)slot[p] - S.bstart(z_bucket(h)), Z_CHAIN) / 8u;
-        }
-        cost = wave_sum_u32(cost);
+        const uint64_t rm = __ballot(p == 0 || p >= n || B8(p) != B8(p - 1));
         if (lane == 0) {
             S.litm[b >> 5] = (uint32_t)m; S.litm[(b >> 5) + 1] = (uint32_t)(m >> 32);
             runb[b >> 5] = (uint32_t)rm; runb[(b >> 5) + 1] = (uint32_t)(rm >> 32);
-            S.wk[b >> 6] = cost;
         }
     }
     __syncthreads();
-    if (wave == 1) {
-        // the work's exclusive prefix per 64 positions, the total at the end
-        constexpr uint32_t NB = (uint32_t)CMAX / 64, K = (NB + 63) / 64;
-        uint32_t v[K], t = 0;
-#pragma unroll
-        for (uint32_t i = 0; i < K; i++) {
-            const uint32_t x = lane * K + i;
-            v[i] = x < NB ? S.wk[x] : 0u;
-            t += v[i];
-        }
-        uint32_t run = wave_incl_sum(t) - t;
-        const uint32_t total = readlane(run + t, 63);
-#pragma unroll
-        for (uint32_t i = 0; i < K; i++) {
-            const uint32_t x = lane * K + i;
-            if (x < NB) S.wk[x] = run;
-            run += v[i];
-        }
-        if (lane == 0) S.wk[NB] = total;
-    }
     if (wave == 0) {
         constexpr uint32_t NWD = (uint32_t)CMAX / 32, K = (NWD + 63) / 64;
         int last = -1;
@@ -339,30 +306,7 @@ __device__ __forceinline__ void z9b_walkers(Z9BSmem<CMAX>& S, uint32_t n, const 
     // lookahead < 262 (65275 for a 65536-byte input); at s = 65274 a hash head of
     // 32768 reads as NIL (inputs < 65536 only: later heads that far are past MAX_DIST)
     const uint32_t nil_at = n < 65536u ? Z_SLIDE : 0xFFFFFFFFu;
-    // walker starts by the estimated work (S.wk, z9b_literal_mask): chains grow along
-    // a text chunk, and with even spacing the last waves' walkers scanned ~8x the
-    // first waves' chains while those waited
-    uint32_t q;
-    {
-        constexpr uint32_t NB = (uint32_t)CMAX / 64;
-        const uint32_t total = S.wk[NB];
-#ifdef AMBC_Z9B_EVEN
-        if (true) {   // (A/B build: even spacing)
-#else
-        if (total == 0 || wid == 0) {
-#endif
-            q = (uint32_t)(((uint64_t)n * wid) / NWK);
-        } else {
-            const uint32_t target = (uint32_t)(((uint64_t)total * wid) / NWK);
-            uint32_t bl = 0;
-#pragma unroll
-            for (uint32_t st = NB / 2; st; st >>= 1)
-                if (bl + st < NB && S.wk[bl + st] <= target) bl += st;
-            const uint32_t w0 = S.wk[bl], w1 = bl + 1 < NB ? S.wk[bl + 1] : total;
-            q = bl * 64 + (w1 > w0 ? (uint32_t)(((uint64_t)(target - w0) * 64) / (w1 - w0)) : 0u);
-            q = min(q, n);
-        }
-    }
+    uint32_t q = (uint32_t)(((uint64_t)n * wid) / NWK);
     uint32_t s = q, P = 2, Pd = 0, c = 0;
     bool clean = true, done = false;
 #pragma unroll 1
