@@ -1242,7 +1242,6 @@ static void inflate_all(const uint8_t* body, const std::vector<ambc_host_chunk>&
 // owning a contiguous range and two pinned buffers, overlap their own DMA with
 // the CPU copy of the previous piece; the host side (memcpy, and the first-touch
 // page faults of a freshly allocated output) runs on all T threads at once.
-constexpr size_t kStagePiece = 8u << 20;
 
 struct StageSet {
     std::vector<void*>* buf;
@@ -1273,7 +1272,7 @@ static int ensure_stage(Dev& d, unsigned T, int set = 0) {
     return AMBC_OK;
 }
 
-static unsigned stage_threads(uint64_t n, unsigned cap = 16) {
+unsigned ambc::stage_threads(uint64_t n, unsigned cap) {
     const char* e = getenv("AMBC_HOST_THREADS");
     unsigned t = e ? (unsigned)std::max(1, atoi(e)) : std::min(cap, std::thread::hardware_concurrency());
     return std::max(1u, std::min<unsigned>(t, (unsigned)(n / kStagePiece) + 1));
@@ -1343,58 +1342,12 @@ int ambc::copy_staged(Dev& d, void* dst, const void* src, uint64_t n, bool to_de
     return AMBC_OK;
 }
 
-// An upload in pieces taken in file order (piece q by thread q % T), each
-// marked done once its DMA has completed, so that a consumer can start on the
-// prefix [0, x) as soon as it has arrived (wait_prefix).
-struct OrderedUpload {
-    std::mutex m;
-    std::condition_variable cv;
-    std::vector<uint8_t> done;
-    uint64_t n = 0, ready = 0;     // ready: the leading pieces all done
-    bool failed = false;
-    std::vector<std::thread> th;
-    // registered mode: the caller's pages pinned piece by piece and copied by
-    // DMA (no staging copy); pieces [a, b) of the host range, their events
-    struct RegPiece { uintptr_t a, b; hipEvent_t ev; bool reg; };
-    std::vector<RegPiece> rp;
-    std::unique_ptr<std::atomic<int>[]> issued;   // piece j's DMA and event record are queued
-    Dev* dev = nullptr;
-    void mark(uint64_t q) {
-        std::lock_guard<std::mutex> lk(m);
-        done[q] = 1;
-        while (ready < done.size() && done[ready]) ready++;
-        cv.notify_all();
-    }
-    void fail_all() {
-        std::lock_guard<std::mutex> lk(m);
-        failed = true;
-        cv.notify_all();
-    }
-    // false when the upload failed
-    bool wait_prefix(uint64_t bytes) {
-        const uint64_t need = std::min<uint64_t>(done.size(), (bytes + kStagePiece - 1) / kStagePiece);
-        std::unique_lock<std::mutex> lk(m);
-        cv.wait(lk, [&] { return failed || ready >= need; });
-        return !failed;
-    }
-    void join() { for (auto& x : th) if (x.joinable()) x.join(); th.clear(); }
-    // registered mode: after join(), wait for the DMAs and unpin
-    void release() {
-        join();
-        for (auto& p : rp) {
-            if (p.ev) { (void)hipEventSynchronize(p.ev); (void)hipEventDestroy(p.ev); p.ev = nullptr; }
-            if (p.reg) { (void)hipHostUnregister(reinterpret_cast<void*>(p.a)); p.reg = false; }
-        }
-    }
-    ~OrderedUpload() { release(); }
-};
-
 // The registered upload: one helper thread pins the body piece by piece (4 KiB
 // aligned interior; the unaligned head and tail bytes are copied first) and
 // queues each piece's DMA on its own stream; a piece counts as done once its
 // DMA's event has fired (a waiter thread marks them in order).  A piece the
 // runtime refuses to pin goes through a staging buffer copy instead.
-static int start_registered_upload(Dev& d, uint8_t* dst, const uint8_t* src, uint64_t n, OrderedUpload& u) {
+int ambc::start_registered_upload(Dev& d, uint8_t* dst, const uint8_t* src, uint64_t n, OrderedUpload& u) {
     constexpr uint64_t PIECE = 64ull << 20;
     const uintptr_t PG = 4096, sb = (uintptr_t)src, se = sb + n;
     const uintptr_t ra = (sb + PG - 1) & ~(PG - 1), rb = se & ~(PG - 1);
@@ -1446,7 +1399,7 @@ static int start_registered_upload(Dev& d, uint8_t* dst, const uint8_t* src, uin
     return AMBC_OK;
 }
 
-static int start_ordered_upload(Dev& d, uint8_t* dst, const uint8_t* src, uint64_t n, unsigned T, OrderedUpload& u) {
+int ambc::start_ordered_upload(Dev& d, uint8_t* dst, const uint8_t* src, uint64_t n, unsigned T, OrderedUpload& u) {
     int rc = ensure_stage(d, T, 0);
     if (rc) return rc;
     const uint64_t np = (n + kStagePiece - 1) / kStagePiece;

@@ -5,6 +5,10 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <memory>
+#include <thread>
 #include <chrono>
 #include <mutex>
 #include <cstdio>
@@ -185,6 +189,66 @@ uint64_t slab_bytes();                                 // host-fed pipelines' sl
 // large pageable <-> device copies through pinned staging buffers on T threads
 constexpr uint64_t kStageMin = 64ull << 20;            // below this the runtime's own path
 int copy_staged(Dev& d, void* dst, const void* src, uint64_t n, bool to_dev, int set = 0, unsigned cap = 16);
+
+constexpr size_t kStagePiece = 8u << 20;               // staged copies' piece
+unsigned stage_threads(uint64_t n, unsigned cap = 16);
+
+// An upload in pieces taken in file order (piece q by thread q % T), each
+// marked done once its DMA has completed, so that a consumer can start on the
+// prefix [0, x) as soon as it has arrived (wait_prefix).
+struct OrderedUpload {
+    std::mutex m;
+    std::condition_variable cv;
+    std::vector<uint8_t> done;
+    uint64_t n = 0, ready = 0;     // ready: the leading pieces all done
+    bool failed = false;
+    std::vector<std::thread> th;
+    // registered mode: the caller's pages pinned piece by piece and copied by
+    // DMA (no staging copy); pieces [a, b) of the host range, their events
+    struct RegPiece { uintptr_t a, b; hipEvent_t ev; bool reg; };
+    std::vector<RegPiece> rp;
+    std::unique_ptr<std::atomic<int>[]> issued;   // piece j's DMA and event record are queued
+    Dev* dev = nullptr;
+    void mark(uint64_t q) {
+        std::lock_guard<std::mutex> lk(m);
+        done[q] = 1;
+        while (ready < done.size() && done[ready]) ready++;
+        cv.notify_all();
+    }
+    void fail_all() {
+        std::lock_guard<std::mutex> lk(m);
+        failed = true;
+        cv.notify_all();
+    }
+    // bytes [0, avail()) are on the device
+    uint64_t avail() {
+        std::lock_guard<std::mutex> lk(m);
+        return ready >= done.size() ? n : ready * kStagePiece;
+    }
+    // false when the upload failed
+    bool wait_prefix(uint64_t bytes) {
+        const uint64_t need = std::min<uint64_t>(done.size(), (bytes + kStagePiece - 1) / kStagePiece);
+        std::unique_lock<std::mutex> lk(m);
+        cv.wait(lk, [&] { return failed || ready >= need; });
+        return !failed;
+    }
+    void join() { for (auto& x : th) if (x.joinable()) x.join(); th.clear(); }
+    // registered mode: after join(), wait for the DMAs and unpin
+    void release() {
+        join();
+        for (auto& p : rp) {
+            if (p.ev) { (void)hipEventSynchronize(p.ev); (void)hipEventDestroy(p.ev); p.ev = nullptr; }
+            if (p.reg) { (void)hipHostUnregister(reinterpret_cast<void*>(p.a)); p.reg = false; }
+        }
+    }
+    ~OrderedUpload() { release(); }
+};
+
+// an ordered upload of n bytes from host src to device dst: the caller's pages
+// pinned and copied by DMA piece by piece (start_registered_upload), or through
+// the pinned staging buffers on T threads (start_ordered_upload)
+int start_registered_upload(Dev& d, uint8_t* dst, const uint8_t* src, uint64_t n, OrderedUpload& u);
+int start_ordered_upload(Dev& d, uint8_t* dst, const uint8_t* src, uint64_t n, unsigned T, OrderedUpload& u);
 
 // collective of the sharded calls (ambc_shard.cpp)
 int shard_allreduce_min(Transport* t, uint64_t* v, int rc_local);

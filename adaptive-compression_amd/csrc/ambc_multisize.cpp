@@ -201,23 +201,21 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
     };
     // the input, uploaded once (64 bytes of slack for the encoders' padded loads)
     HIPCHK(d.in.ensure(n + 64));
-    // (a large upload runs on a thread of its own while the first round is planned;
-    // the first launch waits for it)
-    std::thread upload;
-    int upload_rc = AMBC_OK;
-    struct Joiner {
-        std::thread& t;
-        ~Joiner() { if (t.joinable()) t.join(); }
-    } upload_join{upload};
-    auto await_upload = [&]() -> int {
-        if (upload.joinable()) upload.join();
-        return upload_rc;
-    };
+    // (a large upload runs in ordered pieces beside the walk: its first rounds take
+    // the walks whose chunks have arrived, the others as the pieces come in; the
+    // final encode waits for all of it)
+    std::unique_ptr<OrderedUpload> up;
     if (n >= kStageMin) {
-        upload = std::thread([&] { upload_rc = copy_staged(d, d.in.p, in, n, true, 0, 8); });
+        up.reset(new OrderedUpload());
+        if (int rc = start_ordered_upload(d, d.in.as<uint8_t>(), in, n, stage_threads(n, 8), *up)) return rc;
     } else if (n) {
         HIPCHK(hipMemcpyAsync(d.in.p, in, n, hipMemcpyHostToDevice, s));
     }
+    auto await_upload = [&]() -> int {
+        if (up && !up->wait_prefix(n)) return fail(AMBC_E_DEVICE, "input upload failed");
+        if (up) up->join();
+        return AMBC_OK;
+    };
     HIPCHK(hipMemsetAsync(d.in.as<uint8_t>() + n, 0, 64, s));
     const uint8_t* d_in = d.in.as<uint8_t>();
 
@@ -237,7 +235,7 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
         const uint8_t* d_in;
         uint64_t n;
         std::function<const double*(uint32_t)> ent_of;
-        std::function<int()> await;
+        OrderedUpload* up;
         int launch(int slot, const ambc_params* pk, uint32_t sz, const uint64_t* pos, uint32_t cnt,
                    const uint32_t* subc, uint32_t nsub) {
             Batch& bb = d.msb[slot];
@@ -252,9 +250,17 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
             *lz = d.msb[slot].hlz;
             return AMBC_OK;
         }
-        int await_upload() { return await(); }
+        bool whole;   // AMBC_MS_UPLOAD_FIRST: the walk starts after the whole upload (A/B, tests)
+        uint64_t avail() {
+            if (up && whole) (void)up->wait_prefix(n);
+            return up ? up->avail() : n;
+        }
+        int wait_avail(uint64_t want) {
+            if (up && !up->wait_prefix(std::min(want, n))) return fail(AMBC_E_DEVICE, "input upload failed");
+            return AMBC_OK;
+        }
         int check_size(const ambc_params* pk, uint32_t sz) { return ::ambc::check_size(pk, sz); }
-    } be{d, d_in, n, ent_of, await_upload};
+    } be{d, d_in, n, ent_of, up.get(), getenv("AMBC_MS_UPLOAD_FIRST") != nullptr};
     static const WalkConfig cfg = WalkConfig::from_env();
     WalkOutcome wo;
     if (int rc = walk_decide(be, d.ms_mem, WalkPool::get(), cfg, n, p, cands, hc, wo)) return rc;

@@ -234,7 +234,10 @@ struct WalkOutcome {
 //   int finish(int slot, const uint32_t** plen, const uint8_t** ids, const uint32_t** lz)
 //       wait for slot's batch: per chunk the payload length, the winning id (255:
 //       raw) and lz[q * LZ4_SUB_MAX + j] (prefix j's block, 0xFFFFFFFF: LZ4 gave up)
-//   int await_upload()   the input is where the batches read it (before the first launch)
+//   uint64_t avail()     input bytes a batch may read: [0, avail()) is uploaded (n: all);
+//                        a chunk [pos, pos + s) is launched once pos + s + 64 <= avail()
+//                        or avail() == n, else its request waits for a later round
+//   int wait_avail(uint64_t want)   block until avail() >= min(want, n)
 //   int check_size(const ambc_params* p, uint32_t s)   AMBC_OK when the encoders take
 //       an s-byte chunk with p's eligible methods
 // Returns AMBC_OK with the walk from 0 in `out`, or the error code (g_err set).
@@ -530,7 +533,6 @@ int walk_decide(B& be, WalkMemory& mem, WalkPool& pool, const WalkConfig& cfg, u
         out.wait_ns += now_ns() - tk;
         return AMBC_OK;
     };
-    bool uploaded = false;
     // decide as far as known, then ask for the next positions and launch
     auto advance = [&](Group& G) -> int {
         uint64_t tq = now_ns();
@@ -705,7 +707,29 @@ int walk_decide(B& be, WalkMemory& mem, WalkPool& pool, const WalkConfig& cfg, u
             }
         }
         std::vector<Job> jobs;
+        // the input arrives in pieces (the backend's upload): chunks not all there yet
+        // are forgotten like refused speculative ones and asked for again later (a
+        // walk asks for its own position every round)
+        const uint64_t av = be.avail();
+        uint64_t need = ~0ull;     // the smallest input end a forgotten request needs
+        auto forget = [&](const std::pair<uint32_t, int>& key, uint64_t q) {
+            const Sizes& z = sizes_at(q);
+            PosTable::Rec& rec = T.at(q);
+            if (key.second == 1) rec.mreq = 0;
+            for (uint32_t i = 0; i < nc; i++)
+                if (z.S[i] == key.first) rec.req &= ~(1u << i);
+        };
         for (auto& r : req) {
+            if (av < n) {
+                size_t k = 0;
+                for (uint64_t q : r.second) {
+                    if (q + r.first.first + 64 <= av) { r.second[k++] = q; continue; }
+                    forget(r.first, q);
+                    need = std::min<uint64_t>(need, q + r.first.first + 64);
+                }
+                r.second.resize(k);
+                if (!k) continue;
+            }
             const ambc_params* pk = r.first.second == 1 || !lzshare ? p : &po;
             if (int rc = be.check_size(pk, r.first.first)) {
                 // only an error if a walk itself needs this size (not a speculative position)
@@ -714,13 +738,7 @@ int walk_decide(B& be, WalkMemory& mem, WalkPool& pool, const WalkConfig& cfg, u
                                            [](const Walk& x, const Walk& y) { return x.pos < y.pos; }))
                         return rc;
                 // speculative only: never decided from -- forget the requests
-                for (uint64_t q : r.second) {
-                    const Sizes& z = sizes_at(q);
-                    PosTable::Rec& rec = T.at(q);
-                    if (r.first.second == 1) rec.mreq = 0;
-                    for (uint32_t i = 0; i < nc; i++)
-                        if (z.S[i] == r.first.first) rec.req &= ~(1u << i);
-                }
+                for (uint64_t q : r.second) forget(r.first, q);
                 continue;
             }
             jobs.emplace_back(r.first, std::move(r.second));
@@ -735,10 +753,9 @@ int walk_decide(B& be, WalkMemory& mem, WalkPool& pool, const WalkConfig& cfg, u
         // up to 8 batches at once, each on its own slot; more than 8: the earlier
         // ones are finished here, the last 8 fly
         const uint64_t tk = now_ns();
-        if (!jobs.empty() && !uploaded) {
-            if (int rc = be.await_upload()) return rc;
-            uploaded = true;
-        }
+        // nothing to launch but requests waiting for the input: wait for it
+        if (jobs.empty() && need != ~0ull && G.flight.empty())
+            if (int rc = be.wait_avail(need)) return rc;
         for (size_t j0 = 0; j0 < jobs.size(); j0 += 8) {
             const size_t j1 = std::min(jobs.size(), j0 + 8);
             const uint64_t tl = now_ns();

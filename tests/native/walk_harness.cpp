@@ -239,7 +239,19 @@ struct SynthBackend {
         *lz = slots[slot].lz.data();
         return AMBC_OK;
     }
-    int await_upload() { return AMBC_OK; }
+    // the input arrives in pieces: every call sees `step` more bytes (0: all at once)
+    uint64_t step = 0, av = 0;
+    uint64_t avail() {
+        if (!step) return m.n;
+        const uint64_t a = std::min(av, m.n);
+        av += step;
+        return a;
+    }
+    int wait_avail(uint64_t want) {
+        if (want > m.n) want = m.n;
+        if (av < want) av = want;
+        return AMBC_OK;
+    }
     int check_size(const ambc_params* pk, uint32_t s) {
         if (refuse_dict_above && ms_eligible(pk, s, AMBC_M_DICT) && s > refuse_dict_above)
             return fail(AMBC_E_INVAL, "refused size");
@@ -349,6 +361,8 @@ static void test_walks(unsigned T) {
                 const auto want = serial_walk(m, &p, cand_lists[ci], ms.host);
                 for (const WalkConfig& cfg : cfgs) {
                     SynthBackend be{m};
+                    // (every other configuration: the input arriving in pieces)
+                    if ((&cfg - cfgs) % 2 == 1) be.step = std::max<uint64_t>(4096, n / 7);
                     HostCtx hctx{&m, &p};
                     ambc_host_codecs hc{host_eval, host_emit, &hctx};
                     WalkOutcome wo;

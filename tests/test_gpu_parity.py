@@ -4,12 +4,13 @@ import ctypes as C
 import hashlib
 import json
 import os
+import sys
 import random
 
 import numpy as np
 import pytest
 
-from conftest import GOLDEN, load_golden
+from conftest import GOLDEN, REPO, load_golden
 from oracle import oracle as orc
 from oracle import synth
 
@@ -829,6 +830,25 @@ def test_multisize_refused_size_near_the_end_fails_not_hangs(ctx):
             body = comp._adaptive_compress(data)
         except NotImplementedError:
             continue
+        assert comp._adaptive_decompress(body, len(data)) == data
+
+
+def test_multisize_walk_as_the_input_arrives(ctx, monkeypatch):
+    """A walk over >= 64 MiB starts while the input is still uploading (ordered
+    8 MiB pieces: a chunk is evaluated once its bytes have arrived, the others are
+    asked for again later): the body equals the walk that starts after the whole
+    upload (AMBC_MS_UPLOAD_FIRST), and decodes."""
+    sys.path.insert(0, os.path.join(REPO, "scripts"))
+    from multisize_bench import mixed
+    data = mixed(72 << 20, 17)
+    for methods in ((1, 3, 4, 9), (1, 2, 3, 4, 5)):
+        comp = _compressor(methods=methods)
+        comp.CHUNK_SIZE_CANDIDATES = list(REF_CANDS)
+        monkeypatch.delenv("AMBC_MS_UPLOAD_FIRST", raising=False)
+        body = comp._adaptive_compress(data)
+        monkeypatch.setenv("AMBC_MS_UPLOAD_FIRST", "1")
+        assert comp._adaptive_compress(data) == body, methods
+        monkeypatch.delenv("AMBC_MS_UPLOAD_FIRST")
         assert comp._adaptive_decompress(body, len(data)) == data
 
 
