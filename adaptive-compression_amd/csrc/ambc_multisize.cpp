@@ -204,10 +204,25 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
     // (a large upload runs in ordered pieces beside the walk: its first rounds take
     // the walks whose chunks have arrived, the others as the pieces come in; the
     // final encode waits for all of it)
+    // AMBC_MS_UPLOAD (A/B): "staged" -- pinned staging buffers on 8 threads beside
+    // the walk; "registered" -- the caller's pages pinned piece by piece and copied
+    // by DMA from one thread (few runtime calls beside the walk's launches), staged
+    // where the runtime refuses to pin; "first" -- the walk after the whole upload.
+    // Default, measured on 256 MiB (profiles/r5_upload_ab): registered where every
+    // size runs its own encoders ({1,2,3,4,5} 4.91-5.03 -> 4.99-5.16 GB/s), first with
+    // LZ4 among the methods, whose walk asks six positions ahead and loses more to
+    // the forgotten requests than the overlap gains ({1,3,4,9} 6.17-6.22 vs 5.26-5.88)
+    static const char* upenv = getenv("AMBC_MS_UPLOAD");
+    const char* upmode = upenv ? upenv : ((p->method_mask >> AMBC_M_LZ4) & 1) ? "first" : "registered";
     std::unique_ptr<OrderedUpload> up;
     if (n >= kStageMin) {
         up.reset(new OrderedUpload());
-        if (int rc = start_ordered_upload(d, d.in.as<uint8_t>(), in, n, stage_threads(n, 8), *up)) return rc;
+        int rc = strcmp(upmode, "registered") ? AMBC_E_INVAL
+                                              : start_registered_upload(d, d.in.as<uint8_t>(), in, n, *up);
+        if (rc) {
+            up.reset(new OrderedUpload());
+            if ((rc = start_ordered_upload(d, d.in.as<uint8_t>(), in, n, stage_threads(n, 8), *up))) return rc;
+        }
     } else if (n) {
         HIPCHK(hipMemcpyAsync(d.in.p, in, n, hipMemcpyHostToDevice, s));
     }
@@ -243,6 +258,7 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
             std::memcpy(bb.hpos, pos, (size_t)cnt * 8);
             return launch_batch(bb, d.mss[slot], d_in, n, pk, sz, bb.hpos, cnt, ent_of(sz), true, subc, nsub);
         }
+        bool ready(int slot) { return hipStreamQuery(d.mss[slot]) != hipErrorNotReady; }
         int finish(int slot, const uint32_t** plen, const uint8_t** ids, const uint32_t** lz) {
             HIPCHK(hipStreamSynchronize(d.mss[slot]));
             *plen = d.msb[slot].hplen;
@@ -260,7 +276,7 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
             return AMBC_OK;
         }
         int check_size(const ambc_params* pk, uint32_t sz) { return ::ambc::check_size(pk, sz); }
-    } be{d, d_in, n, ent_of, up.get(), getenv("AMBC_MS_UPLOAD_FIRST") != nullptr};
+    } be{d, d_in, n, ent_of, up.get(), getenv("AMBC_MS_UPLOAD_FIRST") != nullptr || !strcmp(upmode, "first")};
     static const WalkConfig cfg = WalkConfig::from_env();
     WalkOutcome wo;
     if (int rc = walk_decide(be, d.ms_mem, WalkPool::get(), cfg, n, p, cands, hc, wo)) return rc;

@@ -231,6 +231,7 @@ struct WalkOutcome {
 //       evaluate the size-`size` chunks at pos[0..cnt) with p's methods on batch slot
 //       `slot` (0..15; <= 8 in flight; nsub > 0: also the LZ4 block of every prefix
 //       subc[j] below size); pos is only read during the call
+//   bool ready(int slot)  slot's batch is done (no wait)
 //   int finish(int slot, const uint32_t** plen, const uint8_t** ids, const uint32_t** lz)
 //       wait for slot's batch: per chunk the payload length, the winning id (255:
 //       raw) and lz[q * LZ4_SUB_MAX + j] (prefix j's block, 0xFFFFFFFF: LZ4 gave up)
@@ -524,11 +525,24 @@ int walk_decide(B& be, WalkMemory& mem, WalkPool& pool, const WalkConfig& cfg, u
         out.t_fill += now_ns() - tl;
         return AMBC_OK;
     };
-    // the group's batches in flight: wait and take their results
+    // the group's batches in flight: their results as they come (a small size's
+    // batch fills the table while the round's largest -- launched first, on the
+    // high-priority slot -- still runs)
     auto complete = [&](Group& G) -> int {
         const uint64_t tk = now_ns();
-        for (size_t j = 0; j < G.flight.size(); j++)
-            if (int rc = finish_job(G.flight[j], G.slot0 + (int)j)) return rc;
+        std::vector<uint8_t> done(G.flight.size(), 0);
+        size_t left = G.flight.size();
+        while (left) {
+            bool any = false;
+            for (size_t j = 0; j < G.flight.size(); j++) {
+                if (done[j] || (left > 1 && !be.ready(G.slot0 + (int)j))) continue;
+                if (int rc = finish_job(G.flight[j], G.slot0 + (int)j)) return rc;
+                done[j] = 1;
+                left--;
+                any = true;
+            }
+            if (!any) std::this_thread::yield();
+        }
         G.flight.clear();
         out.wait_ns += now_ns() - tk;
         return AMBC_OK;
@@ -743,6 +757,10 @@ int walk_decide(B& be, WalkMemory& mem, WalkPool& pool, const WalkConfig& cfg, u
             }
             jobs.emplace_back(r.first, std::move(r.second));
         }
+        // (requests forgotten for the input: every walk asks its whole guess chain
+        // again next round, so that its speculation resumes once the bytes are there)
+        if (need != ~0ull)
+            for (Walk& w : G.active) w.cs = 0;
         // the largest size first (slot 0, the high-priority stream)
         if (!cfg.noprio)
             std::stable_sort(jobs.begin(), jobs.end(), [](const Job& a, const Job& b) {
