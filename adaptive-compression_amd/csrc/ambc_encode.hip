@@ -580,6 +580,9 @@ __global__ __launch_bounds__(64) AMBC_ENC_ATTR void k_encode(EncArgs A) {
             if (lane == 0) A.lz4sub[(uint64_t)k * LZ4_SUB_MAX + sj] = emitted + add + 1 + ext_len(fl) + fl;
             sj++;
         };
+        // each round's four bytes per position are loaded a round ahead, behind the
+        // candidate read (the in-order load counter then waits on both at once)
+        uint32_t vpre = mlim >= 0 ? lds_rd32(ch, lane) : 0u;
 #pragma unroll 1
         for (int base = 0; base <= mlim && (alive || sj < sj_end); base += 64) {
             // control state is wave-uniform: keep it in SGPRs
@@ -589,7 +592,7 @@ __global__ __launch_bounds__(64) AMBC_ENC_ATTR void k_encode(EncArgs A) {
             const int i = base + (int)lane;
             const bool act = i <= mlim;
             // loads run for every lane (past n: padding / work[] bytes of inactive lanes)
-            const uint32_t v = lds_rd32(ch, (uint32_t)i);
+            const uint32_t v = vpre;
             const uint32_t h = (v * 2654435761u) >> (32 - LZ4_HASH_BITS);
             // candidate: the last earlier 64-position window's position with my hash
             int cand = (int)last[h] - 1;
@@ -607,6 +610,7 @@ __global__ __launch_bounds__(64) AMBC_ENC_ATTR void k_encode(EncArgs A) {
             // the window's highest position per hash (the reads above see earlier windows only)
             atomicMax(&last[h], (uint32_t)i + 1u);
             const uint32_t cv = lds_rd32(ch, (uint32_t)max(cand, 0));
+            if (base + 64 <= mlim) vpre = lds_rd32(ch, (uint32_t)i + 64u);
             const bool valid = act && cand >= 0 && cv == v;
             const uint64_t vm = __ballot(valid);
             wave_sync();

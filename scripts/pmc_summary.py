@@ -6,8 +6,12 @@
 * HBM traffic of k_encode per launch from the two PMC passes (FETCH_SIZE and
   WRITE_SIZE cannot share a pass on gfx950), with the MI355X_MICROARCH.md
   correction: FETCH_SIZE counts half the bytes of 16-B-per-lane streaming
-  reads (k_encode's loads are global_load_dwordx4), so it is doubled;
-  WRITE_SIZE is taken as is.  Both counters are in KiB.
+  reads, so it is doubled.  Round 5 calibrated the other widths the encoder
+  uses (profiles/r5_pmc_calibration.json, scripts/pmc_calib.hip): every read
+  reaches EA as 128-B requests, which FETCH_SIZE's expression counts as 64 B
+  (its TCC_BUBBLE term stays 0 on gfx950), so the doubling holds for dword,
+  byte and unaligned reads too; WRITE_SIZE is exact (+2 % for byte stores)
+  and taken as is.  Both counters are in KiB.
   -> profiles/pmc_<round>.json (read by bench.py for roofline.traffic)
 """
 import argparse
@@ -64,7 +68,7 @@ def main():
                "fetch_size_kib_raw": f_kib, "write_size_kib": w_kib,
                "fetch_bytes_corrected": f_kib * 1024 * 2, "write_bytes": w_kib * 1024,
                "hbm_bytes_per_launch": int(f_kib * 1024 * 2 + w_kib * 1024),
-               "note": "FETCH_SIZE x2 (gfx950: 16-B-per-lane streaming reads count half), "
+               "note": "FETCH_SIZE x2 (gfx950: 128-B read requests count half, every width; profiles/r5_pmc_calibration.json), "
                        "separate --pmc passes, median over launches"}
         # whole compress call: every kernel of the call (encode, scan, segment
         # bases, compaction, stats, end chunk, fills/copies), per call
