@@ -566,11 +566,15 @@ __global__ __launch_bounds__(64) AMBC_ENC_ATTR void k_encode(EncArgs A) {
         wave_sync();
         // LZ4 wins iff block < budget; forced (single-method) encodes fall back to a
         // stored block once the compressed block would reach n (LZ4F rule)
-        const uint32_t budget = force ? n : best - 41;
-        const int mlim = (int)n - 12;       // last position a match may start; <0: none
+        // (the walk's control values are wave-uniform; said so explicitly, the loop
+        // compiles to scalar branches instead of exec-mask bookkeeping per round)
+        const uint32_t budget = __builtin_amdgcn_readfirstlane(force ? n : best - 41);
+        const int mlim = __builtin_amdgcn_readfirstlane((int)n - 12);   // last match start; <0: none
         uint8_t* blk = slot + 19;
         uint32_t emitted = 0, anchor = 0, nextp = 0;
-        bool alive = lz4_main;              // the chunk's own LZ4 can still win
+        bool alive = __builtin_amdgcn_readfirstlane((int)lz4_main) != 0;   // its own LZ4 can still win
+        sj = __builtin_amdgcn_readfirstlane(sj);
+        sj_end = __builtin_amdgcn_readfirstlane(sj_end);
         constexpr uint32_t LCAP = 16;       // per-lane precomputed match length cap
         // prefix sub_c[sj] is done: its block = emitted + add (this round's sequences
         // that start by b - 12) + the final literals from endp
