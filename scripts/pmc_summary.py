@@ -54,6 +54,7 @@ def main():
     ap.add_argument("--fetch")
     ap.add_argument("--write")
     ap.add_argument("--bench")
+    ap.add_argument("--req", help="pass with TCC_EA0_RDREQ_{32B,64B,128B}_sum: EA read bytes per request size")
     args = ap.parse_args()
     out = os.path.join(REPO, "profiles")
     os.makedirs(out, exist_ok=True)
@@ -83,6 +84,14 @@ def main():
                                                                          round(wk.get(k, 0) / calls)]
                                                 for k in sorted(set(fk) | set(wk))
                                                 if not any(x in k for x in skip)}}
+        if args.req:
+            # the same traffic from the read requests by size (no FETCH_SIZE correction)
+            q = {n: counter(args.req, n) for n in ("TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum",
+                                                   "TCC_EA0_RDREQ_128B_sum")}
+            per = [32 * a + 64 * b + 128 * c for a, b, c in zip(q["TCC_EA0_RDREQ_32B_sum"], q["TCC_EA0_RDREQ_64B_sum"],
+                                                                 q["TCC_EA0_RDREQ_128B_sum"])]
+            rec["fetch_bytes_from_requests"] = int(statistics.median(per))
+            rec["fetch_check"] = "k_encode EA read bytes from TCC_EA0_RDREQ_{32B,64B,128B} x size, median over launches"
         if args.bench:
             with open(args.bench) as fh:
                 b = json.loads(fh.read().strip().splitlines()[-1])
