@@ -270,20 +270,32 @@ __global__ __launch_bounds__(64) AMBC_ENC_ATTR void k_encode(EncArgs A) {
     const bool fast_samples = step == 4;
     uint32_t pairs = 0, samp = 0, dsamp = 0;
     int rs_carry = -1;
-    const uint32_t* c32 = reinterpret_cast<const uint32_t*>(ch);
+    uint32_t pw_carry = 0;      // the previous round's last dword (lane 63's block end)
 #pragma unroll 1
     for (int r = 0; r < (need_a ? ROUNDS : 0); r++) {
         const uint32_t b0 = (uint32_t)(r * 64 + lane) * BS;
-        // (GL: a lane block starting at or past n reads nothing -- its bytes are all
-        // masked, and past n + 64 the input may end)
-        const bool rd = !GL || b0 < n;
+        // (GL: a lane block starting at or past n is masked by nv below -- its load
+        // is clamped to the last 16-aligned BS bytes the 64-byte input padding covers)
+        // The block's 16-byte loads issue together and unconditionally, ahead of the
+        // LDS atomics (which the compiler will not move loads across): the chunk's
+        // first read from HBM waits one latency, not one per piece, and no other
+        // load precedes it -- the run byte is the block's first, the previous
+        // word the previous lane's last (lane 0: the previous round's lane 63)
+        const uint32_t ab = GL ? min(b0, (n + 64u - (uint32_t)BS) & ~15u) : b0;
+        uint4 pv[BS / 16];
+#pragma unroll
+        for (int q = 0; q < BS / 16; q++)   // (a masked block's bytes are never counted)
+            pv[q] = *reinterpret_cast<const uint4*>(ch + ab + 16 * q);
+        const uint32_t lastw = pv[BS / 16 - 1].w;
         // previous byte; position 0 always starts a run (the reference's prev = None)
-        uint32_t pw = b0 ? (rd ? c32[(b0 >> 2) - 1] : 0u) : ~((uint32_t)ch[0] << 24);
+        uint32_t pw = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane + 63u) & 63u) << 2), (int)lastw);
+        if (lane == 0) pw = r ? pw_carry : ~((pv[0].x & 0xFFu) << 24);
+        pw_carry = readlane(lastw, 63);
         int lb = -1, fc = -1;
-        uint32_t starts = 0, cur = rd ? ch[b0] : 0u, rc = 0;
-#pragma unroll 1
+        uint32_t starts = 0, cur = pv[0].x & 0xFFu, rc = 0;
+#pragma unroll
         for (int q = 0; q < BS / 16; q++) {
-            const uint4 v4 = rd ? *reinterpret_cast<const uint4*>(ch + b0 + 16 * q) : make_uint4(0, 0, 0, 0);
+            const uint4 v4 = pv[q];
             const uint32_t wv[4] = {v4.x, v4.y, v4.z, v4.w};
 #pragma unroll
             for (int e = 0; e < 4; e++) {
