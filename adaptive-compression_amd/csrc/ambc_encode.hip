@@ -486,13 +486,20 @@ __global__ __launch_bounds__(64) AMBC_ENC_ATTR void k_encode(EncArgs A) {
     if ((eligible(3) || analyze) && (n >= 100 || force)) {
         double part = 0.0;
         uint32_t kc = 0;
+        // numpy's per-count terms p log2 p, tabulated on the host for full chunks
+        // and the tail (an fp64 log2 per symbol cost ~6 % of a mixed chunk's issue)
+        const double* etab = n == A.chunk_size ? A.ent_full : A.ent_tail;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const uint32_t c = S.hist()[lane + 64 * j];
             if (c) {
                 kc++;
-                const double p = (double)c / (double)n;
-                part += p * log2(p);
+                if (etab) {
+                    part += etab[c];
+                } else {
+                    const double p = (double)c / (double)n;
+                    part += p * log2(p);
+                }
             }
         }
         kdist = wave_sum_u32(kc);

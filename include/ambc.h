@@ -84,9 +84,10 @@ typedef struct {
     uint32_t pref_min[16];  /* method_chunk_prefs (adaptive_compressor.py:114-127) */
     uint32_t pref_max[16];
     /* Optional numpy-exact entropy terms p*np.log2(p) indexed by count
-     * (HuffmanCompression.should_use, compression_methods.py:566-574); used only
-     * when the fp64 entropy lies within 1e-9 of the 7.0 threshold.  NULL: the
-     * device log2 is used for those near-ties too. */
+     * (HuffmanCompression.should_use, compression_methods.py:566-574): the
+     * encoder sums them in place of a device log2 per symbol, and near the 7.0
+     * threshold (within 1e-9) re-adds them in numpy's first-occurrence order.
+     * NULL: the device log2 is used for both. */
     const double* ent_full; /* n == chunk_size, length chunk_size+1 */
     const double* ent_tail; /* n == total % chunk_size, length (total % chunk_size)+1 */
 } ambc_params;
