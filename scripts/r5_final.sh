@@ -5,7 +5,7 @@
 # k_encode's SQ counters per input class; each GPU step under its own limit
 set -e
 export TMPDIR=/tmp
-O=gpurun_out/r5f
+O=gpurun_out/${EV_OUT:-r5f}
 mkdir -p $O
 H="python3 bench.py --no-cpu-baseline --api-bytes 0 --no-e2e --alt-methods= --walk-bytes 0 --ref-walk-bytes 0 --ref-full-walk-bytes 0"
 timeout -k 10 600 python3 -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > $O/tests.log 2>&1
