@@ -37,7 +37,7 @@ def _norm(stats):
     return st
 
 
-def analyze(ctx, data, chunk, methods=(1, 3, 4, 9), prefs=None):
+def analyze(ctx, data, chunk, methods=(1, 3, 4, 9), prefs=None, tables=True):
     from ambc import _lib
     from ambc.compressor import entropy_terms
     from ambc.registry import METHOD_CHUNK_PREFS, method_mask
@@ -51,9 +51,9 @@ def analyze(ctx, data, chunk, methods=(1, 3, 4, 9), prefs=None):
         lo, hi = prefs.get(i, (1, 0))
         p.pref_min[i], p.pref_max[i] = lo, min(hi, 0xFFFFFFFF)
     tf = entropy_terms(chunk)
-    p.ent_full = tf.ctypes.data
+    p.ent_full = tf.ctypes.data if tables else None
     tt = entropy_terms(n % chunk) if n % chunk else None
-    p.ent_tail = tt.ctypes.data if tt is not None else None
+    p.ent_tail = tt.ctypes.data if tt is not None and tables else None
     ids = (C.c_uint8 * M)()
     pl = (C.c_uint32 * M)()
     su = (C.c_uint8 * M)()
@@ -1097,3 +1097,18 @@ def _large_body_walks(npk):
         orc.decompress_body(bytes(bad), len(pieces[0]) - 18)
     with pytest.raises(ValueError, match="Marker mismatch"):
         comp._adaptive_decompress(bytes(bad), orig)
+
+
+@pytest.mark.parametrize("chunk", [1024, 4096, 16384])
+def test_entropy_tables_and_device_log2_agree(ctx, chunk):
+    """Huffman's should_use entropy is summed from the host's numpy term tables
+    when the caller passes them (ambc_params.ent_full / ent_tail) and from a
+    device log2 per symbol when it does not: the per-chunk decisions, sizes and
+    should_use bits agree on mixed data, text and skewed bytes, ragged tail
+    included."""
+    rng = np.random.default_rng(chunk)
+    skew = np.minimum(rng.geometric(0.02, size=300000), 255).astype(np.uint8).tobytes()
+    for data in (synth.generate((3 << 20) + 77, 11), skew):
+        a = analyze(ctx, data, chunk, tables=True)
+        b = analyze(ctx, data, chunk, tables=False)
+        assert a == b
