@@ -488,6 +488,11 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     uint32_t p = 0;
     int fcarry = 0;  // max match end so far (frequency count)
     const uint32_t* c32 = reinterpret_cast<const uint32_t*>(ch);
+    // each round's four bytes per position are loaded a round ahead as the two
+    // aligned words around them (clamped to n: past n the word is zero, as the
+    // padded LDS chunk has it and the in-place input may end 64 bytes after n),
+    // issued behind the candidate read, so their wait falls in the next round
+    uint32_t nlo = c32[min(lane, n) >> 2], nhi = c32[(min(lane, n) >> 2) + 1];
 #pragma unroll 1
     for (int r = 0; r < ROUNDS; r++) {
         const int base = r * 64;
@@ -498,9 +503,7 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
         ns = __builtin_amdgcn_readfirstlane(ns);
         const int i = base + (int)lane;
         const bool act = i <= hl;
-        // loads run for every lane (the chunk is zero padded past n + 63)
-        // (EV: lanes past n read nothing -- the input may end 64 bytes after n)
-        const uint32_t v = !NOCHUNK || i < (int)n ? ld32(ch, (uint32_t)i) : 0u;
+        const uint32_t v = i < (int)n ? __builtin_amdgcn_alignbyte(nhi, nlo, lane & 3u) : 0u;
         const uint32_t h = (v * 2654435761u) >> 21;
         const uint32_t c16 = last[h];
         // lanes with my 11-bit hash: one shared hash (runs) is the active mask; else
@@ -527,6 +530,12 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
         const int cand = lower ? base + 63 - (int)__clzll((long long)lower)
                                : (c16 == 0xFFFFu ? -1 : (int)c16);
         const uint32_t cv = ld32(ch, (uint32_t)max(cand, 0));
+        {
+            uint32_t na = min((uint32_t)i + 64u, n);
+            asm volatile("" : "+v"(na) : "v"(v));   // (v formed: the registers are free)
+            nlo = c32[na >> 2];
+            nhi = c32[(na >> 2) + 1];
+        }
         const bool valid = act && cand >= 0 && i - cand <= 32768 && cv == v;
         const uint64_t vm = __ballot(valid);
         wave_sync();
