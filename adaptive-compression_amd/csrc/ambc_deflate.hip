@@ -807,10 +807,30 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     uint32_t adler;
     {
         uint64_t asum = 0, bsum = 0;
-        for (uint32_t i = lane; i < n; i += 64) {
-            const uint32_t c = ch[i];
-            asum += c;
-            bsum += (uint64_t)(n - i) * c;
+        // 16 bytes per lane per load, four loads in flight (a byte per lane per
+        // iteration had waited on one load at a time: half a zero-run chunk's
+        // emission phase); the 16-byte piece at q covers [q, q + 16) & [0, n)
+        const uint32_t nq = (n + 15) / 16;
+#pragma unroll 1
+        for (uint32_t q0 = 0; q0 < nq; q0 += 256) {
+            uint4 w[4];
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                const uint32_t q = q0 + (uint32_t)t * 64 + lane;
+                w[t] = q < nq ? *reinterpret_cast<const uint4*>(ch + 16 * q) : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                const uint32_t q = q0 + (uint32_t)t * 64 + lane;
+                const uint32_t ww[4] = {w[t].x, w[t].y, w[t].z, w[t].w};
+#pragma unroll
+                for (int b = 0; b < 16; b++) {
+                    const uint32_t i = 16 * q + (uint32_t)b;
+                    const uint32_t c = i < n ? (ww[b >> 2] >> (8 * (b & 3))) & 0xFFu : 0u;
+                    asum += c;
+                    bsum += (uint64_t)(n - i) * c;
+                }
+            }
         }
         asum = wave_sum<uint64_t>(asum);
         bsum = wave_sum<uint64_t>(bsum);
@@ -925,6 +945,9 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
         int carry = 0;
         uint32_t sb = 0;   // matches before this round
         const uint64_t lt = (1ull << lane) - 1;
+        // each position's byte is read a round ahead (wave-uniform rp: the round it
+        // belongs to; a round skipped inside a match reads its own)
+        uint32_t rp = 0, cp = chb(min(lane, n - 1));
 #pragma unroll 1
         for (uint32_t r = 0; r < nrounds; r++) {
             const uint32_t i = r * 64 + lane;
@@ -948,7 +971,14 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
             const int E = max(carry, wave_incl_max_i32(e));
             carry = max(carry, wave_max_i32(e));
             const bool lit = i < n && E <= (int)i;
-            const uint32_t c = lit ? chb(i) : 0u;
+            uint32_t cb = rp == r ? cp : chb(min(i, n - 1));
+            {
+                uint32_t na = min(i + 64u, n - 1);
+                asm volatile("" : "+v"(na) : "v"(cb));   // (cb formed: cp's register is free)
+                cp = chb(na);
+                rp = r + 1;
+            }
+            const uint32_t c = lit ? cb : 0u;
             if (lit) cost = S.ll[c];
             const uint32_t incl = wave_incl_sum(cost);
             uint32_t b = bp + incl - cost;
