@@ -804,38 +804,7 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     } else {
 
     // ---- Adler-32 of the chunk (before a BIG chunk's bits overwrite it) ----
-    uint32_t adler;
-    {
-        uint64_t asum = 0, bsum = 0;
-        // 16 bytes per lane per load, four loads in flight (a byte per lane per
-        // iteration had waited on one load at a time: half a zero-run chunk's
-        // emission phase); the 16-byte piece at q covers [q, q + 16) & [0, n)
-        const uint32_t nq = (n + 15) / 16;
-#pragma unroll 1
-        for (uint32_t q0 = 0; q0 < nq; q0 += 256) {
-            uint4 w[4];
-#pragma unroll
-            for (int t = 0; t < 4; t++) {
-                const uint32_t q = q0 + (uint32_t)t * 64 + lane;
-                w[t] = q < nq ? *reinterpret_cast<const uint4*>(ch + 16 * q) : make_uint4(0, 0, 0, 0);
-            }
-#pragma unroll
-            for (int t = 0; t < 4; t++) {
-                const uint32_t q = q0 + (uint32_t)t * 64 + lane;
-                const uint32_t ww[4] = {w[t].x, w[t].y, w[t].z, w[t].w};
-#pragma unroll
-                for (int b = 0; b < 16; b++) {
-                    const uint32_t i = 16 * q + (uint32_t)b;
-                    const uint32_t c = i < n ? (ww[b >> 2] >> (8 * (b & 3))) & 0xFFu : 0u;
-                    asum += c;
-                    bsum += (uint64_t)(n - i) * c;
-                }
-            }
-        }
-        asum = wave_sum<uint64_t>(asum);
-        bsum = wave_sum<uint64_t>(bsum);
-        adler = (uint32_t)(((n + bsum) % 65521) << 16 | ((1 + asum) % 65521));
-    }
+    const uint32_t adler = adler32_wave(ch, n, lane);
     // literal bytes during the emission: LDS, or the input (L2) for BIG chunks
     constexpr bool BIG = GdSmem<CMAX, NOCHUNK>::BIG;
     auto chb = [&](uint32_t q) -> uint32_t { return BIG || NOCHUNK ? (uint32_t)src[q] : (uint32_t)S.chunk[q]; };

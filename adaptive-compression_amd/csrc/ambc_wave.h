@@ -149,4 +149,45 @@ __device__ __forceinline__ T* uniform_ptr(T* p) {
     return reinterpret_cast<T*>(uniform_u64(reinterpret_cast<uint64_t>(p)));
 }
 
+// zlib's Adler-32 of n bytes at src, by one whole wave: whole 16-byte pieces of a
+// 16-byte aligned source as vector loads four in flight per lane, each dword's
+// byte sum (v_sad_u8) and index-weighted sum (v_dot4) folded in at once; the rest
+// (and any unaligned source) a byte per lane; nothing is read at or past src + n.
+// (A byte per lane per iteration waits on one load at a time: 64 serial load
+// latencies for a 4 KiB chunk.)
+__device__ __forceinline__ uint32_t adler32_wave(const uint8_t* src, uint32_t n, uint32_t lane) {
+    uint64_t asum = 0, bsum = 0;
+    const uint32_t nq = (reinterpret_cast<uintptr_t>(src) & 15) == 0 ? n / 16 : 0;
+#pragma unroll 1
+    for (uint32_t q0 = 0; q0 < nq; q0 += 256) {
+        uint4 w[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const uint32_t q = q0 + (uint32_t)t * 64 + lane;
+            w[t] = q < nq ? reinterpret_cast<const uint4*>(src)[q] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const uint32_t i0 = 16 * (q0 + (uint32_t)t * 64 + lane);
+            const uint32_t ww[4] = {w[t].x, w[t].y, w[t].z, w[t].w};
+#pragma unroll
+            for (int d = 0; d < 4; d++) {
+                // bytes c_j at i0 + 4d + j: sum c_j (n - i0 - 4d - j) = (n - i0 - 4d) sum c_j - sum j c_j
+                const uint32_t s0 = __builtin_amdgcn_sad_u8(ww[d], 0u, 0u);
+                const uint32_t s1 = __builtin_amdgcn_udot4(ww[d], 0x03020100u, 0u, false);
+                asum += s0;
+                bsum += (uint64_t)((n - i0 - 4u * (uint32_t)d) * s0 - s1);   // (zero for pieces past nq)
+            }
+        }
+    }
+    for (uint32_t i = 16 * nq + lane; i < n; i += 64) {
+        const uint32_t c = src[i];
+        asum += c;
+        bsum += (uint64_t)(n - i) * c;
+    }
+    asum = wave_sum<uint64_t>(asum);
+    bsum = wave_sum<uint64_t>(bsum);
+    return (uint32_t)(((n + bsum) % 65521) << 16 | ((1 + asum) % 65521));
+}
+
 }  // namespace ambc

@@ -861,18 +861,7 @@ __global__ __launch_bounds__(64) void k_z9_code(EncArgs A) {
     const uint32_t total = 2 + body + 4;
     if (total + 18 >= T) { ZSTAMP_FLUSH; return; }
     // ---- Adler-32 of the chunk ----
-    uint32_t adler;
-    {
-        uint64_t asum = 0, bsum = 0;
-        for (uint32_t i = lane; i < n; i += 64) {
-            const uint32_t c = src[i];
-            asum += c;
-            bsum += (uint64_t)(n - i) * c;
-        }
-        asum = wave_sum<uint64_t>(asum);
-        bsum = wave_sum<uint64_t>(bsum);
-        adler = (uint32_t)(((n + bsum) % 65521) << 16 | ((1 + asum) % 65521));
-    }
+    const uint32_t adler = adler32_wave(src, n, lane);
     uint8_t* slot = A.slots + (uint64_t)k * A.slot_stride;
     const uint8_t* bb = reinterpret_cast<const uint8_t*>(S.bits);
     for (uint32_t i = lane; i < total; i += 64) {

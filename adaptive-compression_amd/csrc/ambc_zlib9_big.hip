@@ -1008,18 +1008,7 @@ __global__ __launch_bounds__(64) void k_z9_code_big(EncArgs A) {
         bp += S.ecl[256] >> 16;
     }
     // ---- Adler-32 of the chunk, big-endian after the byte boundary ----
-    uint32_t adler;
-    {
-        uint64_t asum = 0, bsum = 0;
-        for (uint32_t i = lane; i < n; i += 64) {
-            const uint32_t c = src[i];
-            asum += c;
-            bsum += (uint64_t)(n - i) * c;
-        }
-        asum = wave_sum<uint64_t>(asum);
-        bsum = wave_sum<uint64_t>(bsum);
-        adler = (uint32_t)(((n + bsum) % 65521) << 16 | ((1 + asum) % 65521));
-    }
+    const uint32_t adler = adler32_wave(src, n, lane);
     bp = (bp + 7) & ~7u;
     wave_sync();
     if (lane == 0)
