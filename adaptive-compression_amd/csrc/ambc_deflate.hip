@@ -488,11 +488,53 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     uint32_t p = 0;
     int fcarry = 0;  // max match end so far (frequency count)
     const uint32_t* c32 = reinterpret_cast<const uint32_t*>(ch);
-    // each round's four bytes per position are loaded a round ahead as the two
-    // aligned words around them (clamped to n: past n the word is zero, as the
-    // padded LDS chunk has it and the in-place input may end 64 bytes after n),
-    // issued behind the candidate read, so their wait falls in the next round
-    uint32_t nlo = c32[min(lane, n) >> 2], nhi = c32[(min(lane, n) >> 2) + 1];
+    // The probe runs a round ahead, its loads kept as raw aligned words until used
+    // (their waits fall in the next round): at the top of round r, round r's
+    // positions enter the table (last[] then holds everything before round r + 1,
+    // as the serial order needs), then round r + 1's hashes, candidates and the
+    // candidates' bytes, and round r + 2's own bytes (clamped to n: past n the word
+    // is zero, as the padded LDS chunk has it and the in-place input may end 64
+    // bytes after n).  The loads are unconditional, so the load counter stays exact.
+    auto raw_at = [&](uint32_t pos, uint32_t& lo, uint32_t& hi) { lo = c32[pos >> 2]; hi = c32[(pos >> 2) + 1]; };
+    // round rr's candidates (base rb, positions i = rb + lane with their words vv)
+    auto probe = [&](int rb, uint32_t vv, uint32_t& hh, uint64_t& pp) -> int {
+        const int ii = rb + (int)lane;
+        const bool aa = ii <= hl;
+        hh = (vv * 2654435761u) >> 21;
+        const uint32_t c16 = last[hh];
+        // lanes with my 11-bit hash: one shared hash (runs) is the active mask; else
+        // an order-free LDS OR per 8-bit bucket, then 3 ballots for the top bits
+        const uint64_t actm = rb + 63 <= hl ? ~0ull : __ballot(aa);
+        const uint32_t h0 = __builtin_amdgcn_readfirstlane(hh);
+        if (__ballot(hh != h0) == 0ull) {
+            pp = actm;
+        } else {
+            atomicOr(&bk[hh & 63], aa ? 1ull << lane : 0ull);
+            wave_sync();
+            pp = bk[hh & 63] & actm;
+#pragma unroll
+            for (int b = 6; b < 11; b++) {
+                const uint64_t m = __ballot((hh >> b) & 1u);
+                const uint64_t flip = 0ull - (uint64_t)((hh >> b) & 1u);
+                pp &= ~(m ^ flip);
+            }
+            wave_sync();
+            bk[hh & 63] = 0;
+        }
+        const uint64_t lower = pp & ((1ull << lane) - 1ull);
+        return lower ? rb + 63 - (int)__clzll((long long)lower) : (c16 == 0xFFFFu ? -1 : (int)c16);
+    };
+    uint32_t nlo, nhi, clo, chi, v_cur, h_cur;
+    uint64_t peers_cur;
+    int cand_cur;
+    {
+        uint32_t lo, hi;
+        raw_at(min(lane, n), lo, hi);
+        v_cur = lane < n ? __builtin_amdgcn_alignbyte(hi, lo, lane & 3u) : 0u;
+        cand_cur = probe(0, v_cur, h_cur, peers_cur);
+        raw_at((uint32_t)max(cand_cur, 0), clo, chi);
+        raw_at(min(lane + 64u, n), nlo, nhi);
+    }
 #pragma unroll 1
     for (int r = 0; r < ROUNDS; r++) {
         const int base = r * 64;
@@ -503,43 +545,26 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
         ns = __builtin_amdgcn_readfirstlane(ns);
         const int i = base + (int)lane;
         const bool act = i <= hl;
-        const uint32_t v = i < (int)n ? __builtin_amdgcn_alignbyte(nhi, nlo, lane & 3u) : 0u;
-        const uint32_t h = (v * 2654435761u) >> 21;
-        const uint32_t c16 = last[h];
-        // lanes with my 11-bit hash: one shared hash (runs) is the active mask; else
-        // an order-free LDS OR per 8-bit bucket, then 3 ballots for the top bits
-        const uint64_t actm = base + 63 <= hl ? ~0ull : __ballot(act);
-        const uint32_t h0 = __builtin_amdgcn_readfirstlane(h);
-        uint64_t peers;
-        if (__ballot(h != h0) == 0ull) {
-            peers = actm;
-        } else {
-            atomicOr(&bk[h & 63], act ? 1ull << lane : 0ull);
-            wave_sync();
-            peers = bk[h & 63] & actm;
-#pragma unroll
-            for (int b = 6; b < 11; b++) {
-                const uint64_t m = __ballot((h >> b) & 1u);
-                const uint64_t flip = 0ull - (uint64_t)((h >> b) & 1u);
-                peers &= ~(m ^ flip);
-            }
-            wave_sync();
-            bk[h & 63] = 0;
-        }
-        const uint64_t lower = peers & ((1ull << lane) - 1ull);
-        const int cand = lower ? base + 63 - (int)__clzll((long long)lower)
-                               : (c16 == 0xFFFFu ? -1 : (int)c16);
-        const uint32_t cv = ld32(ch, (uint32_t)max(cand, 0));
-        {
-            uint32_t na = min((uint32_t)i + 64u, n);
-            asm volatile("" : "+v"(na) : "v"(v));   // (v formed: the registers are free)
-            nlo = c32[na >> 2];
-            nhi = c32[(na >> 2) + 1];
+        const uint32_t v = v_cur;
+        const int cand = cand_cur;
+        // (the candidate bytes are consumed before their registers take the next round's)
+        const uint32_t cv = __builtin_amdgcn_alignbyte(chi, clo, (uint32_t)max(cand, 0) & 3u);
+        // round r's positions into the table: each hash's highest position
+        if (act && (peers_cur >> lane) == 1ull) last[h_cur] = (uint16_t)i;
+        wave_sync();
+        if (base + 64 < (int)n) {
+            const uint32_t vn = i + 64 < (int)n ? __builtin_amdgcn_alignbyte(nhi, nlo, lane & 3u) : 0u;
+            const int cn = probe(base + 64, vn, h_cur, peers_cur);
+            uint32_t ca = (uint32_t)max(cn, 0), na = min((uint32_t)i + 128u, n);
+            asm volatile("" : "+v"(ca), "+v"(na) : "v"(cv), "v"(vn));   // (issued after cv, vn are formed)
+            raw_at(ca, clo, chi);
+            raw_at(na, nlo, nhi);
+            v_cur = vn;
+            cand_cur = cn;
         }
         const bool valid = act && cand >= 0 && i - cand <= 32768 && cv == v;
         const uint64_t vm = __ballot(valid);
         wave_sync();
-        if (act && (peers >> lane) == 1ull) last[h] = (uint16_t)i;
         uint32_t L = 0;
         uint64_t selm = 0;
         const uint32_t ns0 = ns;
