@@ -1970,7 +1970,10 @@ int ambc::decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t ori
             up.ns = now_ns() - t1;
         });
     } else if (blen) {
-        HIPCHK(hipMemcpyAsync(d.body.p, body, blen, hipMemcpyHostToDevice, s));
+        // through the library's own pinned staging, not the runtime's pageable
+        // path: the caller's buffer may reuse addresses of pages an earlier call
+        // registered for DMA (the intermittent decode-time fault)
+        if (int rc = copy_staged(d, d.body.p, body, blen, true)) return rc;
     }
     uint64_t h2d = 0;
     std::map<uint32_t, uint64_t> known;
@@ -2090,12 +2093,10 @@ int ambc::decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t ori
     t = now_ns();
     if (d_out_ext) {   // device-resident output (multi-GPU decode): no copy back
         if (orig_size) HIPCHK(hipMemcpyAsync(d_out_ext, d.dout.p, orig_size, hipMemcpyDeviceToDevice, s));
-    } else if (orig_size >= kStageMin) {
+    } else if (orig_size) {   // (any size through the staging, as the body upload above)
         HIPCHK(hipStreamSynchronize(s));
         int rc = copy_staged(d, out, d.dout.p, orig_size, false);
         if (rc) return rc;
-    } else {
-        HIPCHK(hipMemcpyAsync(out, d.dout.p, orig_size, hipMemcpyDeviceToHost, s));
     }
     HIPCHK(hipStreamSynchronize(s));
     const uint64_t d2h_ns = now_ns() - t;
