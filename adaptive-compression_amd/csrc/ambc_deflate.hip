@@ -672,7 +672,7 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
             }
             const int E = max(fcarry, wave_incl_max_i32(e));
             fcarry = max(fcarry, wave_max_i32(e));
-            if (i < (int)n && E <= i) atomicAdd(&S.lf[ch[i]], 1u);
+            if (i < (int)n && E <= i) atomicAdd(&S.lf[v & 0xFFu], 1u);   // (the position's byte: v's first)
             mcov += wave_sum_u32(st ? L : 0u);
         }
         ns = ns0 + (uint32_t)__popcll(selm);
