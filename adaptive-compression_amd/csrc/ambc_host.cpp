@@ -1347,7 +1347,18 @@ int ambc::copy_staged(Dev& d, void* dst, const void* src, uint64_t n, bool to_de
 // queues each piece's DMA on its own stream; a piece counts as done once its
 // DMA's event has fired (a waiter thread marks them in order).  A piece the
 // runtime refuses to pin goes through a staging buffer copy instead.
+// DMA straight from / to the caller's pages (hipHostRegister) is opt-in
+// (AMBC_REGISTER_HOST=1): the suite saw an intermittent illegal-address report in
+// the calls after a large decode whose buffers had been registered and released
+// (DESIGN §9); the default moves caller bytes through the library's own pinned
+// staging, which never maps a caller's address into the GPU.
+static bool register_host() {
+    static const bool on = getenv("AMBC_REGISTER_HOST") && atoi(getenv("AMBC_REGISTER_HOST")) != 0;
+    return on;
+}
+
 int ambc::start_registered_upload(Dev& d, uint8_t* dst, const uint8_t* src, uint64_t n, OrderedUpload& u) {
+    if (!register_host()) return AMBC_E_INVAL;   // (the caller falls back to the staged upload)
     constexpr uint64_t PIECE = 64ull << 20;
     const uintptr_t PG = 4096, sb = (uintptr_t)src, se = sb + n;
     const uintptr_t ra = (sb + PG - 1) & ~(PG - 1), rb = se & ~(PG - 1);
@@ -1491,7 +1502,8 @@ struct OutDMA {
                         if (x >= pc.a) *reinterpret_cast<volatile uint8_t*>(x) = 0;   // (fresh output: zeros)
                 });
             for (auto& x : th) x.join();
-            pc.reg = hipHostRegister(reinterpret_cast<void*>(pc.a), pc.b - pc.a, hipHostRegisterDefault) == hipSuccess;
+            pc.reg = register_host() &&
+                     hipHostRegister(reinterpret_cast<void*>(pc.a), pc.b - pc.a, hipHostRegisterDefault) == hipSuccess;
             { std::lock_guard<std::mutex> lk(m); prepped = j + 1; }
             cv.notify_all();
         }
