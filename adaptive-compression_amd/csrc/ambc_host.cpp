@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -1451,8 +1452,10 @@ int ambc::start_ordered_upload(Dev& d, uint8_t* dst, const uint8_t* src, uint64_
 // output: its pages are faulted in (2 MiB pages where the kernel grants them)
 // and registered with the runtime piece by piece, ahead of the decode, on a
 // helper thread; each decoded range is then one DMA on the copy stream after the
-// kernels that wrote it -- no staging copy on the host.  The page-unaligned head
-// and tail bytes (and any piece the runtime refuses to register) go through the
+// kernels that wrote it -- no staging copy on the host.  Without registration
+// (the default, §9 of DESIGN.md) each decoded piece goes through the pinned
+// staging on a worker thread as soon as its kernels are done, overlapping the
+// decode of later pieces; the page-unaligned head and tail bytes go through the
 // staged copy at the end.
 struct OutDMA {
     static constexpr uintptr_t PG = 4096, HP = 2u << 20, PIECE = 128u << 20;
@@ -1470,6 +1473,11 @@ struct OutDMA {
     size_t pnext = 0;                   // first piece not yet copied
     std::vector<std::pair<uint64_t, uint64_t>> staged;   // ranges the DMA does not cover
     std::thread prep;
+    struct StageJob { uint64_t lo, hi; hipEvent_t after; };
+    std::deque<StageJob> sq;            // unregistered pieces for the staging worker
+    bool sq_done = false, sq_abort = false;
+    int sq_rc = AMBC_OK;
+    std::thread stg;
 
     OutDMA(Dev& dv, uint8_t* o, uint64_t len, const uint8_t* s) : d(dv), out(o), n(len), src(s) {
         ob = (uintptr_t)out;
@@ -1487,6 +1495,36 @@ struct OutDMA {
         prep = std::thread([this] { run_prep(); });
     }
     ~OutDMA() { unreg_all(); }
+
+    void run_stage() {
+        if (hipSetDevice(d.id) != hipSuccess) { std::lock_guard<std::mutex> lk(m); sq_rc = AMBC_E_DEVICE; }
+        for (;;) {
+            StageJob j;
+            {
+                std::unique_lock<std::mutex> lk(m);
+                cv.wait(lk, [&] { return sq_abort || sq_done || !sq.empty(); });
+                if (sq_abort || sq_rc || sq.empty()) return;   // (sq_done with nothing left)
+                j = sq.front();
+                sq.pop_front();
+            }
+            int rc = AMBC_OK;
+            if (j.after && hipEventSynchronize(j.after) != hipSuccess) rc = AMBC_E_DEVICE;
+            else if (j.hi - j.lo >= kStageMin) rc = copy_staged(d, out + j.lo, src + j.lo, j.hi - j.lo, false, 1);
+            else if (hipMemcpy(out + j.lo, src + j.lo, j.hi - j.lo, hipMemcpyDeviceToHost) != hipSuccess) rc = AMBC_E_DEVICE;
+            if (rc) { std::lock_guard<std::mutex> lk(m); sq_rc = rc; return; }
+        }
+    }
+    // wait for the worker (drain: finish every queued piece; else drop the rest)
+    int join_stage(bool drain) {
+        {
+            std::lock_guard<std::mutex> lk(m);
+            if (drain) sq_done = true; else sq_abort = true;
+        }
+        cv.notify_all();
+        if (stg.joinable()) stg.join();
+        std::lock_guard<std::mutex> lk(m);
+        return sq_rc;
+    }
 
     void run_prep() {
         if (hipSetDevice(d.id) != hipSuccess) { std::lock_guard<std::mutex> lk(m); prepped = pcs.size(); cv.notify_all(); return; }
@@ -1512,6 +1550,7 @@ struct OutDMA {
         cv.notify_all();
     }
     void unreg_all() {
+        (void)join_stage(false);
         { std::lock_guard<std::mutex> lk(m); stop_prep = true; }
         if (prep.joinable()) prep.join();
         (void)hipStreamSynchronize(d.xs[1]);
@@ -1528,7 +1567,9 @@ struct OutDMA {
                 if (after) HIPCHK(hipStreamWaitEvent(d.xs[1], after, 0));
                 HIPCHK(hipMemcpyAsync(out + lo, src + lo, hi - lo, hipMemcpyDeviceToHost, d.xs[1]));
             } else {
-                staged.emplace_back(lo, hi);
+                sq.push_back(StageJob{lo, hi, after});
+                if (!stg.joinable()) stg = std::thread([this] { run_stage(); });
+                cv.notify_all();
             }
             pnext++;
         }
@@ -1538,6 +1579,8 @@ struct OutDMA {
     int finish(hipEvent_t after) {
         int rc = copy_ready(n, after);
         if (rc) { unreg_all(); return rc; }
+        rc = join_stage(true);
+        if (rc) { unreg_all(); return fail(rc, "staged copy failed"); }
         HIPCHK(hipStreamSynchronize(d.xs[1]));
         unreg_all();
         if (ra > ob || rb <= ra) staged.emplace_back(0, std::min<uint64_t>(n, rb > ra ? ra - ob : n));
@@ -1799,12 +1842,12 @@ static int decompress_devwalk(Dev& d, const uint8_t* body, uint64_t blen, uint64
         if (rc) return rc;
     }
     OrderedUpload& up = *upp;
-    OutDMA od(d, out, orig_size, d.dout.as<uint8_t>());
     std::vector<hipEvent_t> evs;   // per piece: decode start, decode end, after the check
     struct EvFree {
         std::vector<hipEvent_t>& v;
         ~EvFree() { for (auto e : v) if (e) (void)hipEventDestroy(e); }
     } evfree{evs};
+    OutDMA od(d, out, orig_size, d.dout.as<uint8_t>());   // (after evs: joins its copies before they go)
     auto abort_all = [&](int code) {
         od.unreg_all();
         up.release();
