@@ -1343,74 +1343,6 @@ int ambc::copy_staged(Dev& d, void* dst, const void* src, uint64_t n, bool to_de
     return AMBC_OK;
 }
 
-// The registered upload: one helper thread pins the body piece by piece (4 KiB
-// aligned interior; the unaligned head and tail bytes are copied first) and
-// queues each piece's DMA on its own stream; a piece counts as done once its
-// DMA's event has fired (a waiter thread marks them in order).  A piece the
-// runtime refuses to pin goes through a staging buffer copy instead.
-// DMA straight from / to the caller's pages (hipHostRegister) is opt-in
-// (AMBC_REGISTER_HOST=1): the suite saw an intermittent illegal-address report in
-// the calls after a large decode whose buffers had been registered and released
-// (DESIGN §9); the default moves caller bytes through the library's own pinned
-// staging, which never maps a caller's address into the GPU.
-static bool register_host() {
-    static const bool on = getenv("AMBC_REGISTER_HOST") && atoi(getenv("AMBC_REGISTER_HOST")) != 0;
-    return on;
-}
-
-int ambc::start_registered_upload(Dev& d, uint8_t* dst, const uint8_t* src, uint64_t n, OrderedUpload& u) {
-    if (!register_host()) return AMBC_E_INVAL;   // (the caller falls back to the staged upload)
-    constexpr uint64_t PIECE = 64ull << 20;
-    const uintptr_t PG = 4096, sb = (uintptr_t)src, se = sb + n;
-    const uintptr_t ra = (sb + PG - 1) & ~(PG - 1), rb = se & ~(PG - 1);
-    if (rb <= ra + PG) return AMBC_E_INVAL;   // (too small: the staged upload)
-    HIPCHK(hipSetDevice(d.id));
-    // the edges first, synchronously (a few KiB)
-    if (ra > sb) HIPCHK(hipMemcpy(dst, src, ra - sb, hipMemcpyHostToDevice));
-    if (se > rb) HIPCHK(hipMemcpy(dst + (rb - sb), src + (rb - sb), se - rb, hipMemcpyHostToDevice));
-    for (uintptr_t x = ra; x < rb; x += PIECE)
-        u.rp.push_back(OrderedUpload::RegPiece{x, std::min<uintptr_t>(rb, x + PIECE), nullptr, false});
-    for (auto& p : u.rp) HIPCHK(hipEventCreateWithFlags(&p.ev, hipEventDisableTiming));
-    u.issued.reset(new std::atomic<int>[u.rp.size()]);
-    for (size_t j = 0; j < u.rp.size(); j++) u.issued[j].store(0);
-    // piece j covers body bytes [a - sb, b - sb); done[] is kept per kStagePiece as
-    // in the staged mode: the waiter marks the staged-size pieces a DMA covers
-    const uint64_t np = (n + kStagePiece - 1) / kStagePiece;
-    u.n = n;
-    u.done.assign(np, 0);
-    u.dev = &d;
-    if (!d.xs[0]) HIPCHK(hipStreamCreateWithFlags(&d.xs[0], hipStreamNonBlocking));
-    u.th.emplace_back([&d, &u, dst, src, sb] {
-        if (hipSetDevice(d.id) != hipSuccess) { u.fail_all(); return; }
-        for (auto& p : u.rp) {
-            const uint64_t off = p.a - sb, len = p.b - p.a;
-            p.reg = hipHostRegister(reinterpret_cast<void*>(p.a), len, hipHostRegisterDefault) == hipSuccess;
-            const hipError_t e = p.reg ? hipMemcpyAsync(dst + off, src + off, len, hipMemcpyHostToDevice, d.xs[0])
-                                       : hipMemcpy(dst + off, src + off, len, hipMemcpyHostToDevice);
-            if (e != hipSuccess || hipEventRecord(p.ev, d.xs[0]) != hipSuccess) { u.fail_all(); return; }
-            u.issued[&p - u.rp.data()].store(1, std::memory_order_release);
-        }
-    });
-    u.th.emplace_back([&u, sb, n, np] {
-        // mark the staged-size pieces whose bytes are all on the device
-        uint64_t q = 0;
-        for (auto& p : u.rp) {
-            // (an event not yet recorded reads as complete: wait for the record first)
-            while (!u.issued[&p - u.rp.data()].load(std::memory_order_acquire)) {
-                { std::lock_guard<std::mutex> lk(u.m); if (u.failed) return; }
-                std::this_thread::sleep_for(std::chrono::microseconds(20));
-            }
-            hipError_t e;
-            while ((e = hipEventQuery(p.ev)) == hipErrorNotReady) std::this_thread::sleep_for(std::chrono::microseconds(50));
-            if (e != hipSuccess) { u.fail_all(); return; }
-            const uint64_t upto = (&p == &u.rp.back()) ? n : p.b - sb;
-            while (q < np && std::min<uint64_t>(n, (q + 1) * kStagePiece) <= upto) u.mark(q++);
-        }
-        while (q < np) u.mark(q++);
-    });
-    return AMBC_OK;
-}
-
 int ambc::start_ordered_upload(Dev& d, uint8_t* dst, const uint8_t* src, uint64_t n, unsigned T, OrderedUpload& u) {
     int rc = ensure_stage(d, T, 0);
     if (rc) return rc;
@@ -1448,53 +1380,46 @@ int ambc::start_ordered_upload(Dev& d, uint8_t* dst, const uint8_t* src, uint64_
     return AMBC_OK;
 }
 
-// The copy back of a decode goes straight from the device into the caller's
-// output: its pages are faulted in (2 MiB pages where the kernel grants them)
-// and registered with the runtime piece by piece, ahead of the decode, on a
-// helper thread; each decoded range is then one DMA on the copy stream after the
-// kernels that wrote it -- no staging copy on the host.  Without registration
-// (the default, §9 of DESIGN.md) each decoded piece goes through the pinned
-// staging on a worker thread as soon as its kernels are done, overlapping the
-// decode of later pieces; the page-unaligned head and tail bytes go through the
-// staged copy at the end.
-struct OutDMA {
-    static constexpr uintptr_t PG = 4096, HP = 2u << 20, PIECE = 128u << 20;
-    struct Piece { uintptr_t a, b; bool reg; };
+// The copy back of a decode: the caller's output is cut into pieces of about
+// PIECE bytes (ends on 2 MiB page boundaries); a helper thread faults each piece
+// in ahead of the decode (2 MiB pages where the kernel grants them, 8 threads),
+// and each decoded piece goes down through the library's pinned staging on a
+// worker thread as soon as the kernels that wrote it are done, overlapping the
+// decode and upload of later pieces.  The caller's pages are never mapped into
+// the GPU (no hipHostRegister of caller memory).
+struct OutCopy {
+    static constexpr uint64_t PG = 4096, HP = 2u << 20, PIECE = 128u << 20;
+    struct Piece { uint64_t lo, hi; };  // output offsets
     Dev& d;
     uint8_t* out;
     uint64_t n;
     const uint8_t* src;                 // device bytes
-    uintptr_t ob, oe, ra, rb;           // registrable [ra, rb)
     std::vector<Piece> pcs;
     std::mutex m;
     std::condition_variable cv;
-    size_t prepped = 0;                 // pieces [0, prepped) faulted in and (if reg) registered
+    size_t prepped = 0;                 // pieces [0, prepped) faulted in
     bool stop_prep = false;
-    size_t pnext = 0;                   // first piece not yet copied
-    std::vector<std::pair<uint64_t, uint64_t>> staged;   // ranges the DMA does not cover
+    size_t pnext = 0;                   // first piece not yet queued
     std::thread prep;
     struct StageJob { uint64_t lo, hi; hipEvent_t after; };
-    std::deque<StageJob> sq;            // unregistered pieces for the staging worker
+    std::deque<StageJob> sq;            // decoded pieces for the staging worker
     bool sq_done = false, sq_abort = false;
     int sq_rc = AMBC_OK;
     std::thread stg;
 
-    OutDMA(Dev& dv, uint8_t* o, uint64_t len, const uint8_t* s) : d(dv), out(o), n(len), src(s) {
-        ob = (uintptr_t)out;
-        oe = ob + n;
-        ra = (ob + PG - 1) & ~(PG - 1);
-        rb = oe & ~(PG - 1);
-        if (rb > ra) {
-            for (uintptr_t x = ra; x < rb;) {
-                const uintptr_t y = std::min<uintptr_t>(rb, ((x + PIECE) & ~(HP - 1)) > x ? ((x + PIECE) & ~(HP - 1)) : rb);
-                pcs.push_back(Piece{x, y, false});
-                x = y;
-            }
+    OutCopy(Dev& dv, uint8_t* o, uint64_t len, const uint8_t* s) : d(dv), out(o), n(len), src(s) {
+        const uintptr_t ob = (uintptr_t)out;
+        for (uint64_t x = 0; x < n;) {
+            uint64_t y = ((ob + x + PIECE) & ~(uintptr_t)(HP - 1)) - ob;
+            if (y <= x) y = x + PIECE;
+            y = std::min(y, n);
+            pcs.push_back(Piece{x, y});
+            x = y;
         }
         hugepage_advice(out, n);
         prep = std::thread([this] { run_prep(); });
     }
-    ~OutDMA() { unreg_all(); }
+    ~OutCopy() { abort(); }
 
     void run_stage() {
         if (hipSetDevice(d.id) != hipSuccess) { std::lock_guard<std::mutex> lk(m); sq_rc = AMBC_E_DEVICE; }
@@ -1527,21 +1452,20 @@ struct OutDMA {
     }
 
     void run_prep() {
-        if (hipSetDevice(d.id) != hipSuccess) { std::lock_guard<std::mutex> lk(m); prepped = pcs.size(); cv.notify_all(); return; }
         const unsigned TP = std::max(1u, std::min(8u, stage_threads(n, 8)));
+        const uintptr_t ob = (uintptr_t)out;
         for (size_t j = 0; j < pcs.size(); j++) {
             { std::lock_guard<std::mutex> lk(m); if (stop_prep) break; }
-            Piece& pc = pcs[j];
+            const Piece pc = pcs[j];
             std::vector<std::thread> th;
             for (unsigned t = 0; t < TP; t++)
-                th.emplace_back([&pc, t, TP] {
-                    const uintptr_t a = pc.a + (pc.b - pc.a) * t / TP, b = pc.a + (pc.b - pc.a) * (t + 1) / TP;
-                    for (uintptr_t x = a & ~(PG - 1); x < b; x += PG)
-                        if (x >= pc.a) *reinterpret_cast<volatile uint8_t*>(x) = 0;   // (fresh output: zeros)
+                th.emplace_back([pc, t, TP, ob] {
+                    const uintptr_t a = ob + pc.lo + (pc.hi - pc.lo) * t / TP, b = ob + pc.lo + (pc.hi - pc.lo) * (t + 1) / TP;
+                    // one byte of every page in [a, b) (a fresh output: zeros)
+                    for (uintptr_t x = a; x < b; x = (x & ~(uintptr_t)(PG - 1)) + PG)
+                        *reinterpret_cast<volatile uint8_t*>(x) = 0;
                 });
             for (auto& x : th) x.join();
-            pc.reg = register_host() &&
-                     hipHostRegister(reinterpret_cast<void*>(pc.a), pc.b - pc.a, hipHostRegisterDefault) == hipSuccess;
             { std::lock_guard<std::mutex> lk(m); prepped = j + 1; }
             cv.notify_all();
         }
@@ -1549,51 +1473,31 @@ struct OutDMA {
         prepped = pcs.size();
         cv.notify_all();
     }
-    void unreg_all() {
+    // drop what is queued, stop faulting in, join both helpers
+    void abort() {
         (void)join_stage(false);
         { std::lock_guard<std::mutex> lk(m); stop_prep = true; }
         if (prep.joinable()) prep.join();
-        (void)hipStreamSynchronize(d.xs[1]);
-        for (auto& pc : pcs) if (pc.reg) { (void)hipHostUnregister(reinterpret_cast<void*>(pc.a)); pc.reg = false; }
     }
-    // DMA of the pieces entirely below output offset upto, after event `after`
+    // queue the pieces entirely below output offset upto, to go after event `after`
     int copy_ready(uint64_t upto, hipEvent_t after) {
         std::unique_lock<std::mutex> lk(m);
-        while (pnext < pcs.size() && pcs[pnext].b <= ob + upto) {
+        while (pnext < pcs.size() && pcs[pnext].hi <= upto) {
             cv.wait(lk, [&] { return prepped > pnext; });
-            const Piece& pc = pcs[pnext];
-            const uint64_t lo = pc.a - ob, hi = pc.b - ob;
-            if (pc.reg) {
-                if (after) HIPCHK(hipStreamWaitEvent(d.xs[1], after, 0));
-                HIPCHK(hipMemcpyAsync(out + lo, src + lo, hi - lo, hipMemcpyDeviceToHost, d.xs[1]));
-            } else {
-                sq.push_back(StageJob{lo, hi, after});
-                if (!stg.joinable()) stg = std::thread([this] { run_stage(); });
-                cv.notify_all();
-            }
+            sq.push_back(StageJob{pcs[pnext].lo, pcs[pnext].hi, after});
+            if (!stg.joinable()) stg = std::thread([this] { run_stage(); });
+            cv.notify_all();
             pnext++;
         }
         return AMBC_OK;
     }
-    // the rest after `after`, then the unaligned edges and the unregistered pieces
+    // the rest after `after`; returns when every byte is in the output
     int finish(hipEvent_t after) {
         int rc = copy_ready(n, after);
-        if (rc) { unreg_all(); return rc; }
+        if (rc) { abort(); return rc; }
         rc = join_stage(true);
-        if (rc) { unreg_all(); return fail(rc, "staged copy failed"); }
-        HIPCHK(hipStreamSynchronize(d.xs[1]));
-        unreg_all();
-        if (ra > ob || rb <= ra) staged.emplace_back(0, std::min<uint64_t>(n, rb > ra ? ra - ob : n));
-        if (rb > ra && oe > rb) staged.emplace_back(rb - ob, n);
-        for (auto& r : staged) {
-            if (r.second <= r.first) continue;
-            if (r.second - r.first >= kStageMin) {
-                rc = copy_staged(d, out + r.first, src + r.first, r.second - r.first, false, 1);
-                if (rc) return rc;
-            } else {
-                HIPCHK(hipMemcpy(out + r.first, src + r.first, r.second - r.first, hipMemcpyDeviceToHost));
-            }
-        }
+        abort();
+        if (rc) return fail(rc, "staged copy failed");
         return AMBC_OK;
     }
 };
@@ -1617,14 +1521,9 @@ static int decompress_pipelined(Dev& d, const uint8_t* body, uint64_t blen, uint
     hipStream_t s = d.stream;
     HIPCHK(d.body.ensure(blen + 64));
     std::unique_ptr<OrderedUpload> upp(new OrderedUpload());
-    // the body by DMA from its own (pinned) pages, else through the staging buffers
-    int rc = getenv("AMBC_STAGED_UPLOAD") ? AMBC_E_INVAL
-                                          : start_registered_upload(d, d.body.as<uint8_t>(), body, blen, *upp);
-    if (rc) {
-        upp.reset(new OrderedUpload());
-        rc = start_ordered_upload(d, d.body.as<uint8_t>(), body, blen, stage_threads(blen, 8), *upp);
-        if (rc) return rc;
-    }
+    // the body through the pinned staging buffers, in order
+    int rc = start_ordered_upload(d, d.body.as<uint8_t>(), body, blen, stage_threads(blen, 8), *upp);
+    if (rc) return rc;
     OrderedUpload& up = *upp;
     // the header walk meanwhile, on the host body
     std::map<uint32_t, uint64_t> known;
@@ -1694,20 +1593,20 @@ static int decompress_pipelined(Dev& d, const uint8_t* body, uint64_t blen, uint
         HIPCHK(hipEventCreate(&evb[q]));
         HIPCHK(hipEventCreate(&eve[q]));
     }
-    OutDMA od(d, out, orig_size, d.dout.as<uint8_t>());
+    OutCopy od(d, out, orig_size, d.dout.as<uint8_t>());
     const uint64_t tk = now_ns();
     for (size_t q = 0; q < S; q++) {
-        if (!up.wait_prefix(bneed[q])) { od.unreg_all(); up.release(); return fail(AMBC_E_DEVICE, "staged body upload failed"); }
+        if (!up.wait_prefix(bneed[q])) { od.abort(); up.release(); return fail(AMBC_E_DEVICE, "staged body upload failed"); }
         HIPCHK(hipEventRecord(evb[q], s));
         for (int k = 0; k < DEC_KINDS; k++) {
             a.list = d.list.as<uint32_t>() + lbase[q * DEC_KINDS + k];
             a.n_list = lcnt[q * DEC_KINDS + k];
             const hipError_t e = launch_decode(k, a, s);
-            if (e != hipSuccess) { od.unreg_all(); up.release(); return fail(AMBC_E_DEVICE, hipGetErrorString(e)); }
+            if (e != hipSuccess) { od.abort(); up.release(); return fail(AMBC_E_DEVICE, hipGetErrorString(e)); }
         }
         HIPCHK(hipEventRecord(eve[q], s));
         const int rc2 = od.copy_ready(o0[q + 1], eve[q]);
-        if (rc2) { od.unreg_all(); up.release(); return rc2; }
+        if (rc2) { od.abort(); up.release(); return rc2; }
     }
     up.release();
     const uint64_t h2d_ns = now_ns() - t0;
@@ -1806,9 +1705,8 @@ static int walk_buffers(Dev& d, uint64_t piece) {
 // up in order; each piece of kWalkPiece bytes of header positions is walked on
 // the walk stream as soon as it (plus the 17 bytes after it) has arrived, its
 // jobs are decoded on the decode stream once the payloads they read are up, and
-// the decoded range goes back by DMA into the caller's registered output -- the
-// walk of piece k + 1, the decode of piece k, the upload and the copy back all
-// overlap.  The host sees a few counters per piece (kernel grids) and, at the
+// the decoded range goes back through the pinned staging (OutCopy) -- the walk of
+// piece k + 1, the decode of piece k, the upload and the copy back all overlap.  The host sees a few counters per piece (kernel grids) and, at the
 // end, the packages left to host codecs.  PIPE_FALLBACK as decompress_pipelined.
 static int decompress_devwalk(Dev& d, const uint8_t* body, uint64_t blen, uint64_t orig_size,
                               const uint64_t reg[4], uint8_t* out, std::vector<ambc_host_chunk>& host,
@@ -1834,22 +1732,17 @@ static int decompress_devwalk(Dev& d, const uint8_t* body, uint64_t blen, uint64
     }
     HIPCHK(hipMemsetAsync(w.state.p, 0, sizeof(WalkState), w.ws));
     std::unique_ptr<OrderedUpload> upp(new OrderedUpload());
-    rc = getenv("AMBC_STAGED_UPLOAD") ? AMBC_E_INVAL
-                                      : start_registered_upload(d, d.body.as<uint8_t>(), body, blen, *upp);
-    if (rc) {
-        upp.reset(new OrderedUpload());
-        rc = start_ordered_upload(d, d.body.as<uint8_t>(), body, blen, stage_threads(blen, 8), *upp);
-        if (rc) return rc;
-    }
+    rc = start_ordered_upload(d, d.body.as<uint8_t>(), body, blen, stage_threads(blen, 8), *upp);
+    if (rc) return rc;
     OrderedUpload& up = *upp;
     std::vector<hipEvent_t> evs;   // per piece: decode start, decode end, after the check
     struct EvFree {
         std::vector<hipEvent_t>& v;
         ~EvFree() { for (auto e : v) if (e) (void)hipEventDestroy(e); }
     } evfree{evs};
-    OutDMA od(d, out, orig_size, d.dout.as<uint8_t>());   // (after evs: joins its copies before they go)
+    OutCopy od(d, out, orig_size, d.dout.as<uint8_t>());   // (after evs: joins its copies before they go)
     auto abort_all = [&](int code) {
-        od.unreg_all();
+        od.abort();
         up.release();
         (void)hipStreamSynchronize(w.ws);
         (void)hipStreamSynchronize(s);
@@ -2025,9 +1918,7 @@ int ambc::decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t ori
             up.ns = now_ns() - t1;
         });
     } else if (blen) {
-        // through the library's own pinned staging, not the runtime's pageable
-        // path: the caller's buffer may reuse addresses of pages an earlier call
-        // registered for DMA (the intermittent decode-time fault)
+        // through the library's own pinned staging (one thread for a small body)
         if (int rc = copy_staged(d, d.body.p, body, blen, true)) return rc;
     }
     uint64_t h2d = 0;

@@ -203,12 +203,6 @@ struct OrderedUpload {
     uint64_t n = 0, ready = 0;     // ready: the leading pieces all done
     bool failed = false;
     std::vector<std::thread> th;
-    // registered mode: the caller's pages pinned piece by piece and copied by
-    // DMA (no staging copy); pieces [a, b) of the host range, their events
-    struct RegPiece { uintptr_t a, b; hipEvent_t ev; bool reg; };
-    std::vector<RegPiece> rp;
-    std::unique_ptr<std::atomic<int>[]> issued;   // piece j's DMA and event record are queued
-    Dev* dev = nullptr;
     void mark(uint64_t q) {
         std::lock_guard<std::mutex> lk(m);
         done[q] = 1;
@@ -233,21 +227,12 @@ struct OrderedUpload {
         return !failed;
     }
     void join() { for (auto& x : th) if (x.joinable()) x.join(); th.clear(); }
-    // registered mode: after join(), wait for the DMAs and unpin
-    void release() {
-        join();
-        for (auto& p : rp) {
-            if (p.ev) { (void)hipEventSynchronize(p.ev); (void)hipEventDestroy(p.ev); p.ev = nullptr; }
-            if (p.reg) { (void)hipHostUnregister(reinterpret_cast<void*>(p.a)); p.reg = false; }
-        }
-    }
+    void release() { join(); }
     ~OrderedUpload() { release(); }
 };
 
-// an ordered upload of n bytes from host src to device dst: the caller's pages
-// pinned and copied by DMA piece by piece (start_registered_upload), or through
-// the pinned staging buffers on T threads (start_ordered_upload)
-int start_registered_upload(Dev& d, uint8_t* dst, const uint8_t* src, uint64_t n, OrderedUpload& u);
+// an ordered upload of n bytes from host src to device dst through the pinned
+// staging buffers on T threads (the caller's pages are never registered)
 int start_ordered_upload(Dev& d, uint8_t* dst, const uint8_t* src, uint64_t n, unsigned T, OrderedUpload& u);
 
 // collective of the sharded calls (ambc_shard.cpp)

@@ -205,24 +205,18 @@ extern "C" int ambc_compress_multisize_ex(ambc_ctx* ctx, const uint8_t* in, uint
     // the walks whose chunks have arrived, the others as the pieces come in; the
     // final encode waits for all of it)
     // AMBC_MS_UPLOAD (A/B): "staged" -- pinned staging buffers on 8 threads beside
-    // the walk; "registered" -- the caller's pages pinned piece by piece and copied
-    // by DMA from one thread (few runtime calls beside the walk's launches), staged
-    // where the runtime refuses to pin; "first" -- the walk after the whole upload.
-    // Default, measured on 256 MiB (profiles/r5_upload_ab): registered where every
-    // size runs its own encoders ({1,2,3,4,5} 4.91-5.03 -> 4.99-5.16 GB/s), first with
-    // LZ4 among the methods, whose walk asks six positions ahead and loses more to
-    // the forgotten requests than the overlap gains ({1,3,4,9} 6.17-6.22 vs 5.26-5.88)
+    // the walk; "first" -- the walk after the whole upload.  Default, measured on
+    // 256 MiB (profiles/r5_upload_ab): staged where every size runs its own encoders,
+    // first with LZ4 among the methods, whose walk asks six positions ahead and loses
+    // more to the forgotten requests than the overlap gains ({1,3,4,9} 6.17-6.22 vs
+    // 5.26-5.88).  (Round 5's third mode pinned the caller's pages for DMA; the
+    // library no longer maps caller memory into the GPU)
     static const char* upenv = getenv("AMBC_MS_UPLOAD");
-    const char* upmode = upenv ? upenv : ((p->method_mask >> AMBC_M_LZ4) & 1) ? "first" : "registered";
+    const char* upmode = upenv ? upenv : ((p->method_mask >> AMBC_M_LZ4) & 1) ? "first" : "staged";
     std::unique_ptr<OrderedUpload> up;
     if (n >= kStageMin) {
         up.reset(new OrderedUpload());
-        int rc = strcmp(upmode, "registered") ? AMBC_E_INVAL
-                                              : start_registered_upload(d, d.in.as<uint8_t>(), in, n, *up);
-        if (rc) {
-            up.reset(new OrderedUpload());
-            if ((rc = start_ordered_upload(d, d.in.as<uint8_t>(), in, n, stage_threads(n, 8), *up))) return rc;
-        }
+        if (int rc = start_ordered_upload(d, d.in.as<uint8_t>(), in, n, stage_threads(n, 8), *up)) return rc;
     } else if (n) {
         HIPCHK(hipMemcpyAsync(d.in.p, in, n, hipMemcpyHostToDevice, s));
     }

@@ -112,3 +112,13 @@ def test_integration_doc_quotes_the_binding_verbatim():
     with open(os.path.join(REPO, "integration", "ambc_binding.py")) as f:
         src = f.read()
     assert "```python\n" + src + "```" in doc
+
+
+def test_library_never_registers_caller_memory():
+    """DESIGN §9 (round 6): caller buffers move through the library's own pinned
+    staging only; the shipped library imports no host-registration entry point,
+    so no caller page is ever mapped into the GPU."""
+    with open(os.path.join(REPO, "adaptive-compression_amd", "ambc", "libambc_hip.so"), "rb") as f:
+        blob = f.read()
+    for sym in (b"hipHostRegister", b"hipHostUnregister", b"hsa_amd_memory_lock"):
+        assert sym not in blob, sym
