@@ -296,7 +296,7 @@ class DeviceBuffer:
 
 
 _ctx = None
-_plugin_ctx = None
+_plugin_ctx = {}   # device list -> the per-chunk plugins' context on those devices
 
 
 def default_context(devices=None):
@@ -307,13 +307,17 @@ def default_context(devices=None):
         return _ctx
 
 
-def plugin_context():
+def plugin_context(devices=None):
     """The per-chunk plugins' own context (methods.py): a plugin called from a
     host-codec callback while a walk holds the default context's lock (the
     reference-side binding scores the instance's own method objects on host
-    threads) must not wait for that lock."""
-    global _plugin_ctx
+    threads) must not wait for that lock.  It lives on the devices given, else
+    on those of the active default context (a rank process on GPU LOCAL_RANK
+    keeps its plugins there), else on device 0 -- one context per device list."""
     with _lock:
-        if _plugin_ctx is None:
-            _plugin_ctx = Context()
-        return _plugin_ctx
+        if devices is None:
+            devices = _ctx.devices if _ctx is not None else [0]
+        key = tuple(devices)
+        if key not in _plugin_ctx:
+            _plugin_ctx[key] = Context(list(key))
+        return _plugin_ctx[key]

@@ -12,11 +12,16 @@ strict minimum of len + 18 below the chunk's own length, ids ascending; the
 library then joins it with the GPU's winner in id order.  bz2 / lzma release the
 GIL while they compress, so a thread pool runs the pairs in parallel.
 
+Each round's (pair, codec) evaluations go to the pool as separate tasks, the
+costliest first (LZMA, then bz2, larger chunks first), so that a round's host
+time is about max(largest task, total / threads) rather than a pair's serial
+sum; the pair's answer is then joined in id order exactly as the loop would.
+
 Memory: an LZMA encoder with the reference's 16 MiB dictionary holds about
-190 MiB of state; methods.py keeps at most 8 of them (re-initialised, not
-rebuilt, per call) and a call waits for a free one, so the rest of the pool keeps
-bz2 / zstd busy meanwhile: a walk peaks near 1.5 GiB of host memory for LZMA
-(like_reference(full_set=True)).
+190 MiB of state; methods.py keeps as many as its memory budget allows (a
+quarter of the host's memory, at most 8 GiB: 32 on a large host) and a call
+waits for a free one, so the rest of the pool keeps bz2 / zstd busy meanwhile;
+close() ends the idle encoders, so nothing stays resident after the walk.
 """
 import ctypes as C
 import os
@@ -45,7 +50,8 @@ class HostScorer:
         self.cache = {}
         self.cached = 0
         self.error = None
-        self.pool = ThreadPoolExecutor(workers or min(32, os.cpu_count() or 4))
+        env = os.environ.get("AMBC_HOST_CODEC_THREADS")
+        self.pool = ThreadPoolExecutor(workers or (int(env) if env else min(32, os.cpu_count() or 4)))
         # the callbacks must outlive the call: keep them on the instance
         self._eval_cb = EVAL_FN(self._eval)
         self._emit_cb = EMIT_FN(self._emit)
@@ -54,27 +60,53 @@ class HostScorer:
     def close(self):
         self.pool.shutdown(wait=True)
         self.cache.clear()
+        from .methods import _XZEncoders
+        _XZEncoders.release()
+
+    def _eligible(self, m, size):
+        lo, hi = self.prefs.get(m.type_id, (1, 999999999))
+        return lo <= size <= hi
+
+    def _one(self, m, pos, size):
+        """method m at data[pos:pos+size]: its payload, or None (should_use false, or it raised)"""
+        chunk = self.data[pos:pos + size]
+        if not m.should_use(chunk):
+            return None
+        try:
+            return m.compress(chunk)
+        except Exception:  # noqa: BLE001 -- the reference's loop skips a raising method
+            return None
+
+    def _join(self, size, outs):
+        """the reference's per-size loop over the host codecs (adaptive_compressor.py:
+        559-579): ids ascending, strict minimum below len + 18 < size"""
+        win, wl, pay = 0, size - 18, None
+        for m in self.methods:
+            c = outs.get(m.type_id)
+            if c is not None and len(c) < wl:
+                win, wl, pay = m.type_id, len(c), c
+        return win, pay
 
     def best(self, pos, size):
         """(id, payload) of the host codecs' winner at data[pos:pos+size], or (0, None)."""
-        chunk = self.data[pos:pos + size]
-        win, wl, pay = 0, size - 18, None          # a winner needs len + 18 < size
-        for m in self.methods:
-            lo, hi = self.prefs.get(m.type_id, (1, 999999999))
-            if not lo <= size <= hi or not m.should_use(chunk):
-                continue
-            try:
-                c = m.compress(chunk)
-            except Exception:  # noqa: BLE001 -- the reference's loop skips a raising method
-                continue
-            if len(c) < wl:
-                win, wl, pay = m.type_id, len(c), c
-        return win, pay
+        outs = {m.type_id: self._one(m, pos, size) for m in self.methods if self._eligible(m, size)}
+        return self._join(size, outs)
+
+    @staticmethod
+    def _cost(m, size):
+        return (0 if m.type_id == 7 else 1 if m.type_id == 6 else 2, -size)
 
     def _eval(self, _user, pos, size, count, out_id, out_len):
         try:
             pairs = [(int(pos[i]), int(size[i])) for i in range(count)]
-            for i, (w, pay) in enumerate(self.pool.map(lambda ps: self.best(*ps), pairs)):
+            tasks = [(i, m) for i, (_p, sz) in enumerate(pairs) for m in self.methods if self._eligible(m, sz)]
+            tasks.sort(key=lambda t: self._cost(t[1], pairs[t[0]][1]))
+            futs = [(i, m.type_id, self.pool.submit(self._one, m, *pairs[i])) for i, m in tasks]
+            outs = [dict() for _ in pairs]
+            for i, mid, f in futs:
+                outs[i][mid] = f.result()
+            for i, (_p, sz) in enumerate(pairs):
+                w, pay = self._join(sz, outs[i])
                 out_id[i] = w
                 out_len[i] = len(pay) if w else 0
                 if w and self.cached + len(pay) <= self.CACHE_BYTES:

@@ -22,6 +22,7 @@ C-ABI call for the whole body.
 import bz2
 import ctypes as C
 import lzma
+import os
 import queue
 import struct
 import threading
@@ -113,21 +114,25 @@ def _gpu_should_use(data):
 
 
 def _gpu_decode(mid, data, original_length):
-    """method.decompress through the batched GPU decoder (one package)."""
+    """method.decompress through the batched GPU decoder (one package).  The
+    output is sized max(orig, 1): Huffman appends a symbol before it compares the
+    length with original_length (compression_methods.py:462-468), so orig 0 still
+    yields one byte; the other codecs produce nothing there."""
     data = bytes(data)
     body = MARKER_BYTES + _HDR.pack(mid, 0, original_length, original_length, len(data)) + data + _END
     ctx = _ctx()
-    out = (C.c_uint8 * max(1, original_length))()
+    osz = max(1, original_length)
+    out = (C.c_uint8 * osz)()
     st = _lib.Stats()
     reg = (C.c_uint64 * 4)()
     for t in (1, 2, 3, 4, 9, 255):
         reg[t >> 6] |= 1 << (t & 63)
     nh = C.c_uint32()
     with ctx.lock:
-        _lib.check(ctx.lib.ambc_decompress_ex(ctx.h, _lib.addr(body), len(body), original_length, reg,
+        _lib.check(ctx.lib.ambc_decompress_ex(ctx.h, _lib.addr(body), len(body), osz, reg,
                                               C.addressof(out), None, 0, C.byref(nh), C.byref(st)),
                    ctx.lib)
-    produced = min(int(st.payload_bytes), original_length)
+    produced = min(int(st.payload_bytes), osz)
     return bytes(out[:produced])
 
 
@@ -305,9 +310,14 @@ class _XZEncoders:
     6 with the 16 MiB dictionary: what _lzma builds from that spec), same
     check, one LZMA_FINISH pass: the same bytes -- checked against Python's lzma
     on a probe when the pool is first used; a mismatch (or no liblzma) leaves
-    Python's lzma in charge.  At most SIZE encoders exist; a caller waits for one."""
+    Python's lzma in charge.  At most size() encoders exist -- set by a memory
+    budget (AMBC_LZMA_MEM bytes, default a quarter of the host's memory capped at
+    8 GiB, ~190 MiB per encoder), at most 64 -- and a caller waits for one (the
+    Python fallback is bounded the same way).  release() ends the idle encoders
+    (lzma_end): the host scorer calls it when a walk is done, so the ~190 MiB each
+    are not kept between calls."""
 
-    SIZE = 8
+    ENC_BYTES = 190 << 20
 
     class _Stream(C.Structure):          # lzma_stream (LZMA_STREAM_INIT: all zeros)
         _fields_ = [("next_in", C.c_void_p), ("avail_in", C.c_size_t), ("total_in", C.c_uint64),
@@ -319,11 +329,31 @@ class _XZEncoders:
 
     _pool = None
     _lock = threading.Lock()
+    _size = None
+    _sem = None
+
+    @classmethod
+    def size(cls):
+        """encoders at once, from the memory budget"""
+        if cls._size is None:
+            budget = os.environ.get("AMBC_LZMA_MEM")
+            if budget:
+                budget = int(budget)
+            else:
+                try:
+                    phys = os.sysconf("SC_PHYS_PAGES") * os.sysconf("SC_PAGE_SIZE")
+                except (ValueError, OSError):
+                    phys = 8 << 30
+                budget = min(8 << 30, phys // 4)
+            cls._size = max(1, min(64, budget // cls.ENC_BYTES))
+            cls._sem = threading.BoundedSemaphore(cls._size)
+        return cls._size
 
     @classmethod
     def pool(cls):
         """the encoder pool, or None when the liblzma path is unavailable"""
         with cls._lock:
+            cls.size()
             if cls._pool is None:
                 cls._pool = False
                 try:
@@ -339,7 +369,7 @@ class _XZEncoders:
                     lib.lzma_end.argtypes = [C.POINTER(cls._Stream)]
                     cls.lib = lib
                     free = queue.LifoQueue()
-                    for _ in range(cls.SIZE):
+                    for _ in range(cls._size):
                         free.put(cls())
                     probe = bytes(range(256)) * 40 + b"abcabcabd" * 300
                     if cls._encode(free, probe) == cls._python(probe):
@@ -356,6 +386,11 @@ class _XZEncoders:
         C.c_uint32.from_buffer(self.opt, 0).value = 1 << 24     # dict_size, the struct's first field
         self.flt = (self._Filter * 2)(self._Filter(0x21, C.addressof(self.opt)),   # LZMA_FILTER_LZMA2
                                       self._Filter((1 << 64) - 1, None))           # LZMA_VLI_UNKNOWN
+        self.strm = self._Stream()
+
+    def end(self):
+        """free the encoder's state (lzma_end); the next run() builds it again"""
+        type(self).lib.lzma_end(C.byref(self.strm))
         self.strm = self._Stream()
 
     def run(self, data):
@@ -389,7 +424,26 @@ class _XZEncoders:
     def compress(cls, data):
         free = cls.pool()
         data = bytes(data)
-        return cls._encode(free, data) if free is not None else cls._python(data)
+        if free is not None:
+            return cls._encode(free, data)
+        with cls._sem:
+            return cls._python(data)
+
+    @classmethod
+    def release(cls):
+        """lzma_end on every idle pooled encoder (their memory goes back now)"""
+        free = cls._pool
+        if not free:
+            return
+        held = []
+        while True:
+            try:
+                held.append(free.get_nowait())
+            except queue.Empty:
+                break
+        for enc in held:
+            enc.end()
+            free.put(enc)
 
 
 class LZMACompression(CompressionMethod):

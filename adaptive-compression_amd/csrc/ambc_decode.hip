@@ -282,7 +282,8 @@ __device__ int64_t dec_huffman(const uint8_t* p, uint32_t plen, uint32_t orig, u
         int have = 0;
         uint64_t nextbyte = 0;
         const uint64_t nbytes = (nbits + 7) / 8;
-        while (bp < nbits && o < orig) {
+        const uint64_t lim = orig ? orig : 1;   // (the reference tests len(out) >= orig after appending)
+        while (bp < nbits && o < lim) {
             while (have <= 56) {
                 const uint64_t b = nextbyte < nbytes ? bitsrc[nextbyte] : 0;
                 nextbyte++;
@@ -1189,6 +1190,8 @@ hipError_t launch_decode(int kind, const DecArgs& a, hipStream_t s) {
     case DEC_KIND_INFLATE_16K:
     case DEC_KIND_INFLATE_32K:
     case DEC_KIND_INFLATE_G: return launch_inflate(kind, a, s);
+    case DEC_KIND_HUFF_4K:
+    case DEC_KIND_HUFF_8K: return launch_huff(kind, a, s);
     default: hipLaunchKernelGGL(k_decode, dim3(a.n_list), dim3(64), 0, s, a); break;
     }
     return hipGetLastError();

@@ -16,6 +16,7 @@
 #include <cstring>
 #include <deque>
 #include <map>
+#include <set>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -70,6 +71,15 @@ int ambc_init(const int* device_ids, int n_devices, ambc_ctx** out) {
         return fail(AMBC_E_DEVICE, "no HIP device available (libambc_hip has no CPU fallback)");
     std::unique_ptr<ambc_ctx> ctx(new ambc_ctx());
     int nd = n_devices > 0 ? n_devices : 1;
+    if (device_ids && nd > 1) {
+        // in-process RCCL ranks (ambc_shard.cpp make_transports): every connection
+        // at ncclCommInitAll rather than inside a rank thread's first collective
+        // (RCCL 2.27 connects lazily and waits for its peers there).  Set here, once,
+        // when a multi-device ctx is made -- before any of the library's threads
+        // exist -- and only if the caller has not chosen (setenv's overwrite = 0).
+        std::set<int> distinct(device_ids, device_ids + nd);
+        if ((int)distinct.size() > 1) setenv("NCCL_RUNTIME_CONNECT", "0", 0);
+    }
     for (int i = 0; i < nd; i++) {
         Dev d;
         d.id = device_ids ? device_ids[i] : i;
@@ -944,6 +954,13 @@ bool make_job(const uint8_t* body, uint64_t blen, uint64_t hp, uint32_t ord, con
         kind = DEC_KIND_LIGHT;
     } else {
         if (t == 255 || t == 1 || t == 4) kind = DEC_KIND_LIGHT;
+        if (t == 3) {
+            // AMBC_HUFF_ROUTE (A/B, tests): 0 = the serial k_decode, 8 = the 8 KiB kernel
+            static const char* hr = getenv("AMBC_HUFF_ROUTE");
+            kind = huff_kind(orig, clen);
+            if (hr && atoi(hr) == 0) kind = DEC_KIND_HEAVY;
+            else if (hr && atoi(hr) == 8 && kind == DEC_KIND_HUFF_4K) kind = DEC_KIND_HUFF_8K;
+        }
         j.type = t;
         if (t == 9 && clen) {
             const uint64_t cb = lz4_content_bound(body + pos, clen);

@@ -97,7 +97,12 @@ enum : int { DEC_KIND_LIGHT = 0, DEC_KIND_LZ4_4K = 1, DEC_KIND_LZ4_8K = 2, DEC_K
              DEC_KIND_LZ4_G = 4, DEC_KIND_INFLATE_4K = 5, DEC_KIND_INFLATE_8K = 6,
              DEC_KIND_INFLATE_16K = 7, DEC_KIND_HEAVY = 8, DEC_KIND_DICT_4K = 9, DEC_KIND_DICT_8K = 10,
              DEC_KIND_DICT_16K = 11, DEC_KIND_INFLATE_32K = 12,
-             DEC_KIND_INFLATE_G = 13, DEC_KINDS = 14 };
+             DEC_KIND_INFLATE_G = 13, DEC_KIND_HUFF_4K = 14, DEC_KIND_HUFF_8K = 15, DEC_KINDS = 16 };
+// Huffman packages for k_decode_huff<4096|8192> (ambc_huffdec.hip), else k_decode
+__host__ __device__ constexpr int huff_kind(uint32_t orig, uint32_t clen) {
+    return clen && orig <= 4096 && clen <= 4096 ? DEC_KIND_HUFF_4K
+         : clen && orig <= 8192 && clen <= 8192 ? DEC_KIND_HUFF_8K : DEC_KIND_HEAVY;
+}
 constexpr uint32_t DEC_PRODUCED_HOST = 0xFFFFFFFEu;  // k_decode_inflate: output too large, inflate on host
 
 constexpr uint32_t DEC_VERBATIM = 256;
@@ -199,6 +204,7 @@ hipError_t scan_sizes(const uint64_t* sizes, uint64_t* off, uint32_t count, void
 hipError_t launch_copy(uint8_t* dst, const uint8_t* src, uint64_t len, hipStream_t s);
 hipError_t launch_decode(int kind, const DecArgs& a, hipStream_t s);
 hipError_t launch_inflate(int kind, const DecArgs& a, hipStream_t s);   // ambc_inflate.hip
+hipError_t launch_huff(int kind, const DecArgs& a, hipStream_t s);      // ambc_huffdec.hip
 // the fixed-Huffman (btype 1) decode tables, built once per device into out
 constexpr int INF_LUTB = 9;   // primary lookup bits of the inflate tables (longer codes: canonical search)
 constexpr size_t INF_FIXED_U16 = 2 * (1 << INF_LUTB) + 2 * 288 + 3 * 2 * 16;

@@ -52,6 +52,11 @@ struct Transport {
     virtual void abort() {}
 };
 
+// connect_group's Send / Recv warm-up: every rank sends rank 0 one piece of
+// this size, as the gather does (RCCL spreads a p2p operation of a size over the
+// peer's channels and connects each on first use: an 8-byte warm-up connects one)
+constexpr uint64_t kP2pPiece = 64ull << 20;
+
 // ---------------------------------------------------------------------------
 // RCCL (one rank per device)
 // ---------------------------------------------------------------------------
@@ -111,8 +116,10 @@ struct RcclTransport : Transport {
     }
     int gather(const uint8_t* src, uint8_t* dst, const uint64_t* offs, const uint64_t* lens, int root) override {
         HIPCHK(hipSetDevice(d.id));
-        // pieces of at most 1 GiB per send/recv (both sides cut the same way)
-        constexpr uint64_t PIECE = 1ull << 30;
+        // pieces of kP2pPiece bytes per send/recv (both sides cut the same way):
+        // the size connect_group's warm-up sent, so no piece needs a p2p channel
+        // that the warm-up left unconnected (§7 of DESIGN.md)
+        const uint64_t PIECE = kP2pPiece;
         int rc = enqueue([&](ncclComm_t c) -> int {
             NCCLCHK(ncclGroupStart());
             if (r == root) {
@@ -423,20 +430,31 @@ static int connect_group(ambc_ctx* ctx) {
         }
         NCCLCHK(ncclGroupEnd());
     }
-    NCCLCHK(ncclGroupStart());
+    // the gather's Send / Recv pairs at its piece size and at a small size
+    // (device scratch: rank 0 receives G - 1 pieces)
+    std::vector<Buf> wb(G);
     for (int g = 0; g < G; g++) {
-        Dev& d = ctx->devs[g];
-        uint8_t* buf = d.coll.as<uint8_t>();
-        if (g == 0) {
-            for (int q = 1; q < G; q++) NCCLCHK(ncclRecv(buf + 8 * q, 8, ncclUint8, q, ctx->dev_comms[0], d.stream));
-        } else {
-            NCCLCHK(ncclSend(buf, 8, ncclUint8, 0, ctx->dev_comms[g], d.stream));
-        }
+        HIPCHK(hipSetDevice(ctx->devs[g].id));
+        HIPCHK(wb[g].ensure((size_t)(g == 0 ? std::max(1, G - 1) : 1) * kP2pPiece));
     }
-    NCCLCHK(ncclGroupEnd());
+    for (uint64_t bytes : {kP2pPiece, (uint64_t)8}) {
+        NCCLCHK(ncclGroupStart());
+        for (int g = 0; g < G; g++) {
+            Dev& d = ctx->devs[g];
+            uint8_t* buf = wb[g].as<uint8_t>();
+            if (g == 0) {
+                for (int q = 1; q < G; q++)
+                    NCCLCHK(ncclRecv(buf + (q - 1) * kP2pPiece, bytes, ncclUint8, q, ctx->dev_comms[0], d.stream));
+            } else {
+                NCCLCHK(ncclSend(buf, bytes, ncclUint8, 0, ctx->dev_comms[g], d.stream));
+            }
+        }
+        NCCLCHK(ncclGroupEnd());
+    }
     for (int g = 0; g < G; g++) {
         HIPCHK(hipSetDevice(ctx->devs[g].id));
         HIPCHK(hipStreamSynchronize(ctx->devs[g].stream));
+        wb[g].release();
     }
     return AMBC_OK;
 }
@@ -454,10 +472,9 @@ static int make_transports(ambc_ctx* ctx, std::unique_ptr<Hub>& hub, std::vector
             std::vector<int> dl;
             for (auto& d : ctx->devs) dl.push_back(d.id);
             ctx->dev_comms.assign(G, nullptr);
-            // every connection at init (RCCL 2.27 connects lazily inside a rank's
-            // first collective, where it waits for its peers) -- unless the caller
-            // chose otherwise -- and the warm-up below connects the rest
-            setenv("NCCL_RUNTIME_CONNECT", "0", 0);
+            // every connection at init (NCCL_RUNTIME_CONNECT=0, set by ambc_init
+            // for a multi-device ctx unless the caller chose otherwise), and the
+            // warm-up below connects whatever the init leaves to the first call
             NCCLCHK(ncclCommInitAll(ctx->dev_comms.data(), G, dl.data()));
             ctx->comm_gate.reset();
             if (int rc = connect_group(ctx)) {

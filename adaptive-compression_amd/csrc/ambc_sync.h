@@ -154,8 +154,12 @@ struct Hub {
 // the aborter raises the flag, waits until no enqueue is in progress, then aborts.
 // (seq_cst on both sides: an enqueuer that saw the flag down is seen by the
 // aborter's count.)  An enqueue returns without waiting for peers because the
-// communicators are connected eagerly when they are created (ambc_shard.cpp,
-// make_transports), so the aborter's wait is short.
+// communicators are connected eagerly when they are created -- every collective
+// kind at every size the calls use, and the gather's Send / Recv at its piece
+// size (ambc_shard.cpp, connect_group) -- so the aborter's wait is short.  It is
+// bounded all the same (AMBC_ABORT_WAIT_MS, default 20 s): an enqueue still
+// inside its call by then is stuck on a peer that will never join, and only the
+// abort can release it, so kill() runs anyway (abort() then returns false).
 struct AbortGate {
     std::atomic<int> inflight{0};
     std::atomic<bool> aborted{false};
@@ -167,13 +171,24 @@ struct AbortGate {
         return true;
     }
     void leave() { inflight.fetch_sub(1); }
-    // kill() runs once, after every enqueue in progress has left; later enter()s fail
+    static uint64_t default_wait_ms() {
+        const char* e = getenv("AMBC_ABORT_WAIT_MS");
+        return e && *e ? strtoull(e, nullptr, 10) : 20000;
+    }
+    // kill() runs once, after every enqueue in progress has left or after wait_ms
+    // (false: it ran with an enqueue still inside); later enter()s fail
     template <typename F>
-    void abort(F&& kill) {
+    bool abort(F&& kill, uint64_t wait_ms = default_wait_ms()) {
         std::lock_guard<std::mutex> g(abort_mu);
-        if (aborted.exchange(true)) return;
-        while (inflight.load() != 0) std::this_thread::yield();
+        if (aborted.exchange(true)) return true;
+        const auto t0 = std::chrono::steady_clock::now();
+        bool clean = true;
+        while (inflight.load() != 0) {
+            if (std::chrono::steady_clock::now() - t0 >= std::chrono::milliseconds(wait_ms)) { clean = false; break; }
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
         kill();
+        return clean;
     }
     void reset() { aborted.store(false); }   // a fresh group (no rank thread running)
 };

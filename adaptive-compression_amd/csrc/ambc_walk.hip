@@ -419,6 +419,7 @@ __device__ __forceinline__ void walk_job(const WalkArgs& A, uint32_t r, uint64_t
             kind = DEC_KIND_LIGHT;
         } else {
             if (t == 255 || t == 1 || t == 4) kind = DEC_KIND_LIGHT;
+            if (t == 3) kind = huff_kind(orig, clen);
             j.type = t;
             if (t == 9 && clen) {
                 const uint8_t* pl = h + 18;

@@ -198,6 +198,13 @@ struct WalkConfig {
     bool noprio = false;        // launch the round's sizes in request order
     bool launch_desc = false;   // launch them largest first (default: largest, then smallest first)
     bool noshare = false;       // no LZ4 parse shared across sizes
+    // host-scored codecs (ids 6 / 7 / 8, ambc_host_codecs): the positions of a walk's
+    // guess chain that also get the host codecs (0: the walk's own position only;
+    // -1: by default, below), and whether breadth positions get them (default no):
+    // a host evaluation costs ~100 ms of a core per position (bz2 at eight sizes,
+    // LZMA at five), a device one microseconds
+    int hspec = -1;
+    bool hbreadth = false;
     static WalkConfig from_env() {
         WalkConfig c;
         if (const char* e = getenv("AMBC_MS_WALKS")) c.walks = strtoull(e, nullptr, 10);
@@ -209,6 +216,8 @@ struct WalkConfig {
         c.noprio = getenv("AMBC_MS_NOPRIO") != nullptr;
         c.launch_desc = getenv("AMBC_MS_LAUNCH_DESC") != nullptr;
         c.noshare = getenv("AMBC_MS_NOSHARE") != nullptr;
+        if (const char* e = getenv("AMBC_MS_HSPEC")) c.hspec = atoi(e);
+        c.hbreadth = getenv("AMBC_MS_HBREADTH") != nullptr;
         return c;
     }
 };
@@ -399,7 +408,7 @@ int walk_decide(B& be, WalkMemory& mem, WalkPool& pool, const WalkConfig& cfg, u
         }
         req[(size_t)req_in[ci]].second.push_back(pos);
     };
-    auto request = [&](uint64_t pos) {
+    auto request = [&](uint64_t pos, bool host) {
         const Sizes& z = sizes_at(pos);
         const bool in = &z == &inner;
         PosTable::Rec& r = T.at(pos);
@@ -409,7 +418,7 @@ int walk_decide(B& be, WalkMemory& mem, WalkPool& pool, const WalkConfig& cfg, u
         }
         for (uint32_t i = 0; i < nc; i++) {
             if (!((z.canon >> i) & 1)) continue;
-            if (hc && !(((r.hhave | r.hreq) >> i) & 1)) {
+            if (hc && host && !(((r.hhave | r.hreq) >> i) & 1)) {
                 r.hreq |= 1u << i;
                 hpos.push_back(pos);
                 hsize.push_back(z.S[i]);
@@ -496,6 +505,7 @@ int walk_decide(B& be, WalkMemory& mem, WalkPool& pool, const WalkConfig& cfg, u
     // 0.31 / 0.34 / 0.28, profiles/r4_spec_ab)
     const bool z9walk = (p->flags & AMBC_FLAG_ZLIB9) && ((p->method_mask >> AMBC_M_DEFLATE) & 1);
     const int SPEC = cfg.spec >= 0 ? cfg.spec : (lzshare ? 6 : z9walk ? 1 : 0);
+    const int HSPEC = cfg.hspec >= 0 ? cfg.hspec : SPEC;
     const int GROUPS = cfg.groups;
     using Job = std::pair<std::pair<uint32_t, int>, std::vector<uint64_t>>;
     struct Group {
@@ -620,12 +630,15 @@ int walk_decide(B& be, WalkMemory& mem, WalkPool& pool, const WalkConfig& cfg, u
                 // the walk's own position is always asked for again (its record
                 // knows what is requested already): a speculative request there
                 // may have been forgotten (a size check_size refuses), and the walk
-                // would otherwise wait for it forever
-                ask(w.pos);
+                // would otherwise wait for it forever; host codecs skipped on a guess
+                // are asked for here once the walk stands on it
+                ask(w.pos, true);
+                // (host codecs for the guesses within HSPEC that the skipped prefix holds)
+                for (int kk = 1; kk < k && kk <= HSPEC; kk++) ask(w.pos + (uint64_t)kk * w.last, true);
             }
             for (; k <= SPEC && q < n; k++, q += w.last) {
                 if (k && rec_of(q).decided) break;
-                ask(q);
+                ask(q, k <= HSPEC);
             }
             w.cs = w.last;
             w.cq = q;
@@ -655,7 +668,7 @@ int walk_decide(B& be, WalkMemory& mem, WalkPool& pool, const WalkConfig& cfg, u
                     }
                     L.b[(size_t)bi].second.push_back(pos);
                 };
-                auto ask = [&](uint64_t pos) {
+                auto ask = [&](uint64_t pos, bool host) {
                     const Sizes& z = sizes_in(pos, scr);
                     const bool in = &z == &inner;
                     PosTable::Rec& r = T.touch(pos);
@@ -667,7 +680,7 @@ int walk_decide(B& be, WalkMemory& mem, WalkPool& pool, const WalkConfig& cfg, u
                     const uint32_t have = __atomic_load_n(&r.have, __ATOMIC_ACQUIRE);
                     for (uint32_t i = 0; i < nc; i++) {
                         if (!((z.canon >> i) & 1)) continue;
-                        if (hc && !((hhave >> i) & 1)) hwant |= 1u << i;
+                        if (hc && host && !((hhave >> i) & 1)) hwant |= 1u << i;
                         if (needs_o(z, i) && !((have >> i) & 1)) want |= 1u << i;
                     }
                     if (hwant) {
@@ -715,7 +728,7 @@ int walk_decide(B& be, WalkMemory& mem, WalkPool& pool, const WalkConfig& cfg, u
                     uint64_t q = w.pos + z.S[i];
                     for (uint64_t k = 0; k < depth && q < n; k++, q += z.S[i]) {
                         if (T.at(q).decided) break;
-                        request(q);
+                        request(q, cfg.hbreadth);
                     }
                 }
             }

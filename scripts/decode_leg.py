@@ -1,5 +1,6 @@
 """Repeat the bench's decode leg (AdaptiveCompressor._adaptive_decompress of a
-device-compressed 4 GiB body) to see its spread: python scripts/decode_leg.py [reps]"""
+device-compressed 4 GiB body) to see its spread:
+python scripts/decode_leg.py [reps] [--methods 1,3,4]"""
 import ctypes as C
 import os
 import sys
@@ -12,13 +13,19 @@ sys.path[:0] = [REPO, os.path.join(REPO, "adaptive-compression_amd")]
 from ambc import AdaptiveCompressor, _lib  # noqa: E402
 
 n = 4 << 30
-reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+args = [a for a in sys.argv[1:]]
+methods = (1, 3, 4, 9)
+if "--methods" in args:
+    i = args.index("--methods")
+    methods = tuple(int(x) for x in args[i + 1].split(","))
+    del args[i:i + 2]
+reps = int(args[0]) if args else 3
 lib = _lib.load()
 data = np.empty(n, dtype=np.uint8)
 lib.ambc_synth_fill(data.ctypes.data_as(C.POINTER(C.c_uint8)), n, 20250418)
 raw = data.tobytes()
 del data
-comp = AdaptiveCompressor(chunk_size=4096)
+comp = AdaptiveCompressor(chunk_size=4096, methods=methods)
 body = comp._adaptive_compress(raw)
 for _ in range(reps):
     t = time.perf_counter()

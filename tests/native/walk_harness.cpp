@@ -144,6 +144,30 @@ static void test_gate() {
         CHECK(!gate.enter(), "gate: enter after abort");
         for (auto& c : comms) delete c;
     }
+    // an enqueuer that never returns by itself (a peer that never joins): abort()
+    // still completes after its bounded wait, kills the communicators -- which is
+    // what releases the stuck enqueuer -- and reports that it did not wait clean
+    {
+        AbortGate gate;
+        FakeComm* comm = new FakeComm();
+        std::atomic<bool> killed{false}, entered{false};
+        std::thread stuck([&] {
+            if (!gate.enter()) return;
+            comm->ops.fetch_add(1);                             // (the enqueue's last use of it)
+            entered = true;
+            while (!killed.load()) std::this_thread::sleep_for(std::chrono::milliseconds(1));   // "inside the call"
+            gate.leave();                                       // released by the abort: no further use
+        });
+        while (!entered.load()) std::this_thread::yield();
+        const auto t0 = std::chrono::steady_clock::now();
+        const bool clean = gate.abort([&] { delete comm; comm = nullptr; killed = true; }, 150);
+        const auto ms = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
+        stuck.join();
+        CHECK(!clean, "gate: a stuck enqueuer reported as clean");
+        CHECK(comm == nullptr, "gate: communicator not killed after the bounded wait");
+        CHECK(ms >= 140 && ms < 5000, "gate: bounded wait took %lld ms", (long long)ms);
+        CHECK(!gate.enter(), "gate: enter after a bounded abort");
+    }
 }
 
 // ---------------------------------------------------------------------------
