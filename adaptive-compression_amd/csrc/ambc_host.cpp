@@ -1995,6 +1995,12 @@ int ambc::decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t ori
             HIPCHK(hipMemsetAsync(d.seg.p, 0, (size_t)nj * 64, s));
             a.stamps = d.seg.as<unsigned long long>();
         }
+        const bool hdbg = getenv("AMBC_HUFF_DEBUG") && nj;   // k_decode_huff: per-lane segments of job 0
+        if (hdbg) {
+            HIPCHK(d.seg.ensure((size_t)nj * 4096));
+            HIPCHK(hipMemsetAsync(d.seg.p, 0, (size_t)nj * 4096, s));
+            a.stamps = d.seg.as<unsigned long long>();
+        }
         HIPCHK(hipEventRecord(d.ev[0], s));
         for (int k = 0; k < DEC_KINDS; k++) {
             a.list = d.list.as<uint32_t>() + base[k];
@@ -2002,7 +2008,16 @@ int ambc::decompress_on(Dev& d, const uint8_t* body, uint64_t blen, uint64_t ori
             HIPCHK(launch_decode(k, a, s));
         }
         HIPCHK(hipEventRecord(d.ev[1], s));
-        if (a.stamps) {
+        if (hdbg) {
+            std::vector<unsigned long long> sv(512);
+            HIPCHK(hipMemcpyAsync(sv.data(), d.seg.p, 4096, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            fprintf(stderr, "[ambc huff] nbits %llu rounds %llu\n", sv[7] >> 32, sv[7] & 0xFFFFFFFFull);
+            for (int l = 0; l < 64; l++)
+                fprintf(stderr, "[ambc huff] lane %2d s %6llu | pass1 f %10llu cnt %5llu ex %10llu | final f %10llu cnt %5llu ex %10llu\n",
+                        l, sv[l * 8], sv[l * 8 + 1], sv[l * 8 + 2], sv[l * 8 + 3], sv[l * 8 + 4], sv[l * 8 + 5], sv[l * 8 + 6]);
+            a.stamps = nullptr;
+        } else if (a.stamps) {
             std::vector<unsigned long long> sv((size_t)nj * 8);
             HIPCHK(hipMemcpyAsync(sv.data(), d.seg.p, (size_t)nj * 64, hipMemcpyDeviceToHost, s));
             HIPCHK(hipStreamSynchronize(s));

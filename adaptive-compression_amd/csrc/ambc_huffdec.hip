@@ -180,12 +180,13 @@ __device__ __forceinline__ void huff_scan(const HuffSmem<OUTMAX>& S, uint32_t st
 
 // returns the bytes produced into S.out, or -1 for a Python exception
 template <uint32_t OUTMAX>
-__device__ int64_t huff_decode(const uint8_t* p, uint32_t plen, uint32_t orig, HuffSmem<OUTMAX>& S, uint32_t lane) {
+__device__ int64_t huff_decode(const uint8_t* p, uint32_t plen, uint32_t orig, HuffSmem<OUTMAX>& S, uint32_t lane,
+                               unsigned long long* dbg) {
     // 1. the frequency table
     const uint32_t k = uniform_u32(p[0]);
     if (k && 1 + 5 * (k - 1) >= plen) return -1;
     for (uint32_t s = lane; s < 256; s += 64) S.t.last[s] = 0;
-    wave_sync();
+    __syncthreads();
     uint32_t eb[4], ec[4];
 #pragma unroll
     for (int t = 0; t < 4; t++) {
@@ -198,13 +199,13 @@ __device__ int64_t huff_decode(const uint8_t* p, uint32_t plen, uint32_t orig, H
             atomicMax(&S.t.last[eb[t]], e + 1);
         }
     }
-    wave_sync();
+    __syncthreads();
 #pragma unroll
     for (int t = 0; t < 4; t++) {
         const uint32_t e = lane + 64u * t;
         if (e < k && S.t.last[eb[t]] == e + 1) S.t.cnt[eb[t]] = ec[t];
     }
-    wave_sync();
+    __syncthreads();
     uint64_t key[4];
     uint32_t nid[4];
     uint32_t nf = 0;
@@ -239,7 +240,7 @@ __device__ int64_t huff_decode(const uint8_t* p, uint32_t plen, uint32_t orig, H
             }
         }
     }
-    wave_sync();
+    __syncthreads();
     const uint32_t root = 256 + nf - 2;
     // 3. the lookup table: 16 entries per lane, walked down together
     {
@@ -283,7 +284,7 @@ __device__ int64_t huff_decode(const uint8_t* p, uint32_t plen, uint32_t orig, H
             S.bits[w] = v;
         }
     }
-    wave_sync();
+    __syncthreads();
     // 5. 64 segments decoded at once, checked against each other
     const uint32_t seg = max(32u, ((nbits + 63) / 64 + 31) & ~31u);
     const uint32_t s = lane * seg;
@@ -294,7 +295,9 @@ __device__ int64_t huff_decode(const uint8_t* p, uint32_t plen, uint32_t orig, H
     } else {
         huff_scan(S, lane == 0 ? 0u : (s > HWARM ? s - HWARM : 0u), s, e, nbits, f, cnt, ex);
     }
-    for (int round = 0; round < 64; round++) {
+    if (dbg) { dbg[lane * 8 + 0] = s; dbg[lane * 8 + 1] = f; dbg[lane * 8 + 2] = cnt; dbg[lane * 8 + 3] = ex; }
+    int rounds = 0;
+    for (int round = 0; round < 64; round++, rounds++) {
         const uint32_t prev = AMBC_DPP(TERM, ex, 0x138, 0xF, 0xF, false);   // wave_shr:1 -> lane l-1's exit
         const bool bad = lane != 0 && f != prev;
         if (!__any(bad)) break;
@@ -303,13 +306,18 @@ __device__ int64_t huff_decode(const uint8_t* p, uint32_t plen, uint32_t orig, H
             else huff_scan(S, prev, s, e, nbits, f, cnt, ex);
         }
     }
+    if (dbg) { dbg[lane * 8 + 4] = f; dbg[lane * 8 + 5] = cnt; dbg[lane * 8 + 6] = ex; dbg[lane * 8 + 7] = rounds | (uint64_t)nbits << 32; }
     // 6. offsets, then every lane's symbols into the LDS output
     const uint32_t incl = wave_incl_sum(cnt);
     const uint32_t total = readlane(incl, 63);
     const uint32_t lim = max(orig, 1u);
     const uint32_t produced = min(total, lim);
-    uint32_t o = incl - cnt;
-    const uint32_t n = o < produced ? min(cnt, produced - o) : 0u;
+    const uint32_t o = incl - cnt;
+    // symbols this lane writes: those below `produced` (signed arithmetic: the
+    // unsigned form `o < produced ? min(cnt, produced - o) : 0` lost its guard in
+    // this kernel's code -- lanes past `produced` then wrote past the LDS output)
+    const int32_t room = (int32_t)produced - (int32_t)o;
+    const uint32_t n = room > 0 ? (uint32_t)min((int32_t)cnt, room) : 0u;
     if (n) {
         BitRd b;
         br_init(b, S.bits, f);
@@ -338,8 +346,8 @@ __global__ __launch_bounds__(64) void k_decode_huff(DecArgs A) {
     const uint32_t orig = uniform_u32(J.orig), clen = uniform_u32(J.clen);
     int64_t produced = 0;
     if (clen) {
-        const int64_t r = huff_decode<OUTMAX>(p, clen, orig, S, lane);
-        wave_sync();
+        const int64_t r = huff_decode<OUTMAX>(p, clen, orig, S, lane, A.stamps ? A.stamps + (uint64_t)blockIdx.x * 512 : nullptr);
+        __syncthreads();
         if (r < 0) {
             for (uint32_t i = lane; i < orig; i += 64) out[i] = 0;
             produced = orig;

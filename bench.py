@@ -357,6 +357,7 @@ def ref_walk_leg(ctx, nbytes, full_set=False, check_bytes=0):
     dt = time.perf_counter() - t
     steps, ev, wns, ens = C.c_uint32(), C.c_uint64(), C.c_uint64(), C.c_uint64()
     ctx.lib.ambc_last_multisize_info(comp._ctx().h, C.byref(steps), C.byref(ev), C.byref(wns), C.byref(ens))
+    cs = dict(comp.chunk_stats)                  # (the timed call's: the check below compresses again)
     ok = comp._adaptive_decompress(body, nbytes) == data
     ids = [m.type_id for m in comp.compression_methods]
     check = None
@@ -378,7 +379,7 @@ def ref_walk_leg(ctx, nbytes, full_set=False, check_bytes=0):
             "candidates": comp.CHUNK_SIZE_CANDIDATES, "bytes": nbytes,
             "input": "runs / text / skewed random, 8-64 KiB segments (scripts/multisize_bench.py mixed, seed 7)",
             "GBps": round(nbytes / dt / 1e9, 3), "seconds": round(dt, 4), "ratio": round(len(body) / nbytes, 5),
-            "packages": comp.chunk_stats["total_chunks"], "method_usage": comp.chunk_stats["method_usage"],
+            "packages": cs["total_chunks"], "method_usage": cs["method_usage"],
             "walk_rounds": steps.value, "chunk_encodes": ev.value,
             "walk_ms": round(wns.value / 1e6, 2), "final_encode_ms": round(ens.value / 1e6, 2),
             "round_trip_bit_exact": ok}
