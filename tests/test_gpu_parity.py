@@ -821,7 +821,8 @@ def test_multisize_refused_size_near_the_end_fails_not_hangs(ctx):
     ask again and fail (NotImplementedError), not wait forever.  Without that
     position on the path the body equals the oracle's walk."""
     text = synth.generate(5 * 4096 + 10000, 7)
-    for data in (text, bytes(4096) + text[4096:], bytes(len(text))):
+    zeros = bytes(len(text))        # its path is 0 -> 16384 -> end: never at the refused size
+    for data in (text, bytes(4096) + text[4096:], zeros):
         comp = _compressor(methods=(1, 2, 3, 4, 9))
         comp.CHUNK_SIZE_CANDIDATES = [16384, 4096]
         comp.method_chunk_prefs = dict(comp.method_chunk_prefs)
@@ -829,8 +830,14 @@ def test_multisize_refused_size_near_the_end_fails_not_hangs(ctx):
         try:
             body = comp._adaptive_compress(data)
         except NotImplementedError:
+            assert data is not zeros, "the all-zero input never stands at the refused position"
             continue
         assert comp._adaptive_decompress(body, len(data)) == data
+        if data is zeros:
+            prefs = dict(orc.PREFS)
+            prefs[2] = (128, 12288)
+            ref, _ = orc.compress_body_multisize(data, [16384, 4096], (1, 2, 3, 4, 9, 255), prefs=prefs)
+            assert body == ref
 
 
 def test_multisize_walk_as_the_input_arrives(ctx, monkeypatch):
