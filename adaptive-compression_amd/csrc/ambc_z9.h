@@ -71,6 +71,10 @@ __device__ __forceinline__ bool z9_gate(const EncArgs& A, uint32_t k, uint32_t n
 // block with its 16383rd symbol: chunks <= 16382 bytes hold one block, 64 KiB
 // at most five.
 constexpr uint32_t Z9B_NOSTORE = 1;   // flushed after the window slid, begun before 32768: no stored block
+// record word 1 of a chunk <= 8192 (one block): k_z9_parse found that id 5 cannot
+// win (no 3-byte string occurs twice, and the all-literal block's lower bound
+// loses); k_z9_heap / k_z9_code skip the chunk
+constexpr uint32_t Z9_LOSES = 0xFFFFFFFFu;
 template <int CMAX> struct Z9Rec {
     static constexpr uint32_t NBLK = (uint32_t)CMAX / 16383u + 1u;
     static constexpr uint32_t BLK = 2, MASK = BLK + 4 * NBLK, MATCH = MASK + CMAX / 32;
@@ -137,6 +141,7 @@ __global__ __launch_bounds__(64) void k_z9_heap(EncArgs A) {
     uint32_t T = 0;
     if (n > (uint32_t)CMAX || !z9_gate(A, k, n, T)) return;
     uint32_t* R = A.z9rec + (uint64_t)k * Z9Rec<CMAX>::STRIDE;
+    if (R[1] == Z9_LOSES) return;
     if (NB > 1 && blk >= R[1]) return;
     const uint16_t* F = reinterpret_cast<const uint16_t*>(R + Z9Rec<CMAX>::FREQ + 158 * blk);
     uint32_t* MG = R + Z9Rec<CMAX>::MERGE + 316 * blk;

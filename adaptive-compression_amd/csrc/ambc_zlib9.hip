@@ -457,6 +457,70 @@ __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t
     }
 }
 
+// A chunk id 5 cannot win, decided before the parse (round 6).  When no 3-byte
+// string occurs twice in the chunk, zlib's longest_match finds nothing anywhere
+// and deflate emits n literals in one block (n <= 8192 < 16383 symbols); that
+// block is at least min(dynamic, static, stored) long: dynamic >= 3 + 14 (HLIT,
+// HDIST, HCLEN) + 12 (four code-length codes) + n H0 (any prefix code of the
+// literals: Gibbs' inequality) + 1 (end of block) bits, static exactly 3 + 8 / 9
+// bits a literal + 7, stored n + 5 bytes; zlib adds 2 + 4 bytes.  If even that
+// bound loses (len + 18 >= T), so does id 5.  Random chunks (a third of the mixed
+// input) are decided here, without the sort, the walkers, k_z9_heap and
+// k_z9_code.  The repeat test is a hash set of the 3-byte strings in the sort's
+// arrays (lst .. seg, free until the sort): a string met twice, or a probe run
+// past 64 slots, means "maybe a match" (no decision).
+template <int CMAX>
+__device__ bool z9_cannot_win(Z9Smem<CMAX>& S, uint32_t n, uint32_t T, uint32_t wave, uint32_t lane) {
+    constexpr uint32_t NW = Z9Smem<CMAX>::NW, TT = 64u * NW, TB = 2u * (uint32_t)CMAX;
+    static_assert(offsetof(Z9Smem<CMAX>, slot) == offsetof(Z9Smem<CMAX>, lst) + 2 * CMAX &&
+                  offsetof(Z9Smem<CMAX>, bend32) == offsetof(Z9Smem<CMAX>, slot) + 2 * CMAX &&
+                  offsetof(Z9Smem<CMAX>, seg) == offsetof(Z9Smem<CMAX>, bend32) + 2 * ZNB &&
+                  4 * TB <= 4 * CMAX + 2 * ZNB + 4 * CMAX, "the hash set spans lst .. seg");
+    const uint32_t tid = wave * 64u + lane;
+    uint32_t* hist = S.seg + CMAX - 256;          // (the set's last slots hold no string yet)
+    for (uint32_t i = tid; i < 256; i += TT) hist[i] = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += TT) atomicAdd(&hist[S.ch[i]], 1u);
+    __syncthreads();
+    if (wave == 0) {
+        double ent = 0.0;
+        uint32_t stat = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t sy = lane + 64u * j, c = hist[sy];
+            if (c) ent += (double)c * log2((double)n / (double)c);
+            stat += c * (sy < 144 ? 8u : 9u);
+        }
+        ent = wave_sum<double>(ent);
+        stat = wave_sum_u32(stat);
+        const uint64_t dyn = 30 + (uint64_t)floor(ent * (1.0 - 1e-12));
+        const uint64_t sta = 3 + (uint64_t)stat + 7;
+        const uint64_t body = min((min(dyn, sta) + 7) / 8, (uint64_t)n + 5);
+        if (lane == 0) S.nmatch = body + 6 + 18 >= T ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!S.nmatch) return false;
+    uint32_t* tab = reinterpret_cast<uint32_t*>(S.lst);
+    for (uint32_t i = tid; i < TB; i += TT) tab[i] = 0;
+    __syncthreads();
+    bool rep = false;
+    for (uint32_t i = tid; i + 3 <= n; i += TT) {
+        const uint32_t g = z_gram(S, i) + 1u;
+        uint32_t h = (g * 2654435761u) >> (32 - __builtin_ctz(TB));
+        for (int pr = 0; pr < 64; pr++) {
+            const uint32_t old = atomicCAS(&tab[h], 0u, g);
+            if (old == 0u) break;
+            if (old == g || pr == 63) { rep = true; break; }
+            h = (h + 1u) & (TB - 1u);
+        }
+    }
+    if (lane == 0) S.nmatch = 0;
+    __syncthreads();
+    if (__any(rep) && lane == 0) S.nmatch = 1;   // (wave-level any, then one LDS flag)
+    __syncthreads();
+    return S.nmatch == 0;
+}
+
 #ifdef AMBC_STAMPS
 // diagnostic build only: wave 0's phase cycles per parsed chunk in
 // A.stamps[(2 M + k) * 8 + phase] (k_dict's slots; phase 7 = 1 marks a parse)
@@ -506,6 +570,14 @@ __global__ __launch_bounds__(64 * Z9Cfg<CMAX>::NW) void k_z9_parse(EncArgs A) {
     }
     __syncthreads();
     PSTAMP(0);
+    {
+        uint32_t* R0 = A.z9rec + (uint64_t)k * Z9Rec<CMAX>::STRIDE;
+        if (z9_cannot_win(S, n, T, wave, lane)) {
+            if (threadIdx.x == 0) R0[1] = Z9_LOSES;
+            return;
+        }
+        if (threadIdx.x == 0) R0[1] = 0;
+    }
     z9_sort(S, n - 2, wave, lane);
     for (uint32_t i = threadIdx.x; i < (uint32_t)CMAX; i += 64u * NW) S.seg[i] = 0;
     z9_literal_mask(S, n, wave, lane);
@@ -647,6 +719,7 @@ __global__ __launch_bounds__(64) void k_z9_code(EncArgs A) {
     ZSTAMP_DECL
     const uint8_t* src = A.in + pos0;
     const uint32_t* R = A.z9rec + (uint64_t)k * Z9Rec<CMAX>::STRIDE;
+    if (R[1] == Z9_LOSES) return;                    // (k_z9_parse: id 5 cannot win)
     const uint32_t* rec = R + Z9Rec<CMAX>::MATCH;   // the path's matches, L | dist << 16
     constexpr uint32_t nblk = Z_NBLK;
     static_assert(CMAX < (int)Z_BLKSYM, "one block per chunk");

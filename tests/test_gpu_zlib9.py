@@ -180,3 +180,55 @@ def test_zlib9_big_random_chunk_contents(ctx):
     data = b"".join(parts)
     for chunk in (9008, 16384, 24576, 32768, 65536):
         assert _check(data, chunk, (5,), modes=("native",)) > 0
+
+
+def _de_bruijn(k, n):
+    """de Bruijn sequence B(k, n): every n-symbol string over k symbols exactly once"""
+    a, seq = [0] * k * n, []
+
+    def db(t, p):
+        if t > n:
+            if n % p == 0:
+                seq.extend(a[1:p + 1])
+        else:
+            a[t] = a[t - p]
+            db(t + 1, p)
+            for j in range(a[t - p] + 1, k):
+                a[t] = j
+                db(t + 1, t)
+    db(1, 1)
+    return seq
+
+
+def test_zlib9_no_repeat_chunks_decided_before_the_parse(ctx):
+    """k_z9_parse decides chunks without a repeated 3-byte string from a lower
+    bound of the all-literal block (round 6): bodies still equal the oracle with
+    the system zlib, whether the bound loses (uniform random chunks) or not
+    (repeat-free chunks over 16 symbols, which zlib-9 compresses by Huffman
+    alone), and chunks with a single repeated string next to random bytes"""
+    rng = random.Random(77)
+    db16 = bytes(0x41 + x for x in _de_bruijn(16, 3))          # 4096 distinct 3-grams over 16 bytes
+    parts = []
+    for q in range(48):
+        kind = q % 6
+        if kind == 0:
+            parts.append(bytes(rng.getrandbits(8) for _ in range(4096)))
+        elif kind == 1:
+            s = rng.randrange(0, len(db16))
+            parts.append((db16 * 2)[s:s + 4096])
+        elif kind == 2:
+            b = bytearray(rng.getrandbits(8) for _ in range(4096))
+            b[3000:3003] = b[100:103]                               # one 3-byte repeat
+            parts.append(bytes(b))
+        elif kind == 3:
+            b = bytearray(rng.getrandbits(8) for _ in range(4096))
+            b[4093:4096] = b[7:10]                                  # the repeat ends the chunk
+            parts.append(bytes(b))
+        elif kind == 4:
+            parts.append(bytes(rng.choice(b"0123456789abcdef") for _ in range(4096)))   # many repeats
+        else:
+            parts.append(bytes(rng.getrandbits(7) for _ in range(4096)))                  # H0 ~ 7 bits
+    data = b"".join(parts)
+    for chunk, methods in ((4096, (1, 3, 4, 5)), (4096, (5,)), (2048, (1, 3, 5)), (8192, (1, 3, 4, 5, 9)),
+                           (1024, (5,))):
+        _check(data, chunk, methods)
