@@ -7,7 +7,8 @@ exceptions raised like the reference's.
 
 * ids 1, 2, 3, 4, 9 (RLE, Dictionary, Huffman, Delta, LZ4) and 255 run on the
   GPU through libambc_hip (single-chunk calls of the same kernels the batched
-  path uses; Dictionary emits the reference's own bytes for chunks <= 8192);
+  path uses; Dictionary emits the reference's own bytes for any window,
+  lookahead and length);
 * ids 5, 6, 7 are the reference's own stdlib library wrappers
   (advanced_compression.py:71-213) and id 8 its zstandard wrapper (:219-261,
   here over the system libzstd), registered so that reference-produced files
@@ -22,6 +23,7 @@ C-ABI call for the whole body.
 import bz2
 import ctypes as C
 import lzma
+import operator
 import os
 import queue
 import struct
@@ -152,23 +154,47 @@ class RLECompression(CompressionMethod):
         return _gpu_should_use(data)[1]
 
 
+def _gpu_dict_any(data, window, look):
+    """DictionaryCompression(window, look).compress(data) on k_da_* (any window,
+    lookahead and length)."""
+    ctx = _ctx()
+    n = len(data)
+    cap = 2 * n + 16                      # every token covers >= 1 byte with <= 2 bytes per byte
+    out = (C.c_uint8 * cap)()
+    olen = C.c_uint64()
+    clamp = lambda v: max(-(1 << 62), min(1 << 62, v))
+    with ctx.lock:
+        rc = ctx.lib.ambc_dict_encode(ctx.h, _lib.addr(data), n, clamp(window), clamp(look),
+                                      C.addressof(out), cap, C.byref(olen))
+    if rc == _lib.AMBC_E_CODEC:
+        # compression_methods.py:227: bytearray.append(match_len) with a match > 255 bytes
+        raise ValueError("byte must be in range(0, 256)")
+    _lib.check(rc, ctx.lib)
+    return bytes(out[:olen.value])
+
+
 class DictionaryCompression(CompressionMethod):
-    """compression_methods.py:183-343 on the GPU (k_dict: the reference's greedy
-    window-4096 / lookahead-32 parse, byte for byte; inputs up to 8192 bytes,
-    the method's preferred maximum chunk)."""
+    """compression_methods.py:183-343 on the GPU, byte for byte.  The reference's
+    defaults (window 4096, lookahead 32) on inputs up to 8192 bytes -- the
+    method's preferred maximum chunk -- run k_dict (the batched engine's kernel);
+    any other window, lookahead or length runs k_da_* (ambc_dictany.hip).  The
+    window and lookahead must be integers (operator.index; the reference's own
+    arithmetic raises TypeError for most other values as well)."""
     type_id = 2
 
     def __init__(self, window_size=4096, lookahead_size=32):
-        if (window_size, lookahead_size) != (4096, 32):
-            raise NotImplementedError("the GPU Dictionary encoder implements the reference's "
-                                      "defaults (window_size=4096, lookahead_size=32)")
         self.window_size = window_size
         self.lookahead_size = lookahead_size
 
     def compress(self, data):
-        if len(data) > 8192:
-            raise NotImplementedError("the GPU Dictionary encoder takes at most 8192 bytes")
-        return _gpu_encode(2, data)
+        data = bytes(data)
+        if not data:
+            return b""
+        window = operator.index(self.window_size)
+        look = operator.index(self.lookahead_size)
+        if (window, look) == (4096, 32) and len(data) <= 8192:
+            return _gpu_encode(2, data)
+        return _gpu_dict_any(data, window, look)
 
     def decompress(self, data, original_length):
         if not data:
@@ -176,7 +202,9 @@ class DictionaryCompression(CompressionMethod):
         return _gpu_decode(2, data, original_length)
 
     def should_use(self, data, threshold=0.9):
-        return _gpu_should_use(data)[2]
+        # :315-343 reads the first min(n, 1003) bytes, and from n >= 1003 on the
+        # same 1000 3-grams over a 1000-byte sample: the prefix decides
+        return _gpu_should_use(bytes(data[:1003]))[2]
 
 
 class HuffmanCompression(CompressionMethod):

@@ -835,6 +835,60 @@ extern "C" int ambc_encode_method(ambc_ctx* ctx, int method_id, const uint8_t* i
     return AMBC_OK;
 }
 
+extern "C" int ambc_dict_encode(ambc_ctx* ctx, const uint8_t* in, uint64_t n, int64_t window_size,
+                                int64_t lookahead_size, uint8_t* out, uint64_t out_cap, uint64_t* out_len) {
+    if (!ctx || ctx->devs.empty() || !out_len || (!in && n) || (!out && out_cap)) return fail(AMBC_E_INVAL, "NULL argument");
+    if (n == 0) { *out_len = 0; return AMBC_OK; }            // :202-203 empty -> b''
+    if (n >= (1ull << 32) - (1ull << 24)) return fail(AMBC_E_INVAL, "ambc_dict_encode takes n < 2^32 - 2^24");
+    Dev& d = ctx->devs[0];
+    HIPCHK(hipSetDevice(d.id));
+    hipStream_t s = d.stream;
+    struct Scratch {
+        Buf in, tok, tab, gtab, gent, gbase, bent, bbase, res, out;
+        ~Scratch() { for (Buf* b : {&in, &tok, &tab, &gtab, &gent, &gbase, &bent, &bbase, &res, &out}) b->release(); }
+    } sc;
+    const uint32_t nb = dict_any_blocks(n), ng = dict_any_groups(n);
+    HIPCHK(sc.in.ensure(n + 64));
+    HIPCHK(sc.tok.ensure(n * 4));
+    HIPCHK(sc.tab.ensure(dict_any_table_bytes(n)));
+    HIPCHK(sc.gtab.ensure(dict_any_gtable_bytes(n)));
+    HIPCHK(sc.gent.ensure((size_t)ng * 4));
+    HIPCHK(sc.gbase.ensure((size_t)ng * 8));
+    HIPCHK(sc.bent.ensure((size_t)nb * 4));
+    HIPCHK(sc.bbase.ensure((size_t)nb * 8));
+    HIPCHK(sc.res.ensure(8));
+    HIPCHK(hipMemsetAsync(sc.in.as<uint8_t>() + n, 0, 64, s));
+    HIPCHK(hipMemcpyAsync(sc.in.p, in, n, hipMemcpyHostToDevice, s));
+    DictAnyArgs a{};
+    a.in = sc.in.as<uint8_t>();
+    a.n = (uint32_t)n;
+    const int64_t lim = 1ll << 62;
+    a.window = std::max(-lim, std::min(lim, window_size));
+    a.look = std::max(-lim, std::min(lim, lookahead_size));
+    a.tok = sc.tok.as<uint32_t>();
+    a.tab = sc.tab.as<uint64_t>();
+    a.gtab = sc.gtab.as<uint64_t>();
+    a.gent = sc.gent.as<uint32_t>();
+    a.gbase = sc.gbase.as<uint64_t>();
+    a.bent = sc.bent.as<uint32_t>();
+    a.bbase = sc.bbase.as<uint64_t>();
+    a.res = sc.res.as<uint64_t>();
+    HIPCHK(launch_dict_any_parse(a, s));
+    uint64_t res = 0;
+    HIPCHK(hipMemcpyAsync(&res, a.res, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (res >> 63) return fail(AMBC_E_CODEC, "a match longer than 255 bytes (the reference's bytearray.append raises)");
+    const uint64_t olen = res & ((1ull << 48) - 1);
+    *out_len = olen;
+    if (olen > out_cap) return fail(AMBC_E_CAPACITY, "output buffer too small");
+    HIPCHK(sc.out.ensure(olen + 16));
+    a.out = sc.out.as<uint8_t>();
+    HIPCHK(launch_dict_any_emit(a, s));
+    HIPCHK(hipMemcpyAsync(out, a.out, olen, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return AMBC_OK;
+}
+
 extern "C" int ambc_analyze(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const ambc_params* p,
                             uint8_t* ids_out, uint32_t* plen_out, uint8_t* su_out) {
     if (!ctx || ctx->devs.empty() || (!in && n)) return fail(AMBC_E_INVAL, "NULL argument");

@@ -182,6 +182,28 @@ hipError_t launch_walk_check(const WalkArgs& a, hipStream_t s);
 hipError_t launch_encode(const EncArgs& a, hipStream_t s);
 hipError_t launch_deflate(const EncArgs& a, hipStream_t s);   // ambc_deflate.hip
 hipError_t launch_dict(const EncArgs& a, uint32_t cmax, hipStream_t s);   // ambc_dict.hip
+// DictionaryCompression(window, lookahead) for any window / lookahead / length
+// (ambc_dictany.hip): device scratch sized by the dict_any_* helpers
+struct DictAnyArgs {
+    const uint8_t* in;     // n bytes + 64 zero bytes of padding
+    uint32_t n;
+    int64_t window, look;  // the plugin's window_size / lookahead_size (clamped to +-2^62)
+    uint32_t* tok;         // n: every position's token
+    uint64_t* tab;         // dict_any_table_bytes(n): per block and entry offset
+    uint64_t* gtab;        // dict_any_gtable_bytes(n): per group and entry offset
+    uint32_t* gent;        // groups: entry offset
+    uint64_t* gbase;       // groups: output base
+    uint32_t* bent;        // blocks: entry offset
+    uint64_t* bbase;       // blocks: output base
+    uint64_t* res;         // [0] = body bytes | 1 << 63 when a path token is longer than 255 bytes
+    uint8_t* out;          // the body (emit)
+};
+uint32_t dict_any_blocks(uint64_t n);
+uint32_t dict_any_groups(uint64_t n);
+uint64_t dict_any_table_bytes(uint64_t n);
+uint64_t dict_any_gtable_bytes(uint64_t n);
+hipError_t launch_dict_any_parse(const DictAnyArgs& a, hipStream_t s);
+hipError_t launch_dict_any_emit(const DictAnyArgs& a, hipStream_t s);
 // id 5 as zlib.compress(data, 9) (ambc_zlib9.hip): chunk_size <= z9 limit; the
 // record scratch is n_chunks x z9_rec_words(z9_cmax(chunk_size)) u32 words
 uint32_t z9_cmax(uint32_t chunk);   // 0: no zlib-9 encoder for this chunk size

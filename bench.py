@@ -82,7 +82,7 @@ def parse():
     ap.add_argument("--ref-walk-check-bytes", type=int, default=4 << 20,
                     help="prefix on which the cpu_baseline leg times the oracle's reference walk and "
                          "compares its body with the GPU's")
-    ap.add_argument("--ref-full-walk-bytes", type=int, default=4 << 20,
+    ap.add_argument("--ref-full-walk-bytes", type=int, default=16 << 20,
                     help="the reference's default compress() path with its whole stdlib method set "
                          "(like_reference(full_set=True): {1..7}, bz2 / LZMA scored on host threads) "
                          "on this many bytes; 0: skip")

@@ -219,6 +219,14 @@ int ambc_encode_method(ambc_ctx* ctx, int method_id, const uint8_t* in, uint32_t
                        uint32_t out_cap, uint32_t* out_len);
 int ambc_analyze(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const ambc_params* p, uint8_t* ids,
                  uint32_t* payload_len, uint8_t* should_use);
+/* DictionaryCompression(window_size, lookahead_size).compress(data) for any
+ * window, lookahead and length n < 2^32 - 2^24 (replaces compression_methods.py:
+ * 187-233 with :279-313; the lookahead is Python's slice data[pos:pos+lookahead],
+ * window <= 0 finds no match).  AMBC_E_CODEC where the reference raises (a
+ * match longer than 255 bytes reaches bytearray.append), AMBC_E_CAPACITY with
+ * *out_len = the body's size when out_cap is short. */
+int ambc_dict_encode(ambc_ctx* ctx, const uint8_t* in, uint64_t n, int64_t window_size,
+                     int64_t lookahead_size, uint8_t* out, uint64_t out_cap, uint64_t* out_len);
 
 /* ---------------------------------------------------------------------------
  * Multi-GPU.  The reference is single-threaded

@@ -171,6 +171,47 @@ EXPORT int64_t orc_dict_encode(const uint8_t* d, uint32_t n, uint8_t* out) {
     return o;
 }
 
+/* DictionaryCompression(window_size, lookahead_size).compress for any window,
+ * lookahead and length (compression_methods.py:187-233,279-313): the window
+ * start max(0, pos - window) (:294), the lookahead as Python's slice
+ * data[pos:pos + lookahead] (:295, negative stops wrap once), the earliest of
+ * the longest matches (:301-311).  Returns the output length, or -2 where the
+ * reference raises ValueError: a match longer than 255 bytes reaches
+ * bytearray.append (:227). */
+static int64_t py_slice_len(int64_t p, int64_t look, int64_t n) {
+    int64_t stop = p + look;
+    if (stop < 0) { stop += n; if (stop < 0) stop = 0; }
+    if (stop > n) stop = n;
+    return stop > p ? stop - p : 0;
+}
+EXPORT int64_t orc_dict_encode_wl(const uint8_t* d, uint32_t n, int64_t window, int64_t lookahead, uint8_t* out) {
+    if (n == 0) return 0;
+    int64_t o = 0;
+    uint32_t pos = 0;
+    while (pos < n) {
+        int64_t st = (int64_t)pos - window;
+        if (st < 0) st = 0;
+        const int64_t look = py_slice_len(pos, lookahead, n);
+        uint32_t best_pos = 0;
+        int64_t best_len = 0;
+        for (int64_t i = st; i < (int64_t)pos; i++) {
+            int64_t l = 0;
+            while (l < look && pos + l < n && d[i + l] == d[pos + l]) l++;
+            if (l > best_len) { best_pos = (uint32_t)i; best_len = l; }
+        }
+        if (best_len > 2) {
+            if (best_len > 255) return -2;
+            const uint32_t dist = pos - best_pos;
+            if (out) { out[o] = 1; out[o + 1] = dist & 0xFF; out[o + 2] = (dist >> 8) & 0xFF; out[o + 3] = (uint8_t)best_len; }
+            o += 4; pos += (uint32_t)best_len;
+        } else {
+            if (out) { out[o] = 0; out[o + 1] = d[pos]; }
+            o += 2; pos += 1;
+        }
+    }
+    return o;
+}
+
 static int cmp_u32(const void* a, const void* b) {
     uint32_t x = *(const uint32_t*)a, y = *(const uint32_t*)b;
     return x < y ? -1 : x > y;

@@ -62,6 +62,8 @@ def lib():
             getattr(_lib, name).argtypes = [u8p, u32]
             getattr(_lib, name).restype = C.c_int
         _lib.orc_huff_should_use.argtypes = [u8p, u32, u8p]
+        _lib.orc_dict_encode_wl.argtypes = [u8p, u32, C.c_int64, C.c_int64, u8p]
+        _lib.orc_dict_encode_wl.restype = i64
         _lib.orc_gd_parse.argtypes = [u8p, u32, u8p]
         _lib.orc_gd_parse.restype = u32
         _lib.orc_huff_should_use.restype = C.c_int
@@ -129,6 +131,21 @@ def huff_encode(d):
 
 def dict_encode(d):
     return _call_enc("orc_dict_encode", d, 2 * len(d) + 4)
+
+
+def dict_encode_wl(d, window_size, lookahead_size):
+    """DictionaryCompression(window_size, lookahead_size).compress(d) for any
+    window, lookahead and length (orc_dict_encode_wl); ValueError where the
+    reference's bytearray.append raises (a match longer than 255 bytes)."""
+    L = lib()
+    src = _buf(d)
+    out = (C.c_uint8 * max(1, 2 * len(d) + 4))()
+    clamp = lambda v: max(-(1 << 62), min(1 << 62, int(v)))
+    r = L.orc_dict_encode_wl(C.addressof(src), len(d), clamp(window_size), clamp(lookahead_size),
+                             C.addressof(out))
+    if r == -2:
+        raise ValueError("byte must be in range(0, 256)")
+    return bytes(out[:r])
 
 
 def lz4_frame_encode(d):

@@ -76,13 +76,10 @@ def test_dict_forced_matches_oracle(ctx):
         assert m.should_use(d) == orc.should_use(2, d), len(d)
 
 
-def test_dict_encode_limits(ctx):
+def test_dict_encode_empty(ctx):
     from ambc.methods import DictionaryCompression
     assert DictionaryCompression().compress(b"") == b""
-    with pytest.raises(NotImplementedError):
-        DictionaryCompression().compress(bytes(8193))
-    with pytest.raises(NotImplementedError):
-        DictionaryCompression(window_size=1024)
+    assert DictionaryCompression(window_size=7, lookahead_size=-3).compress(b"") == b""
 
 
 def _text_heavy(n, seed):
