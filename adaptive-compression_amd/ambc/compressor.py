@@ -155,7 +155,9 @@ class AdaptiveCompressor:
             self._warn_defaults = False
             warnings.warn("AdaptiveCompressor() defaults here are chunk_size=4096, mode='native', "
                           "methods (1, 3, 4, 9) -- not the reference's 8-candidate walk with its stdlib "
-                          "codecs; use AdaptiveCompressor.like_reference() for the closest match",
+                          "codecs; id-9 (LZ4) packages need python-lz4 on the reading side.  Use "
+                          "AdaptiveCompressor.like_reference() for the closest match, or methods=(1, 3, 4, 5) "
+                          "for files a stdlib-only reference decodes",
                           DefaultsWarning, stacklevel=3)
 
     @property
