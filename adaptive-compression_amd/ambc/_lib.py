@@ -37,7 +37,7 @@ MAX_CHUNK = 65536
 EXPORTS = (
     "ambc_abi_version", "ambc_last_error", "ambc_device_count", "ambc_init", "ambc_destroy",
     "ambc_compress_bound", "ambc_compress_batch", "ambc_decompress_batch", "ambc_decompress_ex",
-    "ambc_compress_device", "ambc_encode_method", "ambc_analyze", "ambc_dict_encode", "ambc_host_alloc",
+    "ambc_compress_device", "ambc_encode_method", "ambc_analyze", "ambc_dict_encode", "ambc_encode_any", "ambc_analyze_any", "ambc_host_alloc",
     "ambc_host_free", "ambc_device_alloc", "ambc_device_free", "ambc_memcpy_h2d",
     "ambc_memcpy_d2h", "ambc_synchronize", "ambc_synth_fill", "ambc_synth_device",
     "ambc_last_kernel_times", "ambc_split_body", "ambc_decompress_device",
@@ -111,6 +111,8 @@ def _declare(lib):
         "ambc_encode_method": ([vp, i32, u8p, u32, u8p, u32, C.POINTER(u32)], i32),
         "ambc_analyze": ([vp, u8p, u64, C.POINTER(Params), u8p, u8p, u8p], i32),
         "ambc_dict_encode": ([vp, u8p, u64, C.c_int64, C.c_int64, u8p, u64, C.POINTER(u64)], i32),
+        "ambc_encode_any": ([vp, i32, u8p, u64, u8p, u64, C.POINTER(u64)], i32),
+        "ambc_analyze_any": ([vp, u8p, u64, u64, C.POINTER(u32)], i32),
         "ambc_host_alloc": ([u64], vp),
         "ambc_host_free": ([vp], None),
         "ambc_device_alloc": ([vp, i32, u64], vp),

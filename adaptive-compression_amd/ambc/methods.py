@@ -67,13 +67,32 @@ def _ctx():
     return _lib.plugin_context()
 
 
+def _gpu_encode_any(mid, data):
+    """method.compress(data) past one chunk (RLE / Huffman / Delta / LZ4 at any
+    length: ambc_encode_any, ambc_anylen.hip)."""
+    n = len(data)
+    ctx = _ctx()
+    cap = 2 * n + 1344 if mid != 9 else n + n // 255 + 64 + 4 * (n // 65536 + 1)
+    out = (C.c_uint8 * cap)()
+    olen = C.c_uint64()
+    with ctx.lock:
+        rc = ctx.lib.ambc_encode_any(ctx.h, mid, _lib.addr(data), n, C.addressof(out), cap, C.byref(olen))
+    if rc == _lib.AMBC_E_CODEC:
+        raise ValueError(f"method {mid} cannot encode this input")
+    if rc == _lib.AMBC_E_RANGE:
+        # compression_methods.py:397: num_bits.to_bytes(4, 'little') past 2^32 bits
+        raise OverflowError("int too big to convert")
+    _lib.check(rc, ctx.lib)
+    return bytes(out[:olen.value])
+
+
 def _gpu_encode(mid, data):
     data = bytes(data)
     n = len(data)
     if n == 0:
         return b""
     if n > _lib.MAX_CHUNK:
-        raise ValueError(f"single-chunk GPU encode is limited to {_lib.MAX_CHUNK} bytes")
+        return _gpu_encode_any(mid, data)
     ctx = _ctx()
     cap = 2 * n + 1344                    # RLE worst case 2n; Huffman table + ~1.13n bits
     out = (C.c_uint8 * cap)()
@@ -95,7 +114,7 @@ def _gpu_should_use(data):
     if n == 0:
         return {1: False, 2: False, 3: False, 4: False}
     if n > _lib.MAX_CHUNK:
-        raise ValueError(f"single-chunk analysis is limited to {_lib.MAX_CHUNK} bytes")
+        return _gpu_should_use_any(data)
     from .compressor import entropy_terms
     ctx = _ctx()
     p = _lib.Params()
@@ -136,6 +155,33 @@ def _gpu_decode(mid, data, original_length):
                    ctx.lib)
     produced = min(int(st.payload_bytes), osz)
     return bytes(out[:produced])
+
+
+def _gpu_should_use_any(data):
+    """should_use past one chunk: the device's statistics (ambc_analyze_any: the
+    sampled pairs of RLE / Delta, the byte counts and first positions), the
+    reference's comparisons on them -- RLE (compression_methods.py:166-180) and
+    Delta (:652-667) over 1000 samples, Huffman's entropy summed in Counter order
+    with numpy's log2 (:562-574, the same float operations), Dictionary from the
+    first 1003 bytes (:329-343 read no more)."""
+    n = len(data)
+    ctx = _ctx()
+    step = max(1, n // 1000)
+    st = (C.c_uint32 * 514)()
+    with ctx.lock:
+        _lib.check(ctx.lib.ambc_analyze_any(ctx.h, _lib.addr(data), n, step, st), ctx.lib)
+    ss = min(1000, n)
+    rle = n >= 4 and st[0] / (ss - 1) > 0.3
+    delta = n >= 4 and st[1] / (ss - 1) > 0.5
+    huff = False
+    if n >= 100:
+        present = sorted((st[258 + b], st[2 + b]) for b in range(256) if st[2 + b])
+        entropy = 0
+        for _, count in present:
+            p = count / n
+            entropy -= p * np.log2(p)
+        huff = bool(entropy < 7.0)
+    return {1: bool(rle), 2: _gpu_should_use(bytes(data[:1003]))[2], 3: huff, 4: bool(delta)}
 
 
 class RLECompression(CompressionMethod):

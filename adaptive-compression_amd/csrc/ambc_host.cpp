@@ -889,6 +889,138 @@ extern "C" int ambc_dict_encode(ambc_ctx* ctx, const uint8_t* in, uint64_t n, in
     return AMBC_OK;
 }
 
+// one-block frames of k_encode (forced LZ4, 64 KiB chunks) -> one frame of
+// independent 64 KiB blocks (the same bytes as ambc_encode_method up to 64 KiB)
+static int lz4_any(Dev& d, const uint8_t* in, uint64_t n, Buf& dout, uint64_t* olen) {
+    ambc_params p{};
+    p.chunk_size = 65536;
+    p.method_mask = 1u << AMBC_M_LZ4;
+    for (int i = 0; i < 16; i++) { p.pref_min[i] = 0; p.pref_max[i] = 0xFFFFFFFFu; }
+    std::vector<uint8_t> ids;
+    std::vector<uint32_t> plen;
+    int rc = run_encode_only(d, in, n, &p, ENC_FORCE, ids, plen, nullptr, nullptr);
+    if (rc) return rc;
+    const uint32_t M = (uint32_t)plen.size();
+    std::vector<uint64_t> off(M + 1);
+    uint64_t o = 15;                                    // the frame header
+    for (uint32_t k = 0; k < M; k++) {
+        if (ids[k] != AMBC_M_LZ4 || plen[k] < 23) return fail(AMBC_E_DEVICE, "LZ4 block encode failed");
+        off[k] = o;
+        o += plen[k] - 19;                              // size field + block
+    }
+    off[M] = o;
+    *olen = o + 4;                                      // + the end mark
+    Buf doff;
+    struct Rel { Buf& b; ~Rel() { b.release(); } } rel{doff};
+    HIPCHK(doff.ensure((M + 1) * 8));
+    HIPCHK(dout.ensure(*olen + 16));
+    hipStream_t s = d.stream;
+    HIPCHK(hipMemcpyAsync(doff.p, off.data(), (M + 1) * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(launch_lz4_assemble(d.slots.as<uint8_t>(), slot_stride_for(65536, true), d.plen.as<uint32_t>(),   // (run_encode_only's, still on the device)
+                               doff.as<uint64_t>(), M, n, dout.as<uint8_t>(), s));
+    HIPCHK(hipStreamSynchronize(s));
+    return AMBC_OK;
+}
+
+extern "C" int ambc_encode_any(ambc_ctx* ctx, int method_id, const uint8_t* in, uint64_t n, uint8_t* out,
+                               uint64_t out_cap, uint64_t* out_len) {
+    if (!ctx || ctx->devs.empty() || !out_len || (!in && n) || (!out && out_cap)) return fail(AMBC_E_INVAL, "NULL argument");
+    if (method_id != AMBC_M_RLE && method_id != AMBC_M_HUFFMAN && method_id != AMBC_M_DELTA && method_id != AMBC_M_LZ4)
+        return fail(AMBC_E_INVAL, "ambc_encode_any supports ids 1, 3, 4 and 9 (id 2: ambc_dict_encode)");
+    if (n == 0) { *out_len = 0; return AMBC_OK; }
+    if (n >= (1ull << 32) - (1ull << 24)) return fail(AMBC_E_INVAL, "ambc_encode_any takes n < 2^32 - 2^24");
+    Dev& d = ctx->devs[0];
+    HIPCHK(hipSetDevice(d.id));
+    hipStream_t s = d.stream;
+    struct Scratch {
+        Buf in, out, a, b, c, e;
+        ~Scratch() { for (Buf* x : {&in, &out, &a, &b, &c, &e}) x->release(); }
+    } sc;
+    uint64_t olen = 0;
+    if (method_id == AMBC_M_LZ4) {
+        int rc = lz4_any(d, in, n, sc.out, &olen);
+        if (rc) return rc;
+    } else {
+        HIPCHK(sc.in.ensure(n + 64));
+        HIPCHK(hipMemcpyAsync(sc.in.p, in, n, hipMemcpyHostToDevice, s));
+        const uint8_t* din = sc.in.as<uint8_t>();
+        const uint32_t nb = any_blocks(n);
+        if (method_id == AMBC_M_DELTA) {
+            olen = n;
+            HIPCHK(sc.out.ensure(n));
+            HIPCHK(launch_delta_any(din, n, sc.out.as<uint8_t>(), s));
+        } else if (method_id == AMBC_M_RLE) {
+            HIPCHK(sc.a.ensure((size_t)(nb + 1) * 8));     // carry
+            HIPCHK(sc.b.ensure((size_t)(nb + 1) * 8));     // pair counts -> bases
+            HIPCHK(launch_rle_any_count(din, n, sc.a.as<int64_t>(), sc.b.as<int64_t>(), s));
+            int64_t np = 0;
+            HIPCHK(hipMemcpyAsync(&np, sc.b.as<int64_t>() + nb, 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            olen = 2ull * (uint64_t)np;
+            HIPCHK(sc.c.ensure((size_t)np * 4 + 4));
+            HIPCHK(sc.out.ensure(olen + 16));
+            HIPCHK(launch_rle_any_emit(din, n, sc.a.as<int64_t>(), sc.b.as<int64_t>(), sc.c.as<uint32_t>(), (uint64_t)np,
+                                       sc.out.as<uint8_t>(), s));
+        } else {   // Huffman
+            HIPCHK(sc.a.ensure(256 * 4 * 2 + 256 * 8 + 16));   // hist, first, codes, info
+            uint32_t* hist = sc.a.as<uint32_t>();
+            uint32_t* first = hist + 256;
+            uint64_t* codes = reinterpret_cast<uint64_t*>(first + 256);
+            int32_t* info = reinterpret_cast<int32_t*>(codes + 256);
+            HIPCHK(hipMemsetAsync(hist, 0, 1024, s));
+            HIPCHK(hipMemsetAsync(first, 0xFF, 1024, s));
+            HIPCHK(hipMemsetAsync(info, 0, 16, s));
+            HIPCHK(sc.e.ensure(1 + 5 * 256 + 4 + 16));         // the table and nbits
+            HIPCHK(launch_huff_any_hist(din, n, hist, first, s));
+            HIPCHK(launch_huff_any_tree(hist, first, codes, sc.e.as<uint8_t>(), info, s));
+            int32_t hi[4];
+            HIPCHK(hipMemcpyAsync(hi, info, 16, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            if (hi[0] == AMBC_E_CODEC) return fail(AMBC_E_CODEC, "Huffman on 1 or 256 distinct bytes (the reference raises)");
+            if (hi[0] == AMBC_E_RANGE) return fail(AMBC_E_RANGE, "Huffman bit count >= 2^32 (the reference's to_bytes(4) raises)");
+            const uint64_t hdr = (uint32_t)hi[1];
+            const uint64_t nbits = (uint64_t)(uint32_t)hi[2] | (uint64_t)(uint32_t)hi[3] << 32;
+            const uint64_t nbytes = (nbits + 7) / 8;
+            olen = hdr + nbytes;
+            HIPCHK(sc.b.ensure((size_t)(nb + 1) * 8));
+            HIPCHK(sc.c.ensure((size_t)(nbits / 32 + 2) * 4));
+            HIPCHK(hipMemsetAsync(sc.c.p, 0, (size_t)(nbits / 32 + 2) * 4, s));
+            HIPCHK(sc.out.ensure(olen + 16));
+            HIPCHK(hipMemcpyAsync(sc.out.p, sc.e.p, hdr, hipMemcpyDeviceToDevice, s));
+            HIPCHK(launch_huff_any_bits(din, n, codes, sc.b.as<int64_t>(), sc.c.as<uint32_t>(), nbytes,
+                                        sc.out.as<uint8_t>() + hdr, s));
+        }
+    }
+    *out_len = olen;
+    if (olen > out_cap) return fail(AMBC_E_CAPACITY, "output buffer too small");
+    HIPCHK(hipMemcpyAsync(out, sc.out.p, olen, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return AMBC_OK;
+}
+
+extern "C" int ambc_analyze_any(ambc_ctx* ctx, const uint8_t* in, uint64_t n, uint64_t step, uint32_t* stats) {
+    if (!ctx || ctx->devs.empty() || !stats || (!in && n) || step == 0) return fail(AMBC_E_INVAL, "bad argument");
+    if (n >= (1ull << 32) - (1ull << 24)) return fail(AMBC_E_INVAL, "ambc_analyze_any takes n < 2^32 - 2^24");
+    Dev& d = ctx->devs[0];
+    HIPCHK(hipSetDevice(d.id));
+    hipStream_t s = d.stream;
+    Buf din, st;
+    struct Rel { Buf& a; Buf& b; ~Rel() { a.release(); b.release(); } } rel{din, st};
+    HIPCHK(din.ensure(n + 64));
+    HIPCHK(st.ensure(514 * 4));
+    uint32_t* sv = st.as<uint32_t>();
+    HIPCHK(hipMemsetAsync(sv, 0, 258 * 4, s));
+    HIPCHK(hipMemsetAsync(sv + 258, 0xFF, 256 * 4, s));
+    if (n) {
+        HIPCHK(hipMemcpyAsync(din.p, in, n, hipMemcpyHostToDevice, s));
+        HIPCHK(launch_su_samples(din.as<uint8_t>(), n, step, sv, s));
+        HIPCHK(launch_huff_any_hist(din.as<uint8_t>(), n, sv + 2, sv + 258, s));
+    }
+    HIPCHK(hipMemcpyAsync(stats, sv, 514 * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return AMBC_OK;
+}
+
 extern "C" int ambc_analyze(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const ambc_params* p,
                             uint8_t* ids_out, uint32_t* plen_out, uint8_t* su_out) {
     if (!ctx || ctx->devs.empty() || (!in && n)) return fail(AMBC_E_INVAL, "NULL argument");

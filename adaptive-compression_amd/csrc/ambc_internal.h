@@ -204,6 +204,20 @@ uint64_t dict_any_table_bytes(uint64_t n);
 uint64_t dict_any_gtable_bytes(uint64_t n);
 hipError_t launch_dict_any_parse(const DictAnyArgs& a, hipStream_t s);
 hipError_t launch_dict_any_emit(const DictAnyArgs& a, hipStream_t s);
+// single-call plugins at any length (ambc_anylen.hip): blocks of 4 KiB, n < 2^32
+uint32_t any_blocks(uint64_t n);
+hipError_t launch_delta_any(const uint8_t* d, uint64_t n, uint8_t* out, hipStream_t s);
+hipError_t launch_rle_any_count(const uint8_t* d, uint64_t n, int64_t* carry, int64_t* cnt, hipStream_t s);
+hipError_t launch_rle_any_emit(const uint8_t* d, uint64_t n, const int64_t* carry, int64_t* cnt, uint32_t* pos,
+                               uint64_t np, uint8_t* out, hipStream_t s);
+hipError_t launch_huff_any_hist(const uint8_t* d, uint64_t n, uint32_t* hist, uint32_t* first, hipStream_t s);
+hipError_t launch_huff_any_tree(const uint32_t* hist, const uint32_t* first, uint64_t* codes, uint8_t* hdr, int32_t* info,
+                                hipStream_t s);
+hipError_t launch_huff_any_bits(const uint8_t* d, uint64_t n, const uint64_t* codes, int64_t* bb, uint32_t* be,
+                                uint64_t nbytes, uint8_t* out, hipStream_t s);
+hipError_t launch_su_samples(const uint8_t* d, uint64_t n, uint64_t step, uint32_t* out2, hipStream_t s);
+hipError_t launch_lz4_assemble(const uint8_t* slots, uint64_t stride, const uint32_t* plen, const uint64_t* off,
+                               uint32_t m, uint64_t n, uint8_t* out, hipStream_t s);
 // id 5 as zlib.compress(data, 9) (ambc_zlib9.hip): chunk_size <= z9 limit; the
 // record scratch is n_chunks x z9_rec_words(z9_cmax(chunk_size)) u32 words
 uint32_t z9_cmax(uint32_t chunk);   // 0: no zlib-9 encoder for this chunk size

@@ -64,7 +64,7 @@ extern "C" {
 
 /* GPU-routable method ids (bit i of method_mask = method id i) */
 #define AMBC_M_RLE 1
-#define AMBC_M_DICT 2  /* GPU encoder k_dict: the reference's bytes; chunks <= 8192 */
+#define AMBC_M_DICT 2  /* GPU encoder k_dict: the reference's bytes; batched chunks <= 8192 (any length: ambc_dict_encode) */
 #define AMBC_M_HUFFMAN 3
 #define AMBC_M_DELTA 4 /* never selected: payload length == n (compression_methods.py:598-608) */
 #define AMBC_M_DEFLATE 5 /* GPU encoder "ambc-deflate v1" (chunk_size <= 65536) or zlib-9 (AMBC_FLAG_ZLIB9,
@@ -227,6 +227,21 @@ int ambc_analyze(ambc_ctx* ctx, const uint8_t* in, uint64_t n, const ambc_params
  * *out_len = the body's size when out_cap is short. */
 int ambc_dict_encode(ambc_ctx* ctx, const uint8_t* in, uint64_t n, int64_t window_size,
                      int64_t lookahead_size, uint8_t* out, uint64_t out_cap, uint64_t* out_len);
+/* method.compress(data) for RLE (1), Huffman (3), Delta (4) and LZ4 (9) at any
+ * length n < 2^32 - 2^24, where ambc_encode_method takes one chunk of at most
+ * 65536 bytes (replaces compression_methods.py:78-113, 358-405, 586-607 and
+ * advanced_compression.py:266-281; LZ4: one frame of independent 64 KiB blocks,
+ * the same bytes as ambc_encode_method up to 64 KiB).  AMBC_E_CODEC where the
+ * reference raises (Huffman on 1 or 256 distinct bytes), AMBC_E_RANGE where its
+ * 4-byte bit count overflows, AMBC_E_CAPACITY with *out_len = the size. */
+int ambc_encode_any(ambc_ctx* ctx, int method_id, const uint8_t* in, uint64_t n, uint8_t* out,
+                    uint64_t out_cap, uint64_t* out_len);
+/* should_use statistics at any length (compression_methods.py:154-180, 540-574,
+ * 640-667): stats[0] = pairs i = 0, step, 2 step, ... < n - 1 with
+ * data[i] == data[i + 1], stats[1] = those with |data[i] - data[i + 1]| < 32,
+ * stats[2 + b] = count of byte b, stats[258 + b] = its first position
+ * (0xFFFFFFFF: absent). */
+int ambc_analyze_any(ambc_ctx* ctx, const uint8_t* in, uint64_t n, uint64_t step, uint32_t* stats);
 
 /* ---------------------------------------------------------------------------
  * Multi-GPU.  The reference is single-threaded

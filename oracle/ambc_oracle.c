@@ -518,8 +518,37 @@ EXPORT int64_t orc_lz4_block_encode(const uint8_t* d, uint32_t n, uint8_t* out) 
     return o;
 }
 
+/* more than 64 KiB (the single-call plugin at any length): one frame, the same
+ * header with the whole content size, independent 64 KiB blocks each encoded
+ * (or stored) as the one-block frame does, then the end mark */
+static int64_t lz4_frame_multi(const uint8_t* d, uint32_t n, uint8_t* out) {
+    int64_t o = 15;
+    for (uint32_t b0 = 0; b0 < n; b0 += 65536) {
+        const uint32_t m = n - b0 < 65536 ? n - b0 : 65536;
+        int64_t blk = orc_lz4_block_encode(d + b0, m, NULL);
+        int stored = blk >= (int64_t)m;
+        if (out) {
+            uint32_t bs = stored ? (m | 0x80000000U) : (uint32_t)blk;
+            for (int b = 0; b < 4; b++) out[o + b] = (uint8_t)(bs >> (8 * b));
+            if (stored) memcpy(out + o + 4, d + b0, m);
+            else orc_lz4_block_encode(d + b0, m, out + o + 4);
+        }
+        o += 4 + (stored ? m : blk);
+    }
+    if (out) {
+        uint8_t* h = out;
+        h[0] = 0x04; h[1] = 0x22; h[2] = 0x4D; h[3] = 0x18;
+        h[4] = 0x68; h[5] = 0x40;
+        for (int b = 0; b < 8; b++) h[6 + b] = (uint8_t)((uint64_t)n >> (8 * b));
+        h[14] = (uint8_t)((orc_xxh32(h + 4, 10, 0) >> 8) & 0xFF);
+        memset(out + o, 0, 4);
+    }
+    return o + 4;
+}
+
 EXPORT int64_t orc_lz4_frame_encode(const uint8_t* d, uint32_t n, uint8_t* out) {
     if (n == 0) return 0;                  /* LZ4Compression.compress: empty -> b'' */
+    if (n > 65536) return lz4_frame_multi(d, n, out);
     int64_t blk = orc_lz4_block_encode(d, n, NULL);
     int stored = blk >= (int64_t)n;
     int64_t total = 15 + 4 + (stored ? n : blk) + 4;

@@ -173,6 +173,37 @@ def test_lz4_frames_decode_with_system_liblz4():
         assert orc.decode_chunk(9, fr, len(d)) == d
 
 
+def test_multi_block_lz4_frames_decode_with_system_liblz4():
+    """past 64 KiB (the single-call plugin at any length): one frame of
+    independent 64 KiB blocks, every block decoded alone by the system liblz4"""
+    lz = _liblz4()
+    lz.LZ4_decompress_safe.argtypes = [C.c_char_p, C.c_void_p, C.c_int, C.c_int]
+    lz.LZ4_decompress_safe.restype = C.c_int
+    mixed = synth.generate(1 << 20, 4)
+    for d in (mixed[:65537], mixed[1000:1000 + 300000], bytes(200000), os.urandom(140000), mixed):
+        fr = orc.lz4_frame_encode(d)
+        assert fr[:6] == b"\x04\x22\x4d\x18\x68\x40"
+        assert int.from_bytes(fr[6:14], "little") == len(d)
+        assert fr[14] == (orc.xxh32(fr[4:14]) >> 8) & 0xFF
+        pos, got = 15, bytearray()
+        while True:
+            bs = int.from_bytes(fr[pos:pos + 4], "little")
+            pos += 4
+            if bs == 0:
+                break
+            if bs & 0x80000000:
+                got += fr[pos:pos + (bs & 0x7FFFFFFF)]
+                pos += bs & 0x7FFFFFFF
+                continue
+            out = C.create_string_buffer(65536 + 16)
+            r = lz.LZ4_decompress_safe(fr[pos:pos + bs], out, bs, 65536 + 16)
+            assert 0 < r <= 65536
+            got += out.raw[:r]
+            pos += bs
+        assert pos == len(fr) and bytes(got) == d
+        assert orc.decode_chunk(9, fr, len(d)) == d
+
+
 def test_gdeflate_streams_are_valid_zlib():
     """"ambc-deflate v1" (the GPU's id-5 definition): every stream inflates with
     the same zlib the reference's DeflateCompression.decompress uses, for edge
