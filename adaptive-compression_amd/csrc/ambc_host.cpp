@@ -1485,6 +1485,8 @@ unsigned ambc::stage_threads(uint64_t n, unsigned cap) {
 static void hugepage_advice(void* dst, uint64_t n) {
     // a fresh output (calloc'd bytes) is faulted in on first touch: ask for 2 MiB
     // pages so that 4 GiB is 2048 faults, not a million (advice only)
+    static const bool off = getenv("AMBC_NO_HUGEPAGE") != nullptr;   // (measurements)
+    if (off) return;
     const uintptr_t lo = ((uintptr_t)dst + (2u << 20) - 1) & ~(uintptr_t)((2u << 20) - 1);
     const uintptr_t hi = ((uintptr_t)dst + n) & ~(uintptr_t)((2u << 20) - 1);
     if (hi > lo) (void)madvise((void*)lo, hi - lo, MADV_HUGEPAGE);
@@ -1655,7 +1657,8 @@ struct OutCopy {
     }
 
     void run_prep() {
-        const unsigned TP = std::max(1u, std::min(8u, stage_threads(n, 8)));
+        static const unsigned tp_env = getenv("AMBC_PREP_THREADS") ? (unsigned)std::max(1, atoi(getenv("AMBC_PREP_THREADS"))) : 8u;
+        const unsigned TP = std::max(1u, std::min(tp_env, stage_threads(n, tp_env)));
         const uintptr_t ob = (uintptr_t)out;
         for (size_t j = 0; j < pcs.size(); j++) {
             { std::lock_guard<std::mutex> lk(m); if (stop_prep) break; }
