@@ -83,7 +83,7 @@ def _gpu_encode_any(mid, data):
         # compression_methods.py:397: num_bits.to_bytes(4, 'little') past 2^32 bits
         raise OverflowError("int too big to convert")
     _lib.check(rc, ctx.lib)
-    return bytes(out[:olen.value])
+    return C.string_at(C.addressof(out), olen.value)
 
 
 def _gpu_encode(mid, data):
@@ -104,7 +104,7 @@ def _gpu_encode(mid, data):
         # the reference raises here (Huffman on 1 or 256 distinct symbols)
         raise ValueError(f"method {mid} cannot encode this input")
     _lib.check(rc, ctx.lib)
-    return bytes(out[:olen.value])
+    return C.string_at(C.addressof(out), olen.value)
 
 
 def _gpu_should_use(data):
@@ -154,7 +154,7 @@ def _gpu_decode(mid, data, original_length):
                                               C.addressof(out), None, 0, C.byref(nh), C.byref(st)),
                    ctx.lib)
     produced = min(int(st.payload_bytes), osz)
-    return bytes(out[:produced])
+    return C.string_at(C.addressof(out), produced)
 
 
 def _gpu_should_use_any(data):
@@ -216,7 +216,7 @@ def _gpu_dict_any(data, window, look):
         # compression_methods.py:227: bytearray.append(match_len) with a match > 255 bytes
         raise ValueError("byte must be in range(0, 256)")
     _lib.check(rc, ctx.lib)
-    return bytes(out[:olen.value])
+    return C.string_at(C.addressof(out), olen.value)
 
 
 class DictionaryCompression(CompressionMethod):
