@@ -45,6 +45,9 @@ __device__ __forceinline__ uint32_t z_h15(uint32_t g) {
     return (((g & 0xFFu) << 10) ^ (((g >> 8) & 0xFFu) << 5) ^ ((g >> 16) & 0xFFu)) & 0x7FFFu;
 }
 __device__ __forceinline__ uint32_t z_bucket(uint32_t h15) { return (h15 * 2654435761u) >> 21; }
+// the same hash to BITS bits (the small-chunk parse's bucket count)
+template <uint32_t BITS>
+__device__ __forceinline__ uint32_t z_bucket_b(uint32_t h15) { return (h15 * 2654435761u) >> (32 - BITS); }
 
 __device__ __forceinline__ uint32_t ffbl_raw(uint32_t x) {
     uint32_t r;

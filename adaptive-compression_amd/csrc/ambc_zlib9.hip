@@ -15,7 +15,7 @@
 //   1. the chunk in LDS (zeros past n: zlib's WIN_INIT padding is what its
 //      match scan reads beyond the input);
 //   2. positions 1..n-3 (zlib inserts every position with 3 bytes of
-//      lookahead; position 0 is its NIL) counting-sorted by an 11-bit hash OF
+//      lookahead; position 0 is its NIL) counting-sorted by a 10-bit hash OF
 //      THE 15-bit zlib hash, stably: a bucket's entries below p, read downward,
 //      are p's hash chain (most recent first) plus other-hash entries that the
 //      search skips by recomputing their 15-bit hash;
@@ -62,6 +62,22 @@ namespace {
 #ifndef AMBC_Z9_G
 #define AMBC_Z9_G 8
 #endif
+// Compact LDS (round 6): 1024 sort buckets (10 bits of the 15-bit hash) and the
+// segments' match distances inside the segment words -- 51 -> 40 KB at 4 KiB,
+// four workgroups per CU instead of three: {1,3,4,5z} 21.66 -> 23.92 GB/s
+// same-box (profiles/r6_z9_compact_ab/)
+constexpr uint32_t ZBITS = 10u;
+constexpr uint32_t ZB4 = 1u << ZBITS;   // the small parse's sort buckets
+__device__ __forceinline__ uint32_t zb(uint32_t h15) { return z_bucket_b<ZBITS>(h15); }
+// segment words: bit 31 set; a run of c literals (c < 2^22), or a match of L
+// (3..258) at distance d (< 2^13) after c lazy literals (c < 256: each lazy step
+// finds a strictly longer match)
+__device__ __forceinline__ uint32_t seg_lits(uint32_t c) { return 0x80000000u | c; }
+__device__ __forceinline__ uint32_t seg_match(uint32_t L, uint32_t d, uint32_t c) { return 0x80000000u | L << 22 | d << 9 | c; }
+__device__ __forceinline__ uint32_t seg_L(uint32_t t) { return (t >> 22) & 0x1FFu; }
+__device__ __forceinline__ uint32_t seg_c(uint32_t t) { return seg_L(t) ? (t & 0x1FFu) : (t & 0x3FFFFFu); }
+__device__ __forceinline__ uint32_t seg_d(uint32_t t) { return (t >> 9) & 0x1FFFu; }
+
 template <int CMAX> struct Z9Cfg {
     static constexpr int NW = CMAX <= 1024 ? 2 : (CMAX <= 2048 ? 4 : (CMAX <= 4096 ? AMBC_Z9_NW4096 : 16));
     static constexpr int G = AMBC_Z9_G;
@@ -73,12 +89,11 @@ struct Z9Smem {
     alignas(16) uint8_t ch[CMAX + 320];      // the chunk, zeros past n
     alignas(16) uint16_t lst[CMAX];          // positions by bucket, ascending inside one
     alignas(16) uint16_t slot[CMAX];         // position -> its index in lst
-    alignas(16) uint32_t bend32[ZNB / 2];    // bucket ends (u16 pairs)
-    // the sort's per-range cursors [NR][ZNB] u16; then the parse: seg[q] = 0
+    alignas(16) uint32_t bend32[ZB4 / 2];    // bucket ends (u16 pairs)
+    // the sort's per-range cursors [NR][ZB4] u16; then the parse: seg[q] = 0
     // (not reached) or 1 << 31 | L << 16 | c for a clean position q: c
     // literals, then a match of L (0: none); the next clean position is q + c + L
     alignas(16) uint32_t seg[CMAX];
-    alignas(16) uint16_t sd[CMAX];           // the segment's match distance
     uint16_t entry[CMAX / 64], rbase[CMAX / 64];   // the path: entry lane / match rank per window
     uint16_t wrs[CMAX / 32];                 // the walk: the byte run holding position 32 w starts here
     uint32_t mask[CMAX / 32];                // the path's match starts
@@ -94,29 +109,29 @@ __device__ __forceinline__ uint32_t z_gram(const Z9Smem<CMAX>& S, uint32_t i) {
     return __builtin_amdgcn_alignbyte(c32[(i >> 2) + 1], c32[i >> 2], i & 3) & 0xFFFFFFu;
 }
 
-// Stable counting sort of positions [1, m) into lst[] by z_bucket(z_h15) --
+// Stable counting sort of positions [1, m) into lst[] by zb(z_h15) --
 // ambc_dict.hip's build_buckets with the zlib hash and each position's slot.
 template <int CMAX>
 __device__ void z9_sort(Z9Smem<CMAX>& S, uint32_t m, uint32_t wave, uint32_t lane) {
     constexpr uint32_t NW = Z9Smem<CMAX>::NW, T = 64u * NW;
     constexpr uint32_t NR = (uint32_t)CMAX / 1024, GR = 16;
-    static_assert(NR >= 1 && NR <= NW && NR * ZNB * 2 <= (uint32_t)CMAX * 4, "cursor arrays live in seg[]");
+    static_assert(NR >= 1 && NR <= NW && NR * ZB4 * 2 <= (uint32_t)CMAX * 4, "cursor arrays live in seg[]");
     uint16_t* cnt = reinterpret_cast<uint16_t*>(S.seg);
     const uint32_t tid = wave * 64u + lane;
-    for (uint32_t b = tid; b < NR * ZNB / 2; b += T) S.seg[b] = 0;
+    for (uint32_t b = tid; b < NR * ZB4 / 2; b += T) S.seg[b] = 0;
     __syncthreads();
     const uint64_t below = (1ull << lane) - 1ull;
     uint32_t loc[GR];
     if (wave < NR) {
-        uint16_t* c = cnt + wave * ZNB;
+        uint16_t* c = cnt + wave * ZB4;
 #pragma unroll
         for (uint32_t g = 0; g < GR; g++) {
             const uint32_t i = (wave * GR + g) * 64 + lane;
             const bool v = i >= 1 && i < m;
-            const uint32_t h = v ? z_bucket(z_h15(z_gram(S, i))) : 0u;
+            const uint32_t h = v ? zb(z_h15(z_gram(S, i))) : 0u;
             uint64_t peers = __ballot(v);
 #pragma unroll
-            for (int b = 0; b < 11; b++) {
+            for (int b = 0; b < (int)ZBITS; b++) {
                 const uint64_t mb = __ballot(v && ((h >> b) & 1u));
                 peers &= ((h >> b) & 1u) ? mb : ~mb;
             }
@@ -126,29 +141,30 @@ __device__ void z9_sort(Z9Smem<CMAX>& S, uint32_t m, uint32_t wave, uint32_t lan
         }
     }
     __syncthreads();
-    for (uint32_t h = tid; h < ZNB; h += T) {
+    for (uint32_t h = tid; h < ZB4; h += T) {
         uint32_t run = 0;
 #pragma unroll
         for (uint32_t r = 0; r < NR; r++) {
-            const uint32_t x = cnt[r * ZNB + h];
-            cnt[r * ZNB + h] = (uint16_t)run;
+            const uint32_t x = cnt[r * ZB4 + h];
+            cnt[r * ZB4 + h] = (uint16_t)run;
             run += x;
         }
         S.bend()[h] = (uint16_t)run;
     }
     __syncthreads();
     if (wave == 0) {
-        uint32_t c[16], t = 0;
+        constexpr int WPL = (int)ZB4 / 128;   // u16 pairs per lane
+        uint32_t c[WPL], t = 0;
 #pragma unroll
-        for (int j = 0; j < 16; j++) {
-            c[j] = S.bend32[lane * 16 + j];
+        for (int j = 0; j < WPL; j++) {
+            c[j] = S.bend32[lane * WPL + j];
             t += (c[j] & 0xFFFFu) + (c[j] >> 16);
         }
         uint32_t run = wave_incl_sum(t) - t;
 #pragma unroll
-        for (int j = 0; j < 16; j++) {
+        for (int j = 0; j < WPL; j++) {
             const uint32_t r0 = run + (c[j] & 0xFFFFu), r1 = r0 + (c[j] >> 16);
-            S.bend32[lane * 16 + j] = r0 | r1 << 16;
+            S.bend32[lane * WPL + j] = r0 | r1 << 16;
             run = r1;
         }
     }
@@ -158,7 +174,7 @@ __device__ void z9_sort(Z9Smem<CMAX>& S, uint32_t m, uint32_t wave, uint32_t lan
         for (uint32_t g = 0; g < GR; g++) {
             if (loc[g] != ~0u) {
                 const uint32_t h = loc[g] >> 16;
-                const uint32_t idx = S.bstart(h) + cnt[wave * ZNB + h] + (loc[g] & 0xFFFFu);
+                const uint32_t idx = S.bstart(h) + cnt[wave * ZB4 + h] + (loc[g] & 0xFFFFu);
                 const uint32_t pos = (wave * GR + g) * 64 + lane;
                 S.lst[idx] = (uint16_t)pos;
                 S.slot[pos] = (uint16_t)idx;
@@ -183,7 +199,7 @@ __device__ __forceinline__ void z9_literal_mask(Z9Smem<CMAX>& S, uint32_t n, uin
         bool lit = true;
         if (s >= 1 && s + 3 <= n) {
             const uint32_t h = z_h15(z_gram(S, s));
-            const uint32_t lo = S.bstart(z_bucket(h)), j = S.slot[s];
+            const uint32_t lo = S.bstart(zb(h)), j = S.slot[s];
             if (j > lo + 4) {
                 lit = false;
             } else {
@@ -268,7 +284,7 @@ __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t
                 if (e >= n) break;
             }
             e = min(e, n);
-            if (r == 0) vs[q] = 0x80000000u | (e - q);
+            if (r == 0) vs[q] = seg_lits(e - q);
             q = e;
             s = q;
             skip = true;
@@ -290,7 +306,7 @@ __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t
 #pragma unroll
                 for (int t = 0; t < 4; t++) tg[t] = __builtin_amdgcn_alignbyte(w[t + 1], w[t], ss);
                 h = z_h15(tg[0] & 0xFFFFFFu);
-                lo = S.bstart(z_bucket(h));
+                lo = S.bstart(zb(h));
                 j = S.slot[s];
                 nice = min(Z_MAXM, n - s);
             }
@@ -426,7 +442,7 @@ __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t
             if (clean) {
                 if (ML < 3) {
                     // a literal; the next position is clean again
-                    if (r == 0) vs[q] = 0x80000000u | 1u;
+                    if (r == 0) vs[q] = seg_lits(1u);
                     q++;
                     s = q;
                 } else {
@@ -439,8 +455,7 @@ __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t
             } else if (ML <= P) {
                 // the pending match at s - 1 is emitted: its end is clean
                 if (r == 0) {
-                    S.sd[q] = (uint16_t)Pd;
-                    vs[q] = 0x80000000u | P << 16 | c;
+                    vs[q] = seg_match(P, Pd, c);
                 }
                 q = s - 1 + P;
                 s = q;
@@ -474,8 +489,8 @@ __device__ bool z9_cannot_win(Z9Smem<CMAX>& S, uint32_t n, uint32_t T, uint32_t 
     constexpr uint32_t NW = Z9Smem<CMAX>::NW, TT = 64u * NW, TB = 2u * (uint32_t)CMAX;
     static_assert(offsetof(Z9Smem<CMAX>, slot) == offsetof(Z9Smem<CMAX>, lst) + 2 * CMAX &&
                   offsetof(Z9Smem<CMAX>, bend32) == offsetof(Z9Smem<CMAX>, slot) + 2 * CMAX &&
-                  offsetof(Z9Smem<CMAX>, seg) == offsetof(Z9Smem<CMAX>, bend32) + 2 * ZNB &&
-                  4 * TB <= 4 * CMAX + 2 * ZNB + 4 * CMAX, "the hash set spans lst .. seg");
+                  offsetof(Z9Smem<CMAX>, seg) == offsetof(Z9Smem<CMAX>, bend32) + 2 * ZB4 &&
+                  4 * TB <= 4 * CMAX + 2 * ZB4 + 4 * CMAX, "the hash set spans lst .. seg");
     const uint32_t tid = wave * 64u + lane;
     uint32_t* hist = S.seg + CMAX - 256;          // (the set's last slots hold no string yet)
     for (uint32_t i = tid; i < 256; i += TT) hist[i] = 0;
@@ -600,8 +615,8 @@ __global__ __launch_bounds__(64 * Z9Cfg<CMAX>::NW) void k_z9_parse(EncArgs A) {
     for (uint32_t w = wave; w < nwin; w += NW) {
         const uint32_t p = w * 64 + lane;
         const uint32_t t = p < n ? S.seg[p] : 0u;
-        uint32_t J = t ? lane + (t & 0xFFFFu) + ((t >> 16) & 0x1FFu) : lane + 1;
-        uint32_t M = (t >> 16) & 0x1FFu ? 1u : 0u;
+        uint32_t J = t ? lane + seg_c(t) + seg_L(t) : lane + 1;
+        uint32_t M = seg_L(t) ? 1u : 0u;
 #pragma unroll
         for (int it = 0; it < 6; it++) {
             const int src = (int)(min(J, 63u) << 2);
@@ -636,7 +651,7 @@ __global__ __launch_bounds__(64 * Z9Cfg<CMAX>::NW) void k_z9_parse(EncArgs A) {
         if (e == 0xFFFFu) continue;
         const uint32_t p = w * 64 + lane;
         const uint32_t t = p < n ? S.seg[p] : 0u;
-        const uint32_t c = t & 0xFFFFu, L = (t >> 16) & 0x1FFu;
+        const uint32_t c = seg_c(t), L = seg_L(t);
         const uint32_t J1 = lane + max(1u, c + L);   // (t != 0 on the path; never stall)
         uint64_t on = 0;
         for (uint32_t q = e; q < 64;) {
@@ -646,7 +661,7 @@ __global__ __launch_bounds__(64 * Z9Cfg<CMAX>::NW) void k_z9_parse(EncArgs A) {
         const bool mt = ((on >> lane) & 1u) && L != 0;
         const uint64_t mm = __ballot(mt);
         if (mt) {
-            const uint32_t ms = p + c, d = S.sd[p];
+            const uint32_t ms = p + c, d = seg_d(t);
             atomicOr(&S.mask[ms >> 5], 1u << (ms & 31));
             R[Z9Rec<CMAX>::MATCH + S.rbase[w] + (uint32_t)__popcll(mm & below)] = L | d << 16;
             for (uint32_t b = ms, e2 = ms + L; b < e2;) {
