@@ -114,29 +114,38 @@ __device__ __forceinline__ uint32_t grp_bits(uint64_t m, uint32_t g) {
 // each step pops) -- everything gen_bitlen needs (k_z9_code rebuilds the
 // parent links and the heap_max order from it).
 constexpr uint32_t ZH_N = 290;
+// chunks (lanes) per wave: the heaps of 64 chunks fill 74 KB of LDS, two waves
+// per CU; fewer lanes per wave keep about as many heaps resident in more waves,
+// which hide each other's dependent LDS reads ({1,3,4,5z} same-box: 64 -> 16 ->
+// 8 lanes 23.9 -> 24.4 -> 24.9 GB/s, profiles/r6_z9_heap_lanes_ab/)
+#ifndef AMBC_ZH_L
+#define AMBC_ZH_L 8
+#endif
+constexpr uint32_t ZH_L = AMBC_ZH_L;
 __device__ __forceinline__ void zh_down(uint32_t* H, uint32_t lane, uint32_t heap_len, uint32_t k) {
-    const uint32_t v = H[k * 64 + lane], kv = v >> 10;
+    const uint32_t v = H[k * ZH_L + lane], kv = v >> 10;
     uint32_t j = k << 1;
     while (j <= heap_len) {
-        uint32_t hj = H[j * 64 + lane];
+        uint32_t hj = H[j * ZH_L + lane];
         if (j < heap_len) {
-            const uint32_t hj1 = H[(j + 1) * 64 + lane];
+            const uint32_t hj1 = H[(j + 1) * ZH_L + lane];
             if ((hj1 >> 10) <= (hj >> 10)) { j++; hj = hj1; }
         }
         if (kv <= (hj >> 10)) break;
-        H[k * 64 + lane] = hj;
+        H[k * ZH_L + lane] = hj;
         k = j;
         j <<= 1;
     }
-    H[k * 64 + lane] = v;
+    H[k * ZH_L + lane] = v;
 }
 
 template <int CMAX>
 __global__ __launch_bounds__(64) void k_z9_heap(EncArgs A) {
-    __shared__ uint32_t H[ZH_N * 64];
+    __shared__ uint32_t H[ZH_N * ZH_L];
     constexpr uint32_t NB = Z9Rec<CMAX>::NBLK;   // one lane per (chunk, block)
     const uint32_t lane = threadIdx.x;
-    const uint32_t item = blockIdx.x * 64 + lane;
+    if (lane >= ZH_L) return;
+    const uint32_t item = blockIdx.x * ZH_L + lane;
     const uint32_t k = item / NB, blk = item % NB;
     if (k >= A.n_chunks) return;
     const uint64_t pos0 = A.coff ? A.coff[k] : (uint64_t)k * A.chunk_size;
@@ -157,26 +166,26 @@ __global__ __launch_bounds__(64) void k_z9_heap(EncArgs A) {
         for (uint32_t s = 0; s < elems; s++) {
             const uint32_t f = (uint32_t)F[fb + s] + (tree == 0 && s == 256 ? 1u : 0u);   // + the end of block
             if (f) {
-                H[(++heap_len) * 64 + lane] = f << 16 | s;
+                H[(++heap_len) * ZH_L + lane] = f << 16 | s;
                 max_code = (int)s;
             }
         }
         while (heap_len < 2) {   // at least two codes
             const int node = max_code < 2 ? ++max_code : 0;
-            H[(++heap_len) * 64 + lane] = 1u << 16 | (uint32_t)node;
+            H[(++heap_len) * ZH_L + lane] = 1u << 16 | (uint32_t)node;
         }
         for (uint32_t q = heap_len / 2; q >= 1; q--) zh_down(H, lane, heap_len, q);
         uint32_t node = elems, i = 0;
         do {
-            const uint32_t hn = H[64 + lane];
-            H[64 + lane] = H[heap_len * 64 + lane];
+            const uint32_t hn = H[ZH_L + lane];
+            H[ZH_L + lane] = H[heap_len * ZH_L + lane];
             heap_len--;
             zh_down(H, lane, heap_len, 1);
-            const uint32_t hm = H[64 + lane];
+            const uint32_t hm = H[ZH_L + lane];
             MG[mb + i++] = (hn & 1023u) | (hm & 1023u) << 16;
             const uint32_t f = (hn >> 16) + (hm >> 16);
             const uint32_t dep = max((hn >> 10) & 63u, (hm >> 10) & 63u) + 1u;
-            H[64 + lane] = f << 16 | dep << 10 | node;
+            H[ZH_L + lane] = f << 16 | dep << 10 | node;
             node++;
             zh_down(H, lane, heap_len, 1);
         } while (heap_len >= 2);

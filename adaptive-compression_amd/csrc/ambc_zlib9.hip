@@ -972,7 +972,7 @@ __global__ __launch_bounds__(64) void k_z9_code(EncArgs A) {
 template <int CMAX>
 hipError_t launch_z9_t(const EncArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_z9_parse<CMAX>, dim3(a.n_chunks), dim3(64 * Z9Cfg<CMAX>::NW), 0, s, a);
-    hipLaunchKernelGGL(k_z9_heap<CMAX>, dim3((a.n_chunks + 63) / 64), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_z9_heap<CMAX>, dim3((a.n_chunks + ZH_L - 1) / ZH_L), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_z9_code<CMAX>, dim3(a.n_chunks), dim3(64), 0, s, a);
     return hipGetLastError();
 }

@@ -1027,7 +1027,7 @@ hipError_t launch_z9b_t(const EncArgs& a, hipStream_t s) {
     const uint32_t g = min(a.n_chunks, ZB_GRID);
     constexpr uint32_t NB = Z9Rec<CMAX>::NBLK;
     hipLaunchKernelGGL(k_z9_parse_big<CMAX>, dim3(g), dim3(64 * ZB_NW), 0, s, a);
-    hipLaunchKernelGGL(k_z9_heap<CMAX>, dim3((a.n_chunks * NB + 63) / 64), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_z9_heap<CMAX>, dim3((a.n_chunks * NB + ZH_L - 1) / ZH_L), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_z9_code_big<CMAX>, dim3(a.n_chunks), dim3(64), 0, s, a);
     return hipGetLastError();
 }
