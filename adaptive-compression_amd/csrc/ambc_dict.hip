@@ -46,7 +46,14 @@
 namespace ambc {
 namespace {
 
-constexpr uint32_t DNB = 2048;      // 3-gram hash buckets (11 bits)
+// 1024 buckets (round 6): their cursor arrays for all eight waves' ranges fit
+// tok[] (2048 buckets: four waves rank, four wait) -- {1,2,3,4} 98.1 -> 99.0 GB/s
+// same-box (profiles/r6_dict_nb10_ab/)
+#ifndef AMBC_DICT_NB10
+#define AMBC_DICT_NB10 1
+#endif
+constexpr uint32_t DBITS = AMBC_DICT_NB10 ? 10u : 11u;
+constexpr uint32_t DNB = 1u << DBITS;   // 3-gram hash buckets
 constexpr uint32_t DWIN = 4096;     // compression_methods.py:187 window_size
 constexpr uint32_t DLOOK = 32;      // :187 lookahead_size
 
@@ -102,7 +109,7 @@ __device__ __forceinline__ uint32_t ffbl_raw(uint32_t x) {
     return r;
 }
 
-__device__ __forceinline__ uint32_t h3(uint32_t v) { return ((v & 0xFFFFFFu) * 2654435761u) >> 21; }
+__device__ __forceinline__ uint32_t h3(uint32_t v) { return ((v & 0xFFFFFFu) * 2654435761u) >> (32 - DBITS); }
 
 // the 3-gram at position i (bytes i..i+2, little-endian)
 template <int CMAX>
@@ -122,7 +129,8 @@ __device__ __forceinline__ uint32_t gram_at(const DictSmem<CMAX>& S, uint32_t i)
 template <int CMAX>
 __device__ void build_buckets(DictSmem<CMAX>& S, uint32_t m, uint32_t wave, uint32_t lane) {
     constexpr uint32_t NW = DictSmem<CMAX>::NW, T = 64u * NW;
-    constexpr uint32_t NR = (uint32_t)CMAX / 1024, GR = 16;
+    constexpr uint32_t NR = AMBC_DICT_NB10 ? ((uint32_t)CMAX / 512 < NW ? (uint32_t)CMAX / 512 : NW) : (uint32_t)CMAX / 1024;
+    constexpr uint32_t GR = (uint32_t)CMAX / (64 * NR);
     static_assert(NR >= 1 && NR <= NW && NR * DNB * 2 <= (uint32_t)CMAX * 4, "cursor arrays live in tok[]");
     uint16_t* cnt = reinterpret_cast<uint16_t*>(S.tok);   // [NR][DNB]
     const uint32_t tid = wave * 64u + lane;
@@ -139,7 +147,7 @@ __device__ void build_buckets(DictSmem<CMAX>& S, uint32_t m, uint32_t wave, uint
             const uint32_t h = v ? h3(gram_at(S, i)) : 0u;
             uint64_t peers = __ballot(v);
 #pragma unroll
-            for (int b = 0; b < 11; b++) {
+            for (int b = 0; b < (int)DBITS; b++) {
                 const uint64_t mb = __ballot(v && ((h >> b) & 1u));
                 peers &= ((h >> b) & 1u) ? mb : ~mb;
             }
@@ -163,17 +171,18 @@ __device__ void build_buckets(DictSmem<CMAX>& S, uint32_t m, uint32_t wave, uint
     __syncthreads();
     if (wave == 0) {
         // inclusive scan in place (32 buckets per lane): bucket ends
-        uint32_t c[16], t = 0;
+        constexpr int WPL = (int)DNB / 128;   // u16 pairs per lane
+        uint32_t c[WPL], t = 0;
 #pragma unroll
-        for (int j = 0; j < 16; j++) {
-            c[j] = S.bend32[lane * 16 + j];
+        for (int j = 0; j < WPL; j++) {
+            c[j] = S.bend32[lane * WPL + j];
             t += (c[j] & 0xFFFFu) + (c[j] >> 16);
         }
         uint32_t run = wave_incl_sum(t) - t;
 #pragma unroll
-        for (int j = 0; j < 16; j++) {
+        for (int j = 0; j < WPL; j++) {
             const uint32_t r0 = run + (c[j] & 0xFFFFu), r1 = r0 + (c[j] >> 16);
-            S.bend32[lane * 16 + j] = r0 | r1 << 16;
+            S.bend32[lane * WPL + j] = r0 | r1 << 16;
             run = r1;
         }
     }
