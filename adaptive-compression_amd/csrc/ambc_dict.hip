@@ -64,6 +64,11 @@ constexpr uint32_t DG = AMBC_DICT_DG;   // lanes per walker (8 or 16)
 #ifndef AMBC_DICT_2STAGE
 #define AMBC_DICT_2STAGE 1
 #endif
+// the winner's tokens staged in LDS and stored 16 bytes at a time (round 6):
+// {1,2,3,4} 98.9 -> 103.1 GB/s same-box (profiles/r6_dict_stage_ab/)
+#ifndef AMBC_DICT_STAGE
+#define AMBC_DICT_STAGE 1
+#endif
 #ifndef AMBC_DICT_NW4K
 #define AMBC_DICT_NW4K 8
 #endif
@@ -544,6 +549,15 @@ __global__ __launch_bounds__(64 * DictCfg<CMAX>::NW) void k_dict(EncArgs A) {
     uint8_t* slot = A.slots + (uint64_t)k * A.slot_stride;
     uint16_t* s16 = reinterpret_cast<uint16_t*>(slot);
     const uint32_t o = S.olen;
+    // the tokens staged in LDS (lst[] past the path tables, dead after the walk)
+    // and copied out with 16-byte stores, instead of 2-byte stores scattered over
+    // the slot; a forced encode (plugins, up to 2n bytes) writes directly
+    constexpr uint32_t SOFF = 2048;
+    static_assert(sizeof(S.path) <= SOFF, "the path tables stay below the staging area");
+    const bool stg = AMBC_DICT_STAGE && !force && o + SOFF <= 2u * (uint32_t)CMAX &&
+                     (reinterpret_cast<uintptr_t>(slot) & 15) == 0;
+    typedef __attribute__((address_space(3))) uint16_t lds_u16;
+    lds_u16* L16 = (lds_u16*)(reinterpret_cast<uint8_t*>(S.lst) + SOFF);
     if (!(A.flags & ENC_EVAL)) {   // (the multi-size walk's decision-only batches: no bytes)
         uint32_t e = S.path.be[wave], ob = S.path.bo[wave];
 #pragma unroll 1
@@ -566,13 +580,22 @@ __global__ __launch_bounds__(64 * DictCfg<CMAX>::NW) void k_dict(EncArgs A) {
             const uint32_t off = ob + 2u * (uint32_t)(__popcll(on & below) + __popcll(mm & below));
             if (mt) {
                 const uint32_t d = t & 0xFFFFu;
-                s16[off >> 1] = (uint16_t)(1u | (d & 0xFFu) << 8);
-                s16[(off >> 1) + 1] = (uint16_t)((d >> 8) | L << 8);
+                const uint16_t w0 = (uint16_t)(1u | (d & 0xFFu) << 8), w1 = (uint16_t)((d >> 8) | L << 8);
+                if (stg) { L16[off >> 1] = w0; L16[(off >> 1) + 1] = w1; }
+                else { s16[off >> 1] = w0; s16[(off >> 1) + 1] = w1; }
             } else if (me) {
-                s16[off >> 1] = (uint16_t)(S.ch[p0 + lane] << 8);
+                const uint16_t w0 = (uint16_t)(S.ch[p0 + lane] << 8);
+                if (stg) L16[off >> 1] = w0;
+                else s16[off >> 1] = w0;
             }
             ob += 2u * (uint32_t)(__popcll(on) + __popcll(mm));
             e = q - 64;
+        }
+        if (stg) {
+            __syncthreads();
+            const uint4* src4 = reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(S.lst) + SOFF);
+            uint4* dst4 = reinterpret_cast<uint4*>(slot);
+            for (uint32_t q = threadIdx.x; q < (o + 15) / 16; q += 64u * NW) dst4[q] = src4[q];
         }
     }
     if (threadIdx.x == 0) {
