@@ -46,14 +46,20 @@
 namespace ambc {
 namespace {
 
-// 1024 buckets (round 6): their cursor arrays for all eight waves' ranges fit
-// tok[] (2048 buckets: four waves rank, four wait) -- {1,2,3,4} 98.1 -> 99.0 GB/s
-// same-box (profiles/r6_dict_nb10_ab/)
+// 1024 buckets up to 4 KiB (round 6): their cursor arrays for all eight waves'
+// ranges fit tok[] (2048 buckets: four waves rank, four wait) -- {1,2,3,4} 98.1 ->
+// 99.0 GB/s same-box (profiles/r6_dict_nb10_ab/); 8 KiB keeps 2048 (all its waves
+// rank already; 1024 there: the {1,2,3,4,5} walk 5.6 -> 5.4 GB/s,
+// profiles/r6_dict_nb_walk_ab/)
 #ifndef AMBC_DICT_NB10
 #define AMBC_DICT_NB10 1
 #endif
-constexpr uint32_t DBITS = AMBC_DICT_NB10 ? 10u : 11u;
-constexpr uint32_t DNB = 1u << DBITS;   // 3-gram hash buckets
+// 3-gram hash buckets per chunk size: 1024 up to 4 KiB (1: 8 KiB keeps 2048,
+// whose eight ranges already fill tok[] and every wave; 2: 1024 everywhere)
+template <int CMAX> struct DictHash {
+    static constexpr uint32_t BITS = AMBC_DICT_NB10 == 0 ? 11u : AMBC_DICT_NB10 == 2 ? 10u : (CMAX >= 8192 ? 11u : 10u);
+    static constexpr uint32_t NB = 1u << BITS;
+};
 constexpr uint32_t DWIN = 4096;     // compression_methods.py:187 window_size
 constexpr uint32_t DLOOK = 32;      // :187 lookahead_size
 
@@ -95,7 +101,7 @@ struct DictSmem {
     };
     // counts (u16 pairs, 32-bit atomics) -> bucket starts (the scatter's cursors)
     // -> bucket ends: after the scatter bucket h is lst[h ? bend[h-1] : 0, bend[h])
-    alignas(16) uint32_t bend32[DNB / 2];
+    alignas(16) uint32_t bend32[DictHash<CMAX>::NB / 2];
     // the sort: per range and bucket a cursor (u16);
     // the parse: tok[p] = 0 (not visited) or 1 << 31 | len << 16 | dist (a
     // literal: len 1) for every position a walker has visited
@@ -114,7 +120,8 @@ __device__ __forceinline__ uint32_t ffbl_raw(uint32_t x) {
     return r;
 }
 
-__device__ __forceinline__ uint32_t h3(uint32_t v) { return ((v & 0xFFFFFFu) * 2654435761u) >> (32 - DBITS); }
+template <int CMAX>
+__device__ __forceinline__ uint32_t h3(uint32_t v) { return ((v & 0xFFFFFFu) * 2654435761u) >> (32 - DictHash<CMAX>::BITS); }
 
 // the 3-gram at position i (bytes i..i+2, little-endian)
 template <int CMAX>
@@ -134,7 +141,8 @@ __device__ __forceinline__ uint32_t gram_at(const DictSmem<CMAX>& S, uint32_t i)
 template <int CMAX>
 __device__ void build_buckets(DictSmem<CMAX>& S, uint32_t m, uint32_t wave, uint32_t lane) {
     constexpr uint32_t NW = DictSmem<CMAX>::NW, T = 64u * NW;
-    constexpr uint32_t NR = AMBC_DICT_NB10 ? ((uint32_t)CMAX / 512 < NW ? (uint32_t)CMAX / 512 : NW) : (uint32_t)CMAX / 1024;
+    constexpr uint32_t DBITS = DictHash<CMAX>::BITS, DNB = DictHash<CMAX>::NB;
+    constexpr uint32_t NR = DBITS == 10 ? ((uint32_t)CMAX / 512 < NW ? (uint32_t)CMAX / 512 : NW) : (uint32_t)CMAX / 1024;
     constexpr uint32_t GR = (uint32_t)CMAX / (64 * NR);
     static_assert(NR >= 1 && NR <= NW && NR * DNB * 2 <= (uint32_t)CMAX * 4, "cursor arrays live in tok[]");
     uint16_t* cnt = reinterpret_cast<uint16_t*>(S.tok);   // [NR][DNB]
@@ -149,7 +157,7 @@ __device__ void build_buckets(DictSmem<CMAX>& S, uint32_t m, uint32_t wave, uint
         for (uint32_t g = 0; g < GR; g++) {
             const uint32_t i = (wave * GR + g) * 64 + lane;
             const bool v = i < m;
-            const uint32_t h = v ? h3(gram_at(S, i)) : 0u;
+            const uint32_t h = v ? h3<CMAX>(gram_at(S, i)) : 0u;
             uint64_t peers = __ballot(v);
 #pragma unroll
             for (int b = 0; b < (int)DBITS; b++) {
@@ -264,7 +272,7 @@ __device__ bool dict_su_exact(DictSmem<CMAX>& S, uint32_t n, uint32_t wave, uint
     uint32_t rep = 0;
     for (uint32_t i = tid; i < lim; i += T) {
         const uint32_t g = gram_at(S, i);
-        for (uint32_t j = S.bstart(h3(g));; j++) {
+        for (uint32_t j = S.bstart(h3<CMAX>(g));; j++) {
             const uint32_t q = S.lst[j];
             if (q >= i) break;
             if (gram_at(S, q) == g) { rep++; break; }
@@ -336,7 +344,7 @@ __device__ __forceinline__ void dict_walkers(DictSmem<CMAX>& S, uint32_t n, uint
         }
         if (__all(done)) break;
         const uint32_t look = done ? 0u : min(DLOOK, n - p);
-        const uint32_t h = h3(tg[0]);
+        const uint32_t h = h3<CMAX>(tg[0]);
         uint32_t j = S.bstart(h);
         const uint32_t e = look >= 3 ? (uint32_t)S.bend()[h] : j;
         if (CMAX > (int)DWIN) {
