@@ -689,15 +689,24 @@ __global__ __launch_bounds__(64 * Z9Cfg<CMAX>::NW) void k_z9_parse(EncArgs A) {
 template <int CMAX>
 struct Z9CSmem {
     static constexpr int WORDS = (CMAX + 5 * (int)Z_NBLK + 64) / 4 + 4;
-    alignas(16) uint32_t bits[WORDS];        // the deflate body, LSB first
+    // the body's bits only exist once the trees are built: they share the literal
+    // tree's heap and the pointer-jumping scratch (round 6: 15.2 -> 11.0 KB at 4
+    // KiB, 14 waves per CU instead of 10; {1,3,4,5z} 25.0 -> 25.9 GB/s same-box,
+    // profiles/r6_z9_code_union_ab/)
+    union {
+        alignas(16) uint32_t bits[WORDS];    // the deflate body, LSB first
+        struct {
+            uint32_t heapL[LT_N + 1];
+            uint16_t pjd[LT_N + 3], pja[LT_N + 3];   // z9_build_w's pointer-jumping scratch
+        } tr;
+    };
     uint32_t mstart[CMAX / 32 + 2];          // match starts (bitmask by position)
     uint32_t ecl[288], ecd[32];              // emission codes: code | len << 16
-    uint32_t heapL[LT_N + 1], heapD[DT_N + 1];
+    uint32_t heapD[DT_N + 1];
     uint16_t lfreq[LT_N + 1], ldad[LT_N + 1], lcode[288];
     uint16_t dfreq[DT_N + 1], ddad[DT_N + 1], dcode[32];
     uint16_t bfreq[BT_N + 1], bdad[BT_N + 1], bcode[20];
     uint16_t blcL[16], blcD[16], blcB[16];
-    uint16_t pjd[LT_N + 3], pja[LT_N + 3];   // z9_build_w's pointer-jumping scratch
     uint32_t blc32[16], cnt32[20];
     uint8_t llen[LT_N + 1], dlen[DT_N + 1], blen[BT_N + 1];
     uint32_t misc[16];
@@ -740,14 +749,13 @@ __global__ __launch_bounds__(64) void k_z9_code(EncArgs A) {
     static_assert(CMAX < (int)Z_BLKSYM, "one block per chunk");
     const uint64_t below = (1ull << lane) - 1ull;
     l32* W = (l32*)S.bits;
-    const Z9Tree LT{(l16*)S.lfreq, (l16*)S.ldad, (l8*)S.llen, (l16*)S.lcode, (l32*)S.heapL, (l16*)S.blcL};
+    const Z9Tree LT{(l16*)S.lfreq, (l16*)S.ldad, (l8*)S.llen, (l16*)S.lcode, (l32*)S.tr.heapL, (l16*)S.blcL};
     const Z9Tree DT{(l16*)S.dfreq, (l16*)S.ddad, (l8*)S.dlen, (l16*)S.dcode, (l32*)S.heapD, (l16*)S.blcD};
     const Z9Tree BT{(l16*)S.bfreq, (l16*)S.bdad, (l8*)S.blen, (l16*)S.bcode, (l32*)S.heapD, (l16*)S.blcB};
 
     // ---- the parse's match starts ----
     for (uint32_t i = lane; i < (uint32_t)CMAX / 32 + 2; i += 64)
         S.mstart[i] = i < (uint32_t)CMAX / 32 ? R[Z9Rec<CMAX>::MASK + i] : 0u;
-    for (uint32_t i = lane; i < (uint32_t)Z9CSmem<CMAX>::WORDS; i += 64) S.bits[i] = 0;
     wave_sync();
 
     // the block's symbols over [bs, be), position-major, written from bit bp
@@ -829,8 +837,8 @@ __global__ __launch_bounds__(64) void k_z9_code(EncArgs A) {
         wave_sync();
         ZSTAMP(0);
         // ---- the trees: build_tree x 2, scan_tree x 2, build_bl_tree ----
-        l16* PJD = (l16*)S.pjd;
-        l16* PJA = (l16*)S.pja;
+        l16* PJD = (l16*)S.tr.pjd;
+        l16* PJA = (l16*)S.tr.pja;
         l32* BLC = (l32*)S.blc32;
         l32* MISC = (l32*)(S.misc + 12);
         uint32_t optL = 0, statL = 0, optD = 0, statD = 0, optB = 0, statB = 0;
@@ -878,6 +886,9 @@ __global__ __launch_bounds__(64) void k_z9_code(EncArgs A) {
                 return;
             }
         }
+        // the trees are done: their scratch becomes the body's bits
+        for (uint32_t i = lane; i < (uint32_t)Z9CSmem<CMAX>::WORDS; i += 64) S.bits[i] = 0;
+        wave_sync();
         if (kind == 0) {
             // stored: the 3 header bits, byte alignment, LEN / NLEN, the bytes
             const uint32_t stored_len = be - bs;
