@@ -419,7 +419,7 @@ __global__ __launch_bounds__(64) void k_deflate(EncArgs A) {
     const uint32_t lane = threadIdx.x;
     const uint32_t k = blockIdx.x;
     const uint64_t pos0 = A.coff ? A.coff[k] : (uint64_t)k * A.chunk_size;
-    const uint32_t n = A.coff ? A.clen[k] : (uint32_t)min((uint64_t)A.chunk_size, A.n_total - pos0);
+    const uint32_t n = A.coff ? (A.clen ? A.clen[k] : A.clen_all) : (uint32_t)min((uint64_t)A.chunk_size, A.n_total - pos0);
     GSTAMP_DECL
     // prefs gate (adaptive_compressor.py:565-567) and should_use's n >= 64
     if (!((A.method_mask >> 5) & 1) || n < A.pref_min[5] || n > A.pref_max[5] || n < 64) GRET;

@@ -432,7 +432,7 @@ __global__ __launch_bounds__(64 * DictCfg<CMAX>::NW) void k_dict(EncArgs A) {
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t k = blockIdx.x;
     const uint64_t pos0 = A.coff ? A.coff[k] : (uint64_t)k * A.chunk_size;
-    const uint32_t n = A.coff ? A.clen[k] : (uint32_t)min((uint64_t)A.chunk_size, A.n_total - pos0);
+    const uint32_t n = A.coff ? (A.clen ? A.clen[k] : A.clen_all) : (uint32_t)min((uint64_t)A.chunk_size, A.n_total - pos0);
     const bool force = A.flags & ENC_FORCE;
     const bool analyze = A.flags & ENC_ANALYZE;
     const bool elig = ((A.method_mask >> 2) & 1u) && n >= A.pref_min[2] && n <= A.pref_max[2] &&

@@ -218,7 +218,7 @@ __global__ __launch_bounds__(64) AMBC_ENC_ATTR void k_encode(EncArgs A) {
     const uint32_t lane = threadIdx.x;
     const uint32_t k = blockIdx.x;
     const uint64_t pos0 = A.coff ? A.coff[k] : (uint64_t)k * A.chunk_size;
-    const uint32_t n = A.coff ? A.clen[k] : (uint32_t)min((uint64_t)A.chunk_size, A.n_total - pos0);
+    const uint32_t n = A.coff ? (A.clen ? A.clen[k] : A.clen_all) : (uint32_t)min((uint64_t)A.chunk_size, A.n_total - pos0);
     const uint8_t* src = A.in + pos0;
     uint8_t* const slot0 = A.slots + (uint64_t)k * A.slot_stride;   // the chunk's scratch slot
     uint8_t* slot = slot0;              // where the payload goes
@@ -1086,7 +1086,7 @@ __device__ __forceinline__ void compact_package(const CompactArgs& A, uint32_t k
     const uint32_t P = HDR + pl;
     const uint32_t type = A.ids[k];
     const uint64_t p0 = (uint64_t)k * A.chunk_size;
-    const uint32_t n = A.clen ? A.clen[k] : (uint32_t)min((uint64_t)A.chunk_size, A.n_total - p0);
+    const uint32_t n = A.clen ? A.clen[k] : A.clen_all ? A.clen_all : (uint32_t)min((uint64_t)A.chunk_size, A.n_total - p0);
     const uint8_t* __restrict__ sl = type == 255 && A.in ? A.in + p0 : A.slots + (uint64_t)k * A.slot_stride;
     uint8_t* const dst = A.out + o;                       // the package's first byte
     const uint64_t da = reinterpret_cast<uintptr_t>(dst);
@@ -1187,6 +1187,19 @@ __global__ __launch_bounds__(256) void k_stats(const uint8_t* ids, const uint32_
 }
 
 // bulk copy to an arbitrary byte offset (reference-mode raw remainder)
+// a walk batch's results into its pinned host arrays (device stores to host memory)
+__global__ __launch_bounds__(256) void k_results_to_host(const uint32_t* plen, const uint8_t* ids, const uint32_t* lz,
+                                                         uint32_t cnt, uint32_t nlz, uint32_t* hplen, uint8_t* hids,
+                                                         uint32_t* hlz) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < cnt) {
+        hplen[i] = plen[i];
+        hids[i] = ids[i];
+    }
+    if (lz)
+        for (uint32_t j = i; j < cnt * nlz; j += gridDim.x * blockDim.x) hlz[j] = lz[j];
+}
+
 __global__ __launch_bounds__(256) void k_copy(uint8_t* dst, const uint8_t* src, uint64_t len) {
     const uint64_t mis = (4 - (reinterpret_cast<uintptr_t>(dst) & 3)) & 3;
     const uint64_t head = mis < len ? mis : len;
@@ -1357,6 +1370,14 @@ hipError_t launch_stats(const uint8_t* ids, const uint32_t* plen, uint32_t n_chu
     uint32_t blocks = (n_chunks + 255) / 256;
     if (blocks > 1024) blocks = 1024;
     hipLaunchKernelGGL(k_stats, dim3(blocks), dim3(256), 0, s, ids, plen, n_chunks, n_total, C, acc);
+    return hipGetLastError();
+}
+
+hipError_t launch_results_to_host(const uint32_t* plen, const uint8_t* ids, const uint32_t* lz, uint32_t cnt, uint32_t nlz,
+                                  uint32_t* hplen, uint8_t* hids, uint32_t* hlz, hipStream_t s) {
+    if (cnt == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_results_to_host, dim3((cnt + 255) / 256), dim3(256), 0, s, plen, ids, lz, cnt, nlz, hplen, hids,
+                       hlz);
     return hipGetLastError();
 }
 

@@ -38,6 +38,7 @@ struct EncArgs {
     uint32_t pref_max[16];
     const uint64_t* coff;    // optional chunk table (multi-size walk): chunk k = in[coff[k], coff[k] + clen[k])
     const uint32_t* clen;    //   (else chunk k = in[k * chunk_size, ...) clamped to n_total)
+    uint32_t clen_all;       //   coff without clen: every chunk is clen_all bytes (the walk's batches)
     // ENC_EVAL + lz4sub: the LZ4 block length of every prefix [0, b) of the chunk
     // for b in sub_c[] (ascending) with b < n and id 9's prefs, from the chunk's
     // own parse ("ambc-lz4 greedy v2" is prefix-consistent: the prefix's parse is
@@ -58,7 +59,8 @@ struct CompactArgs {
     const uint64_t* off;     // exclusive scan of sizes (n_chunks+1)
     const uint64_t* base;    // optional: body offset added to off[] (pipelined segments)
     uint32_t n_chunks;       // packages to write
-    const uint32_t* clen;    // optional: original length of package k (else chunk_size clamped to n_total)
+    const uint32_t* clen;    // optional: original length of package k (else clen_all, or chunk_size clamped to n_total)
+    uint32_t clen_all;       // nonzero without clen: every package's original length (a walk's final batch)
     uint32_t resident;       // > 0: a grid of this many workgroups striding over the packages
     uint64_t n_total;
     uint32_t chunk_size;
@@ -238,6 +240,8 @@ hipError_t launch_stats(const uint8_t* ids, const uint32_t* plen, uint32_t n_chu
 hipError_t scan_sizes(const uint64_t* sizes, uint64_t* off, uint32_t count, void* tmp,
                       size_t* tmp_bytes, hipStream_t s);
 hipError_t launch_copy(uint8_t* dst, const uint8_t* src, uint64_t len, hipStream_t s);
+hipError_t launch_results_to_host(const uint32_t* plen, const uint8_t* ids, const uint32_t* lz, uint32_t cnt, uint32_t nlz,
+                                  uint32_t* hplen, uint8_t* hids, uint32_t* hlz, hipStream_t s);
 hipError_t launch_decode(int kind, const DecArgs& a, hipStream_t s);
 hipError_t launch_inflate(int kind, const DecArgs& a, hipStream_t s);   // ambc_inflate.hip
 hipError_t launch_huff(int kind, const DecArgs& a, hipStream_t s);      // ambc_huffdec.hip

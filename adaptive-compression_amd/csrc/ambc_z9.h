@@ -149,7 +149,7 @@ __global__ __launch_bounds__(64) void k_z9_heap(EncArgs A) {
     const uint32_t k = item / NB, blk = item % NB;
     if (k >= A.n_chunks) return;
     const uint64_t pos0 = A.coff ? A.coff[k] : (uint64_t)k * A.chunk_size;
-    const uint32_t n = A.coff ? A.clen[k] : (uint32_t)min((uint64_t)A.chunk_size, A.n_total - pos0);
+    const uint32_t n = A.coff ? (A.clen ? A.clen[k] : A.clen_all) : (uint32_t)min((uint64_t)A.chunk_size, A.n_total - pos0);
     uint32_t T = 0;
     if (n > (uint32_t)CMAX || !z9_gate(A, k, n, T)) return;
     uint32_t* R = A.z9rec + (uint64_t)k * Z9Rec<CMAX>::STRIDE;

@@ -566,7 +566,7 @@ __global__ __launch_bounds__(64 * Z9Cfg<CMAX>::NW) void k_z9_parse(EncArgs A) {
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t k = blockIdx.x;
     const uint64_t pos0 = A.coff ? A.coff[k] : (uint64_t)k * A.chunk_size;
-    const uint32_t n = A.coff ? A.clen[k] : (uint32_t)min((uint64_t)A.chunk_size, A.n_total - pos0);
+    const uint32_t n = A.coff ? (A.clen ? A.clen[k] : A.clen_all) : (uint32_t)min((uint64_t)A.chunk_size, A.n_total - pos0);
     uint32_t T = 0;
     if (n > (uint32_t)CMAX || !z9_gate(A, k, n, T)) return;
     PSTAMP_DECL
@@ -737,7 +737,7 @@ __global__ __launch_bounds__(64) void k_z9_code(EncArgs A) {
     const uint32_t lane = threadIdx.x;
     const uint32_t k = blockIdx.x;
     const uint64_t pos0 = A.coff ? A.coff[k] : (uint64_t)k * A.chunk_size;
-    const uint32_t n = A.coff ? A.clen[k] : (uint32_t)min((uint64_t)A.chunk_size, A.n_total - pos0);
+    const uint32_t n = A.coff ? (A.clen ? A.clen[k] : A.clen_all) : (uint32_t)min((uint64_t)A.chunk_size, A.n_total - pos0);
     uint32_t T = 0;
     if (n > (uint32_t)CMAX || !z9_gate(A, k, n, T)) return;
     ZSTAMP_DECL

@@ -544,7 +544,7 @@ __global__ __launch_bounds__(64 * ZB_NW) void k_z9_parse_big(EncArgs A) {
     for (uint32_t k = blockIdx.x; k < A.n_chunks; k += gridDim.x) {
         __syncthreads();   // (the previous chunk's last LDS reads)
         const uint64_t pos0 = A.coff ? A.coff[k] : (uint64_t)k * A.chunk_size;
-        const uint32_t n = A.coff ? A.clen[k] : (uint32_t)min((uint64_t)A.chunk_size, A.n_total - pos0);
+        const uint32_t n = A.coff ? (A.clen ? A.clen[k] : A.clen_all) : (uint32_t)min((uint64_t)A.chunk_size, A.n_total - pos0);
         uint32_t T = 0;
         if (n > (uint32_t)CMAX || !z9_gate(A, k, n, T)) continue;
         const uint8_t* src = A.in + pos0;
@@ -785,7 +785,7 @@ __global__ __launch_bounds__(64) void k_z9_code_big(EncArgs A) {
     const uint32_t lane = threadIdx.x;
     const uint32_t k = blockIdx.x;
     const uint64_t pos0 = A.coff ? A.coff[k] : (uint64_t)k * A.chunk_size;
-    const uint32_t n = A.coff ? A.clen[k] : (uint32_t)min((uint64_t)A.chunk_size, A.n_total - pos0);
+    const uint32_t n = A.coff ? (A.clen ? A.clen[k] : A.clen_all) : (uint32_t)min((uint64_t)A.chunk_size, A.n_total - pos0);
     uint32_t T = 0;
     if (n > (uint32_t)CMAX || !z9_gate(A, k, n, T)) return;
     const uint8_t* src = A.in + pos0;
