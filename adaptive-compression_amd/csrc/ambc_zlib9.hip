@@ -22,7 +22,7 @@
 //   3. the lazy parse by walkers (8-lane groups).  zlib's longest_match at p
 //      is the first chain entry reaching the longest length (capped at
 //      min(258, n - p)), over the first 4096 entries -- or 1024 when the
-//      previous match was >= 32 long: both answers come out of one scan.  After
+//      previous match was >= 32 long (the walker knows which).  After
 //      a match the parser state is fresh, so the step from one fresh position
 //      to the next (literals, then the match that ends the segment) is a pure
 //      function of the position: walkers start from spread positions, record
@@ -291,10 +291,12 @@ __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t
         }
 #endif
         const bool act = !done && !skip && s >= 1 && s + 3 <= n && P < 258;   // position 0 is zlib's NIL
-        // ---- longest_match(s): k0 over the first 4096 chain entries, k1 over
-        // the first 1024; key = min(len, nice) << 16 | candidate (the longest,
-        // then the most recent) ----
-        uint32_t k0 = 0, k1 = 0;
+        // ---- longest_match(s) over the first lim chain entries (zlib's
+        // max_chain 4096, a quarter when the pending match is >= good_match);
+        // key = min(len, nice) << 16 | candidate (the longest, then the most
+        // recent) ----
+        uint32_t k0 = 0;
+        const uint32_t lim = P >= Z_GOOD ? Z_CHAIN / 4 : Z_CHAIN;
         {
             uint32_t tg[4] = {0, 0, 0, 0}, h = 0, lo = 0, j = 0, nice = 0;
             const uint32_t ss = s & 3u;
@@ -332,13 +334,12 @@ __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t
                 if (re >= s + 3 && B >= 8 && B <= j - lo) {
                     const uint32_t key = min(min(re - s, Z_MAXM), nice) << 16 | (s - 1);
                     k0 = key;
-                    k1 = key;
                     cnt = B;
                     j -= B;
                 }
             }
 #endif
-            bool gd = !act || j <= lo || cnt >= Z_CHAIN || (k0 >> 16) >= nice;
+            bool gd = !act || j <= lo || cnt >= lim || (k0 >> 16) >= nice;
 #pragma unroll 1
             while (__any(!gd)) {
                 const int idx = (int)j - 1 - (int)r;
@@ -354,8 +355,10 @@ __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t
                 const bool same = v && z_h15(x[0] & 0xFFFFFFu) == h;
                 const uint32_t sm = grp_bits<G>(__ballot(same), g);
                 const uint32_t kidx = cnt + (uint32_t)__popc(sm & ((1u << r) - 1u)) + 1u;
-                const bool inwin = s - c <= Z_MAXD;
-                const bool ok = same && inwin && kidx <= Z_CHAIN;
+                // (a chunk of at most MAX_DIST bytes has every candidate in the window)
+                constexpr bool WIN_ALL = (uint32_t)CMAX <= Z_MAXD;
+                const bool inwin = WIN_ALL || s - c <= Z_MAXD;
+                const bool ok = same && inwin && kidx <= lim;
                 uint32_t fm = ~0u;
 #pragma unroll
                 for (int t = 0; t < 4; t++) fm = min(fm, ffbl_raw(x[t] ^ tg[t]) | (uint32_t)t << 5);
@@ -425,17 +428,16 @@ __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t
                 const uint32_t Lp = min(min(len, Z_MAXM), nice);
                 const uint32_t key = ok && can ? (Lp << 16 | c) : 0u;
                 k0 = max(k0, grp_max<G>(key));
-                k1 = max(k1, grp_max<G>(ok && kidx <= Z_CHAIN / 4 ? key : 0u));
                 cnt += (uint32_t)__popc(sm);
-                const uint32_t far = grp_bits<G>(__ballot(v && !inwin), g);
+                const uint32_t far = WIN_ALL ? 0u : grp_bits<G>(__ballot(v && !inwin), g);
                 j = j > lo + G ? j - G : lo;
-                gd = gd || j <= lo || far != 0 || cnt >= Z_CHAIN || (k0 >> 16) >= nice;
+                gd = gd || j <= lo || far != 0 || cnt >= lim || (k0 >> 16) >= nice;
             }
         }
         if (!done && !skip) {
             uint32_t ML = 2, MD = 0;
             if (act) {
-                const uint32_t key = P >= Z_GOOD ? k1 : k0;
+                const uint32_t key = k0;
                 const uint32_t L = key >> 16, d = s - (key & 0xFFFFu);
                 if (L >= 3 && !(L == 3 && d > Z_TOOFAR)) { ML = L; MD = d; }
             }
