@@ -340,11 +340,17 @@ __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t
             }
 #endif
             bool gd = !act || j <= lo || cnt >= lim || (k0 >> 16) >= nice;
+            int ji = (int)j;
+            // the chain limit can only bind where the bucket below s holds more
+            // entries than are left to count (runs, long repeats): elsewhere the
+            // counting is skipped for the whole wave
+            const bool cnt_live = __any(act && cnt + (j - lo) > lim);
 #pragma unroll 1
             while (__any(!gd)) {
-                const int idx = (int)j - 1 - (int)r;
-                const bool v = !gd && idx >= (int)lo;
-                const uint32_t c = v ? (uint32_t)S.lst[idx] : 0u;
+                const int idx = ji - 1 - (int)r;
+                const bool v = !gd & (idx >= (int)lo);
+                // every lane loads (an index in range; a lane past the chain is masked by v)
+                const uint32_t c = (uint32_t)S.lst[max(idx, 0)];
                 const uint32_t a = c >> 2, sh = c & 3u;
                 uint32_t w[5];
 #pragma unroll
@@ -352,13 +358,17 @@ __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t
                 uint32_t x[4];
 #pragma unroll
                 for (int t = 0; t < 4; t++) x[t] = __builtin_amdgcn_alignbyte(w[t + 1], w[t], sh);
-                const bool same = v && z_h15(x[0] & 0xFFFFFFu) == h;
-                const uint32_t sm = grp_bits<G>(__ballot(same), g);
-                const uint32_t kidx = cnt + (uint32_t)__popc(sm & ((1u << r) - 1u)) + 1u;
+                const bool same = v & (z_h15(x[0] & 0xFFFFFFu) == h);
+                uint32_t sm = 0;
+                bool klim = true;
+                if (cnt_live) {
+                    sm = grp_bits<G>(__ballot(same), g);
+                    klim = cnt + (uint32_t)__popc(sm & ((1u << r) - 1u)) + 1u <= lim;
+                }
                 // (a chunk of at most MAX_DIST bytes has every candidate in the window)
                 constexpr bool WIN_ALL = (uint32_t)CMAX <= Z_MAXD;
                 const bool inwin = WIN_ALL || s - c <= Z_MAXD;
-                const bool ok = same && inwin && kidx <= lim;
+                const bool ok = same & inwin & klim;
                 uint32_t fm = ~0u;
 #pragma unroll
                 for (int t = 0; t < 4; t++) fm = min(fm, ffbl_raw(x[t] ^ tg[t]) | (uint32_t)t << 5);
@@ -430,8 +440,8 @@ __device__ __forceinline__ void z9_walkers(Z9Smem<CMAX>& S, uint32_t n, uint32_t
                 k0 = max(k0, grp_max<G>(key));
                 cnt += (uint32_t)__popc(sm);
                 const uint32_t far = WIN_ALL ? 0u : grp_bits<G>(__ballot(v && !inwin), g);
-                j = j > lo + G ? j - G : lo;
-                gd = gd || j <= lo || far != 0 || cnt >= lim || (k0 >> 16) >= nice;
+                ji -= (int)G;
+                gd = gd | (ji <= (int)lo) | (far != 0) | (cnt >= lim) | ((k0 >> 16) >= nice);
             }
         }
         if (!done && !skip) {
