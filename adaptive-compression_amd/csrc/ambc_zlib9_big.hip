@@ -386,7 +386,8 @@ __device__ __forceinline__ void z9b_walkers(Z9BSmem<CMAX>& S, uint32_t n, const 
             }
             bool gd = !act || rgd || j <= lo || cnt >= lim || (k0 >> 16) >= nice;
             int idx = (int)j - 1 - (int)r;
-            uint32_t cn = !gd && idx >= (int)lo ? (uint32_t)lst[idx] : 0u;
+            // every lane loads (an index in range; lanes past the chain are masked by v)
+            uint32_t cn = (uint32_t)lst[max(idx, 0)];
             uint32_t wn[5];
 #pragma unroll
             for (int t = 0; t < 5; t++) wn[t] = W32((cn >> 2) + t);
@@ -398,27 +399,27 @@ __device__ __forceinline__ void z9b_walkers(Z9BSmem<CMAX>& S, uint32_t n, const 
 #ifdef AMBC_STAMPS
                 c_st++;
 #endif
-                const bool v = !gd && idx >= (int)lo;
-                const uint32_t c = v ? cn : 0u;
+                const bool v = !gd & (idx >= (int)lo);
+                const uint32_t c = cn;
                 uint32_t w[5];
 #pragma unroll
                 for (int t = 0; t < 5; t++) w[t] = wn[t];
                 // the next step's candidate and its words, issued now
                 idx -= (int)G;
-                cn = !gd && idx >= (int)lo ? (uint32_t)lst[idx] : 0u;
+                cn = (uint32_t)lst[max(idx, 0)];
 #pragma unroll
                 for (int t = 0; t < 5; t++) wn[t] = W32((cn >> 2) + t);
                 const uint32_t sh = c & 3u;
                 uint32_t x[4];
 #pragma unroll
-                for (int t = 0; t < 4; t++) x[t] = __builtin_amdgcn_alignbyte(w[t + 1], w[t], v ? sh : 0u);
-                const bool same = v && z_h15(x[0] & 0xFFFFFFu) == h;
+                for (int t = 0; t < 4; t++) x[t] = __builtin_amdgcn_alignbyte(w[t + 1], w[t], sh);
+                const bool same = v & (z_h15(x[0] & 0xFFFFFFu) == h);
                 const uint32_t sm = grp_bits<G>(__ballot(same), g);
                 const uint32_t kidx = cnt + (uint32_t)__popc(sm & ((1u << r) - 1u)) + 1u;
                 // the hash head may lie MAX_DIST back (deflate_slow's test is <=);
                 // later chain entries must lie above limit = s - MAX_DIST
                 const bool inwin = s - c < Z_MAXD || (s - c == Z_MAXD && kidx == 1u);
-                const bool ok = same && inwin && kidx <= lim;
+                const bool ok = same & inwin & (kidx <= lim);
                 // the slide step: a head of 32768 is NIL, no search at all
                 const bool nilh = grp_bits<G>(__ballot(same && kidx == 1u && c == Z_WSZ && s == nil_at), g) != 0;
                 uint32_t fm = ~0u;
