@@ -103,6 +103,8 @@ int ambc_init(const int* device_ids, int n_devices, ambc_ctx** out) {
             HIPCHK(hipStreamCreateWithFlags(&d.cs, hipStreamNonBlocking));
         }
         for (auto& ev : d.pev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        HIPCHK(hipStreamCreateWithFlags(&d.zs, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&d.zev, hipEventDisableTiming));
         ctx->devs.push_back(d);
     }
     *out = ctx.release();
@@ -137,6 +139,8 @@ void ambc_destroy(ambc_ctx* ctx) {
         for (auto& ev : d.pev) (void)hipEventDestroy(ev);
         (void)hipStreamSynchronize(d.cs);
         (void)hipStreamDestroy(d.cs);
+        if (d.zs) { (void)hipStreamSynchronize(d.zs); (void)hipStreamDestroy(d.zs); }
+        if (d.zev) (void)hipEventDestroy(d.zev);
         (void)hipStreamDestroy(d.stream);
     }
     delete ctx;
@@ -372,17 +376,33 @@ static int compress_on_body(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_
         e.kbase = k0;
         return e;
     };
+    // zlib-9 over pipelined segments (chunks up to 8 KiB, every scratch array per
+    // chunk): a segment's trees, emission and pending payloads go to d.zs behind
+    // its parse, so they run beside the next segment's encode and parse (the
+    // parse is issue-bound at 4 workgroups per CU, the tree / emission kernels
+    // latency-bound at low occupancy); its compaction waits for them
+    static const bool z9_one_stream = getenv("AMBC_Z9_ONESTREAM") != nullptr;
+    bool z9split = false;
     auto encode_range = [&](const EncArgs& e) -> int {
         HIPCHK(launch_encode(e, s));
         if (dict) HIPCHK(launch_dict(e, dict_cmax(p), s));   // id 2 against k_encode's winner
         // id 5 after 1/2/3/4, against LZ4 (ties -> 5)
-        if (deflate) HIPCHK(z9 ? launch_zlib9(e, s) : launch_deflate(e, s));
+        hipStream_t ts = s;
+        if (deflate && z9 && z9split) {
+            HIPCHK(launch_zlib9_parse(e, s));
+            HIPCHK(hipEventRecord(d.zev, s));
+            HIPCHK(hipStreamWaitEvent(d.zs, d.zev, 0));
+            ts = d.zs;
+            HIPCHK(launch_zlib9_tail(e, ts));
+        } else if (deflate) {
+            HIPCHK(z9 ? launch_zlib9(e, s) : launch_deflate(e, s));
+        }
         if (deflate || dict) {
             EncArgs ep = e;                 // RLE/Huffman payloads ids 2 / 5 did not replace
             ep.flags |= ENC_EMIT_PENDING;
             ep.bestpre = nullptr;
             ep.stamps = nullptr;
-            HIPCHK(launch_encode(ep, s));
+            HIPCHK(launch_encode(ep, ts));
         }
         return AMBC_OK;
     };
@@ -396,6 +416,7 @@ static int compress_on_body(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_
     static const uint32_t nseg = getenv("AMBC_NSEG") ? std::max(1, std::min(8, atoi(getenv("AMBC_NSEG")))) : NSEG;
     const uint32_t S = (p->mode != AMBC_MODE_REFERENCE && M >= 16384 && !ea.stamps) ? nseg : 1;
     d.n_launch = S;
+    z9split = z9 && S > 1 && z9_cmax(C) <= 8192 && !z9_one_stream;
     HIPCHK(hipEventRecord(d.ev[0], s));
     if (S > 1) {
         size_t tmpb = 0;
@@ -409,8 +430,9 @@ static int compress_on_body(Dev& d, const uint8_t* d_in, uint64_t n, const ambc_
             const uint32_t k0 = (uint32_t)((uint64_t)M * i / S), k1 = (uint32_t)((uint64_t)M * (i + 1) / S);
             rc = encode_range(seg_args(k0, k1));
             if (rc) return rc;
+            HIPCHK(hipEventRecord(d.pev[i], z9split ? d.zs : s));
+            if (z9split && i + 1 == S) HIPCHK(hipStreamWaitEvent(s, d.pev[i], 0));   // the statistics read every id
             if (i + 1 == S) HIPCHK(hipEventRecord(d.ev[1], s));
-            HIPCHK(hipEventRecord(d.pev[i], s));
             HIPCHK(hipStreamWaitEvent(d.cs, d.pev[i], 0));
             size_t tb = tmpb;
             HIPCHK(scan_sizes(d.sizes.as<uint64_t>() + k0, d.off.as<uint64_t>() + k0, k1 - k0, d.scan_tmp.p,

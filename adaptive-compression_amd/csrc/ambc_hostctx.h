@@ -141,6 +141,8 @@ struct Dev {
     uint32_t n_launch = 1;      // k_encode launches of the last compress call (pipelined segments)
     hipStream_t cs = nullptr;   // scan + compaction of pipelined segments
     hipEvent_t pev[8] = {};     // segment i encoded
+    hipStream_t zs = nullptr;   // zlib-9 trees + emission of segment i beside the parse of i + 1
+    hipEvent_t zev = nullptr;   // segment i parsed
     Buf segbase;                // body offset of every segment (device)
     // pinned staging for large pageable copies: 2 buffers + 2 events per copy
     // thread; set 0 uploads, set 1 downloads (the decode pipeline runs both at once)

@@ -229,6 +229,9 @@ size_t z9_scratch_bytes(uint32_t cmax, uint32_t n_chunks);
 size_t z9_rec_words_big(uint32_t cmax);
 hipError_t launch_zlib9_big(const EncArgs& a, hipStream_t s);
 hipError_t launch_zlib9(const EncArgs& a, hipStream_t s);
+// the small-chunk zlib-9 path in two parts: the parse, then trees + emission (chunks <= 8 KiB)
+hipError_t launch_zlib9_parse(const EncArgs& a, hipStream_t s);
+hipError_t launch_zlib9_tail(const EncArgs& a, hipStream_t s);
 hipError_t launch_compact(const CompactArgs& a, hipStream_t s);
 hipError_t launch_end_chunk(uint8_t* dst, hipStream_t s);
 // out == null: only *off into acc_slot[0]

@@ -993,11 +993,20 @@ __global__ __launch_bounds__(64) void k_z9_code(EncArgs A) {
 }
 
 template <int CMAX>
-hipError_t launch_z9_t(const EncArgs& a, hipStream_t s) {
+hipError_t launch_z9_parse_t(const EncArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_z9_parse<CMAX>, dim3(a.n_chunks), dim3(64 * Z9Cfg<CMAX>::NW), 0, s, a);
+    return hipGetLastError();
+}
+template <int CMAX>
+hipError_t launch_z9_tail_t(const EncArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_z9_heap<CMAX>, dim3((a.n_chunks + ZH_L - 1) / ZH_L), dim3(64), 0, s, a);
     hipLaunchKernelGGL(k_z9_code<CMAX>, dim3(a.n_chunks), dim3(64), 0, s, a);
     return hipGetLastError();
+}
+template <int CMAX>
+hipError_t launch_z9_t(const EncArgs& a, hipStream_t s) {
+    const hipError_t e = launch_z9_parse_t<CMAX>(a, s);
+    return e != hipSuccess ? e : launch_z9_tail_t<CMAX>(a, s);
 }
 
 }  // namespace
@@ -1014,6 +1023,28 @@ size_t z9_rec_words(uint32_t cmax) {
         case 4096: return Z9Rec<4096>::STRIDE;
         case 8192: return Z9Rec<8192>::STRIDE;
         default: return z9_rec_words_big(cmax);
+    }
+}
+
+hipError_t launch_zlib9_parse(const EncArgs& a, hipStream_t s) {
+    if (a.n_chunks == 0) return hipSuccess;
+    switch (z9_cmax(a.chunk_size)) {
+        case 1024: return launch_z9_parse_t<1024>(a, s);
+        case 2048: return launch_z9_parse_t<2048>(a, s);
+        case 4096: return launch_z9_parse_t<4096>(a, s);
+        case 8192: return launch_z9_parse_t<8192>(a, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_zlib9_tail(const EncArgs& a, hipStream_t s) {
+    if (a.n_chunks == 0) return hipSuccess;
+    switch (z9_cmax(a.chunk_size)) {
+        case 1024: return launch_z9_tail_t<1024>(a, s);
+        case 2048: return launch_z9_tail_t<2048>(a, s);
+        case 4096: return launch_z9_tail_t<4096>(a, s);
+        case 8192: return launch_z9_tail_t<8192>(a, s);
+        default: return hipErrorInvalidValue;
     }
 }
 

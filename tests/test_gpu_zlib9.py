@@ -71,6 +71,15 @@ def test_zlib9_bodies_match_zlib(ctx, n, seed, chunk, methods):
     assert _check(synth.generate(n, seed), chunk, methods) > 0
 
 
+def test_zlib9_segmented_call_matches_zlib(ctx):
+    """16385 chunks: the native call runs as pipelined segments, each segment's
+    zlib-9 trees, emission and pending payloads on a second stream beside the next
+    segment's encode and parse (ambc_host.cpp encode_range); body equal to the
+    oracle's, every id-5 package equal to zlib.compress(chunk, 9)"""
+    data = synth.generate((16 << 20) + 77, 31)
+    assert _check(data, 1024, (1, 3, 4, 5), modes=("native",)) > 0
+
+
 def _biased(n, p, seed):
     rng = random.Random(seed)
     return bytes(97 if rng.random() < p else 98 for _ in range(n))
